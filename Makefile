@@ -1,0 +1,31 @@
+# Builds every native artefact in-tree (the .so files travel to the GPU box).
+#   orb_slam_fusion_amd/lib/liborbgpu.so   HIP kernels + C ABI (gfx950)
+#   orb_slam_fusion_amd/lib/liborbsynth.so synthetic workloads (host)
+#   oracle/_build/liborboracle.so          CPU oracle (test infrastructure)
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+CSRC     := orb_slam_fusion_amd/csrc
+LIB      := orb_slam_fusion_amd/lib
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall
+GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/orb_plan.cpp \
+            $(CSRC)/orb_api.cpp $(CSRC)/pose_api.cpp
+GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
+
+all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so oracle
+
+$(LIB)/liborbgpu.so: $(GPU_SRCS) $(GPU_HDRS)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_SRCS)
+
+$(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
+	@mkdir -p $(LIB)
+	$(CXX) -std=c++17 -O2 -fPIC -shared -o $@ $<
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(LIB) oracle/_build
+
+.PHONY: all oracle clean

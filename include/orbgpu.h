@@ -1,0 +1,165 @@
+/*
+ * orbgpu -- MI355X (gfx950) ORB front-end and pose/bundle-adjustment back-end.
+ *
+ * C ABI: plain pointers, sizes and POD structs; integer status codes; one
+ * handle per calling thread (each owns its HIP stream and workspace); no global
+ * mutable state.  Every entry point below names the reference interface it
+ * replaces (paths under J094/orb_slam_fusion).
+ */
+#ifndef ORBGPU_H
+#define ORBGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int orbgpu_status;
+#define ORBGPU_OK 0
+#define ORBGPU_ERR_INVALID (-1)  /* bad argument / unsupported geometry        */
+#define ORBGPU_ERR_EMPTY (-2)    /* empty image: reference operator() returns -1 */
+#define ORBGPU_ERR_CAPACITY (-3) /* caller buffer or internal bound too small  */
+#define ORBGPU_ERR_DEVICE (-4)   /* HIP runtime error                          */
+#define ORBGPU_ERR_NOMEM (-5)
+
+/* OrbExtractor(int num_feats, float scale_factor, int num_levs,
+ *              int ini_th_fast, int min_th_fast)
+ *   include/cam/orb_feature/orb_extractor.h:48-49, orb_extractor.cc:407-465 */
+typedef struct orbgpu_orb_params {
+  int num_features;
+  float scale_factor;
+  int num_levels;
+  int ini_th_fast;
+  int min_th_fast;
+} orbgpu_orb_params;
+
+/* Field order and size (28 B) of cv::KeyPoint {pt.x, pt.y, size, angle,
+ * response, octave, class_id}: the shim copies these straight into the
+ * caller's std::vector<cv::KeyPoint>. */
+typedef struct orbgpu_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbgpu_keypoint;
+
+typedef struct orbgpu_extractor orbgpu_extractor;
+
+/* Creates an extractor bound to `device` with workspace for batches of up to
+ * `max_images` images of at most max_width x max_height.
+ * Replaces: OrbExtractor::OrbExtractor (orb_extractor.cc:407). */
+orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int device, int max_width,
+                                      int max_height, int max_images, orbgpu_extractor** out);
+void orbgpu_extractor_destroy(orbgpu_extractor* h);
+
+/* Scale tables, `num_levels` floats each (any pointer may be NULL).
+ * Replaces: GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares (orb_extractor.h:60-74). */
+orbgpu_status orbgpu_extractor_scales(const orbgpu_extractor* h, float* scale, float* inv_scale,
+                                      float* sigma2, float* inv_sigma2);
+int orbgpu_extractor_levels(const orbgpu_extractor* h);
+/* Upper bound on keypoints one image can produce at the given geometry. */
+int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height);
+
+/* Host-buffer extraction of one grayscale 8-bit image.
+ * Replaces: int OrbExtractor::operator()(InputArray img, InputArray msk,
+ *   vector<KeyPoint>& kps, OutputArray descs, vector<int>& lapping_areas)
+ *   (orb_extractor.h:56-58, orb_extractor.cc:1011-1091).
+ * Writes n keypoints and n x 32 descriptor bytes (row i = keypoint i) when
+ * n <= cap; *n_out always receives n.  *mono_out receives operator()'s return
+ * value (keypoints with lapping[0] <= x <= lapping[1] fill the tail in reverse
+ * order, the rest the head).  Empty image -> ORBGPU_ERR_EMPTY (reference: -1).
+ * The mask argument of the reference is ignored there too (orb_extractor.h:54). */
+orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width, int height,
+                             int stride, const int lapping[2], orbgpu_keypoint* kps,
+                             uint8_t* descs, int cap, int* n_out, int* mono_out);
+
+/* Host copy of pyramid level `level` from the last orbgpu_extract call
+ * (packed rows, *stride == *width).  Replaces the public member
+ * std::vector<cv::Mat> img_pyramid_ (orb_extractor.h:76) read by
+ * Frame::ComputeStereoMatches (frame.cc:834,913-933).  The pointer stays valid
+ * until the next extract/destroy on this handle. */
+orbgpu_status orbgpu_extractor_pyramid_level(orbgpu_extractor* h, int level, const uint8_t** data,
+                                             int* width, int* height, int* stride);
+
+/* Device-resident batched extraction: n_images images at d_imgs + i*image_pitch
+ * (row stride `stride`), all in device memory; outputs go to device buffers
+ * d_kps[n_images][cap_per_image], d_descs[n_images][cap_per_image][32],
+ * d_n[n_images], d_mono[n_images].  Asynchronous on `hip_stream` (NULL = the
+ * handle's own stream).  This is the throughput path: N stereo frames ->
+ * 2N images per call, one HIP-graph-friendly launch sequence. */
+orbgpu_status orbgpu_extract_batch(orbgpu_extractor* h, const uint8_t* d_imgs, int n_images,
+                                   int width, int height, int stride, size_t image_pitch,
+                                   const int lapping[2], orbgpu_keypoint* d_kps, uint8_t* d_descs,
+                                   int cap_per_image, int* d_n, int* d_mono, void* hip_stream);
+
+/* Synchronises the handle's last batch and returns the first device-side
+ * error (ORBGPU_ERR_CAPACITY when an internal bound was hit), else ORBGPU_OK. */
+orbgpu_status orbgpu_extractor_check(orbgpu_extractor* h);
+
+/* Per-stage timing of the next `max_calls` orbgpu_extract_batch calls with
+ * HIP events recorded on the launch stream between the kernel stages
+ * (0 resize, 1 blur, 2 FAST cells, 3 octree, 4 describe, 5 assemble).
+ * orbgpu_extractor_profile_read waits for them, writes the summed
+ * milliseconds per stage (6 doubles) and returns the number of calls timed. */
+orbgpu_status orbgpu_extractor_profile(orbgpu_extractor* h, int max_calls);
+int orbgpu_extractor_profile_read(orbgpu_extractor* h, double* ms_per_stage);
+
+/* Diagnostics: internal stage buffers of image 0 of the last call (used by
+ * the parity tests to localise a mismatch).  which = 0: blurred level plane
+ * (w*h bytes); 1: FAST candidates of the level in the reference's to_dist
+ * order; 2: octree output in node-list order.  Candidates are uint32
+ * x | y << 12 | response << 24 (coordinates relative to the 16-px FAST
+ * border).  Returns the element count, or -1. */
+int orbgpu_extractor_stage(orbgpu_extractor* h, int which, int level, void* out, int cap);
+
+/* ------------------------------------------------------------------------ */
+/* Pose-only optimisation.
+ * Replaces: static int Optimizer::PoseOptimization(Frame* pFrame)
+ *   (include/solver/g2o_solver/optimizer.h:64, optimizer.cc:762-1051),
+ *   pinhole rig (pFrame->cam2_ == NULL).  The shim flattens the Frame: one
+ *   observation per i with pFrame->mvpMapPoints[i] != NULL, in index order. */
+typedef struct orbgpu_camera {
+  float fx, fy, cx, cy, bf; /* Frame::fx, fy, cx, cy, bf_ */
+} orbgpu_camera;
+
+typedef struct orbgpu_pose {
+  float qx, qy, qz, qw; /* Tcw.unit_quaternion()  */
+  float tx, ty, tz;     /* Tcw.translation()      */
+} orbgpu_pose;
+
+typedef struct orbgpu_pose_obs {
+  float Xw[3];      /* MapPoint::GetWorldPos()                           */
+  float u, v;       /* mvKeysUn[i].pt                                    */
+  float ur;         /* mvuRight[i]; < 0 -> monocular edge                */
+  float inv_sigma2; /* mvInvLevelSigma2[mvKeysUn[i].octave]              */
+} orbgpu_pose_obs;
+
+typedef struct orbgpu_pose_ctx orbgpu_pose_ctx;
+
+orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
+                                     orbgpu_pose_ctx** out);
+void orbgpu_pose_ctx_destroy(orbgpu_pose_ctx* c);
+
+/* One problem from host buffers.  Writes the optimised pose (SetPose), the
+ * per-observation outlier flags (mvbOutlier) and returns the inlier count in
+ * *n_inliers (PoseOptimization's return value; 0 and pose unchanged when
+ * n_obs < 3). */
+orbgpu_status orbgpu_pose_opt(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
+                              const orbgpu_pose* Tcw_in, const orbgpu_pose_obs* obs, int n_obs,
+                              orbgpu_pose* Tcw_out, uint8_t* outlier, int* n_inliers);
+
+/* Device-resident batch: problem p uses d_obs[p*obs_stride .. +d_nobs[p]),
+ * one shared camera.  Asynchronous on `hip_stream` (NULL = the context's
+ * stream).  d_pose_out_d (optional) receives the 7 double-precision pose
+ * components before the float cast. */
+orbgpu_status orbgpu_pose_opt_batch(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
+                                    const orbgpu_pose* d_Tcw_in, const orbgpu_pose_obs* d_obs,
+                                    const int* d_nobs, int obs_stride, int n_problems,
+                                    orbgpu_pose* d_Tcw_out, uint8_t* d_outlier, int* d_inliers,
+                                    double* d_pose_out_d, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBGPU_H */

@@ -1,0 +1,170 @@
+"""ORACLE binding (test infrastructure only).
+
+ctypes access to oracle/_build/liborboracle.so -- the CPU restatement of the
+reference hot path.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker / the CPU
+baseline; nothing in orb_slam_fusion_amd/ may.
+"""
+from __future__ import annotations
+
+import ctypes
+from functools import lru_cache
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "_build" / "liborboracle.so"
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+POSE_OBS_DTYPE = np.dtype([("Xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                           ("inv_sigma2", "<f4")])
+
+_P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+
+
+@lru_cache(None)
+def lib() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise OSError(f"{LIB_PATH} missing: run `make -C oracle`")
+    so = ctypes.CDLL(str(LIB_PATH))
+    sig = {
+        "orc_extractor_new": (_P, [_I, _F, _I, _I, _I]),
+        "orc_extractor_free": (None, [_P]),
+        "orc_extract": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P]),
+        "orc_extract_stereo": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P]),
+        "orc_params": (None, [_P, _P, _P, _P, _P, _P, _P]),
+        "orc_pyramid": (None, [_P, _P, _I, _I, _I]),
+        "orc_level_size": (_I, [_P, _I, _P, _P]),
+        "orc_level_copy": (None, [_P, _I, _I, _P]),
+        "orc_stage": (_I, [_P, _I, _I, _P, _I]),
+        "orc_resize": (None, [_P, _I, _I, _P, _I, _I]),
+        "orc_gauss": (None, [_P, _I, _I, _P]),
+        "orc_gauss_kernel": (None, [_P]),
+        "orc_fast": (_I, [_P, _I, _I, _I, _I, _P, _I]),
+        "orc_fast_atan2": (_F, [_F, _F]),
+        "orc_sincosf": (None, [_P, _I, _P, _P]),
+        "orc_sincosf_check_libm": (ctypes.c_long, [ctypes.c_uint, ctypes.c_uint]),
+        "orc_pose_opt": (_I, [_P, _P, _P, _I, _P, _P, _P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(so, name)
+        f.restype, f.argtypes = res, args
+    return so
+
+
+def _p(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class OracleExtractor:
+    """CPU restatement of ORB_SLAM_FUSION::OrbExtractor (see orb_oracle.h)."""
+
+    def __init__(self, num_feats=1000, scale_factor=1.2, num_levs=8, ini_th=20, min_th=7):
+        self.L = num_levs
+        self._h = lib().orc_extractor_new(num_feats, scale_factor, num_levs, ini_th, min_th)
+
+    def __del__(self):
+        try:
+            lib().orc_extractor_free(self._h)
+        except Exception:
+            pass
+
+    def extract(self, img: np.ndarray, lapping=(0, 0)):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        cap = 8192
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        mono = lib().orc_extract(self._h, _p(img), w, h, w, int(lapping[0]), int(lapping[1]),
+                                 _p(kps), _p(desc), cap, ctypes.byref(n))
+        assert n.value <= cap
+        return mono, kps[: n.value].copy(), desc[: n.value].copy()
+
+    def params(self):
+        L = self.L
+        s, i, s2, is2 = (np.zeros(L, np.float32) for _ in range(4))
+        fpl = np.zeros(L, np.int32)
+        umax = np.zeros(16, np.int32)
+        lib().orc_params(self._h, _p(s), _p(i), _p(s2), _p(is2), _p(fpl), _p(umax))
+        return dict(scale=s, inv_scale=i, sigma2=s2, inv_sigma2=is2, feats_per_level=fpl, umax=umax)
+
+    def level(self, lev: int, blurred: bool = False) -> np.ndarray:
+        w, h = ctypes.c_int(), ctypes.c_int()
+        assert lib().orc_level_size(self._h, lev, ctypes.byref(w), ctypes.byref(h)) == 0
+        out = np.zeros((h.value, w.value), np.uint8)
+        lib().orc_level_copy(self._h, lev, int(blurred), _p(out))
+        return out
+
+    def pyramid(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        lib().orc_pyramid(self._h, _p(img), w, h, w)
+        return [self.level(l) for l in range(self.L)]
+
+    def stage(self, lev: int, which: int) -> np.ndarray:
+        """which 0: FAST candidates in to_dist order; 1: octree output in list
+        order.  Rows (x, y, response), coordinates relative to the 16-px border."""
+        cap = 1 << 18
+        buf = np.zeros((cap, 3), np.float32)
+        n = lib().orc_stage(self._h, lev, which, _p(buf), cap)
+        return buf[:n].copy()
+
+
+def resize(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().orc_resize(_p(src), src.shape[1], src.shape[0], _p(out), dw, dh)
+    return out
+
+
+def gauss(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros_like(src)
+    lib().orc_gauss(_p(src), src.shape[1], src.shape[0], _p(out))
+    return out
+
+
+def gauss_kernel():
+    k = np.zeros(7, np.int32)
+    lib().orc_gauss_kernel(_p(k))
+    return k
+
+
+def fast(roi: np.ndarray, th: int) -> np.ndarray:
+    roi = np.ascontiguousarray(roi, np.uint8)
+    cap = roi.size
+    buf = np.zeros((cap, 3), np.int32)
+    n = lib().orc_fast(_p(roi), roi.shape[1], roi.shape[1], roi.shape[0], th, _p(buf), cap)
+    return buf[:n].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return float(lib().orc_fast_atan2(y, x))
+
+
+def sincosf(x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float32)
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    lib().orc_sincosf(_p(x), x.size, _p(s), _p(c))
+    return s, c
+
+
+def sincosf_check_libm(lo_bits: int, hi_bits: int) -> int:
+    return int(lib().orc_sincosf_check_libm(lo_bits, hi_bits))
+
+
+def pose_opt(cam: np.ndarray, pose_in: np.ndarray, obs: np.ndarray):
+    """Returns (inliers, pose_out float32[7], outlier uint8[n], pose_out float64[7])."""
+    cam = np.ascontiguousarray(cam, np.float32)
+    pose_in = np.ascontiguousarray(pose_in, np.float32)
+    obs = np.ascontiguousarray(obs, POSE_OBS_DTYPE)
+    n = len(obs)
+    pout = np.zeros(7, np.float32)
+    pd = np.zeros(7, np.float64)
+    out = np.zeros(max(n, 1), np.uint8)
+    inl = lib().orc_pose_opt(_p(cam), _p(pose_in), _p(obs), n, _p(pout), _p(out), _p(pd))
+    return inl, pout, out[:n].copy(), pd

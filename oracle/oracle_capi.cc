@@ -1,0 +1,143 @@
+// ORACLE (test infrastructure only): flat C entry points so tests/ (ctypes),
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg can drive the CPU
+// restatement.  Nothing in orb_slam_fusion_amd/ links or loads this library.
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "cv_semantics.h"
+#include "glibc_sincosf.h"
+#include "orb_oracle.h"
+
+using oracle::KeyPoint;
+using oracle::OrbExtractor;
+
+extern "C" {
+
+void* orc_extractor_new(int nf, float sf, int nl, int ini, int mn) {
+  return new OrbExtractor(nf, sf, nl, ini, mn);
+}
+void orc_extractor_free(void* h) { delete static_cast<OrbExtractor*>(h); }
+
+// Returns the mono index (or -1), writes n keypoints (cv::KeyPoint layout) and
+// n x 32 descriptor bytes when n <= cap; *n_out always receives n.
+int orc_extract(void* h, const uint8_t* img, int w, int hgt, int stride, int lap0, int lap1,
+                KeyPoint* kps, uint8_t* desc, int cap, int* n_out) {
+  auto* ex = static_cast<OrbExtractor*>(h);
+  std::vector<KeyPoint> k;
+  std::vector<uint8_t> d;
+  const int lap[2] = {lap0, lap1};
+  const int mono = ex->Extract(img, w, hgt, stride, k, d, lap);
+  *n_out = (int)k.size();
+  if ((int)k.size() <= cap) {
+    std::copy(k.begin(), k.end(), kps);
+    std::copy(d.begin(), d.end(), desc);
+  }
+  return mono;
+}
+
+// Two extractors on two threads, as Frame's stereo constructor does
+// (frame.cc:179-182).  Used by the CPU baseline timing.
+int orc_extract_stereo(void* hl, void* hr, const uint8_t* l, const uint8_t* r, int w, int hgt,
+                       int stride, int* n_left, int* n_right) {
+  const int lap[2] = {0, 0};
+  std::vector<KeyPoint> kl, kr;
+  std::vector<uint8_t> dl, dr;
+  std::thread t([&] { static_cast<OrbExtractor*>(hr)->Extract(r, w, hgt, stride, kr, dr, lap); });
+  static_cast<OrbExtractor*>(hl)->Extract(l, w, hgt, stride, kl, dl, lap);
+  t.join();
+  *n_left = (int)kl.size();
+  *n_right = (int)kr.size();
+  return 0;
+}
+
+void orc_params(void* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                int* feats_per_level, int* umax16) {
+  auto* ex = static_cast<OrbExtractor*>(h);
+  const int L = ex->GetLevels();
+  for (int l = 0; l < L; ++l) {
+    scale[l] = ex->GetScaleFactors()[l];
+    inv_scale[l] = ex->GetInverseScaleFactors()[l];
+    sigma2[l] = ex->GetScaleSigmaSquares()[l];
+    inv_sigma2[l] = ex->GetInverseScaleSigmaSquares()[l];
+    feats_per_level[l] = ex->FeaturesPerLevel()[l];
+  }
+  for (int v = 0; v < 16; ++v) umax16[v] = ex->UMax()[v];
+}
+
+void orc_pyramid(void* h, const uint8_t* img, int w, int hgt, int stride) {
+  static_cast<OrbExtractor*>(h)->ComputePyramid(img, w, hgt, stride);
+}
+
+int orc_level_size(void* h, int lev, int* w, int* hgt) {
+  auto* ex = static_cast<OrbExtractor*>(h);
+  if (lev < 0 || lev >= (int)ex->img_pyramid_.size()) return -1;
+  *w = ex->img_pyramid_[lev].w;
+  *hgt = ex->img_pyramid_[lev].h;
+  return 0;
+}
+
+void orc_level_copy(void* h, int lev, int blurred, uint8_t* out) {
+  auto* ex = static_cast<OrbExtractor*>(h);
+  const auto& p = blurred ? ex->blurred_[lev] : ex->img_pyramid_[lev];
+  std::memcpy(out, p.px.data(), p.px.size());
+}
+
+// Stage dumps of the last extract: which = 0 -> FAST candidates (to_dist
+// order), 1 -> octree output (list order).  Rows of (x, y, response).
+int orc_stage(void* h, int lev, int which, float* xyr, int cap) {
+  auto* ex = static_cast<OrbExtractor*>(h);
+  const auto& v = which == 0 ? ex->to_dist_[lev] : ex->octree_[lev];
+  const int n = (int)v.size();
+  for (int i = 0; i < std::min(n, cap); ++i) {
+    xyr[3 * i] = v[i].x;
+    xyr[3 * i + 1] = v[i].y;
+    xyr[3 * i + 2] = v[i].response;
+  }
+  return n;
+}
+
+// Primitive-level entry points.
+void orc_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh) {
+  oracle::resize_linear_u8(src, sw, sh, sw, dst, dw, dh, dw);
+}
+void orc_gauss(const uint8_t* src, int w, int h, uint8_t* dst) {
+  oracle::gaussian7_sigma2_u8(src, w, h, w, dst, w);
+}
+void orc_gauss_kernel(int* k7) { oracle::gaussian7_sigma2_kernel_q8(k7); }
+int orc_fast(const uint8_t* roi, int stride, int cols, int rows, int th, int* xys, int cap) {
+  std::vector<oracle::FastCorner> c;
+  oracle::fast9_16(roi, stride, cols, rows, th, c);
+  for (int i = 0; i < std::min((int)c.size(), cap); ++i) {
+    xys[3 * i] = c[i].x;
+    xys[3 * i + 1] = c[i].y;
+    xys[3 * i + 2] = c[i].score;
+  }
+  return (int)c.size();
+}
+float orc_fast_atan2(float y, float x) { return oracle::fast_atan2(y, x); }
+void orc_sincosf(const float* x, int n, float* s, float* c) {
+  for (int i = 0; i < n; ++i) {
+    s[i] = oracle::glibc_sinf(x[i]);
+    c[i] = oracle::glibc_cosf(x[i]);
+  }
+}
+// Exhaustive check of the sinf/cosf restatement against the host libm over
+// the float bit patterns [lo, hi]; returns the number of mismatches.
+long orc_sincosf_check_libm(unsigned lo, unsigned hi) {
+  long bad = 0;
+  for (unsigned u = lo;; ++u) {
+    float f;
+    std::memcpy(&f, &u, 4);
+    volatile float vf = f;
+    const float s = sinf(vf), c = cosf(vf);
+    const float s2 = oracle::glibc_sinf(f), c2 = oracle::glibc_cosf(f);
+    bad += std::memcmp(&s, &s2, 4) != 0;
+    bad += std::memcmp(&c, &c2, 4) != 0;
+    if (u == hi) break;
+  }
+  return bad;
+}
+
+}  // extern "C"

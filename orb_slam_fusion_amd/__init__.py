@@ -1,0 +1,21 @@
+"""orb_slam_fusion_amd -- MI355X (gfx950) ORB front-end and pose optimisation.
+
+Drop-in for the hot path of J094/orb_slam_fusion:
+``ORB_SLAM_FUSION::OrbExtractor::operator()`` and
+``Optimizer::PoseOptimization``.  The compute runs in hand-written HIP kernels
+(csrc/*.hip) behind the C ABI of include/orbgpu.h; this package is the host
+mirror of the reference interface over that ABI.
+"""
+from ._lib import KEYPOINT_DTYPE, POSE_OBS_DTYPE, OrbGpuError, library_path
+from .extractor import OrbExtractor
+from .optimizer import PoseFrame, PoseOptimizer
+
+__all__ = [
+    "KEYPOINT_DTYPE",
+    "POSE_OBS_DTYPE",
+    "OrbGpuError",
+    "OrbExtractor",
+    "PoseFrame",
+    "PoseOptimizer",
+    "library_path",
+]

@@ -1,0 +1,142 @@
+"""ctypes binding of the C ABI in include/orbgpu.h (liborbgpu.so).
+
+The product path is the in-tree HIP library; there is no CPU fallback.  If the
+library is missing or fails to load, every entry point raises -- loudly -- so a
+GPU box can never pass on a silent fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_DIR = PKG_DIR / "lib"
+REPO_DIR = PKG_DIR.parent
+
+ORBGPU_OK = 0
+ORBGPU_ERR_INVALID = -1
+ORBGPU_ERR_EMPTY = -2
+ORBGPU_ERR_CAPACITY = -3
+ORBGPU_ERR_DEVICE = -4
+ORBGPU_ERR_NOMEM = -5
+
+STATUS_NAMES = {
+    ORBGPU_OK: "OK",
+    ORBGPU_ERR_INVALID: "INVALID",
+    ORBGPU_ERR_EMPTY: "EMPTY",
+    ORBGPU_ERR_CAPACITY: "CAPACITY",
+    ORBGPU_ERR_DEVICE: "DEVICE",
+    ORBGPU_ERR_NOMEM: "NOMEM",
+}
+
+
+class OrbGpuError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        super().__init__(f"{where}: orbgpu status {status} ({STATUS_NAMES.get(status, '?')})")
+        self.status = status
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [
+        ("num_features", ctypes.c_int),
+        ("scale_factor", ctypes.c_float),
+        ("num_levels", ctypes.c_int),
+        ("ini_th_fast", ctypes.c_int),
+        ("min_th_fast", ctypes.c_int),
+    ]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in ("fx", "fy", "cx", "cy", "bf")]
+
+
+# cv::KeyPoint field order (28 bytes)
+KEYPOINT_DTYPE = np.dtype(
+    [
+        ("x", "<f4"),
+        ("y", "<f4"),
+        ("size", "<f4"),
+        ("angle", "<f4"),
+        ("response", "<f4"),
+        ("octave", "<i4"),
+        ("class_id", "<i4"),
+    ]
+)
+assert KEYPOINT_DTYPE.itemsize == 28
+
+# orbgpu_pose_obs: Xw[3], u, v, ur, inv_sigma2
+POSE_OBS_DTYPE = np.dtype(
+    [("Xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("inv_sigma2", "<f4")]
+)
+assert POSE_OBS_DTYPE.itemsize == 28
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/orbgpu.h
+SIGNATURES = {
+    "orbgpu_extractor_create": (_I, [ctypes.POINTER(OrbParams), _I, _I, _I, _I, ctypes.POINTER(_P)]),
+    "orbgpu_extractor_destroy": (None, [_P]),
+    "orbgpu_extractor_scales": (_I, [_P, _P, _P, _P, _P]),
+    "orbgpu_extractor_levels": (_I, [_P]),
+    "orbgpu_extractor_max_keypoints": (_I, [_P, _I, _I]),
+    "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
+    "orbgpu_extractor_pyramid_level": (_I, [_P, _I, ctypes.POINTER(_P), _P, _P, _P]),
+    "orbgpu_extract_batch": (
+        _I,
+        [_P, _P, _I, _I, _I, _I, ctypes.c_size_t, _P, _P, _P, _I, _P, _P, _P],
+    ),
+    "orbgpu_extractor_check": (_I, [_P]),
+    "orbgpu_extractor_stage": (_I, [_P, _I, _I, _P, _I]),
+    "orbgpu_extractor_profile": (_I, [_P, _I]),
+    "orbgpu_extractor_profile_read": (_I, [_P, _P]),
+    "orbgpu_pose_ctx_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
+    "orbgpu_pose_ctx_destroy": (None, [_P]),
+    "orbgpu_pose_opt": (_I, [_P, ctypes.POINTER(Camera), _P, _P, _I, _P, _P, _P]),
+    "orbgpu_pose_opt_batch": (
+        _I,
+        [_P, ctypes.POINTER(Camera), _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
+    ),
+}
+
+_lib = None
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("ORBGPU_LIB", LIB_DIR / "liborbgpu.so"))
+
+
+def lib() -> ctypes.CDLL:
+    """Loads liborbgpu.so (raises if it is absent: no fallback exists)."""
+    global _lib
+    if _lib is None:
+        path = library_path()
+        if not path.exists():
+            raise OSError(
+                f"{path} is missing: build it with `make` (or __graft_entry__.build()); "
+                "the orb_slam_fusion_amd hot path has no CPU fallback"
+            )
+        so = ctypes.CDLL(str(path))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(so, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = so
+    return _lib
+
+
+def check(status: int, where: str) -> None:
+    if status != ORBGPU_OK:
+        raise OrbGpuError(status, where)
+
+
+def ptr(a) -> ctypes.c_void_p:
+    """Raw address of a numpy array or torch tensor (no copy)."""
+    if a is None:
+        return ctypes.c_void_p(0)
+    if isinstance(a, np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+    return ctypes.c_void_p(a.data_ptr())

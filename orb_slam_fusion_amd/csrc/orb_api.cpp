@@ -1,0 +1,456 @@
+// C-ABI implementation of the extractor half of include/orbgpu.h.
+// Owns the per-handle HIP stream, the geometry plan and the device workspace;
+// launches the kernel sequence of orb_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+#include "orb_launch.h"
+#include "orb_plan_host.h"
+
+using namespace orbgpu;
+
+namespace {
+
+template <class T>
+hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+}  // namespace
+
+struct orbgpu_extractor {
+  orbgpu_orb_params params{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int max_w = 0, max_h = 0, max_images = 0;
+
+  HostPlan plan;
+  int plan_w = -1, plan_h = -1;
+  PlanHeader* d_plan = nullptr;
+  Cell* d_cells = nullptr;
+  int* d_rs = nullptr;
+  size_t cells_cap = 0, rs_cap = 0;
+
+  int ws_images = 0;  // workspace sized for this many images of the plan
+  size_t ws_pyr = 0, ws_blur = 0, ws_slots = 0, ws_cells = 0, ws_kp = 0;
+  uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+  uint32_t *d_slots = nullptr, *d_dense = nullptr, *d_oct_out = nullptr;
+  int *d_cell_count = nullptr, *d_knode = nullptr, *d_oct_count = nullptr;
+  float* d_angle = nullptr;
+  uint64_t* d_desc = nullptr;
+  int* d_err = nullptr;
+
+  // single-image (host-buffer) path
+  uint8_t* d_img = nullptr;
+  size_t d_img_bytes = 0;
+  orbgpu_keypoint* d_kps = nullptr;
+  uint8_t* d_descs = nullptr;
+  size_t out_cap = 0;
+  int* d_nm = nullptr;  // n, mono
+  std::vector<uint8_t> host_pyr;
+  bool host_pyr_valid = false;
+  int last_w = 0, last_h = 0;
+
+  // optional per-stage event profiling of batch calls (a ring of event sets)
+  std::vector<hipEvent_t> prof_events;
+  int prof_slots = 0, prof_used = 0;
+};
+
+namespace {
+
+orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
+  if (h->plan_w == w && h->plan_h == ht) return ORBGPU_OK;
+  std::string why;
+  HostPlan p;
+  if (!make_plan(h->params, w, ht, p, why)) return ORBGPU_ERR_INVALID;
+  if (p.cells.size() > h->cells_cap) {
+    dfree(h->d_cells);
+    if (dalloc(&h->d_cells, p.cells.size()) != hipSuccess) return ORBGPU_ERR_NOMEM;
+    h->cells_cap = p.cells.size();
+  }
+  if (p.rs_tab.size() > h->rs_cap) {
+    dfree(h->d_rs);
+    if (dalloc(&h->d_rs, p.rs_tab.size()) != hipSuccess) return ORBGPU_ERR_NOMEM;
+    h->rs_cap = p.rs_tab.size();
+  }
+  if (hipMemcpyAsync(h->d_plan, &p.hdr, sizeof(PlanHeader), hipMemcpyHostToDevice, h->stream) ||
+      hipMemcpyAsync(h->d_cells, p.cells.data(), p.cells.size() * sizeof(Cell),
+                     hipMemcpyHostToDevice, h->stream) ||
+      hipMemcpyAsync(h->d_rs, p.rs_tab.data(), p.rs_tab.size() * sizeof(int),
+                     hipMemcpyHostToDevice, h->stream) ||
+      hipStreamSynchronize(h->stream))
+    return ORBGPU_ERR_DEVICE;
+  if (set_octree_lds_limit(octree_lds_bytes(p.hdr)) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  h->plan = std::move(p);
+  h->plan_w = w;
+  h->plan_h = ht;
+  h->ws_images = 0;  // re-check workspace sizes against the new plan
+  return ORBGPU_OK;
+}
+
+orbgpu_status ensure_workspace(orbgpu_extractor* h, int n) {
+  const PlanHeader& P = h->plan.hdr;
+  if (h->ws_images >= n) return ORBGPU_OK;
+  const size_t pyr = (size_t)n * P.pyr_bytes, blur = (size_t)n * P.blur_bytes;
+  const size_t slots = (size_t)n * P.slots, cells = (size_t)n * P.n_cells;
+  const size_t kp = (size_t)n * P.kp_slots;
+  if (pyr > h->ws_pyr) {
+    dfree(h->d_pyr);
+    if (dalloc(&h->d_pyr, pyr)) return ORBGPU_ERR_NOMEM;
+    h->ws_pyr = pyr;
+  }
+  if (blur > h->ws_blur) {
+    dfree(h->d_blur);
+    if (dalloc(&h->d_blur, blur)) return ORBGPU_ERR_NOMEM;
+    h->ws_blur = blur;
+  }
+  if (slots > h->ws_slots) {
+    dfree(h->d_slots);
+    dfree(h->d_dense);
+    dfree(h->d_knode);
+    if (dalloc(&h->d_slots, slots) || dalloc(&h->d_dense, slots) || dalloc(&h->d_knode, slots))
+      return ORBGPU_ERR_NOMEM;
+    h->ws_slots = slots;
+  }
+  if (cells > h->ws_cells) {
+    dfree(h->d_cell_count);
+    if (dalloc(&h->d_cell_count, cells)) return ORBGPU_ERR_NOMEM;
+    h->ws_cells = cells;
+  }
+  if (kp > h->ws_kp) {
+    dfree(h->d_oct_out);
+    dfree(h->d_angle);
+    dfree(h->d_desc);
+    dfree(h->d_oct_count);
+    if (dalloc(&h->d_oct_out, kp) || dalloc(&h->d_angle, kp) || dalloc(&h->d_desc, kp * 4) ||
+        dalloc(&h->d_oct_count, (size_t)n * kMaxLevels))
+      return ORBGPU_ERR_NOMEM;
+    h->ws_kp = kp;
+  }
+  h->ws_images = n;
+  return ORBGPU_OK;
+}
+
+ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch, int stride,
+                          int n, const int lap[2], void* kps, void* descs, int cap, int* d_n,
+                          int* d_mono) {
+  ExtractLaunch a{};
+  a.host_plan = &h->plan.hdr;
+  a.plan = h->d_plan;
+  a.cells = h->d_cells;
+  a.rs_tab = h->d_rs;
+  a.imgs = imgs;
+  a.image_pitch = pitch;
+  a.stride = stride;
+  a.n_images = n;
+  a.pyr = h->d_pyr;
+  a.blur = h->d_blur;
+  a.slots = h->d_slots;
+  a.cell_count = h->d_cell_count;
+  a.dense = h->d_dense;
+  a.knode = h->d_knode;
+  a.oct_out = h->d_oct_out;
+  a.oct_count = h->d_oct_count;
+  a.angle = h->d_angle;
+  a.desc = h->d_desc;
+  a.octree_lds = octree_lds_bytes(h->plan.hdr);
+  a.lap0 = lap ? lap[0] : 0;
+  a.lap1 = lap ? lap[1] : 0;
+  a.kps_out = kps;
+  a.desc_out = descs;
+  a.cap = cap;
+  a.n_out = d_n;
+  a.mono_out = d_mono;
+  a.err = h->d_err;
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int device, int max_width,
+                                      int max_height, int max_images, orbgpu_extractor** out) {
+  if (!params || !out || max_width <= 0 || max_height <= 0 || max_images <= 0)
+    return ORBGPU_ERR_INVALID;
+  *out = nullptr;
+  HostPlan probe;
+  std::string why;
+  if (!make_plan(*params, max_width, max_height, probe, why)) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  auto* h = new (std::nothrow) orbgpu_extractor();
+  if (!h) return ORBGPU_ERR_NOMEM;
+  h->params = *params;
+  h->device = device;
+  h->max_w = max_width;
+  h->max_h = max_height;
+  h->max_images = max_images;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1) || dalloc(&h->d_nm, 2)) {
+    orbgpu_extractor_destroy(h);
+    return ORBGPU_ERR_DEVICE;
+  }
+  (void)hipMemset(h->d_err, 0, sizeof(int));
+  orbgpu_status st = ensure_plan(h, max_width, max_height);
+  if (st == ORBGPU_OK) st = ensure_workspace(h, max_images);
+  if (st != ORBGPU_OK) {
+    orbgpu_extractor_destroy(h);
+    return st;
+  }
+  *out = h;
+  return ORBGPU_OK;
+}
+
+void orbgpu_extractor_destroy(orbgpu_extractor* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  dfree(h->d_plan);
+  dfree(h->d_cells);
+  dfree(h->d_rs);
+  dfree(h->d_pyr);
+  dfree(h->d_blur);
+  dfree(h->d_slots);
+  dfree(h->d_dense);
+  dfree(h->d_knode);
+  dfree(h->d_cell_count);
+  dfree(h->d_oct_out);
+  dfree(h->d_oct_count);
+  dfree(h->d_angle);
+  dfree(h->d_desc);
+  dfree(h->d_err);
+  dfree(h->d_img);
+  dfree(h->d_kps);
+  dfree(h->d_descs);
+  dfree(h->d_nm);
+  for (hipEvent_t e : h->prof_events) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+orbgpu_status orbgpu_extractor_scales(const orbgpu_extractor* h, float* scale, float* inv_scale,
+                                      float* sigma2, float* inv_sigma2) {
+  if (!h) return ORBGPU_ERR_INVALID;
+  const int L = h->params.num_levels;
+  for (int l = 0; l < L; ++l) {
+    if (scale) scale[l] = h->plan.scale[l];
+    if (inv_scale) inv_scale[l] = h->plan.inv_scale[l];
+    if (sigma2) sigma2[l] = h->plan.sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = h->plan.inv_sigma2[l];
+  }
+  return ORBGPU_OK;
+}
+
+int orbgpu_extractor_levels(const orbgpu_extractor* h) { return h ? h->params.num_levels : 0; }
+
+int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height) {
+  if (!h) return -1;
+  HostPlan p;
+  std::string why;
+  if (!make_plan(h->params, width, height, p, why)) return -1;
+  return p.hdr.kp_slots;
+}
+
+orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width, int height,
+                             int stride, const int lapping[2], orbgpu_keypoint* kps,
+                             uint8_t* descs, int cap, int* n_out, int* mono_out) {
+  if (!h || !n_out) return ORBGPU_ERR_INVALID;
+  *n_out = 0;
+  if (mono_out) *mono_out = -1;
+  if (!img || width <= 0 || height <= 0) return ORBGPU_ERR_EMPTY;
+  if (stride < width || cap < 0 || (cap > 0 && (!kps || !descs))) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu_status st = ensure_plan(h, width, height);
+  if (st == ORBGPU_OK) st = ensure_workspace(h, 1);
+  if (st != ORBGPU_OK) return st;
+  const PlanHeader& P = h->plan.hdr;
+  const size_t bytes = (size_t)width * height;
+  if (bytes > h->d_img_bytes) {
+    dfree(h->d_img);
+    if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
+    h->d_img_bytes = bytes;
+  }
+  if ((size_t)P.kp_slots > h->out_cap) {
+    dfree(h->d_kps);
+    dfree(h->d_descs);
+    if (dalloc(&h->d_kps, P.kp_slots) || dalloc(&h->d_descs, (size_t)P.kp_slots * 32))
+      return ORBGPU_ERR_NOMEM;
+    h->out_cap = P.kp_slots;
+  }
+  if (hipMemcpy2DAsync(h->d_img, width, img, stride, width, height, hipMemcpyHostToDevice,
+                       h->stream) != hipSuccess)
+    return ORBGPU_ERR_DEVICE;
+  const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
+  ExtractLaunch a = make_launch(h, h->d_img, bytes, width, 1, lap, h->d_kps, h->d_descs,
+                                P.kp_slots, h->d_nm, h->d_nm + 1);
+  if (launch_extract(a, h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  int nm[2] = {0, 0}, err = 0;
+  if (hipMemcpyAsync(nm, h->d_nm, sizeof(nm), hipMemcpyDeviceToHost, h->stream) ||
+      hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream) ||
+      hipStreamSynchronize(h->stream))
+    return ORBGPU_ERR_DEVICE;
+  h->host_pyr_valid = false;
+  h->last_w = width;
+  h->last_h = height;
+  if (err) {
+    (void)hipMemset(h->d_err, 0, sizeof(int));
+    return ORBGPU_ERR_CAPACITY;
+  }
+  *n_out = nm[0];
+  if (mono_out) *mono_out = nm[1];
+  if (nm[0] > cap) return ORBGPU_ERR_CAPACITY;
+  if (nm[0] > 0 &&
+      (hipMemcpyAsync(kps, h->d_kps, (size_t)nm[0] * sizeof(orbgpu_keypoint), hipMemcpyDeviceToHost,
+                      h->stream) ||
+       hipMemcpyAsync(descs, h->d_descs, (size_t)nm[0] * 32, hipMemcpyDeviceToHost, h->stream) ||
+       hipStreamSynchronize(h->stream)))
+    return ORBGPU_ERR_DEVICE;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_extractor_pyramid_level(orbgpu_extractor* h, int level, const uint8_t** data,
+                                             int* width, int* height, int* stride) {
+  if (!h || !data || level < 0 || level >= h->params.num_levels || h->last_w == 0)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  const PlanHeader& P = h->plan.hdr;
+  if (!h->host_pyr_valid) {
+    const size_t l0 = (size_t)P.lev[0].w * P.lev[0].h;
+    h->host_pyr.resize(l0 + P.pyr_bytes);
+    if (hipMemcpyAsync(h->host_pyr.data(), h->d_img, l0, hipMemcpyDeviceToHost, h->stream) ||
+        hipMemcpyAsync(h->host_pyr.data() + l0, h->d_pyr, P.pyr_bytes, hipMemcpyDeviceToHost,
+                       h->stream) ||
+        hipStreamSynchronize(h->stream))
+      return ORBGPU_ERR_DEVICE;
+    h->host_pyr_valid = true;
+  }
+  const LevelGeom& g = P.lev[level];
+  const size_t l0 = (size_t)P.lev[0].w * P.lev[0].h;
+  *data = h->host_pyr.data() + (level == 0 ? 0 : l0 + g.pyr_off);
+  if (width) *width = g.w;
+  if (height) *height = g.h;
+  if (stride) *stride = g.w;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_extract_batch(orbgpu_extractor* h, const uint8_t* d_imgs, int n_images,
+                                   int width, int height, int stride, size_t image_pitch,
+                                   const int lapping[2], orbgpu_keypoint* d_kps, uint8_t* d_descs,
+                                   int cap_per_image, int* d_n, int* d_mono, void* hip_stream) {
+  if (!h || !d_imgs || n_images <= 0 || !d_kps || !d_descs || !d_n || !d_mono)
+    return ORBGPU_ERR_INVALID;
+  if (width <= 0 || height <= 0) return ORBGPU_ERR_EMPTY;
+  if (stride < width || image_pitch < (size_t)stride * height) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu_status st = ensure_plan(h, width, height);
+  if (st == ORBGPU_OK) st = ensure_workspace(h, n_images);
+  if (st != ORBGPU_OK) return st;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
+  ExtractLaunch a = make_launch(h, d_imgs, image_pitch, stride, n_images, lap, d_kps, d_descs,
+                                cap_per_image, d_n, d_mono);
+  if (h->prof_used < h->prof_slots) a.events = &h->prof_events[(size_t)h->prof_used++ * (kStages + 1)];
+  if (launch_extract(a, s) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  h->host_pyr_valid = false;
+  h->last_w = 0;  // the host pyramid getter serves the host-buffer path only
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_extractor_profile(orbgpu_extractor* h, int max_calls) {
+  if (!h || max_calls < 0) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  (void)hipDeviceSynchronize();
+  for (hipEvent_t e : h->prof_events) (void)hipEventDestroy(e);
+  h->prof_events.assign((size_t)max_calls * (kStages + 1), nullptr);
+  for (hipEvent_t& e : h->prof_events)
+    if (hipEventCreate(&e) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  h->prof_slots = max_calls;
+  h->prof_used = 0;
+  return ORBGPU_OK;
+}
+
+int orbgpu_extractor_profile_read(orbgpu_extractor* h, double* ms_per_stage) {
+  if (!h || !ms_per_stage) return -1;
+  if (hipSetDevice(h->device) != hipSuccess) return -1;
+  for (int k = 0; k < kStages; ++k) ms_per_stage[k] = 0;
+  for (int c = 0; c < h->prof_used; ++c) {
+    hipEvent_t* ev = &h->prof_events[(size_t)c * (kStages + 1)];
+    if (hipEventSynchronize(ev[kStages]) != hipSuccess) return -1;
+    for (int k = 0; k < kStages; ++k) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ev[k], ev[k + 1]) != hipSuccess) return -1;
+      ms_per_stage[k] += ms;
+    }
+  }
+  const int calls = h->prof_used;
+  h->prof_used = 0;
+  return calls;
+}
+
+int orbgpu_extractor_stage(orbgpu_extractor* h, int which, int level, void* out, int cap) {
+  if (!h || !out || level < 0 || level >= h->params.num_levels || h->plan_w < 0) return -1;
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess)
+    return -1;
+  const PlanHeader& P = h->plan.hdr;
+  const LevelGeom& g = P.lev[level];
+  if (which == 0) {
+    const int n = g.w * g.h;
+    if (n > cap) return -1;
+    return hipMemcpy(out, h->d_blur + g.blur_off, n, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+  }
+  if (which == 1) {
+    std::vector<int> cc(g.cell_end - g.cell_begin);
+    if (hipMemcpy(cc.data(), h->d_cell_count + g.cell_begin, cc.size() * sizeof(int),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    int n = 0;
+    for (int c : cc) n += c;
+    if (n > cap) return -1;
+    return hipMemcpy(out, h->d_dense + g.slot_begin, (size_t)n * 4, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? n
+               : -1;
+  }
+  if (which == 2) {
+    int n = 0;
+    if (hipMemcpy(&n, h->d_oct_count + level, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+        n > cap)
+      return -1;
+    return hipMemcpy(out, h->d_oct_out + g.out_off, (size_t)n * 4, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? n
+               : -1;
+  }
+  return -1;
+}
+
+orbgpu_status orbgpu_extractor_check(orbgpu_extractor* h) {
+  if (!h) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  int err = 0;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return ORBGPU_ERR_DEVICE;
+  if (err) {
+    (void)hipMemset(h->d_err, 0, sizeof(int));
+    return ORBGPU_ERR_CAPACITY;
+  }
+  return ORBGPU_OK;
+}
+
+}  // extern "C"

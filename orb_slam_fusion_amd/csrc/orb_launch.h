@@ -1,0 +1,47 @@
+// Launch descriptor for one batched extraction (device pointers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "orb_plan.h"
+
+namespace orbgpu {
+
+struct ExtractLaunch {
+  const PlanHeader* host_plan;  // host copy (grid sizes)
+  const PlanHeader* plan;       // device copy
+  const Cell* cells;
+  const int* rs_tab;
+  const uint8_t* imgs;
+  size_t image_pitch;
+  int stride;
+  int n_images;
+  uint8_t* pyr;
+  uint8_t* blur;
+  uint32_t* slots;
+  int* cell_count;
+  uint32_t* dense;
+  int* knode;
+  uint32_t* oct_out;
+  int* oct_count;
+  float* angle;
+  uint64_t* desc;
+  size_t octree_lds;
+  int lap0, lap1;
+  void* kps_out;   // orbgpu_keypoint[n_images][cap]
+  void* desc_out;  // uint8_t[n_images][cap][32]
+  int cap;
+  int* n_out;
+  int* mono_out;
+  int* err;
+  hipEvent_t* events;  // optional: kStages + 1 events recorded around the stages
+};
+
+// Stage boundaries recorded when ExtractLaunch::events is set.
+enum Stage : int { kStResize, kStBlur, kStFast, kStOctree, kStDescribe, kStAssemble, kStages };
+
+hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
+hipError_t set_octree_lds_limit(size_t bytes);
+
+}  // namespace orbgpu

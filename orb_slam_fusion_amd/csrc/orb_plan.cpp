@@ -1,0 +1,200 @@
+// Host planner: everything the reference derives from (params, image size)
+// -- scale tables, level sizes, resize taps, the FAST cell grid, octree roots,
+// buffer layout -- computed once per geometry with the reference's float
+// arithmetic (compiled -ffp-contract=off).
+#include "orb_plan_host.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace orbgpu {
+
+namespace {
+inline int cv_round(float v) { return (int)std::lrintf(v); }
+inline short sat_short(float v) {
+  return (short)std::min(std::max(cv_round(v), -32768), 32767);
+}
+}  // namespace
+
+void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::vector<float>& inv,
+                  std::vector<float>& s2, std::vector<float>& inv_s2,
+                  std::vector<int>& feats_per_level) {
+  const int L = p.num_levels;
+  const double sf = p.scale_factor;  // float member widened, orb_extractor.h:91
+  scale.assign(L, 1.0f);
+  s2.assign(L, 1.0f);
+  for (int i = 1; i < L; ++i) {  // orb_extractor.cc:418-421
+    scale[i] = (float)(scale[i - 1] * sf);
+    s2[i] = scale[i] * scale[i];
+  }
+  inv.resize(L);
+  inv_s2.resize(L);
+  for (int i = 0; i < L; ++i) {  // :423-428
+    inv[i] = 1.0f / scale[i];
+    inv_s2[i] = 1.0f / s2[i];
+  }
+  feats_per_level.assign(L, 0);  // :432-444
+  const float factor = (float)(1.0f / sf);
+  float per = (float)p.num_features * (1 - factor) /
+              (1 - (float)std::pow((double)factor, (double)L));
+  int sum = 0;
+  for (int l = 0; l < L - 1; ++l) {
+    feats_per_level[l] = cv_round(per);
+    sum += feats_per_level[l];
+    per *= factor;
+  }
+  feats_per_level[L - 1] = std::max(p.num_features - sum, 0);
+}
+
+bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::string& why) {
+  const int L = p.num_levels;
+  if (L < 1 || L > kMaxLevels) return why = "num_levels out of range", false;
+  if (!(p.scale_factor > 1.0f)) return why = "scale_factor must be > 1", false;
+  if (W <= 0 || H <= 0 || W > 4096 || H > 4096) return why = "image size out of range", false;
+  PlanHeader& P = out.hdr;
+  P = PlanHeader{};
+  P.width = W;
+  P.height = H;
+  P.levels = L;
+  P.ini_th = std::min(std::max(p.ini_th_fast, 0), 255);
+  P.min_th = std::min(std::max(p.min_th_fast, 0), 255);
+  scale_tables(p, out.scale, out.inv_scale, out.sigma2, out.inv_sigma2, out.feats_per_level);
+
+  // umax (:452-464)
+  {
+    int umax[16] = {0};
+    const float r2 = 15.0f * std::sqrt(2.f) / 2;
+    const int vmax = (int)std::floor(r2 + 1), vmin = (int)std::ceil(r2);
+    for (int v = 0; v <= vmax; ++v) umax[v] = (int)std::lrint(std::sqrt(225.0 - v * v));
+    for (int v = 15, v0 = 0; v >= vmin; --v) {
+      while (umax[v0] == umax[v0 + 1]) ++v0;
+      umax[v] = v0;
+      ++v0;
+    }
+    std::copy(umax, umax + 16, P.umax);
+  }
+
+  out.cells.clear();
+  out.rs_tab.clear();
+  int pyr = 0, blur = 0, slots = 0, kps = 0, tiles = 0, max_roi = 0, node_cap = 64;
+  for (int l = 0; l < L; ++l) {
+    LevelGeom& g = P.lev[l];
+    g.w = cv_round((float)W * out.inv_scale[l]);  // :1096
+    g.h = cv_round((float)H * out.inv_scale[l]);
+    g.scale = out.scale[l];
+    g.patch_size = (float)(int)(kPatchSize * out.scale[l]);
+    if (g.w - 2 * kFastBorder < 35 || g.h - 2 * kFastBorder < 35)
+      return why = "pyramid level too small for the FAST grid", false;
+    g.pyr_off = l == 0 ? -1 : pyr;
+    if (l > 0) pyr += g.w * g.h;
+    g.blur_off = blur;
+    blur += g.w * g.h;
+    g.blur_tile_begin = tiles;
+    g.tiles_x = (g.w + kBlurTileW - 1) / kBlurTileW;
+    g.tiles_y = (g.h + kBlurTileH - 1) / kBlurTileH;
+    tiles += g.tiles_x * g.tiles_y;
+
+    // resize taps for level l from level l-1 (cv::resize INTER_LINEAR)
+    if (l > 0) {
+      const LevelGeom& s = P.lev[l - 1];
+      const double scale_x = 1. / ((double)g.w / s.w), scale_y = 1. / ((double)g.h / s.h);
+      g.rs_x = (int)out.rs_tab.size();
+      g.xmax = g.w;
+      for (int dx = 0; dx < g.w; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0.f, sx = 0;
+        if (sx + 1 >= s.w) {
+          g.xmax = std::min(g.xmax, dx);
+          if (sx >= s.w - 1) fx = 0.f, sx = s.w - 1;
+        }
+        const short a0 = sat_short((1.f - fx) * 2048), a1 = sat_short(fx * 2048);
+        out.rs_tab.push_back(sx);
+        out.rs_tab.push_back((int)(uint16_t)a0 | ((int)(uint16_t)a1 << 16));
+      }
+      g.rs_y = (int)out.rs_tab.size();
+      for (int dy = 0; dy < g.h; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        const short b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+        const int r0 = std::min(std::max(sy, 0), s.h - 1), r1 = std::min(std::max(sy + 1, 0), s.h - 1);
+        out.rs_tab.push_back(r0 | (r1 << 16));
+        out.rs_tab.push_back((int)(uint16_t)b0 | ((int)(uint16_t)b1 << 16));
+      }
+      int x = 0;
+      for (; x <= g.w - 16; x += 16) {
+      }
+      g.vec16_end = x;
+      for (; x < g.w - 8; x += 8) {
+      }
+      g.vec8_end = x;
+    }
+
+    // FAST cell grid (:748-825)
+    const int min_b = kFastBorder;
+    const int max_bx = g.w - kEdgeThreshold + 3, max_by = g.h - kEdgeThreshold + 3;
+    const float width = (float)(max_bx - min_b), height = (float)(max_by - min_b);
+    const int ncols = (int)(width / 35.f), nrows = (int)(height / 35.f);
+    const int wc = (int)std::ceil(width / ncols), hc = (int)std::ceil(height / nrows);
+    g.cell_begin = (int)out.cells.size();
+    g.slot_begin = slots;
+    for (int i = 0; i < nrows; ++i) {
+      const float y0 = (float)(min_b + i * hc);
+      float y1 = y0 + hc + 6;
+      if (y0 >= max_by - 3) continue;
+      if (y1 > max_by) y1 = (float)max_by;
+      for (int j = 0; j < ncols; ++j) {
+        const float x0 = (float)(min_b + j * wc);
+        float x1 = x0 + wc + 6;
+        if (x0 >= max_bx - 3) continue;
+        if (x1 > max_bx) x1 = (float)max_bx;
+        Cell c;
+        c.level = l;
+        c.x0 = (int)x0;
+        c.y0 = (int)y0;
+        c.cols = (int)x1 - c.x0;
+        c.rows = (int)y1 - c.y0;
+        const int dw = c.cols - 6, dh = c.rows - 6;
+        c.slot_off = slots;
+        c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
+        slots += c.slot_cap;
+        max_roi = std::max(max_roi, c.cols * c.rows);
+        out.cells.push_back(c);
+      }
+    }
+    g.cell_end = (int)out.cells.size();
+    g.slot_count = slots - g.slot_begin;
+
+    // octree (:546-560)
+    g.budget = out.feats_per_level[l];
+    g.rel_w = max_bx - min_b;
+    g.rel_h = max_by - min_b;
+    g.n_roots = (int)std::round((float)g.rel_w / g.rel_h);
+    if (g.n_roots < 1) return why = "image too tall for the octree roots", false;
+    g.root_w = (float)g.rel_w / g.n_roots;
+    g.out_off = kps;
+    g.out_cap = std::max(g.budget + 3, 4 * g.n_roots);
+    kps += g.out_cap;
+    node_cap = std::max({node_cap, g.out_cap, g.cell_end - g.cell_begin, g.n_roots});
+  }
+  P.n_cells = (int)out.cells.size();
+  P.pyr_bytes = (pyr + 255) & ~255;
+  P.blur_bytes = (blur + 255) & ~255;
+  P.slots = slots;
+  P.kp_slots = kps;
+  P.node_cap = (node_cap + 63) & ~63;
+  P.blur_tiles = tiles;
+  P.max_roi = (max_roi + 15) & ~15;
+  if (P.kp_slots > 4096) return why = "too many keypoints per image for the assembly kernel", false;
+  if (octree_lds_bytes(P) > 160 * 1024) return why = "num_features too large for the octree LDS", false;
+  return true;
+}
+
+size_t octree_lds_bytes(const PlanHeader& P) {
+  const size_t nc = P.node_cap;
+  return nc * 8 + nc * 17 * 4 + nc * 8 * 4 + (256 + 1) * 4 + 16 * 4;
+}
+
+}  // namespace orbgpu

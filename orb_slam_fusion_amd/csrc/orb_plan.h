@@ -1,0 +1,66 @@
+// Geometry plan shared by the host planner (orb_plan.cpp) and the gfx950
+// kernels (orb_kernels.hip).  Everything the reference recomputes per call
+// from the image size (orb_extractor.cc:407-465, 744-849, 1093-1117) is
+// computed once per (params, width, height) and lives in one device buffer.
+#pragma once
+#include <stdint.h>
+
+namespace orbgpu {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdgeThreshold = 19;  // orb_extractor.cc:74
+constexpr int kFastBorder = kEdgeThreshold - 3;  // min_border_x/y (:751)
+constexpr int kPatchSize = 31;      // :72
+
+struct LevelGeom {
+  int w, h;          // level size: cvRound(W * inv_scale), cvRound(H * inv_scale)  (:1096)
+  int pyr_off;       // byte offset of this level in an image's pyramid block (levels >= 1)
+  int blur_off;      // byte offset in an image's blurred block (all levels)
+  float scale;       // scale_factors_[l]
+  float patch_size;  // (float)(int)(31 * scale)                                     (:834)
+  // resize tables (levels >= 1), offsets into Plan::rs_tab
+  int rs_x, rs_y;    // xofs|alpha pairs, yofs|beta pairs
+  int xmax;          // first dst column whose right neighbour is out of range
+  int vec16_end;     // VResizeLinearVec_32s8u: 16-lane blocks end here
+  int vec8_end;      //                          8-lane blocks end here
+  // FAST grid (:748-825)
+  int cell_begin, cell_end;
+  int slot_begin;    // first candidate slot of this level in an image's slot block
+  int slot_count;    // sum of cell capacities of this level
+  // octree (:542-742)
+  int budget;        // num_feats_per_lev_[l]
+  int n_roots;       // round((max_x - min_x) / (max_y - min_y))
+  float root_w;      // (float)(max_x - min_x) / n_roots
+  int rel_w, rel_h;  // max_x - min_x, max_y - min_y
+  int out_off;       // first output slot of this level in an image's keypoint block
+  int out_cap;       // node-count bound: max(budget + 3, 4 * n_roots)
+  // blur tiling
+  int blur_tile_begin, tiles_x, tiles_y;
+};
+
+struct Cell {
+  int level;
+  int x0, y0;       // ROI origin in level pixels
+  int cols, rows;   // ROI size (detection area is the ROI minus 3 px on each side)
+  int slot_off;     // first candidate slot in the image's slot block
+  int slot_cap;     // ceil(dw/2) * ceil(dh/2): bound for 3x3 strict maxima
+};
+
+struct PlanHeader {
+  int width, height, levels;
+  int ini_th, min_th;
+  int n_cells;
+  int pyr_bytes;    // per image, levels 1..L-1
+  int blur_bytes;   // per image, all levels
+  int slots;        // per image candidate slots
+  int kp_slots;     // per image octree-output slots
+  int node_cap;     // LDS node capacity used by the octree kernel
+  int blur_tiles;   // per image
+  int max_roi;      // largest cell ROI (bytes)
+  int umax[16];     // circular patch extents (:452-464)
+  LevelGeom lev[kMaxLevels];
+};
+
+constexpr int kBlurTileW = 64, kBlurTileH = 16;
+
+}  // namespace orbgpu

@@ -1,0 +1,25 @@
+// Host-side planner interface (see orb_plan.cpp).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+#include "orb_plan.h"
+
+namespace orbgpu {
+
+struct HostPlan {
+  PlanHeader hdr;
+  std::vector<Cell> cells;
+  std::vector<int> rs_tab;
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+  std::vector<int> feats_per_level;
+};
+
+void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::vector<float>& inv,
+                  std::vector<float>& s2, std::vector<float>& inv_s2,
+                  std::vector<int>& feats_per_level);
+bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out, std::string& why);
+size_t octree_lds_bytes(const PlanHeader& P);
+
+}  // namespace orbgpu

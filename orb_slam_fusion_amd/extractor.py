@@ -1,0 +1,197 @@
+"""Host mirror of ORB_SLAM_FUSION::OrbExtractor over the gfx950 C ABI.
+
+Same constructor arguments, getters, call semantics and error behaviour as
+the reference class (include/cam/orb_feature/orb_extractor.h:44-104,
+src/cam/orb_feature/orb_extractor.cc:407-465, 1011-1117):
+
+* ``OrbExtractor(num_feats, scale_factor, num_levs, ini_th_fast, min_th_fast)``
+* ``extractor(img, mask, lapping_areas) -> (mono_index, keypoints, descriptors)``
+  where ``keypoints`` is a structured array in cv::KeyPoint field order and
+  ``descriptors`` is N x 32 uint8 (row i describes keypoint i).  An empty image
+  returns ``(-1, empty, None)`` like ``operator()`` returning -1 with
+  ``descs`` untouched; a non-uint8 / non-2-D image raises (the reference
+  asserts CV_8UC1).  The mask is ignored, as in the reference.
+* ``img_pyramid_`` holds the host copies of the pyramid levels of the last
+  call (read by Frame::ComputeStereoMatches, frame.cc:834,913-933).
+* ``extract_batch`` is the device-resident throughput path (torch tensors).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import KEYPOINT_DTYPE, OrbParams, check, lib, ptr
+
+
+class OrbExtractor:
+    def __init__(
+        self,
+        num_feats: int,
+        scale_factor: float,
+        num_levs: int,
+        ini_th_fast: int,
+        min_th_fast: int,
+        *,
+        device: int = 0,
+        max_width: int = 752,
+        max_height: int = 480,
+        max_images: int = 1,
+    ):
+        self._params = OrbParams(num_feats, scale_factor, num_levs, ini_th_fast, min_th_fast)
+        self.num_feats_ = num_feats
+        self.num_levs_ = num_levs
+        self._h = ctypes.c_void_p()
+        check(
+            lib().orbgpu_extractor_create(
+                ctypes.byref(self._params), device, max_width, max_height, max_images,
+                ctypes.byref(self._h),
+            ),
+            "orbgpu_extractor_create",
+        )
+        L = num_levs
+        self._scale = np.zeros(L, np.float32)
+        self._inv_scale = np.zeros(L, np.float32)
+        self._sigma2 = np.zeros(L, np.float32)
+        self._inv_sigma2 = np.zeros(L, np.float32)
+        check(
+            lib().orbgpu_extractor_scales(
+                self._h, ptr(self._scale), ptr(self._inv_scale), ptr(self._sigma2),
+                ptr(self._inv_sigma2),
+            ),
+            "orbgpu_extractor_scales",
+        )
+        self._pyr_valid = False
+        self._pyr = []
+
+    # -- getters (orb_extractor.h:60-74; return copies, like the by-value getters)
+    def GetLevels(self) -> int:
+        return self.num_levs_
+
+    def GetScaleFactor(self) -> float:
+        return float(self._params.scale_factor)
+
+    def GetScaleFactors(self) -> np.ndarray:
+        return self._scale.copy()
+
+    def GetInverseScaleFactors(self) -> np.ndarray:
+        return self._inv_scale.copy()
+
+    def GetScaleSigmaSquares(self) -> np.ndarray:
+        return self._sigma2.copy()
+
+    def GetInverseScaleSigmaSquares(self) -> np.ndarray:
+        return self._inv_sigma2.copy()
+
+    def max_keypoints(self, width: int, height: int) -> int:
+        return int(lib().orbgpu_extractor_max_keypoints(self._h, width, height))
+
+    # -- operator() (orb_extractor.cc:1011-1091)
+    def __call__(
+        self,
+        img: np.ndarray,
+        mask=None,
+        lapping_areas: Sequence[int] = (0, 0),
+    ) -> Tuple[int, np.ndarray, Optional[np.ndarray]]:
+        if img is None or img.size == 0:
+            return -1, np.zeros(0, KEYPOINT_DTYPE), None
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise AssertionError("OrbExtractor expects a CV_8UC1 image")
+        img = np.ascontiguousarray(img)
+        h, w = img.shape
+        cap = max(self.max_keypoints(w, h), 1)
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        descs = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        mono = ctypes.c_int()
+        lap = (ctypes.c_int * 2)(int(lapping_areas[0]), int(lapping_areas[1]))
+        st = lib().orbgpu_extract(
+            self._h, ptr(img), w, h, w, lap, ptr(kps), ptr(descs), cap, ctypes.byref(n),
+            ctypes.byref(mono),
+        )
+        if st == _lib.ORBGPU_ERR_EMPTY:
+            return -1, np.zeros(0, KEYPOINT_DTYPE), None
+        check(st, "orbgpu_extract")
+        self._pyr_valid = False
+        N = n.value
+        return mono.value, kps[:N].copy(), (descs[:N].copy() if N > 0 else None)
+
+    @property
+    def img_pyramid_(self):
+        if not self._pyr_valid:
+            out = []
+            for lev in range(self.num_levs_):
+                data = ctypes.c_void_p()
+                w, h, s = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+                check(
+                    lib().orbgpu_extractor_pyramid_level(
+                        self._h, lev, ctypes.byref(data), ctypes.byref(w), ctypes.byref(h),
+                        ctypes.byref(s),
+                    ),
+                    "orbgpu_extractor_pyramid_level",
+                )
+                buf = (ctypes.c_uint8 * (s.value * h.value)).from_address(data.value)
+                arr = np.frombuffer(buf, np.uint8).reshape(h.value, s.value)[:, : w.value]
+                out.append(arr.copy())
+            self._pyr = out
+            self._pyr_valid = True
+        return self._pyr
+
+    # -- device-resident batch (throughput path)
+    def extract_batch(self, imgs, kps_out, descs_out, n_out, mono_out, lapping_areas=(0, 0),
+                      stream=None) -> None:
+        """imgs: uint8 CUDA tensor [B, H, W]; kps_out: [B, cap, 7] 4-byte elements;
+        descs_out: uint8 [B, cap, 32]; n_out / mono_out: int32 [B].  Asynchronous
+        on ``stream`` (torch stream or raw handle; default the current torch stream)."""
+        B, H, W = imgs.shape
+        cap = descs_out.shape[1]
+        lap = (ctypes.c_int * 2)(int(lapping_areas[0]), int(lapping_areas[1]))
+        s = _stream_handle(stream)
+        check(
+            lib().orbgpu_extract_batch(
+                self._h, ptr(imgs), B, W, H, imgs.stride(1), imgs.stride(0), lap, ptr(kps_out),
+                ptr(descs_out), cap, ptr(n_out), ptr(mono_out), s,
+            ),
+            "orbgpu_extract_batch",
+        )
+
+    STAGES = ("resize", "blur", "fast_cells", "octree", "describe", "assemble")
+
+    def profile(self, max_calls: int) -> None:
+        """Record HIP events between the kernel stages of the next max_calls
+        extract_batch calls (on the launch stream)."""
+        check(lib().orbgpu_extractor_profile(self._h, max_calls), "orbgpu_extractor_profile")
+
+    def profile_read(self):
+        """-> (calls, {stage: summed ms})."""
+        ms = np.zeros(6, np.float64)
+        calls = lib().orbgpu_extractor_profile_read(self._h, ptr(ms))
+        if calls < 0:
+            raise RuntimeError("orbgpu_extractor_profile_read failed")
+        return calls, dict(zip(self.STAGES, ms.tolist()))
+
+    def check(self) -> None:
+        check(lib().orbgpu_extractor_check(self._h), "orbgpu_extractor_check")
+
+    def close(self) -> None:
+        if self._h:
+            lib().orbgpu_extractor_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _stream_handle(stream) -> ctypes.c_void_p:
+    if stream is None:
+        import torch
+
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)

@@ -1,0 +1,166 @@
+"""GPU parity: the gfx950 extractor against the CPU oracle, bit-exact.
+
+Every keypoint field (cv::KeyPoint layout), every descriptor byte, the mono
+index and every pyramid level must equal the oracle's on the same seeded
+input.  On a mismatch the stage buffers (blurred level, FAST candidates,
+octree output) are compared to name the first diverging stage.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import binding as oracle
+from orb_slam_fusion_amd import OrbExtractor, synth
+from orb_slam_fusion_amd._lib import lib, ptr
+
+pytestmark = pytest.mark.gpu
+
+C2 = (1000, 1.2, 8, 20, 7)      # BASELINE config 2 (ORBextractor only)
+EUROC = (1200, 1.2, 8, 20, 7)   # settings/EuRoC.yaml:85-98
+
+
+def _stage(ex, which, lev, cap=1 << 20):
+    buf = np.zeros(cap, np.uint32)
+    n = lib().orbgpu_extractor_stage(ex._h, which, lev, ptr(buf), cap * 4 if which == 0 else cap)
+    assert n >= 0
+    if which == 0:
+        return buf.view(np.uint8)[:n]
+    return buf[:n]
+
+
+def _unpack(u32):
+    return np.stack([(u32 & 0xFFF), (u32 >> 12) & 0xFFF, u32 >> 24], 1).astype(np.float32)
+
+
+def _diagnose(ex, orc, L):
+    lines = []
+    for lev in range(L):
+        ob = orc.level(lev, blurred=True)
+        gb = _stage(ex, 0, lev)
+        if gb.size == ob.size and not np.array_equal(gb.reshape(ob.shape), ob):
+            lines.append(f"level {lev}: blurred plane differs")
+        oc = orc.stage(lev, 0)
+        gc = _unpack(_stage(ex, 1, lev))
+        if not np.array_equal(oc, gc):
+            lines.append(f"level {lev}: FAST candidates differ (oracle {len(oc)}, gpu {len(gc)})")
+            continue
+        oo = orc.stage(lev, 1)
+        go = _unpack(_stage(ex, 2, lev))
+        if not np.array_equal(oo, go):
+            lines.append(f"level {lev}: octree output differs (oracle {len(oo)}, gpu {len(go)})")
+    return "; ".join(lines) or "stages equal"
+
+
+def _compare(params, img, lapping=(0, 0)):
+    h, w = img.shape
+    ex = OrbExtractor(*params, max_width=w, max_height=h)
+    orc = oracle.OracleExtractor(*params)
+    m_ref, k_ref, d_ref = orc.extract(img, lapping)
+    m, k, d = ex(img, None, lapping)
+    ctx = f"{w}x{h} params={params} lapping={lapping}"
+    for lev, lvl in enumerate(ex.img_pyramid_):
+        assert np.array_equal(lvl, orc.level(lev)), f"{ctx}: pyramid level {lev} differs"
+    if len(k) != len(k_ref) or k.tobytes() != k_ref.tobytes() or (
+        len(k) and d.tobytes() != d_ref.tobytes()
+    ):
+        diag = _diagnose(ex, orc, params[2])
+        nk = min(len(k), len(k_ref))
+        bad_k = int(np.sum(k[:nk].view(np.uint8).reshape(nk, 28) != k_ref[:nk].view(np.uint8).reshape(nk, 28)))
+        bad_d = int(np.sum(d[:nk] != d_ref[:nk])) if nk and d is not None else -1
+        pytest.fail(f"{ctx}: n gpu {len(k)} ref {len(k_ref)}, differing kp bytes {bad_k}, "
+                    f"desc bytes {bad_d}; {diag}")
+    assert m == m_ref, f"{ctx}: mono index {m} != {m_ref}"
+    return len(k)
+
+
+@pytest.mark.parametrize("frame", [0, 1, 2])
+def test_stereo_frame_c2_bit_exact(gpu_available, frame):
+    left, right = synth.stereo_frame(frame)
+    assert _compare(C2, left) > 900
+    assert _compare(C2, right) > 900
+
+
+def test_euroc_params_bit_exact(gpu_available):
+    left, _ = synth.stereo_frame(10)
+    assert _compare(EUROC, left) > 1100
+
+
+def test_lapping_partition(gpu_available):
+    left, _ = synth.stereo_frame(3)
+    _compare(C2, left, lapping=(200, 500))
+
+
+def test_noise_image_dense_fast(gpu_available):
+    img = synth.noise_image(99, 320, 256)
+    _compare((500, 1.2, 4, 20, 7), img)
+
+
+@pytest.mark.parametrize("size", [(641, 397), (1024, 768), (400, 300)])
+def test_odd_sizes(gpu_available, size):
+    w, h = size
+    full, _ = synth.stereo_frame(20, w=w, h=h)
+    L = 8 if min(w, h) >= 300 else 6
+    _compare((1000, 1.2, L, 20, 7), full)
+
+
+def test_low_contrast_uses_min_threshold(gpu_available):
+    # contrast below iniThFAST everywhere: every cell falls back to minThFAST
+    left, _ = synth.stereo_frame(5)
+    low = (left.astype(np.int32) // 4 + 64).astype(np.uint8)
+    _compare(C2, low)
+
+
+def test_flat_image_no_keypoints(gpu_available):
+    img = np.full((480, 752), 128, np.uint8)
+    ex = OrbExtractor(*C2)
+    m, k, d = ex(img)
+    assert m == 0 and len(k) == 0 and d is None
+
+
+def test_empty_image_returns_minus_one(gpu_available):
+    ex = OrbExtractor(*C2)
+    m, k, d = ex(np.zeros((0, 0), np.uint8))
+    assert m == -1 and len(k) == 0 and d is None
+
+
+def test_getters_match_oracle(gpu_available):
+    ex = OrbExtractor(*EUROC)
+    p = oracle.OracleExtractor(*EUROC).params()
+    assert np.array_equal(ex.GetScaleFactors(), p["scale"])
+    assert np.array_equal(ex.GetInverseScaleFactors(), p["inv_scale"])
+    assert np.array_equal(ex.GetScaleSigmaSquares(), p["sigma2"])
+    assert np.array_equal(ex.GetInverseScaleSigmaSquares(), p["inv_sigma2"])
+    assert ex.GetLevels() == 8
+
+
+def test_batch_matches_single(gpu_available):
+    import torch
+
+    B = 6
+    imgs = np.stack([synth.stereo_frame(i // 2)[i % 2] for i in range(B)])
+    ex = OrbExtractor(*C2, max_images=B)
+    cap = ex.max_keypoints(752, 480)
+    d_imgs = torch.from_numpy(imgs).cuda()
+    kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    n = torch.zeros(B, dtype=torch.int32, device="cuda")
+    mono = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(d_imgs, kps, desc, n, mono)
+    torch.cuda.synchronize()
+    ex.check()
+    kps_h, desc_h, n_h, mono_h = kps.cpu().numpy(), desc.cpu().numpy(), n.cpu().numpy(), mono.cpu().numpy()
+    orc = oracle.OracleExtractor(*C2)
+    for i in range(B):
+        m_ref, k_ref, d_ref = orc.extract(imgs[i])
+        assert n_h[i] == len(k_ref) and mono_h[i] == m_ref
+        assert kps_h[i, : n_h[i]].tobytes() == k_ref.tobytes(), f"image {i} keypoints"
+        assert desc_h[i, : n_h[i]].tobytes() == d_ref.tobytes(), f"image {i} descriptors"
+
+
+def test_repeat_calls_deterministic(gpu_available):
+    left, _ = synth.stereo_frame(7)
+    ex = OrbExtractor(*C2)
+    r1 = ex(left)
+    r2 = ex(left)
+    assert r1[0] == r2[0] and r1[1].tobytes() == r2[1].tobytes() and r1[2].tobytes() == r2[2].tobytes()

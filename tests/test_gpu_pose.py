@@ -1,0 +1,79 @@
+"""GPU parity: PoseOptimization on gfx950 against the CPU oracle.
+
+Floating point (fp64 LM, float outputs): the tolerance is stated here.  The
+GPU reduces per-sweep sums in a fixed tree while the oracle (like g2o) sums
+sequentially, so poses agree to rounding, not bits:
+  * outlier flags and the inlier count: identical;
+  * pose (float Tcw): |dq|, |dt| <= 1e-5 (absolute, unit quaternion / metres);
+  * pose before the float cast: <= 1e-9 relative.
+"""
+import numpy as np
+import pytest
+
+import binding as oracle
+from orb_slam_fusion_amd import PoseFrame, PoseOptimizer, synth
+
+pytestmark = pytest.mark.gpu
+
+TOL_F = 1e-5
+TOL_D = 1e-9
+
+
+def _run(cam, pose, obs):
+    opt = PoseOptimizer(max_obs=max(len(obs), 1))
+    fr = PoseFrame(cam=cam, pose=pose, obs=obs)
+    inl = opt.PoseOptimization(fr)
+    return inl, fr.pose, fr.outlier
+
+
+@pytest.mark.parametrize("seed", [7, 8, 9, 10, 11])
+def test_pose_matches_oracle(gpu_available, seed):
+    cam, pi, pt, obs = synth.pose_problem(seed, 600, 10)
+    inl_ref, p_ref, out_ref, _ = oracle.pose_opt(cam, pi, obs)
+    inl, p, out = _run(cam, pi, obs)
+    assert inl == inl_ref
+    assert np.array_equal(out, out_ref)
+    assert np.max(np.abs(p - p_ref)) <= TOL_F
+    # sanity against the synthetic truth
+    assert np.linalg.norm(p[4:] - pt[4:]) < 0.01
+
+
+@pytest.mark.parametrize("n,outlier_pct", [(3, 0), (9, 0), (50, 30), (1200, 10)])
+def test_pose_sizes(gpu_available, n, outlier_pct):
+    cam, pi, pt, obs = synth.pose_problem(100 + n, n, outlier_pct)
+    inl_ref, p_ref, out_ref, _ = oracle.pose_opt(cam, pi, obs)
+    inl, p, out = _run(cam, pi, obs)
+    assert inl == inl_ref and np.array_equal(out, out_ref)
+    assert np.max(np.abs(p - p_ref)) <= TOL_F
+
+
+def test_pose_too_few_correspondences(gpu_available):
+    cam, pi, pt, obs = synth.pose_problem(5, 2, 0)
+    inl, p, out = _run(cam, pi, obs)
+    assert inl == 0 and np.array_equal(p, pi)
+
+
+def test_pose_batch_matches_oracle(gpu_available):
+    import torch
+
+    P, N = 16, 600
+    probs = [synth.pose_problem(200 + i, N, 10) for i in range(P)]
+    cam = probs[0][0]
+    obs = np.stack([p[3] for p in probs])
+    pin = np.stack([p[1] for p in probs])
+    d_obs = torch.from_numpy(obs.view(np.float32).reshape(P, N, 7).copy()).cuda()
+    d_pin = torch.from_numpy(pin).cuda()
+    d_n = torch.full((P,), N, dtype=torch.int32, device="cuda")
+    d_pout = torch.zeros((P, 7), dtype=torch.float32, device="cuda")
+    d_pd = torch.zeros((P, 7), dtype=torch.float64, device="cuda")
+    d_out = torch.zeros((P, N), dtype=torch.uint8, device="cuda")
+    d_inl = torch.zeros(P, dtype=torch.int32, device="cuda")
+    opt = PoseOptimizer(max_problems=P, max_obs=N)
+    opt.batch(cam, d_pin, d_obs, d_n, d_pout, d_out, d_inl, d_pd)
+    torch.cuda.synchronize()
+    pout, pd, out, inl = d_pout.cpu().numpy(), d_pd.cpu().numpy(), d_out.cpu().numpy(), d_inl.cpu().numpy()
+    for i, (c, pi, pt, ob) in enumerate(probs):
+        inl_ref, p_ref, out_ref, pd_ref = oracle.pose_opt(c, pi, ob)
+        assert inl[i] == inl_ref and np.array_equal(out[i], out_ref)
+        assert np.max(np.abs(pout[i] - p_ref)) <= TOL_F
+        assert np.max(np.abs(pd[i] - pd_ref) / np.maximum(np.abs(pd_ref), 1.0)) <= TOL_D
