@@ -1,0 +1,73 @@
+// Drop-in replacement header for include/cam/orb_feature/orb_extractor.h of
+// J094/orb_slam_fusion: the same class, members and signatures
+// (orb_extractor.h:29-104), implemented over the gfx950 C ABI (orbgpu.h).
+// Compiled only in a build that has OpenCV (the reference's own dependency);
+// frame.cc / tracking.cc include it unchanged.
+#ifndef ORBEXTRACTOR_H
+#define ORBEXTRACTOR_H
+
+#include <list>
+#include <opencv2/opencv.hpp>
+#include <vector>
+
+#include "orbgpu.h"
+
+namespace ORB_SLAM_FUSION {
+
+class ExtractorNode {  // kept for source compatibility (orb_extractor.h:31-42)
+ public:
+  ExtractorNode() : no_more_(false) {}
+  void DivideNode(ExtractorNode &n_1, ExtractorNode &n_2, ExtractorNode &n_3,
+                  ExtractorNode &n_4);
+  std::vector<cv::KeyPoint> kps_;
+  cv::Point2i UL_, UR_, BL_, BR_;
+  std::list<ExtractorNode>::iterator lit_;
+  bool no_more_;
+};
+
+class OrbExtractor {
+ public:
+  enum { kHarrisScore = 0, kFastScore = 1 };
+
+  OrbExtractor(int num_feats, float scale_factor, int num_levs, int ini_th_fast,
+               int min_th_fast);
+  ~OrbExtractor();
+
+  // Same contract as orb_extractor.cc:1011-1091: returns the mono index, -1 on
+  // an empty image; asserts CV_8UC1; the mask is ignored.
+  int operator()(cv::InputArray img, cv::InputArray msk, std::vector<cv::KeyPoint> &kps,
+                 cv::OutputArray descs, std::vector<int> &lapping_areas);
+
+  int inline GetLevels() { return num_levs_; }
+  float inline GetScaleFactor() { return scale_factor_; }
+  std::vector<float> inline GetScaleFactors() { return scale_factors_; }
+  std::vector<float> inline GetInverseScaleFactors() { return inv_scale_factors_; }
+  std::vector<float> inline GetScaleSigmaSquares() { return lev_sigma_2_; }
+  std::vector<float> inline GetInverseScaleSigmaSquares() { return inv_lev_sigma_2_; }
+
+  // Host levels of the last call (each a ROI inside a 19-px REFLECT_101
+  // frame, as ComputePyramid leaves them); read by Frame::ComputeStereoMatches.
+  std::vector<cv::Mat> img_pyramid_;
+
+  void ComputePyramid(cv::Mat img);
+
+ protected:
+  int num_feats_;
+  double scale_factor_;
+  int num_levs_;
+  int ini_th_fast_;
+  int min_th_fast_;
+  std::vector<float> scale_factors_;
+  std::vector<float> inv_scale_factors_;
+  std::vector<float> lev_sigma_2_;
+  std::vector<float> inv_lev_sigma_2_;
+
+ private:
+  orbgpu_extractor *gpu_ = nullptr;
+  std::vector<orbgpu_keypoint> kp_buf_;
+  cv::Mat desc_buf_;
+};
+
+}  // namespace ORB_SLAM_FUSION
+
+#endif

@@ -1,0 +1,213 @@
+"""Independent pure-Python/numpy restatements used to cross-check the C++
+oracle (test infrastructure only).  Written from the reference's behaviour
+(orb_extractor.cc) and SURVEY.md Appendix A, separately from oracle/*.cc, so a
+transcription slip in either shows up as a mismatch.  Small inputs only."""
+from __future__ import annotations
+
+import numpy as np
+
+CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3),
+          (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def fast_score_def(img: np.ndarray, y: int, x: int) -> int:
+    """max over the 16 nine-pixel arcs of min(v - p) / min(p - v), minus 1."""
+    v = int(img[y, x])
+    d = [v - int(img[y + dy, x + dx]) for dx, dy in CIRCLE]
+    best = -10**9
+    for s in range(16):
+        arc = [d[(s + k) % 16] for k in range(9)]
+        best = max(best, min(arc), min(-a for a in arc))
+    return best - 1
+
+
+def fast_nms_def(roi: np.ndarray, th: int):
+    """cv::FAST(roi, th, nonmax=true) by definition: corners at th in
+    [3, rows-3) x [3, cols-3), strict 3x3 maximum of the in-ROI score map."""
+    rows, cols = roi.shape
+    S = np.zeros((rows, cols), np.int64)
+    for y in range(3, rows - 3):
+        for x in range(3, cols - 3):
+            s = fast_score_def(roi, y, x)
+            if s >= th:
+                S[y, x] = s
+    out = []
+    for y in range(3, rows - 3):
+        for x in range(3, cols - 3):
+            s = S[y, x]
+            if s == 0:
+                continue
+            nb = S[y - 1:y + 2, x - 1:x + 2].copy()
+            nb[1, 1] = -1
+            if s > nb.max():
+                out.append((x, y, int(s)))
+    return out
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    """cv::resize INTER_LINEAR for 8UC1, vectorised."""
+    sh, sw = src.shape
+    sx_scale = 1.0 / (dw / sw)
+    sy_scale = 1.0 / (dh / sh)
+    dx = np.arange(dw)
+    fx = ((dx + 0.5) * sx_scale - 0.5).astype(np.float32)
+    sx = np.floor(fx).astype(np.int64)
+    fx = (fx - sx.astype(np.float32)).astype(np.float32)
+    neg = sx < 0
+    fx[neg], sx[neg] = 0, 0
+    right = sx + 1 >= sw
+    xmax = int(np.argmax(right)) if right.any() else dw
+    clamp = sx >= sw - 1
+    fx[clamp], sx[clamp] = 0, sw - 1
+    a0 = np.clip(np.rint((np.float32(1) - fx) * np.float32(2048)), -32768, 32767).astype(np.int64)
+    a1 = np.clip(np.rint(fx * np.float32(2048)), -32768, 32767).astype(np.int64)
+
+    dy = np.arange(dh)
+    fy = ((dy + 0.5) * sy_scale - 0.5).astype(np.float32)
+    sy = np.floor(fy).astype(np.int64)
+    fy = (fy - sy.astype(np.float32)).astype(np.float32)
+    b0 = np.clip(np.rint((np.float32(1) - fy) * np.float32(2048)), -32768, 32767).astype(np.int64)
+    b1 = np.clip(np.rint(fy * np.float32(2048)), -32768, 32767).astype(np.int64)
+    r0 = np.clip(sy, 0, sh - 1)
+    r1 = np.clip(sy + 1, 0, sh - 1)
+
+    S = src.astype(np.int64)
+    sx1 = np.minimum(sx + 1, sw - 1)
+
+    def hres(rows):
+        H = S[rows][:, sx] * a0 + S[rows][:, sx1] * a1
+        H[:, xmax:] = S[rows][:, sx[xmax:]] * 2048
+        return H
+
+    H0, H1 = hres(r0), hres(r1)
+    B0, B1 = b0[:, None], b1[:, None]
+    # SIMD body: x <= w-16 in 16s, then x < w-8 in 8s
+    x = 0
+    while x <= dw - 16:
+        x += 16
+    while x < dw - 8:
+        x += 8
+    vec_end = x
+
+    def s16(a):
+        return np.clip(a, -32768, 32767)
+
+    m0 = (s16(H0 >> 4) * B0) >> 16
+    m1 = (s16(H1 >> 4) * B1) >> 16
+    vec = np.clip((s16(m0 + m1) + 2) >> 2, 0, 255)
+    sca = np.clip((H0 * B0 + H1 * B1 + (1 << 21)) >> 22, 0, 255)
+    out = sca.copy()
+    out[:, :vec_end] = vec[:, :vec_end]
+    return out.astype(np.uint8)
+
+
+def gauss7(src: np.ndarray) -> np.ndarray:
+    k = np.array([18, 34, 48, 56, 48, 34, 18], np.int64)
+    h, w = src.shape
+
+    def refl(i, n):
+        i = np.abs(i)
+        return np.where(i >= n, 2 * n - 2 - i, i)
+
+    xs = refl(np.arange(w)[:, None] + np.arange(-3, 4)[None, :], w)
+    ys = refl(np.arange(h)[:, None] + np.arange(-3, 4)[None, :], h)
+    S = src.astype(np.int64)
+    Hs = (S[:, xs] * k).sum(-1)             # h x w
+    V = (Hs[ys] * k[None, :, None]).sum(1)  # h x w
+    return np.minimum((V + (1 << 15)) >> 16, 255).astype(np.uint8)
+
+
+def distribute_octree(kps, min_x, max_x, min_y, max_y, n_feats):
+    """DistributeOctTree (orb_extractor.cc:542-742) with Python lists standing
+    in for std::list; kps = [(x, y, response)] in to_dist order.  Returns the
+    kept keypoints in node-list order."""
+    r = float(np.float32(max_x - min_x) / np.float32(max_y - min_y))
+    n_ini = int(np.floor(r + 0.5))  # std::round: half away from zero
+    hx = np.float32(max_x - min_x) / np.float32(n_ini)
+
+    class Node:
+        __slots__ = ("ul", "ur", "bl", "br", "kps", "no_more")
+
+        def __init__(self):
+            self.kps, self.no_more = [], False
+
+    def divide(nd):
+        half_x = int(np.ceil(np.float32(nd.ur[0] - nd.ul[0]) / np.float32(2)))
+        half_y = int(np.ceil(np.float32(nd.br[1] - nd.ul[1]) / np.float32(2)))
+        c = [Node() for _ in range(4)]
+        c[0].ul, c[0].ur = nd.ul, (nd.ul[0] + half_x, nd.ul[1])
+        c[0].bl, c[0].br = (nd.ul[0], nd.ul[1] + half_y), (nd.ul[0] + half_x, nd.ul[1] + half_y)
+        c[1].ul, c[1].ur, c[1].bl, c[1].br = c[0].ur, nd.ur, c[0].br, (nd.ur[0], nd.ul[1] + half_y)
+        c[2].ul, c[2].ur, c[2].bl, c[2].br = c[0].bl, c[0].br, nd.bl, (c[0].br[0], nd.bl[1])
+        c[3].ul, c[3].ur, c[3].bl, c[3].br = c[2].ur, c[1].br, c[2].br, nd.br
+        for kp in nd.kps:
+            if kp[0] < c[0].ur[0]:
+                (c[0] if kp[1] < c[0].br[1] else c[2]).kps.append(kp)
+            else:
+                (c[1] if kp[1] < c[0].br[1] else c[3]).kps.append(kp)
+        for ch in c:
+            if len(ch.kps) == 1:
+                ch.no_more = True
+        return c
+
+    nodes = []
+    roots = []
+    for i in range(n_ini):
+        n = Node()
+        x0 = int(hx * np.float32(i))
+        x1 = int(hx * np.float32(i + 1))
+        n.ul, n.ur, n.bl, n.br = (x0, 0), (x1, 0), (x0, max_y - min_y), (x1, max_y - min_y)
+        nodes.append(n)
+        roots.append(n)
+    for kp in kps:
+        roots[int(np.float32(kp[0]) / hx)].kps.append(kp)
+    nodes = [n for n in nodes if n.kps]
+    for n in nodes:
+        if len(n.kps) == 1:
+            n.no_more = True
+
+    finished = False
+    expand = []
+    while not finished:
+        prev = len(nodes)
+        front = []  # pushed to the list front, newest first
+        expand = []
+        keep = []
+        for n in nodes:
+            if n.no_more:
+                keep.append(n)
+                continue
+            for ch in divide(n):
+                if ch.kps:
+                    front.insert(0, ch)
+                    if len(ch.kps) > 1:
+                        expand.append(ch)
+        nodes = front + keep
+        if len(nodes) >= n_feats or len(nodes) == prev:
+            finished = True
+        elif len(nodes) + 3 * len(expand) > n_feats:
+            while not finished:
+                prev = len(nodes)
+                order = sorted(range(len(expand)), key=lambda j: (len(expand[j].kps), expand[j].ul[0], j))
+                cand = [expand[j] for j in order]
+                expand = []
+                for nd in reversed(cand):
+                    kids = [ch for ch in divide(nd) if ch.kps]
+                    pos = next(i for i, m in enumerate(nodes) if m is nd)
+                    del nodes[pos]
+                    for ch in kids:
+                        nodes.insert(0, ch)
+                        if len(ch.kps) > 1:
+                            expand.append(ch)
+                    if len(nodes) >= n_feats:
+                        break
+                if len(nodes) >= n_feats or len(nodes) == prev:
+                    finished = True
+    out = []
+    for n in nodes:
+        best = n.kps[0]
+        for kp in n.kps[1:]:
+            if kp[2] > best[2]:
+                best = kp
+        out.append(best)
+    return out

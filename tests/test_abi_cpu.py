@@ -1,0 +1,80 @@
+"""CPU checks of the C ABI library (no compute calls: there is no GPU here).
+
+* liborbgpu.so loads and exports every function include/orbgpu.h declares;
+* the binding's signature table covers exactly those functions;
+* argument validation that happens before any HIP call returns the
+  documented status codes;
+* the library contains gfx950 code objects and no CPU fallback symbols.
+"""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from orb_slam_fusion_amd import _lib
+
+REPO = Path(__file__).resolve().parents[1]
+HEADER = REPO / "include" / "orbgpu.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(orbgpu_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for must in ["orbgpu_extractor_create", "orbgpu_extract", "orbgpu_extract_batch",
+                 "orbgpu_extractor_pyramid_level", "orbgpu_pose_opt", "orbgpu_pose_opt_batch"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    so = _lib.lib()
+    missing = [n for n in declared_functions() if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_binding_table_matches_header():
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+
+
+def test_exported_symbols_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (orbgpu_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_carries_gfx950_code_object():
+    data = _lib.library_path().read_bytes()
+    assert b"gfx950" in data
+
+
+def test_invalid_params_rejected_before_device():
+    so = _lib.lib()
+    h = ctypes.c_void_p()
+    bad = _lib.OrbParams(1000, 1.0, 8, 20, 7)  # scale_factor must be > 1
+    assert so.orbgpu_extractor_create(ctypes.byref(bad), 0, 752, 480, 1, ctypes.byref(h)) == \
+        _lib.ORBGPU_ERR_INVALID
+    too_small = _lib.OrbParams(1000, 1.2, 8, 20, 7)
+    assert so.orbgpu_extractor_create(ctypes.byref(too_small), 0, 100, 80, 1, ctypes.byref(h)) == \
+        _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_extract(None, None, 0, 0, 0, None, None, None, 0, None, None) == \
+        _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_pose_opt(None, None, None, None, 0, None, None, None) == _lib.ORBGPU_ERR_INVALID
+
+
+def test_keypoint_struct_is_cv_keypoint_layout():
+    assert _lib.KEYPOINT_DTYPE.itemsize == 28
+    assert list(_lib.KEYPOINT_DTYPE.names) == ["x", "y", "size", "angle", "response", "octave",
+                                               "class_id"]
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setenv("ORBGPU_LIB", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(OSError, match="no CPU fallback"):
+        _lib.lib()
