@@ -75,7 +75,7 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
                              uint8_t* descs, int cap, int* n_out, int* mono_out);
 
 /* Host copy of pyramid level `level` from the last orbgpu_extract call
- * (packed rows, *stride == *width).  Replaces the public member
+ * (rows *stride bytes apart, *stride >= *width).  Replaces the public member
  * std::vector<cv::Mat> img_pyramid_ (orb_extractor.h:76) read by
  * Frame::ComputeStereoMatches (frame.cc:834,913-933).  The pointer stays valid
  * until the next extract/destroy on this handle. */

@@ -80,7 +80,9 @@ int orc_level_size(void* h, int lev, int* w, int* hgt) {
 
 void orc_level_copy(void* h, int lev, int blurred, uint8_t* out) {
   auto* ex = static_cast<OrbExtractor*>(h);
-  const auto& p = blurred ? ex->blurred_[lev] : ex->img_pyramid_[lev];
+  const auto& all = blurred ? ex->blurred_ : ex->img_pyramid_;
+  if (lev < 0 || lev >= (int)all.size()) return;
+  const auto& p = all[lev];
   std::memcpy(out, p.px.data(), p.px.size());
 }
 
@@ -88,7 +90,9 @@ void orc_level_copy(void* h, int lev, int blurred, uint8_t* out) {
 // order), 1 -> octree output (list order).  Rows of (x, y, response).
 int orc_stage(void* h, int lev, int which, float* xyr, int cap) {
   auto* ex = static_cast<OrbExtractor*>(h);
-  const auto& v = which == 0 ? ex->to_dist_[lev] : ex->octree_[lev];
+  const auto& all = which == 0 ? ex->to_dist_ : ex->octree_;
+  if (lev < 0 || lev >= (int)all.size()) return -1;
+  const auto& v = all[lev];
   const int n = (int)v.size();
   for (int i = 0; i < std::min(n, cap); ++i) {
     xyr[3 * i] = v[i].x;

@@ -279,7 +279,8 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   if (st == ORBGPU_OK) st = ensure_workspace(h, 1);
   if (st != ORBGPU_OK) return st;
   const PlanHeader& P = h->plan.hdr;
-  const size_t bytes = (size_t)width * height;
+  const int pitch0 = P.lev[0].pitch;  // 16-byte aligned rows for the vector loads
+  const size_t bytes = (size_t)pitch0 * height;
   if (bytes > h->d_img_bytes) {
     dfree(h->d_img);
     if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
@@ -292,11 +293,11 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
       return ORBGPU_ERR_NOMEM;
     h->out_cap = P.kp_slots;
   }
-  if (hipMemcpy2DAsync(h->d_img, width, img, stride, width, height, hipMemcpyHostToDevice,
+  if (hipMemcpy2DAsync(h->d_img, pitch0, img, stride, width, height, hipMemcpyHostToDevice,
                        h->stream) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
   const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
-  ExtractLaunch a = make_launch(h, h->d_img, bytes, width, 1, lap, h->d_kps, h->d_descs,
+  ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
                                 P.kp_slots, h->d_nm, h->d_nm + 1);
   if (launch_extract(a, h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
   int nm[2] = {0, 0}, err = 0;
@@ -329,8 +330,8 @@ orbgpu_status orbgpu_extractor_pyramid_level(orbgpu_extractor* h, int level, con
     return ORBGPU_ERR_INVALID;
   if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
   const PlanHeader& P = h->plan.hdr;
+  const size_t l0 = (size_t)P.lev[0].pitch * P.lev[0].h;
   if (!h->host_pyr_valid) {
-    const size_t l0 = (size_t)P.lev[0].w * P.lev[0].h;
     h->host_pyr.resize(l0 + P.pyr_bytes);
     if (hipMemcpyAsync(h->host_pyr.data(), h->d_img, l0, hipMemcpyDeviceToHost, h->stream) ||
         hipMemcpyAsync(h->host_pyr.data() + l0, h->d_pyr, P.pyr_bytes, hipMemcpyDeviceToHost,
@@ -340,11 +341,10 @@ orbgpu_status orbgpu_extractor_pyramid_level(orbgpu_extractor* h, int level, con
     h->host_pyr_valid = true;
   }
   const LevelGeom& g = P.lev[level];
-  const size_t l0 = (size_t)P.lev[0].w * P.lev[0].h;
   *data = h->host_pyr.data() + (level == 0 ? 0 : l0 + g.pyr_off);
   if (width) *width = g.w;
   if (height) *height = g.h;
-  if (stride) *stride = g.w;
+  if (stride) *stride = g.pitch;
   return ORBGPU_OK;
 }
 
@@ -411,7 +411,10 @@ int orbgpu_extractor_stage(orbgpu_extractor* h, int which, int level, void* out,
   if (which == 0) {
     const int n = g.w * g.h;
     if (n > cap) return -1;
-    return hipMemcpy(out, h->d_blur + g.blur_off, n, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+    return hipMemcpy2D(out, g.w, h->d_blur + g.blur_off, g.pitch, g.w, g.h,
+                       hipMemcpyDeviceToHost) == hipSuccess
+               ? n
+               : -1;
   }
   if (which == 1) {
     std::vector<int> cc(g.cell_end - g.cell_begin);

@@ -23,7 +23,21 @@ __constant__ int8_t c_pattern[1024] = {
 #include "pattern31.inc"
 };
 
+// Row extents of the 31-px circular patch (orb_extractor.cc:452-464; fixed
+// because kHalfPatchSize is fixed at 15).
+__constant__ int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
 enum : int { kErrNodeCap = 1, kErrOutCap = 2, kErrSlotCap = 4, kErrKpCap = 8 };
+
+// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 labels the
+// XCD group, MI355X_MICROARCH.md).  Consecutive work items share image rows
+// (cell halos, keypoint patches), so give every XCD a contiguous range of
+// them: its private L2 then serves the overlaps.  Bijective for any count.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks >> 3, r = nblocks & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
 
 struct ImgSrc {
   const uint8_t* base;  // image 0, level 0
@@ -38,7 +52,7 @@ __device__ __forceinline__ const uint8_t* level_plane(const PlanHeader* P, const
     pitch = s.stride;
     return s.base + (size_t)img * s.pitch;
   }
-  pitch = P->lev[l].w;
+  pitch = P->lev[l].pitch;
   return pyr + (size_t)img * P->pyr_bytes + P->lev[l].pyr_off;
 }
 
@@ -48,108 +62,205 @@ __device__ __forceinline__ const uint8_t* level_plane(const PlanHeader* P, const
 // precomputed by the planner.  Columns below vec_end use the 128-bit SIMD
 // rounding ((H>>4)*b >> 16 summed, +2 >> 2), the tail the scalar
 // (H0*b0 + H1*b1 + 2^21) >> 22 -- exactly where OpenCV switches.
-// Each thread produces 4 consecutive output pixels.
+// A 256-thread block makes a 256 x 8 output tile: the source window is staged
+// in LDS with dword loads, each thread then produces 8 consecutive pixels
+// (one 8-byte store).
 // --------------------------------------------------------------------------
-__device__ __forceinline__ int h_tap(const uint8_t* S, int x, int xmax, int2 xa) {
-  const int sx = xa.x;
-  const int a0 = (int)(short)(xa.y & 0xffff), a1 = (int)(short)(xa.y >> 16);
-  return x < xmax ? S[sx] * a0 + S[sx + 1] * a1 : S[sx] * 2048;
-}
-
 __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
                                                 const int* __restrict__ rs_tab, ImgSrc src,
                                                 uint8_t* __restrict__ pyr, int l) {
+  // Branch-free by construction: every load and LDS store is unconditional
+  // (clamped indices; duplicates write identical bytes), and single-tap
+  // columns (x >= xmax) carry taps (2048, 0) from the planner.
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int RPT = kResizeTileH / 8;  // output rows per thread
   const LevelGeom& g = P->lev[l];
-  const int x0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  const int img = blockIdx.z;
-  if (x0 >= g.w || y >= g.h) return;
+  const int sw = P->lev[l - 1].w;
+  const int nb = gridDim.x * gridDim.y * gridDim.z;
+  const int wid = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nb);
+  const int img = wid / (g.rs_tiles_x * g.rs_tiles_y);
+  const int tyx = wid - img * (g.rs_tiles_x * g.rs_tiles_y);
+  const int x0 = (tyx % g.rs_tiles_x) * kResizeTileW, y0 = (tyx / g.rs_tiles_x) * kResizeTileH;
+  const int xl = min(x0 + kResizeTileW, g.w) - 1, yl = min(y0 + kResizeTileH, g.h) - 1;
+  const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
+  const int2* yt = reinterpret_cast<const int2*>(rs_tab + g.rs_y);
+  const int c0 = xt[x0].x & ~15;
+  const int c1 = min(xt[xl].x + 1, sw - 1) | 15;
+  const int rr0 = yt[y0].x & 0xffff, rr1 = yt[yl].x >> 16;
+  const int ncol = c1 - c0 + 1, nrow = rr1 - rr0 + 1;  // ncol: multiple of 16
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
-  uint8_t* D = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + (size_t)y * g.w;
-  const int2 yt = reinterpret_cast<const int2*>(rs_tab + g.rs_y)[y];
-  const int r0 = yt.x & 0xffff, r1 = yt.x >> 16;
-  const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)(yt.y >> 16);
-  const uint8_t* S0 = S + (size_t)r0 * sp;
-  const uint8_t* S1 = S + (size_t)r1 * sp;
-  const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
-  uint32_t packed = 0;
-  const int n = min(4, g.w - x0);
+
+  // per-thread taps, fetched up front
+  const int xs = x0 + (threadIdx.x & 31) * 8;
+  int2 xa[8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (k < n) {
-      const int x = x0 + k;
-      const int2 xa = xt[x];
-      const int h0 = h_tap(S0, x, g.xmax, xa), h1 = h_tap(S1, x, g.xmax, xa);
-      int v;
-      if (x < g.vec8_end) {
-        const int m0 = (max(min(h0 >> 4, 32767), -32768) * b0) >> 16;
-        const int m1 = (max(min(h1 >> 4, 32767), -32768) * b1) >> 16;
-        const int s = max(min(m0 + m1, 32767), -32768);
-        v = (s + 2) >> 2;
-      } else {
-        v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+  for (int k = 0; k < 8; ++k) xa[k] = xt[min(xs + k, g.w - 1)];
+  int2 yv[RPT];
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr) yv[rr] = yt[min(y0 + (int)(threadIdx.x >> 5) + 8 * rr, yl)];
+
+  if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && c1 < sp) {
+    const int nq = ncol >> 4, total = nrow * nq;
+    const uint32_t mg = ((1u << 19) + nq - 1) / nq;
+    for (int i0 = 0; i0 < total; i0 += 1024) {
+      uint4 v[4];
+      int at[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = min(i0 + 256 * u + (int)threadIdx.x, total - 1);
+        const int r = (int)(((uint32_t)i * mg) >> 19), q = i - r * nq;
+        v[u] = *reinterpret_cast<const uint4*>(S + (size_t)(rr0 + r) * sp + c0 + 16 * q);
+        at[u] = 16 * i;
       }
-      packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(lds + at[u]) = v[u];
+    }
+  } else {
+    for (int i = threadIdx.x; i < nrow * ncol; i += 256) {
+      const int r = i / ncol, c = i - r * ncol;
+      lds[i] = S[(size_t)(rr0 + r) * sp + min(c0 + c, sw - 1)];
     }
   }
-  if (n == 4 && (((uintptr_t)(D + x0)) & 3) == 0) {
-    *reinterpret_cast<uint32_t*>(D + x0) = packed;
-  } else {
-    for (int k = 0; k < n; ++k) D[x0 + k] = (uint8_t)(packed >> (8 * k));
+  __syncthreads();
+
+  uint8_t* Dbase = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + xs;
+  const int xoff = -c0;
+#pragma unroll
+  for (int rr = 0; rr < RPT; ++rr) {
+    const int r0 = (yv[rr].x & 0xffff) - rr0, r1 = (yv[rr].x >> 16) - rr0;
+    const int b0 = (int)(short)(yv[rr].y & 0xffff), b1 = (int)(short)(yv[rr].y >> 16);
+    const uint8_t* L0 = lds + r0 * ncol + xoff;
+    const uint8_t* L1 = lds + r1 * ncol + xoff;
+    int s00[8], s01[8], s10[8], s11[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // 32 independent LDS reads
+      const int sx = xa[k].x, sx1 = min(sx + 1, c1);
+      s00[k] = L0[sx];
+      s01[k] = L0[sx1];
+      s10[k] = L1[sx];
+      s11[k] = L1[sx1];
+    }
+    uint32_t w[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int a0 = (int)(short)(xa[k].y & 0xffff), a1 = (int)(short)(xa[k].y >> 16);
+      const int h0 = s00[k] * a0 + s01[k] * a1, h1 = s10[k] * a0 + s11[k] * a1;
+      const int m0 = (max(min(h0 >> 4, 32767), -32768) * b0) >> 16;
+      const int m1 = (max(min(h1 >> 4, 32767), -32768) * b1) >> 16;
+      const int vv = (max(min(m0 + m1, 32767), -32768) + 2) >> 2;
+      const int vs = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+      const int v = xs + k < g.vec8_end ? vv : vs;
+      w[k >> 2] |= (uint32_t)min(max(v, 0), 255) << (8 * (k & 3));
+    }
+    const int y = y0 + (int)(threadIdx.x >> 5) + 8 * rr;
+    if (y <= yl && xs < g.w) {
+      uint8_t* D = Dbase + (size_t)y * g.pitch;
+      if (xs + 8 <= g.w) {
+        *reinterpret_cast<uint2*>(D) = make_uint2(w[0], w[1]);
+      } else {
+        for (int k = 0; k < g.w - xs; ++k) D[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+      }
+    }
   }
 }
 
 // --------------------------------------------------------------------------
 // k_blur: GaussianBlur 7x7, sigma 2, BORDER_REFLECT_101, bit-exact fixed point
 // (SURVEY Appendix A.3): Q8 taps [18 34 48 56 48 34 18], horizontal sums kept
-// exact, (sum + 2^15) >> 16 once.  64x16 output tiles through LDS; one launch
-// covers every level of every image.
+// exact, (sum + 2^15) >> 16 once.  Each thread owns 4 adjacent columns and
+// slides a 7-row register window down a 16-row strip (3 dword loads per source
+// row in the interior); a 256-thread block covers 256 x 64 outputs and one
+// launch covers every level of every image.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {
   i = i < 0 ? -i : i;
   return i >= n ? 2 * n - 2 - i : i;
 }
 
+__device__ __forceinline__ int hsum7(int a, int b, int c, int d, int e, int f, int g) {
+  return 18 * (a + g) + 34 * (b + f) + 48 * (c + e) + 56 * d;
+}
+
+template <int R>
+__device__ __forceinline__ void blur_emit(const int (&hw)[R + 6][4], uint8_t* D, int ys, int h,
+                                          int pitch, int nvalid) {
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    if (ys + o < h) {
+      uint32_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t v = 18u * (hw[o][j] + hw[o + 6][j]) + 34u * (hw[o + 1][j] + hw[o + 5][j]) +
+                           48u * (hw[o + 2][j] + hw[o + 4][j]) + 56u * hw[o + 3][j];
+        packed |= min((v + (1u << 15)) >> 16, 255u) << (8 * j);
+      }
+      uint8_t* out = D + (size_t)(ys + o) * pitch;
+      if (nvalid >= 4) {
+        *reinterpret_cast<uint32_t*>(out) = packed;
+      } else {
+        for (int j = 0; j < nvalid; ++j) out[j] = (uint8_t)(packed >> (8 * j));
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
-  constexpr int TW = kBlurTileW, TH = kBlurTileH;
-  constexpr int IW = TW + 6, IH = TH + 6;
-  __shared__ uint8_t tin[IH][IW + 2];
-  __shared__ int thor[IH][TW + 1];
-  const int img = blockIdx.x / P->blur_tiles;
-  int t = blockIdx.x - img * P->blur_tiles;
+  constexpr int R = 8;  // rows per thread
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = wid / P->blur_tiles;
+  int t = wid - img * P->blur_tiles;
   int l = 0;
   while (l + 1 < P->levels && t >= P->lev[l + 1].blur_tile_begin) ++l;
   const LevelGeom& g = P->lev[l];
   t -= g.blur_tile_begin;
   const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
-  const int ox = tx * TW, oy = ty * TH;
+  const int x = tx * kBlurTileW + 4 * (threadIdx.x & 63);
+  const int ys = ty * kBlurTileH + R * (threadIdx.x >> 6);
+  if (x >= g.w || ys >= g.h) return;
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
-  for (int i = threadIdx.x; i < IH * IW; i += 256) {
-    const int r = i / IW, c = i - r * IW;
-    const int yy = reflect101(oy + r - 3, g.h), xx = reflect101(min(ox + c - 3, g.w + 2), g.w);
-    tin[r][c] = S[(size_t)yy * sp + xx];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < IH * TW; i += 256) {
-    const int r = i / TW, c = i - r * TW;
-    const uint8_t* q = &tin[r][c];
-    thor[r][c] = 18 * (q[0] + q[6]) + 34 * (q[1] + q[5]) + 48 * (q[2] + q[4]) + 56 * q[3];
-  }
-  __syncthreads();
-  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off;
-  for (int i = threadIdx.x; i < TH * TW; i += 256) {
-    const int r = i / TW, c = i - r * TW;
-    const int y = oy + r, x = ox + c;
-    if (y < g.h && x < g.w) {
-      const uint32_t s = 18u * (thor[r][c] + thor[r + 6][c]) + 34u * (thor[r + 1][c] + thor[r + 5][c]) +
-                         48u * (thor[r + 2][c] + thor[r + 4][c]) + 56u * thor[r + 3][c];
-      D[(size_t)y * g.w + x] = (uint8_t)min((s + (1u << 15)) >> 16, 255u);
+  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + x;
+  int hw[R + 6][4];
+  if (x >= 4 && x + 8 <= g.w && ((((uintptr_t)S) | (uintptr_t)sp) & 3) == 0) {
+    // interior: 3 dword loads per source row, all issued before any use
+    uint32_t d[R + 6][3];
+#pragma unroll
+    for (int r = 0; r < R + 6; ++r) {
+      const uint8_t* row = S + (size_t)reflect101(ys - 3 + r, g.h) * sp + x - 4;
+      d[r][0] = reinterpret_cast<const uint32_t*>(row)[0];
+      d[r][1] = reinterpret_cast<const uint32_t*>(row)[1];
+      d[r][2] = reinterpret_cast<const uint32_t*>(row)[2];
+    }
+#pragma unroll
+    for (int r = 0; r < R + 6; ++r) {
+      const int b[10] = {(int)((d[r][0] >> 8) & 255), (int)((d[r][0] >> 16) & 255), (int)(d[r][0] >> 24),
+                         (int)(d[r][1] & 255), (int)((d[r][1] >> 8) & 255), (int)((d[r][1] >> 16) & 255),
+                         (int)(d[r][1] >> 24), (int)(d[r][2] & 255), (int)((d[r][2] >> 8) & 255),
+                         (int)((d[r][2] >> 16) & 255)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        hw[r][j] = hsum7(b[j], b[j + 1], b[j + 2], b[j + 3], b[j + 4], b[j + 5], b[j + 6]);
+    }
+  } else {
+    // image borders / unaligned source: byte gathers with reflect-101 columns
+    int cx[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) cx[j] = reflect101(min(x - 3 + j, g.w + 2), g.w);
+#pragma unroll
+    for (int r = 0; r < R + 6; ++r) {
+      const uint8_t* row = S + (size_t)reflect101(ys - 3 + r, g.h) * sp;
+      int b[10];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) b[j] = row[cx[j]];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        hw[r][j] = hsum7(b[j], b[j + 1], b[j + 2], b[j + 3], b[j + 4], b[j + 5], b[j + 6]);
     }
   }
+  blur_emit<R>(hw, D, ys, g.h, g.pitch, g.w - x);
 }
 
 // --------------------------------------------------------------------------
@@ -161,8 +272,10 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
 //   p is a corner at th  <=>  S(p) >= th  (the score is threshold-free then);
 //   NMS keeps p iff S(p) > S'(q) for its 8 neighbours, where S'(q) = S(q) if q
 //   is a corner at th inside the same cell's detection area, else 0.
-// Candidates are compacted in raster order with ballot/mbcnt, giving exactly
-// the reference's per-cell keypoint order.
+// Work per pass: a 5-read compass test (every 9-arc holds one pixel of each
+// opposite pair {0,8}, {4,12}, so it never rejects a corner) compacts the
+// survivors in raster order; only survivors get the full score and the NMS.
+// Output order = raster order = the reference's per-cell keypoint order.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int fast_score(const uint8_t* p, const int* off) {
   const int v = p[0];
@@ -199,73 +312,150 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
                                                    int* __restrict__ cell_count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x;
-  const int img = blockIdx.x / P->n_cells;
-  const int ci = blockIdx.x - img * P->n_cells;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = wid / P->n_cells;
+  const int ci = wid - img * P->n_cells;
   const Cell c = cells[ci];
-  uint8_t* roi = lds;
-  uint8_t* score = lds + P->max_roi;
-  int sp;
-  const uint8_t* S = level_plane(P, src, pyr, img, c.level, sp) + (size_t)c.y0 * sp + c.x0;
-  const int npx = c.rows * c.cols;
-  for (int i = lane; i < npx; i += 64) {
-    const int r = i / c.cols, q = i - r * c.cols;
-    roi[i] = S[(size_t)r * sp + q];
-  }
-  __syncthreads();
-
   const int dw = c.cols - 6, dh = c.rows - 6;
   const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
-  const int th_ini = P->ini_th, th_min = P->min_th;
-  const int th_lo = min(th_ini, th_min);
+  uint32_t* out = slots + (size_t)img * P->slots + c.slot_off;
+  if (nd == 0) {
+    if (lane == 0) cell_count[(size_t)img * P->n_cells + ci] = 0;
+    return;
+  }
+  // LDS: ROI rows of ls bytes (lead bytes keep dword alignment), score map,
+  // u16 survivor list (bit 15 = keypoint flag).
+  const int lead = c.x0 & 3, ls = (c.cols + 6) & ~3;
+  uint8_t* roi = lds;
+  uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
+  uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nd + 15) & ~15));
+
+  int sp;
+  const uint8_t* S = level_plane(P, src, pyr, img, c.level, sp) + (size_t)c.y0 * sp + (c.x0 - lead);
+  if (((((uintptr_t)S) | (uintptr_t)sp) & 3) == 0) {
+    const int ndw = (lead + c.cols + 3) >> 2;
+    const uint32_t mg = ((1u << 19) + ndw - 1) / ndw;
+    const int total = c.rows * ndw;
+    for (int i0 = 0; i0 < total; i0 += 256) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // 4 independent loads in flight per lane
+        const int i = min(i0 + 64 * u + lane, total - 1);
+        const int r = (int)(((uint32_t)i * mg) >> 19), q = i - r * ndw;
+        v[u] = *reinterpret_cast<const uint32_t*>(S + (size_t)r * sp + 4 * q);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 64 * u + lane;
+        if (i < total) {
+          const int r = (int)(((uint32_t)i * mg) >> 19), q = i - r * ndw;
+          *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) = v[u];
+        }
+      }
+    }
+  } else {
+    for (int i = lane; i < c.rows * c.cols; i += 64) {
+      const int r = i / c.cols, q = i - r * c.cols;
+      roi[r * ls + lead + q] = S[(size_t)r * sp + lead + q];
+    }
+  }
+  for (int i = lane; i < ((nd + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
+  __syncthreads();
+
+  const uint32_t magic = ((1u << 19) + dw - 1) / dw;  // exact i / dw for i * dw < 2^19
+  auto row_of = [&](int i) { return (int)(((uint32_t)i * magic) >> 19); };
+  const uint8_t* base = roi + 3 * ls + lead + 3;  // detection pixel (0, 0)
   int off[16];
   {
     const int cx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
     const int cy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) off[k] = cx[k] + cy[k] * c.cols;
+    for (int k = 0; k < 16; ++k) off[k] = cx[k] + cy[k] * ls;
   }
-  for (int i = lane; i < nd; i += 64) {
-    const int r = i / dw, q = i - r * dw;
-    const int s = fast_score(roi + (r + 3) * c.cols + q + 3, off);
-    score[i] = (uint8_t)(s >= th_lo ? s : 0);
-  }
-  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
 
-  auto is_kp = [&](int i, int th) -> bool {
-    if (i >= nd) return false;
-    const int s = score[i];
-    if (s < th) return false;
-    const int r = i / dw, q = i - r * dw;
+  // One threshold pass; returns the number of keypoints, leaves the survivor
+  // list (raster order, kp flag in bit 15) in sv[0..*n_sv).
+  auto pass = [&](int th, int* n_sv) -> int {
+    int ns = 0;
+    for (int b0 = 0; b0 < nd; b0 += 256) {
+      bool f[4];
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        if (dx == 0 && dy == 0) continue;
-        const int rr = r + dy, qq = q + dx;
-        if (rr < 0 || rr >= dh || qq < 0 || qq >= dw) continue;
-        const int t = score[rr * dw + qq];
-        if (s <= (t >= th ? t : 0)) return false;
+      for (int u = 0; u < 4; ++u) {  // 4 pixels per lane: 20 LDS reads in flight
+        const int i = min(b0 + 64 * u + lane, nd - 1);
+        const int r = row_of(i), q = i - r * dw;
+        const uint8_t* p = base + r * ls + q;
+        const int v = p[0];
+        const int dn = p[3 * ls], up = p[-3 * ls], rt = p[3], lf = p[-3];
+        const bool dark = (v - dn > th || v - up > th) && (v - rt > th || v - lf > th);
+        const bool bright = (dn - v > th || up - v > th) && (rt - v > th || lf - v > th);
+        f[u] = (b0 + 64 * u + lane < nd) && (dark || bright);
       }
-    return true;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t m = __ballot(f[u]);
+        if (f[u]) sv[ns + __popcll(m & lt)] = (uint16_t)(b0 + 64 * u + lane);
+        ns += __popcll(m);
+      }
+    }
+    __syncthreads();
+    for (int j = lane; j < ns; j += 64) {
+      const int i = sv[j];
+      const int r = row_of(i), q = i - r * dw;
+      const int s = fast_score(base + r * ls + q, off);
+      sc[i] = (uint8_t)(s >= th ? s : 0);
+    }
+    __syncthreads();
+    int nk = 0;
+    for (int b0 = 0; b0 < ns; b0 += 64) {
+      const int j = b0 + lane;
+      bool kp = false;
+      if (j < ns) {
+        const int i = sv[j];
+        const int s = sc[i];
+        if (s > 0) {
+          const int r = row_of(i), q = i - r * dw;
+          kp = true;
+#pragma unroll
+          for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+              if (dx == 0 && dy == 0) continue;
+              const int rr = r + dy, qq = q + dx;
+              if (rr < 0 || rr >= dh || qq < 0 || qq >= dw) continue;
+              if (s <= sc[rr * dw + qq]) kp = false;
+            }
+        }
+        if (kp) sv[j] = (uint16_t)(i | 0x8000);
+      }
+      nk += __popcll(__ballot(kp));
+    }
+    __syncthreads();
+    *n_sv = ns;
+    return nk;
   };
 
-  int n_ini = 0;
-  for (int base = 0; base < nd; base += 64) n_ini += __popcll(__ballot(is_kp(base + lane, th_ini)));
-  const int th = n_ini > 0 ? th_ini : th_min;
+  int ns = 0;
+  int nk = pass(P->ini_th, &ns);
+  if (nk == 0) {
+    for (int j = lane; j < ns; j += 64) sc[sv[j] & 0x7fff] = 0;
+    __syncthreads();
+    nk = pass(P->min_th, &ns);
+  }
 
-  uint32_t* out = slots + (size_t)img * P->slots + c.slot_off;
   const int xrel0 = c.x0 + 3 - kFastBorder, yrel0 = c.y0 + 3 - kFastBorder;
   int written = 0;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  for (int base = 0; base < nd; base += 64) {
-    const int i = base + lane;
-    const bool k = is_kp(i, th);
+  for (int b0 = 0; b0 < ns; b0 += 64) {
+    const int j = b0 + lane;
+    const int e = j < ns ? sv[j] : 0;
+    const bool k = (e & 0x8000) != 0;
     const uint64_t m = __ballot(k);
     if (k) {
-      const int r = i / dw, q = i - r * dw;
+      const int i = e & 0x7fff;
+      const int r = row_of(i), q = i - r * dw;
       const int pos = written + __popcll(m & lt);
       if (pos < c.slot_cap)
-        out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)score[i] << 24);
+        out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)sc[i] << 24);
     }
     written += __popcll(m);
   }
@@ -629,6 +819,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
 // i/64, so the 4 ballots are the 32 descriptor bytes, LSB-first as
 // ComputeOrbDescriptor packs them.
 // --------------------------------------------------------------------------
+constexpr int kRawW = 36, kRawH = 31;   // 31x31 patch + dword alignment slack
+constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slack
+constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
+
 __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
                                                   const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur,
@@ -636,8 +830,11 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
                                                   const int* __restrict__ oct_count,
                                                   float* __restrict__ angle_out,
                                                   uint64_t* __restrict__ desc_out, int n_img) {
-  const int lane = threadIdx.x & 63;
-  const long gidx = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[4 * ((kDescLds + 15) & ~15)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* raw = lds_all + wave * ((kDescLds + 15) & ~15);
+  uint8_t* blp = raw + kRawW * kRawH;
+  const long gidx = (long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
   if (gidx >= (long)n_img * P->kp_slots) return;  // wave-uniform
   const int img = (int)(gidx / P->kp_slots);
   const int slot = (int)(gidx - (long)img * P->kp_slots);
@@ -649,21 +846,61 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   const uint32_t kp = oct_out[(size_t)img * P->kp_slots + slot];
   const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
 
-  // IC_Angle: lanes 0..61 -> (column u, half), rows -15..0 / 1..15.
+  // Stage both patches with independent dword loads (one memory round trip).
   int sp;
   const uint8_t* img0 = level_plane(P, src, pyr, img, l, sp);
-  int m10 = 0, m01 = 0;
-  if (lane < 62) {
-    const int u = lane % 31 - 15, half = lane / 31;
-    const int au = u < 0 ? -u : u;
-    const int vb = half ? 1 : -15, ve = half ? 15 : 0;
-    for (int v = vb; v <= ve; ++v) {
-      const int av = v < 0 ? -v : v;
-      if (au <= P->umax[av]) {
-        const int val = img0[(size_t)(cy + v) * sp + cx + u];
-        m10 += u * val;
-        m01 += v * val;
+  const uint8_t* B = blur + (size_t)img * P->blur_bytes + g.blur_off;
+  const int rx0 = (cx - 15) & ~3, bx0 = (cx - 18) & ~3;
+  const uint8_t* rsrc = img0 + (size_t)(cy - 15) * sp + rx0;
+  const uint8_t* bsrc = B + (size_t)(cy - 18) * g.pitch + bx0;
+  constexpr int nr = kRawH * (kRawW / 4), nb = kBlurH * (kBlurW / 4);
+  if (((((uintptr_t)img0) | (uintptr_t)sp) & 3) == 0) {
+    uint32_t v[(nr + nb + 63) / 64];
+#pragma unroll
+    for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
+      const int i = min(64 * u + lane, nr + nb - 1);
+      if (i < nr) {
+        const int r = i / (kRawW / 4), q = i - r * (kRawW / 4);
+        v[u] = *reinterpret_cast<const uint32_t*>(rsrc + (size_t)r * sp + 4 * q);
+      } else {
+        const int j = i - nr, r = j / (kBlurW / 4), q = j - r * (kBlurW / 4);
+        v[u] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * g.pitch + 4 * q);
       }
+    }
+#pragma unroll
+    for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
+      const int i = 64 * u + lane;
+      if (i < nr + nb) reinterpret_cast<uint32_t*>(raw)[i] = v[u];
+    }
+  } else {
+    for (int i = lane; i < kRawH * kRawW; i += 64) {
+      const int r = i / kRawW, q = i - r * kRawW;
+      raw[i] = rsrc[(size_t)r * sp + q];
+    }
+    for (int i = lane; i < nb; i += 64) {
+      const int r = i / (kBlurW / 4), q = i - r * (kBlurW / 4);
+      reinterpret_cast<uint32_t*>(blp)[i] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * g.pitch + 4 * q);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // IC_Angle: lanes 0..61 -> (column u, half); rows -15..0 / 1..15.
+  int m10 = 0, m01 = 0;
+  {
+    const int ln = min(lane, 61);
+    const int u = ln % 31 - 15, half = ln / 31;
+    const int au = u < 0 ? -u : u;
+    const uint8_t* colp = raw + 15 * kRawW + (cx - rx0) + u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int v = half ? k + 1 : k - 15;
+      const int av = v < 0 ? -v : v;
+      const int val = colp[min(v, 15) * kRawW];
+      const bool in = lane < 62 && v <= 15 && au <= kUmax[min(av, 15)];
+      m10 += in ? u * val : 0;
+      m01 += in ? v * val : 0;
     }
   }
 #pragma unroll
@@ -675,9 +912,7 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
 
   const float ang = angle * (float)(3.14159265358979323846 / 180.0);
   const float a = dev_cosf(ang), b = dev_sinf(ang);
-  const uint8_t* B = blur + (size_t)img * P->blur_bytes + g.blur_off;
-  const uint8_t* ctr = B + (size_t)cy * g.w + cx;
-  const int step = g.w;
+  const uint8_t* ctr = blp + 18 * kBlurW + (cx - bx0);
   uint64_t words[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
@@ -687,7 +922,7 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
     const int q0 = dev_round(__builtin_fmaf(x0, a, -(y0 * b)));
     const int r1 = dev_round(__builtin_fmaf(x1, b, y1 * a));
     const int q1 = dev_round(__builtin_fmaf(x1, a, -(y1 * b)));
-    const int t0 = ctr[r0 * step + q0], t1 = ctr[r1 * step + q1];
+    const int t0 = ctr[r0 * kBlurW + q0], t1 = ctr[r1 * kBlurW + q1];
     words[w] = __ballot(t0 < t1);
   }
   const size_t o = (size_t)img * P->kp_slots + slot;
@@ -812,14 +1047,14 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   mark(0);
   for (int l = 1; l < H.levels; ++l) {
     const LevelGeom& g = H.lev[l];
-    dim3 grid((g.w + 255) / 256, (g.h + 3) / 4, n), block(64, 4);
-    hipLaunchKernelGGL(k_resize, grid, block, 0, st, a.plan, a.rs_tab, src, a.pyr, l);
+    dim3 grid(g.rs_tiles_x, g.rs_tiles_y, n);
+    hipLaunchKernelGGL(k_resize, grid, dim3(256), H.rs_lds, st, a.plan, a.rs_tab, src, a.pyr, l);
   }
   mark(1);
   hipLaunchKernelGGL(k_blur, dim3(n * H.blur_tiles), dim3(256), 0, st, a.plan, src,
                      (const uint8_t*)a.pyr, a.blur);
   mark(2);
-  hipLaunchKernelGGL(k_fast_cells, dim3(n * H.n_cells), dim3(64), 2 * H.max_roi, st, a.plan,
+  hipLaunchKernelGGL(k_fast_cells, dim3(n * H.n_cells), dim3(64), H.max_roi_lds, st, a.plan,
                      a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count);
   mark(3);
   hipLaunchKernelGGL(k_octree, dim3(n * H.levels), dim3(kOctThreads), a.octree_lds, st, a.plan,

@@ -76,7 +76,8 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
 
   out.cells.clear();
   out.rs_tab.clear();
-  int pyr = 0, blur = 0, slots = 0, kps = 0, tiles = 0, max_roi = 0, node_cap = 64;
+  int pyr = 0, blur = 0, slots = 0, kps = 0, tiles = 0, max_roi = 0, node_cap = 64, rs_lds = 0;
+  int max_roi_lds = 0;
   for (int l = 0; l < L; ++l) {
     LevelGeom& g = P.lev[l];
     g.w = cv_round((float)W * out.inv_scale[l]);  // :1096
@@ -85,10 +86,11 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
     g.patch_size = (float)(int)(kPatchSize * out.scale[l]);
     if (g.w - 2 * kFastBorder < 35 || g.h - 2 * kFastBorder < 35)
       return why = "pyramid level too small for the FAST grid", false;
+    g.pitch = (g.w + kLevelAlign - 1) / kLevelAlign * kLevelAlign;
     g.pyr_off = l == 0 ? -1 : pyr;
-    if (l > 0) pyr += g.w * g.h;
+    if (l > 0) pyr += g.pitch * g.h;
     g.blur_off = blur;
-    blur += g.w * g.h;
+    blur += g.pitch * g.h;
     g.blur_tile_begin = tiles;
     g.tiles_x = (g.w + kBlurTileW - 1) / kBlurTileW;
     g.tiles_y = (g.h + kBlurTileH - 1) / kBlurTileH;
@@ -109,7 +111,8 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
           g.xmax = std::min(g.xmax, dx);
           if (sx >= s.w - 1) fx = 0.f, sx = s.w - 1;
         }
-        const short a0 = sat_short((1.f - fx) * 2048), a1 = sat_short(fx * 2048);
+        short a0 = sat_short((1.f - fx) * 2048), a1 = sat_short(fx * 2048);
+        if (dx >= g.xmax) a0 = 2048, a1 = 0;  // single-tap columns: S[sx] * ONE
         out.rs_tab.push_back(sx);
         out.rs_tab.push_back((int)(uint16_t)a0 | ((int)(uint16_t)a1 << 16));
       }
@@ -123,6 +126,24 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         out.rs_tab.push_back(r0 | (r1 << 16));
         out.rs_tab.push_back((int)(uint16_t)b0 | ((int)(uint16_t)b1 << 16));
       }
+      // largest source window of a kResizeTileW x kResizeTileH output tile
+      g.rs_tiles_x = (g.w + kResizeTileW - 1) / kResizeTileW;
+      g.rs_tiles_y = (g.h + kResizeTileH - 1) / kResizeTileH;
+      g.rs_src_cols = 0;
+      g.rs_src_rows = 0;
+      const int* tab = out.rs_tab.data();
+      for (int tx = 0; tx < g.rs_tiles_x; ++tx) {
+        const int xa = tx * kResizeTileW, xb = std::min(xa + kResizeTileW, g.w) - 1;
+        const int c0 = tab[g.rs_x + 2 * xa] & ~15;
+        const int c1 = std::min(tab[g.rs_x + 2 * xb] + 1, s.w - 1) | 15;  // same as k_resize
+        g.rs_src_cols = std::max(g.rs_src_cols, c1 - c0 + 1);
+      }
+      for (int ty = 0; ty < g.rs_tiles_y; ++ty) {
+        const int ya = ty * kResizeTileH, yb = std::min(ya + kResizeTileH, g.h) - 1;
+        const int r0 = tab[g.rs_y + 2 * ya] & 0xffff, r1 = tab[g.rs_y + 2 * yb] >> 16;
+        g.rs_src_rows = std::max(g.rs_src_rows, r1 - r0 + 1);
+      }
+      rs_lds = std::max(rs_lds, g.rs_src_cols * g.rs_src_rows);
       int x = 0;
       for (; x <= g.w - 16; x += 16) {
       }
@@ -161,6 +182,9 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
         slots += c.slot_cap;
         max_roi = std::max(max_roi, c.cols * c.rows);
+        max_roi_lds = std::max(max_roi_lds, fast_cell_lds_bytes(c.cols, c.rows));
+        if (dw > 0 && dh > 0 && dw * dh * dw >= (1 << 19))
+          return why = "FAST cell too large for the magic division", false;
         out.cells.push_back(c);
       }
     }
@@ -187,9 +211,22 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   P.node_cap = (node_cap + 63) & ~63;
   P.blur_tiles = tiles;
   P.max_roi = (max_roi + 15) & ~15;
+  P.max_roi_lds = (max_roi_lds + 15) & ~15;
+  P.rs_lds = (rs_lds + 15) & ~15;
+  if (P.rs_lds > 64 * 1024) return why = "scale factor too large for the resize tile", false;
+  if (P.max_roi_lds > 64 * 1024) return why = "FAST cell too large", false;
   if (P.kp_slots > 4096) return why = "too many keypoints per image for the assembly kernel", false;
   if (octree_lds_bytes(P) > 160 * 1024) return why = "num_features too large for the octree LDS", false;
   return true;
+}
+
+// LDS of one FAST cell wave (k_fast_cells): ROI staged with 4-aligned rows
+// (+3 lead bytes), a byte score map of the detection area and a u16
+// survivor list.
+int fast_cell_lds_bytes(int cols, int rows) {
+  const int ls = (cols + 3 + 3) & ~3;
+  const int nd = std::max(cols - 6, 0) * std::max(rows - 6, 0);
+  return ((ls * rows + 15) & ~15) + ((nd + 15) & ~15) + 2 * nd + 16;
 }
 
 size_t octree_lds_bytes(const PlanHeader& P) {

@@ -14,6 +14,7 @@ constexpr int kPatchSize = 31;      // :72
 
 struct LevelGeom {
   int w, h;          // level size: cvRound(W * inv_scale), cvRound(H * inv_scale)  (:1096)
+  int pitch;         // row pitch of the pyramid / blurred planes (w rounded up to 16)
   int pyr_off;       // byte offset of this level in an image's pyramid block (levels >= 1)
   int blur_off;      // byte offset in an image's blurred block (all levels)
   float scale;       // scale_factors_[l]
@@ -21,6 +22,8 @@ struct LevelGeom {
   // resize tables (levels >= 1), offsets into Plan::rs_tab
   int rs_x, rs_y;    // xofs|alpha pairs, yofs|beta pairs
   int xmax;          // first dst column whose right neighbour is out of range
+  int rs_tiles_x, rs_tiles_y;  // resize tiles (kResizeTileW x kResizeTileH outputs)
+  int rs_src_cols, rs_src_rows;  // largest source window of a tile (LDS staging)
   int vec16_end;     // VResizeLinearVec_32s8u: 16-lane blocks end here
   int vec8_end;      //                          8-lane blocks end here
   // FAST grid (:748-825)
@@ -34,7 +37,7 @@ struct LevelGeom {
   int rel_w, rel_h;  // max_x - min_x, max_y - min_y
   int out_off;       // first output slot of this level in an image's keypoint block
   int out_cap;       // node-count bound: max(budget + 3, 4 * n_roots)
-  // blur tiling
+  // blur tiling (kBlurTileW x kBlurTileH outputs per 256-thread block)
   int blur_tile_begin, tiles_x, tiles_y;
 };
 
@@ -57,10 +60,14 @@ struct PlanHeader {
   int node_cap;     // LDS node capacity used by the octree kernel
   int blur_tiles;   // per image
   int max_roi;      // largest cell ROI (bytes)
+  int max_roi_lds;  // LDS bytes of one FAST cell (staged ROI + score map + lists)
+  int rs_lds;       // LDS bytes of one resize tile
   int umax[16];     // circular patch extents (:452-464)
   LevelGeom lev[kMaxLevels];
 };
 
-constexpr int kBlurTileW = 64, kBlurTileH = 16;
+constexpr int kBlurTileW = 256, kBlurTileH = 32;    // 64 threads x 4 cols, 4 strips x 8 rows
+constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 256 threads x (4 rows x 8 px)
+constexpr int kLevelAlign = 16;
 
 }  // namespace orbgpu

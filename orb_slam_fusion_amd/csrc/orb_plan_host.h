@@ -21,5 +21,6 @@ void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::ve
                   std::vector<int>& feats_per_level);
 bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out, std::string& why);
 size_t octree_lds_bytes(const PlanHeader& P);
+int fast_cell_lds_bytes(int cols, int rows);
 
 }  // namespace orbgpu

@@ -127,9 +127,6 @@ __device__ __forceinline__ int block_sum_i(int v, int* red) {
 struct PoseShared {
   double red[4 * 27];
   int ired[4];
-  Se3 T, Tnew;
-  double x[6];
-  int ok;
 };
 
 // Robust chi2 of the active (level-0) edges at pose T.
@@ -247,26 +244,28 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       double rho = 0;
       int q = 0;
       do {
-        if (t == 0) {
-          double A[36], x[6], bb[6];
+        // every lane solves the (identical) 6x6 system: no broadcast barrier
+        double A[6][6], bb[6], x[6];
+        {
           int hk = 0;
+#pragma unroll
           for (int r = 0; r < 6; ++r) {
-            for (int c2 = 0; c2 <= r; ++c2) A[r * 6 + c2] = A[c2 * 6 + r] = hb[hk++];
+#pragma unroll
+            for (int c2 = 0; c2 <= r; ++c2) A[r][c2] = A[c2][r] = hb[hk++];
             bb[r] = hb[21 + r];
           }
-          for (int j = 0; j < 6; ++j) A[j * 6 + j] += lambda;
-          sh.ok = ldlt6_solve(A, bb, x) ? 1 : 0;
-          for (int j = 0; j < 6; ++j) sh.x[j] = x[j];
-          sh.Tnew = se3_compose(se3_exp(x), T);
         }
-        __syncthreads();
-        const Se3 Tn = sh.Tnew;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) A[j][j] += lambda;
+        const bool ok = ldlt6_solve(A, bb, x);
+        const Se3 Tn = se3_compose(se3_exp(x), T);
         double tmp = active_chi(obs, level, n, Tn, cam, robust, dmono, dstereo, sh);
         Teval = Tn;
-        if (!sh.ok) tmp = 1.79769313486231570815e+308;
+        if (!ok) tmp = 1.79769313486231570815e+308;
         rho = cur - tmp;
         double scale = 0;
-        for (int j = 0; j < 6; ++j) scale += sh.x[j] * (lambda * sh.x[j] + hb[21 + j]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + hb[21 + j]);
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && isfinite(tmp)) {
@@ -281,7 +280,6 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
           ni *= 2;
         }
         ++q;
-        __syncthreads();
       } while (rho < 0 && q < 10);
       if (q == 10 || rho == 0) break;
       if ((ini - cur) * 1e3 < ini)

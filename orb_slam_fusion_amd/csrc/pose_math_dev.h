@@ -69,16 +69,22 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
   const double O[3][3] = {{0, -w2, w1}, {w2, 0, -w0}, {-w1, w0, 0}};
   double O2[3][3];
+#pragma unroll
   for (int i = 0; i < 3; ++i)
+#pragma unroll
     for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
   double R[3][3], V[3][3];
   if (theta < 0.00001) {
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j) R[i][j] = V[i][j] = (i == j ? 1.0 : 0.0) + O[i][j] + O2[i][j];
   } else {
     const double s = sin(theta), c = cos(theta);
     const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / pow(theta, 3);
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j) {
         const double I = i == j ? 1.0 : 0.0;
         R[i][j] = I + a * O[i][j] + b * O2[i][j];
@@ -86,6 +92,7 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
       }
   }
   Se3 e{0, 0, 0, 1, {0, 0, 0}};
+  // Eigen quaternionbase_assign_impl, the three pivot cases written out
   double t = R[0][0] + R[1][1] + R[2][2];
   if (t > 0) {
     t = sqrt(t + 1.0);
@@ -94,97 +101,149 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
     e.qx = (R[2][1] - R[1][2]) * t;
     e.qy = (R[0][2] - R[2][0]) * t;
     e.qz = (R[1][0] - R[0][1]) * t;
-  } else {
-    int i = 0;
-    if (R[1][1] > R[0][0]) i = 1;
-    if (R[2][2] > R[i][i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double c[3];
-    t = sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
-    c[i] = 0.5 * t;
+  } else if (R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0])) {  // i = 2, j = 0, k = 1
+    t = sqrt(R[2][2] - R[0][0] - R[1][1] + 1.0);
+    e.qz = 0.5 * t;
     t = 0.5 / t;
-    e.qw = (R[k][j] - R[j][k]) * t;
-    c[j] = (R[j][i] + R[i][j]) * t;
-    c[k] = (R[k][i] + R[i][k]) * t;
-    e.qx = c[0];
-    e.qy = c[1];
-    e.qz = c[2];
+    e.qw = (R[1][0] - R[0][1]) * t;
+    e.qx = (R[0][2] + R[2][0]) * t;
+    e.qy = (R[1][2] + R[2][1]) * t;
+  } else if (R[1][1] > R[0][0]) {  // i = 1, j = 2, k = 0
+    t = sqrt(R[1][1] - R[2][2] - R[0][0] + 1.0);
+    e.qy = 0.5 * t;
+    t = 0.5 / t;
+    e.qw = (R[0][2] - R[2][0]) * t;
+    e.qz = (R[2][1] + R[1][2]) * t;
+    e.qx = (R[0][1] + R[1][0]) * t;
+  } else {  // i = 0, j = 1, k = 2
+    t = sqrt(R[0][0] - R[1][1] - R[2][2] + 1.0);
+    e.qx = 0.5 * t;
+    t = 0.5 / t;
+    e.qw = (R[2][1] - R[1][2]) * t;
+    e.qy = (R[1][0] + R[0][1]) * t;
+    e.qz = (R[2][0] + R[0][2]) * t;
   }
+#pragma unroll
   for (int i = 0; i < 3; ++i) e.t[i] = V[i][0] * u[3] + V[i][1] * u[4] + V[i][2] * u[5];
   se3_normalize(e);
   return e;
 }
 
-// Eigen::LDLT of the 6x6 row-major A (lower triangle read), solve A x = b.
-// Returns isPositive() (no negative pivot).
-__device__ __forceinline__ bool ldlt6_solve(double* A, const double* b, double* x) {
-  constexpr int n = 6;
-  int perm[n];
-  double temp[n];
+// Symmetric transposition k <-> p (p > k) touching the lower triangle only,
+// as Eigen's LDLT does.  K and Pp are compile-time after unrolling.
+__device__ __forceinline__ void ldlt_swap(double (&A)[6][6], int k, int pp) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    if (j < k) {
+      const double s = A[k][j];
+      A[k][j] = A[pp][j];
+      A[pp][j] = s;
+    }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    if (i > pp) {
+      const double s = A[i][k];
+      A[i][k] = A[i][pp];
+      A[i][pp] = s;
+    }
+  {
+    const double s = A[k][k];
+    A[k][k] = A[pp][pp];
+    A[pp][pp] = s;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    if (i > k && i < pp) {
+      const double s = A[i][k];
+      A[i][k] = A[pp][i];
+      A[pp][i] = s;
+    }
+}
+
+// Eigen::LDLT of A (lower triangle read; pivot on the not-yet-updated
+// diagonal), then solve A x = b.  Every index is static after unrolling, so A
+// stays in registers.  Returns isPositive() (no negative pivot).
+__device__ __forceinline__ bool ldlt6_solve(double (&A)[6][6], const double (&b)[6],
+                                            double (&x)[6]) {
+  int perm[6];
   bool neg = false;
-  for (int k = 0; k < n; ++k) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
     int p = k;
-    double big = fabs(A[k * n + k]);
-    for (int i = k + 1; i < n; ++i)
-      if (fabs(A[i * n + i]) > big) big = fabs(A[i * n + i]), p = i;
+    double big = fabs(A[k][k]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      if (i > k && fabs(A[i][i]) > big) {
+        big = fabs(A[i][i]);
+        p = i;
+      }
     perm[k] = p;
-    if (p != k) {
-      for (int j = 0; j < k; ++j) {
-        const double s = A[k * n + j];
-        A[k * n + j] = A[p * n + j];
-        A[p * n + j] = s;
-      }
-      for (int i = p + 1; i < n; ++i) {
-        const double s = A[i * n + k];
-        A[i * n + k] = A[i * n + p];
-        A[i * n + p] = s;
-      }
-      const double s = A[k * n + k];
-      A[k * n + k] = A[p * n + p];
-      A[p * n + p] = s;
-      for (int i = k + 1; i < p; ++i) {
-        const double s2 = A[i * n + k];
-        A[i * n + k] = A[p * n + i];
-        A[p * n + i] = s2;
-      }
-    }
+#pragma unroll
+    for (int pp = 0; pp < 6; ++pp)
+      if (pp > k && p == pp) ldlt_swap(A, k, pp);
     if (k > 0) {
+      double temp[6];
       double acc = 0;
-      for (int j = 0; j < k; ++j) {
-        temp[j] = A[j * n + j] * A[k * n + j];
-        acc += A[k * n + j] * temp[j];
-      }
-      A[k * n + k] -= acc;
-      for (int i = k + 1; i < n; ++i) {
-        double s = 0;
-        for (int j = 0; j < k; ++j) s += A[i * n + j] * temp[j];
-        A[i * n + k] -= s;
-      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (j < k) {
+          temp[j] = A[j][j] * A[k][j];
+          acc += A[k][j] * temp[j];
+        }
+      A[k][k] -= acc;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        if (i > k) {
+          double sacc = 0;
+#pragma unroll
+          for (int j = 0; j < 6; ++j)
+            if (j < k) sacc += A[i][j] * temp[j];
+          A[i][k] -= sacc;
+        }
     }
-    const double akk = A[k * n + k];
-    if (fabs(akk) > 0)
-      for (int i = k + 1; i < n; ++i) A[i * n + k] /= akk;
+    const double akk = A[k][k];
+    if (fabs(akk) > 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        if (i > k) A[i][k] /= akk;
+    }
     if (akk < 0) neg = true;
   }
-  for (int i = 0; i < n; ++i) x[i] = b[i];
-  for (int k = 0; k < n; ++k) {
-    const double s = x[k];
-    x[k] = x[perm[k]];
-    x[perm[k]] = s;
-  }
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < i; ++j) x[i] -= A[i * n + j] * x[j];
-  for (int i = 0; i < n; ++i) {
-    const double d = A[i * n + i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = b[i];
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+#pragma unroll
+    for (int pp = 0; pp < 6; ++pp)
+      if (pp > k && perm[k] == pp) {
+        const double s = x[k];
+        x[k] = x[pp];
+        x[pp] = s;
+      }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (j < i) x[i] -= A[i][j] * x[j];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double d = A[i][i];
     x[i] = fabs(d) > 1.0 / 1.79769313486231570815e+308 ? x[i] / d : 0.0;
   }
-  for (int i = n - 1; i >= 0; --i)
-    for (int j = i + 1; j < n; ++j) x[i] -= A[j * n + i] * x[j];
-  for (int k = n - 1; k >= 0; --k) {
-    const double s = x[k];
-    x[k] = x[perm[k]];
-    x[perm[k]] = s;
-  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (j > i) x[i] -= A[j][i] * x[j];
+#pragma unroll
+  for (int k = 5; k >= 0; --k)
+#pragma unroll
+    for (int pp = 0; pp < 6; ++pp)
+      if (pp > k && perm[k] == pp) {
+        const double s = x[k];
+        x[k] = x[pp];
+        x[pp] = s;
+      }
   return !neg;
 }
 
