@@ -168,39 +168,40 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
 // --------------------------------------------------------------------------
 // k_blur: GaussianBlur 7x7, sigma 2, BORDER_REFLECT_101, bit-exact fixed point
 // (SURVEY Appendix A.3): Q8 taps [18 34 48 56 48 34 18], horizontal sums kept
-// exact, (sum + 2^15) >> 16 once.  Each thread owns 4 adjacent columns and
-// slides a 7-row register window down a 16-row strip (3 dword loads per source
-// row in the interior); a 256-thread block covers 256 x 64 outputs and one
-// launch covers every level of every image.
+// exact, (sum + 2^15) >> 16 once.  Interior: each thread owns 4 adjacent
+// columns x 8 rows (3 dword loads per source row, dot4/dot2 taps); a 256-thread
+// block covers 256 x 32 outputs and one launch covers every level of every
+// image.  Edge lanes rebuild their reflected window with
+// v_perm_b32 (see k_blur), so no wave runs a separate border path.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int reflect101(int i, int n) {
   i = i < 0 ? -i : i;
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-__device__ __forceinline__ int hsum7(int a, int b, int c, int d, int e, int f, int g) {
-  return 18 * (a + g) + 34 * (b + f) + 48 * (c + e) + 56 * d;
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ ushort2_t as_us2(uint32_t v) {
+  return __builtin_bit_cast(ushort2_t, v);
 }
 
-template <int R>
-__device__ __forceinline__ void blur_emit(const int (&hw)[R + 6][4], uint8_t* D, int ys, int h,
-                                          int pitch, int nvalid) {
+// Every lane owns output columns x..x+3 (x = 4k) of R rows.  It loads the 12
+// source bytes x-4..x+7 of each row as 3 dwords from an in-row offset clamped
+// to [0, w-12]; lanes at the left/right edge (x = 0, x > w-8) rebuild the
+// reflect-101 window from those bytes with v_perm_b32 and per-lane selectors.
+// Only waves holding an edge lane take that (wave-uniform) branch, and the
+// arithmetic after it is the same for every lane: no divergent border path.
+__device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t (&lo)[3],
+                                                uint32_t (&hi)[3]) {
 #pragma unroll
-  for (int o = 0; o < R; ++o) {
-    if (ys + o < h) {
-      uint32_t packed = 0;
+  for (int v = 0; v < 3; ++v) {
+    lo[v] = 0;
+    hi[v] = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t v = 18u * (hw[o][j] + hw[o + 6][j]) + 34u * (hw[o + 1][j] + hw[o + 5][j]) +
-                           48u * (hw[o + 2][j] + hw[o + 4][j]) + 56u * hw[o + 3][j];
-        packed |= min((v + (1u << 15)) >> 16, 255u) << (8 * j);
-      }
-      uint8_t* out = D + (size_t)(ys + o) * pitch;
-      if (nvalid >= 4) {
-        *reinterpret_cast<uint32_t*>(out) = packed;
-      } else {
-        for (int j = 0; j < nvalid; ++j) out[j] = (uint8_t)(packed >> (8 * j));
-      }
+    for (int b = 0; b < 4; ++b) {
+      const int idx = reflect101(x - 4 + 4 * v + b, w) - base;  // 0..11
+      lo[v] |= (uint32_t)(idx < 8 ? idx : 0x0c) << (8 * b);      // 0x0c selects 0x00
+      hi[v] |= (uint32_t)(idx < 8 ? 0x0c : idx - 8) << (8 * b);
     }
   }
 }
@@ -208,7 +209,7 @@ __device__ __forceinline__ void blur_emit(const int (&hw)[R + 6][4], uint8_t* D,
 __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
-  constexpr int R = 8;  // rows per thread
+  constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
   const int wid = xcd_remap(blockIdx.x, gridDim.x);
   const int img = wid / P->blur_tiles;
   int t = wid - img * P->blur_tiles;
@@ -218,49 +219,79 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
   t -= g.blur_tile_begin;
   const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
   const int x = tx * kBlurTileW + 4 * (threadIdx.x & 63);
-  const int ys = ty * kBlurTileH + R * (threadIdx.x >> 6);
+  // wave-uniform row origin: row addressing and row bounds stay scalar
+  const int ys = ty * kBlurTileH + R * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (x >= g.w || ys >= g.h) return;
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
-  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + x;
-  int hw[R + 6][4];
-  if (x >= 4 && x + 8 <= g.w && ((((uintptr_t)S) | (uintptr_t)sp) & 3) == 0) {
-    // interior: 3 dword loads per source row, all issued before any use
-    uint32_t d[R + 6][3];
+  const uint32_t base = (uint32_t)min(max(x - 4, 0), g.w - 12);
+  // 3 dword loads per source row (unaligned only when the level-0 stride is),
+  // all issued before any use
+  uint32_t d[R + 6][3];
+#pragma unroll
+  for (int r = 0; r < R + 6; ++r) {
+    const uint8_t* row = S + (uint32_t)(reflect101(ys - 3 + r, g.h) * sp);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d[r][k] = *reinterpret_cast<const uint32_t*>(row + base + 4 * k);
+  }
+  if (__builtin_amdgcn_ballot_w64((int)base != x - 4)) {
+    uint32_t lo[3], hi[3];
+    blur_window_sel(x, g.w, (int)base, lo, hi);
 #pragma unroll
     for (int r = 0; r < R + 6; ++r) {
-      const uint8_t* row = S + (size_t)reflect101(ys - 3 + r, g.h) * sp + x - 4;
-      d[r][0] = reinterpret_cast<const uint32_t*>(row)[0];
-      d[r][1] = reinterpret_cast<const uint32_t*>(row)[1];
-      d[r][2] = reinterpret_cast<const uint32_t*>(row)[2];
-    }
+      uint32_t v[3];
 #pragma unroll
-    for (int r = 0; r < R + 6; ++r) {
-      const int b[10] = {(int)((d[r][0] >> 8) & 255), (int)((d[r][0] >> 16) & 255), (int)(d[r][0] >> 24),
-                         (int)(d[r][1] & 255), (int)((d[r][1] >> 8) & 255), (int)((d[r][1] >> 16) & 255),
-                         (int)(d[r][1] >> 24), (int)(d[r][2] & 255), (int)((d[r][2] >> 8) & 255),
-                         (int)((d[r][2] >> 16) & 255)};
+      for (int k = 0; k < 3; ++k)
+        v[k] = __builtin_amdgcn_perm(d[r][1], d[r][0], lo[k]) |
+               __builtin_amdgcn_perm(d[r][2], d[r][2], hi[k]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        hw[r][j] = hsum7(b[j], b[j + 1], b[j + 2], b[j + 3], b[j + 4], b[j + 5], b[j + 6]);
-    }
-  } else {
-    // image borders / unaligned source: byte gathers with reflect-101 columns
-    int cx[10];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) cx[j] = reflect101(min(x - 3 + j, g.w + 2), g.w);
-#pragma unroll
-    for (int r = 0; r < R + 6; ++r) {
-      const uint8_t* row = S + (size_t)reflect101(ys - 3 + r, g.h) * sp;
-      int b[10];
-#pragma unroll
-      for (int j = 0; j < 10; ++j) b[j] = row[cx[j]];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        hw[r][j] = hsum7(b[j], b[j + 1], b[j + 2], b[j + 3], b[j + 4], b[j + 5], b[j + 6]);
+      for (int k = 0; k < 3; ++k) d[r][k] = v[k];
     }
   }
-  blur_emit<R>(hw, D, ys, g.h, g.pitch, g.w - x);
+  // horizontal taps: two v_dot4_u32_u8 per output on windows cut by alignbyte;
+  // sums are <= 65280, so row pairs pack into one dword for the vertical dot2s
+  const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
+  const uint32_t K1 = 48u | (34u << 8) | (18u << 16);
+  uint32_t hw[R + 6][4];
+#pragma unroll
+  for (int r = 0; r < R + 6; ++r) {
+    const uint32_t lo[4] = {__builtin_amdgcn_alignbyte(d[r][1], d[r][0], 1),
+                            __builtin_amdgcn_alignbyte(d[r][1], d[r][0], 2),
+                            __builtin_amdgcn_alignbyte(d[r][1], d[r][0], 3), d[r][1]};
+    const uint32_t hi[4] = {__builtin_amdgcn_alignbyte(d[r][2], d[r][1], 1),
+                            __builtin_amdgcn_alignbyte(d[r][2], d[r][1], 2),
+                            __builtin_amdgcn_alignbyte(d[r][2], d[r][1], 3), d[r][2]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      hw[r][j] = __builtin_amdgcn_udot4(lo[j], K0, __builtin_amdgcn_udot4(hi[j], K1, 0u, false), false);
+  }
+  uint32_t pr[R + 5][4];  // pr[r] = hw[r] | hw[r+1] << 16
+#pragma unroll
+  for (int r = 0; r < R + 5; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pr[r][j] = hw[r][j] | (hw[r + 1][j] << 16);
+  // vertical taps (18,34)(48,56)(48,34)(18,0) as four v_dot2_u32_u16, the
+  // +2^15 rounding in the first accumulator; results < 2^24, so each output
+  // byte is byte 2 of its sum and two v_perm_b32 pack four of them.
+  const ushort2_t k01 = as_us2(18u | (34u << 16)), k23 = as_us2(48u | (56u << 16));
+  const ushort2_t k45 = as_us2(48u | (34u << 16)), k6 = as_us2(18u);
+  // columns past w land in the row's pitch padding (pitch is a multiple of 16)
+  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + (uint32_t)x;
+#pragma unroll
+  for (int o = 0; o < R; ++o) {
+    if (ys + o < g.h) {
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t a = __builtin_amdgcn_udot2(as_us2(pr[o][j]), k01, 1u << 15, false);
+        a = __builtin_amdgcn_udot2(as_us2(pr[o + 2][j]), k23, a, false);
+        a = __builtin_amdgcn_udot2(as_us2(pr[o + 4][j]), k45, a, false);
+        v[j] = __builtin_amdgcn_udot2(as_us2(hw[o + 6][j]), k6, a, false);
+      }
+      *reinterpret_cast<uint32_t*>(D + (uint32_t)((ys + o) * g.pitch)) =
+          __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
+    }
+  }
 }
 
 // --------------------------------------------------------------------------

@@ -66,7 +66,7 @@ struct PlanHeader {
   LevelGeom lev[kMaxLevels];
 };
 
-constexpr int kBlurTileW = 256, kBlurTileH = 32;    // 64 threads x 4 cols, 4 strips x 8 rows
+constexpr int kBlurTileW = 256, kBlurTileH = 64;    // 64 threads x 4 cols, 4 waves x 16 rows
 constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 256 threads x (4 rows x 8 px)
 constexpr int kLevelAlign = 16;
 
