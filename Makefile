@@ -28,4 +28,10 @@ oracle:
 clean:
 	rm -rf $(LIB) oracle/_build
 
-.PHONY: all oracle clean
+# profiling variant: per-phase s_memtime totals (orbgpu_debug_stamps)
+stamps: $(LIB)/liborbgpu_stamps.so
+$(LIB)/liborbgpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS -shared -o $@ $(GPU_SRCS)
+
+.PHONY: all oracle clean stamps

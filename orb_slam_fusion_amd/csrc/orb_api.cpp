@@ -36,6 +36,7 @@ void dfree(T*& p) {
 struct orbgpu_extractor {
   orbgpu_orb_params params{};
   int device = 0;
+  int n_cu = 256;
   hipStream_t stream = nullptr;
   int max_w = 0, max_h = 0, max_images = 0;
 
@@ -152,6 +153,7 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   ExtractLaunch a{};
   a.host_plan = &h->plan.hdr;
   a.plan = h->d_plan;
+  a.n_cu = h->n_cu;
   a.cells = h->d_cells;
   a.rs_tab = h->d_rs;
   a.imgs = imgs;
@@ -200,6 +202,9 @@ orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int devic
   h->max_w = max_width;
   h->max_h = max_height;
   h->max_images = max_images;
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      h->n_cu < 1)
+    h->n_cu = 256;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1) || dalloc(&h->d_nm, 2)) {
     orbgpu_extractor_destroy(h);

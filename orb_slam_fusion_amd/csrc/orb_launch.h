@@ -35,6 +35,7 @@ struct ExtractLaunch {
   int* n_out;
   int* mono_out;
   int* err;
+  int n_cu;            // compute units of the device (persistent grids)
   hipEvent_t* events;  // optional: kStages + 1 events recorded around the stages
 };
 
