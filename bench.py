@@ -132,11 +132,12 @@ def main() -> int:
     # concurrently (frame k's pose overlaps frame k+1's extraction in a
     # pipelined tracker; within a step the B frames are independent).
     s_ex = torch.cuda.Stream(dev)
-    s_pose = torch.cuda.Stream(dev)
+    s_pose = torch.cuda.Stream(dev, priority=-1)  # high-priority pool: its own HW queue
     pose_ev = []
 
     def step(timed: bool):
-        ex.extract_batch(d_imgs, d_kps, d_desc, d_n, d_mono, stream=s_ex)
+        # the pose kernel (64 long-lived blocks) is queued first so its blocks
+        # take their CUs before the extractor's wide grids fill the device
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -145,6 +146,7 @@ def main() -> int:
         if timed:
             e1.record(s_pose)
             pose_ev.append((e0, e1))
+        ex.extract_batch(d_imgs, d_kps, d_desc, d_n, d_mono, stream=s_ex)
 
     for _ in range(args.warmup):
         step(False)

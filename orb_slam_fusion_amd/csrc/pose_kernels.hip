@@ -17,6 +17,34 @@
 
 namespace orbgpu {
 
+// Profiling build only (make stamps): per-phase s_memtime totals, one flush
+// per wave at exit into 64 spread copies (see orb_kernels.hip).
+#ifdef ORB_STAMPS
+__device__ unsigned long long g_pose_stamps[64 * 16];
+#define PSTAMP_INIT                                            \
+  unsigned long long pst_acc_[16] = {};                        \
+  unsigned long long pst_prev_ = __builtin_amdgcn_s_memtime()
+#define PSTAMP(i)                                                     \
+  do {                                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+    pst_acc_[i] += now_ - pst_prev_;                                  \
+    pst_prev_ = now_;                                                 \
+  } while (0)
+#define PSTAMP_ADD(i, v) (pst_acc_[i] += (unsigned long long)(v))
+#define PSTAMP_END                                                                  \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_)                             \
+        if (pst_acc_[i_]) atomicAdd(&g_pose_stamps[(blockIdx.x & 63) * 16 + i_], pst_acc_[i_]); \
+    }                                                                               \
+  } while (0)
+#else
+#define PSTAMP_INIT (void)0
+#define PSTAMP(i) (void)0
+#define PSTAMP_ADD(i, v) (void)0
+#define PSTAMP_END (void)0
+#endif
+
 struct PoseObsDev {
   float Xw[3];
   float u, v, ur;
@@ -28,6 +56,7 @@ struct CamDev {
 };
 
 constexpr int kPoseThreads = 256;
+constexpr int kPoseWaves = kPoseThreads / 64;
 
 __device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3& T, const CamDev& c,
                                            double e[3], bool& stereo) {
@@ -94,24 +123,50 @@ __device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3& T,
   }
 }
 
-// Block-wide sum of NV doubles per thread (fixed tree: wave butterfly, then
-// the 4 wave partials in order).  Result broadcast to every thread.
+// DPP lane move of a double (two 32-bit halves); lanes whose source is out of
+// range or whose row is masked off read 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Wave sum with a fixed tree: in-row prefix by row_shr 1,2,4,8, then
+// row_bcast15 / row_bcast31 carry the row totals up; lane 63 holds the sum.
+__device__ __forceinline__ double wave_sum_to_lane63(double v) {
+  v += dpp_f64<0x111, 0xf>(v);
+  v += dpp_f64<0x112, 0xf>(v);
+  v += dpp_f64<0x114, 0xf>(v);
+  v += dpp_f64<0x118, 0xf>(v);
+  v += dpp_f64<0x142, 0xa>(v);
+  v += dpp_f64<0x143, 0xc>(v);
+  return v;
+}
+
+__device__ __forceinline__ double uniform_f64(double v) {  // wave-uniform value -> SGPRs
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(v)));
+}
+
+// Block-wide sum of NV doubles per thread (fixed tree: DPP wave sums, then the
+// wave partials in wave order).  Result broadcast to every thread.
 template <int NV>
 __device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double x = v[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    v[k] = x;
-  }
-  if (lane == 0)
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum_to_lane63(v[k]);
+  if (lane == 63)
 #pragma unroll
     for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = ((red[k] + red[NV + k]) + red[2 * NV + k]) + red[3 * NV + k];
+  for (int k = 0; k < NV; ++k) {
+    double a = red[k];
+#pragma unroll
+    for (int w = 1; w < kPoseWaves; ++w) a += red[w * NV + k];
+    v[k] = uniform_f64(a);
+  }
   __syncthreads();
 }
 
@@ -119,44 +174,65 @@ __device__ __forceinline__ int block_sum_i(int v, int* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  const int r = red[0] + red[1] + red[2] + red[3];
+  int r = 0;
+#pragma unroll
+  for (int w = 0; w < kPoseWaves; ++w) r += red[w];
   __syncthreads();
   return r;
 }
 
 struct PoseShared {
-  double red[4 * 27];
-  int ired[4];
+  double red[kPoseWaves * 28];
+  double hb[28];  // chi2, H (lower, 21), b (6) at the current pose
+  int ired[kPoseWaves];
 };
 
-// Robust chi2 of the active (level-0) edges at pose T.
-__device__ double active_chi(const PoseObsDev* __restrict__ obs, const uint8_t* level, int n,
-                             const Se3& T, const CamDev& c, bool robust, double dmono,
-                             double dstereo, PoseShared& sh) {
-  double acc[1] = {0.0};
-  for (int i = threadIdx.x; i < n; i += kPoseThreads) {
-    if (level[i]) continue;
-    const PoseObsDev o = obs[i];
-    double e[3];
-    bool st;
-    edge_error(o, T, c, e, st);
-    const double c2 = edge_chi2(e, (double)o.inv_sigma2, st);
-    if (robust) {
-      double r0, r1;
-      huber_rho(c2, st ? dstereo : dmono, r0, r1);
-      acc[0] += r0;
-    } else {
-      acc[0] += c2;
+constexpr int kPoseLdsObs = 4096;  // observations staged in LDS (the rest re-read from HBM)
+
+// One edge's contribution to a sweep at pose T: robust chi2 into acc[0] and
+// BlockSolver::buildSystem's H (lower triangle, 21) and b (6) into
+// acc[1..27].  Every sweep visits a thread's edges in the same order, so the
+// sums are reproducible.
+__device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3& T, const CamDev& cam,
+                                                bool robust, double dmono, double dstereo,
+                                                bool build, double (&acc)[28]) {
+  double e[3];
+  bool st;
+  edge_error(o, T, cam, e, st);
+  const double info = (double)o.inv_sigma2;
+  const double c2 = edge_chi2(e, info, st);
+  double w = 1.0;
+  if (robust) {
+    double r0;
+    huber_rho(c2, st ? dstereo : dmono, r0, w);
+    acc[0] += r0;
+  } else {
+    acc[0] += c2;
+  }
+  if (!build) return;
+  double J[3][6];
+  edge_jacobian(o, T, cam, st, J);
+  const double wi = w * info;
+  int hk = 1;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double g = J[0][r] * (info * e[0]) + J[1][r] * (info * e[1]);
+    if (st) g += J[2][r] * (info * e[2]);
+    acc[22 + r] -= w * g;
+#pragma unroll
+    for (int q = 0; q <= r; ++q) {
+      double h = (J[0][r] * wi) * J[0][q] + (J[1][r] * wi) * J[1][q];
+      if (st) h += (J[2][r] * wi) * J[2][q];
+      acc[hk++] += h;
     }
   }
-  block_sum_d<1>(acc, sh.red);
-  return acc[0];
 }
 
 __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     CamDev cam, const float* __restrict__ pose_in, const PoseObsDev* __restrict__ obs_all,
     const int* __restrict__ nobs, int obs_stride, float* __restrict__ pose_out,
-    uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d) {
+    uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d,
+    int lds_obs) {
   __shared__ PoseShared sh;
   const int p = blockIdx.x, t = threadIdx.x;
   const int n = nobs[p];
@@ -168,7 +244,17 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     if (t == 0) inliers[p] = 0;
     return;
   }
-  for (int i = t; i < n; i += kPoseThreads) level[i] = 0;
+  // observations (and their levels) live in LDS for the whole call: one
+  // HBM read; only n > cap falls back to re-reading per sweep
+  extern __shared__ __attribute__((aligned(16))) uint8_t pose_lds[];
+  const int cap = min(n, lds_obs);
+  PoseObsDev* ob = reinterpret_cast<PoseObsDev*>(pose_lds);
+  uint8_t* lv = pose_lds + (size_t)lds_obs * sizeof(PoseObsDev);
+  for (int i = t; i < cap; i += kPoseThreads) {
+    ob[i] = obs[i];
+    lv[i] = 0;
+  }
+  for (int i = cap + t; i < n; i += kPoseThreads) level[i] = 0;
   Se3 init{0, 0, 0, 1, {0, 0, 0}};
   init.qx = pin[0];
   init.qy = pin[1];
@@ -183,59 +269,100 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
   int nbad_round = 0;
   Se3 T = init;
   __syncthreads();
+  PSTAMP_INIT;
 
+  // computeActiveErrors at pose X (robust chi2, block-reduced).  A thread's
+  // edges i = t + 256 j are taken three at a time: their chains are
+  // independent (ILP), the accumulation stays in edge order.
+  constexpr int kU = 3;
+  auto chi_sweep = [&](const Se3& X) -> double {
+    double acc[28];
+    acc[0] = 0;
+    for (int i0 = t; i0 < cap; i0 += kU * kPoseThreads) {
+      PoseObsDev o[kU];
+      bool live[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * kPoseThreads;
+        live[u] = i < cap && !lv[min(i, cap - 1)];
+        o[u] = ob[min(i, cap - 1)];
+      }
+      double part[kU][28];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        part[u][0] = 0;
+        edge_accumulate(o[u], X, cam, robust, dmono, dstereo, false, part[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (live[u]) acc[0] += part[u][0];
+    }
+    for (int i = cap + t; i < n; i += kPoseThreads)
+      if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, false, acc);
+    double r[1] = {acc[0]};
+    block_sum_d<1>(r, sh.red);
+    return r[0];
+  };
+  // computeActiveErrors + buildSystem at pose X -> sh.hb (chi2, H, b)
+  auto build_sweep = [&](const Se3& X) {
+    double acc[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) acc[k] = 0;
+    for (int i0 = t; i0 < cap; i0 += kU * kPoseThreads) {
+      PoseObsDev o[kU];
+      bool live[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * kPoseThreads;
+        live[u] = i < cap && !lv[min(i, cap - 1)];
+        o[u] = ob[min(i, cap - 1)];
+      }
+      double part[kU][28];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+#pragma unroll
+        for (int k = 0; k < 28; ++k) part[u][k] = 0;
+        edge_accumulate(o[u], X, cam, robust, dmono, dstereo, true, part[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (live[u]) {
+          // g2o adds each edge's block into H/b in edge order; the chi2 term
+          // first as in computeActiveErrors
+          acc[0] += part[u][0];
+#pragma unroll
+          for (int k = 1; k < 28; ++k) acc[k] += part[u][k];
+        }
+    }
+    for (int i = cap + t; i < n; i += kPoseThreads)
+      if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
+    block_sum_d<28>(acc, sh.red);
+    if (t == 0)
+#pragma unroll
+      for (int k = 0; k < 28; ++k) sh.hb[k] = acc[k];
+    __syncthreads();
+  };
+
+  const double* hb = sh.hb;
   for (int it = 0; it < 4; ++it) {
     T = init;
-    Se3 Teval = init;
+    PSTAMP(0);
+    build_sweep(T);  // computeActiveErrors + buildSystem at the round's start
+    PSTAMP(1);
+    PSTAMP_ADD(8, 1);
+    double cur = hb[0];
+    Se3 Teval = T;
     double lambda = 0, ni = 2;
     int nbad = 0;
     for (int iter = 0; iter < 10; ++iter) {
-      // computeActiveErrors + activeRobustChi2 at T
-      double cur = active_chi(obs, level, n, T, cam, robust, dmono, dstereo, sh);
-      Teval = T;
       const double ini = cur;
-      // BlockSolver::buildSystem: H (lower triangle, 21) and b (6)
-      double hb[27];
-#pragma unroll
-      for (int k = 0; k < 27; ++k) hb[k] = 0;
-      for (int i = t; i < n; i += kPoseThreads) {
-        if (level[i]) continue;
-        const PoseObsDev o = obs[i];
-        double e[3];
-        bool st;
-        edge_error(o, T, cam, e, st);
-        const double info = (double)o.inv_sigma2;
-        double w = 1.0;
-        if (robust) {
-          double r0;
-          huber_rho(edge_chi2(e, info, st), st ? dstereo : dmono, r0, w);
-        }
-        double J[3][6];
-        edge_jacobian(o, T, cam, st, J);
-        const double wi = w * info;
-        const int d = st ? 3 : 2;
-        int hk = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          double g = J[0][r] * (info * e[0]) + J[1][r] * (info * e[1]);
-          if (d == 3) g += J[2][r] * (info * e[2]);
-          hb[21 + r] -= w * g;
-#pragma unroll
-          for (int q = 0; q <= r; ++q) {
-            double h = (J[0][r] * wi) * J[0][q] + (J[1][r] * wi) * J[1][q];
-            if (d == 3) h += (J[2][r] * wi) * J[2][q];
-            hb[hk++] += h;
-          }
-        }
-      }
-      block_sum_d<27>(hb, sh.red);
       if (iter == 0) {  // computeLambdaInit: tau * max diag
         double mx = 0;
         int dk = 0;
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
           dk += r;
-          mx = fmax(fabs(hb[dk + r]), mx);
+          mx = fmax(fabs(hb[1 + dk + r]), mx);
         }
         lambda = 1e-5 * mx;
         ni = 2;
@@ -243,29 +370,35 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       }
       double rho = 0;
       int q = 0;
+      bool accepted = false;
       do {
         // every lane solves the (identical) 6x6 system: no broadcast barrier
         double A[6][6], bb[6], x[6];
         {
-          int hk = 0;
+          int hk = 1;
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
 #pragma unroll
             for (int c2 = 0; c2 <= r; ++c2) A[r][c2] = A[c2][r] = hb[hk++];
-            bb[r] = hb[21 + r];
+            bb[r] = hb[22 + r];
           }
         }
 #pragma unroll
         for (int j = 0; j < 6; ++j) A[j][j] += lambda;
+        PSTAMP(0);
         const bool ok = ldlt6_solve(A, bb, x);
+        PSTAMP(2);
         const Se3 Tn = se3_compose(se3_exp(x), T);
-        double tmp = active_chi(obs, level, n, Tn, cam, robust, dmono, dstereo, sh);
+        PSTAMP(3);
+        double tmp = chi_sweep(Tn);
+        PSTAMP(4);
+        PSTAMP_ADD(9, 1);
         Teval = Tn;
         if (!ok) tmp = 1.79769313486231570815e+308;
         rho = cur - tmp;
         double scale = 0;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + hb[21 + j]);
+        for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + hb[22 + j]);
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && isfinite(tmp)) {
@@ -275,6 +408,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
           ni = 2;
           cur = tmp;
           T = Tn;
+          accepted = true;
         } else {
           lambda *= ni;
           ni *= 2;
@@ -287,26 +421,43 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       else
         nbad = 0;
       if (nbad >= 3) break;
+      // next iteration: its computeActiveErrors at T reproduces `cur` (the
+      // accepted trial's sweep at the same pose), so only buildSystem runs;
+      // after a rejected-but-terminal-free exit T is unchanged and so is the
+      // system already in sh.hb
+      PSTAMP(0);
+      if (accepted) {
+        build_sweep(T);
+        PSTAMP(1);
+        PSTAMP_ADD(8, 1);
+      }
     }
 
     // classify (optimizer.cc:966-1037): level-1 edges recompute at T, level-0
     // edges keep the error of the last sweep (at Teval)
     int bad = 0;
-    for (int i = t; i < n; i += kPoseThreads) {
-      const PoseObsDev o = obs[i];
+    auto classify = [&](const PoseObsDev& o, uint8_t& l) {
       double e[3];
       bool st;
-      edge_error(o, level[i] ? T : Teval, cam, e, st);
+      edge_error(o, l ? T : Teval, cam, e, st);
       const float chi2 = (float)edge_chi2(e, (double)o.inv_sigma2, st);
       const bool out = chi2 > (st ? 7.815f : 5.991f);
-      level[i] = out ? 1 : 0;
+      l = out ? 1 : 0;
       bad += out;
+    };
+    for (int i = t; i < cap; i += kPoseThreads) classify(ob[i], lv[i]);
+    for (int i = cap + t; i < n; i += kPoseThreads) {
+      uint8_t l = level[i];
+      classify(obs[i], l);
+      level[i] = l;
     }
     nbad_round = block_sum_i(bad, sh.ired);
+    PSTAMP(5);
     if (it == 2) robust = false;
     if (n < 10) break;
   }
 
+  for (int i = t; i < cap; i += kPoseThreads) level[i] = lv[i];
   if (t == 0) {
     const double o[7] = {T.qx, T.qy, T.qz, T.qw, T.t[0], T.t[1], T.t[2]};
     float f[7];
@@ -319,6 +470,8 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     for (int i = 0; i < 7; ++i) pose_out[7 * p + i] = f[i];
     inliers[p] = n - nbad_round;
   }
+  PSTAMP(0);
+  PSTAMP_END;
 }
 
 hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const void* d_obs,
@@ -326,10 +479,35 @@ hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const vo
                            uint8_t* d_outlier, int* d_inliers, double* d_pose_out_d,
                            hipStream_t st) {
   CamDev c{cam[0], cam[1], cam[2], cam[3], cam[4]};
-  hipLaunchKernelGGL(k_pose_opt, dim3(n_problems), dim3(kPoseThreads), 0, st, c, d_pose_in,
+  const int lds_obs = obs_stride < kPoseLdsObs ? obs_stride : kPoseLdsObs;
+  const size_t lds = ((size_t)lds_obs * (sizeof(PoseObsDev) + 1) + 15) & ~(size_t)15;
+  if (lds > 64 * 1024) {
+    static bool raised = false;  // > 64 KB dynamic LDS needs the opt-in once
+    if (!raised &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pose_opt),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+      return hipErrorInvalidValue;
+    raised = true;
+  }
+  hipLaunchKernelGGL(k_pose_opt, dim3(n_problems), dim3(kPoseThreads), lds, st, c, d_pose_in,
                      reinterpret_cast<const PoseObsDev*>(d_obs), d_nobs, obs_stride, d_pose_out,
-                     d_outlier, d_inliers, d_pose_out_d);
+                     d_outlier, d_inliers, d_pose_out_d, lds_obs);
   return hipGetLastError();
 }
 
 }  // namespace orbgpu
+
+#ifdef ORB_STAMPS
+extern "C" int orbgpu_debug_pose_stamps(unsigned long long* out, int n) {
+  if (n > 16) n = 16;
+  static unsigned long long buf[64 * 16];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(orbgpu::g_pose_stamps), sizeof(buf)) != hipSuccess) return -1;
+  for (int i = 0; i < n; ++i) {
+    out[i] = 0;
+    for (int c = 0; c < 64; ++c) out[i] += buf[c * 16 + i];
+  }
+  static const unsigned long long z[64 * 16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_pose_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -74,7 +74,8 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
   double R[3][3], V[3][3];
-  if (theta < 0.00001) {
+  // all lanes evaluate the same exp: wave-uniform branches (scalar, no exec masking)
+  if (__builtin_amdgcn_readfirstlane(theta < 0.00001 ? 1 : 0)) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -94,21 +95,23 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   Se3 e{0, 0, 0, 1, {0, 0, 0}};
   // Eigen quaternionbase_assign_impl, the three pivot cases written out
   double t = R[0][0] + R[1][1] + R[2][2];
-  if (t > 0) {
+  const int qcase = __builtin_amdgcn_readfirstlane(
+      t > 0 ? 0 : R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0]) ? 1 : R[1][1] > R[0][0] ? 2 : 3);
+  if (qcase == 0) {
     t = sqrt(t + 1.0);
     e.qw = 0.5 * t;
     t = 0.5 / t;
     e.qx = (R[2][1] - R[1][2]) * t;
     e.qy = (R[0][2] - R[2][0]) * t;
     e.qz = (R[1][0] - R[0][1]) * t;
-  } else if (R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0])) {  // i = 2, j = 0, k = 1
+  } else if (qcase == 1) {  // i = 2, j = 0, k = 1
     t = sqrt(R[2][2] - R[0][0] - R[1][1] + 1.0);
     e.qz = 0.5 * t;
     t = 0.5 / t;
     e.qw = (R[1][0] - R[0][1]) * t;
     e.qx = (R[0][2] + R[2][0]) * t;
     e.qy = (R[1][2] + R[2][1]) * t;
-  } else if (R[1][1] > R[0][0]) {  // i = 1, j = 2, k = 0
+  } else if (qcase == 2) {  // i = 1, j = 2, k = 0
     t = sqrt(R[1][1] - R[2][2] - R[0][0] + 1.0);
     e.qy = 0.5 * t;
     t = 0.5 / t;
@@ -177,10 +180,16 @@ __device__ __forceinline__ bool ldlt6_solve(double (&A)[6][6], const double (&b)
         big = fabs(A[i][i]);
         p = i;
       }
+    // every lane holds the same matrix: make the pivot wave-uniform so the
+    // swap below is a scalar branch, not exec-masked divergent code
+    p = __builtin_amdgcn_readfirstlane(p);
     perm[k] = p;
 #pragma unroll
     for (int pp = 0; pp < 6; ++pp)
-      if (pp > k && p == pp) ldlt_swap(A, k, pp);
+      if (pp > k && p == pp) {
+        asm volatile("" ::: "memory");  // keep a real (scalar) branch: no if-conversion
+        ldlt_swap(A, k, pp);
+      }
     if (k > 0) {
       double temp[6];
       double acc = 0;
