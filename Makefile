@@ -29,9 +29,10 @@ clean:
 	rm -rf $(LIB) oracle/_build
 
 # profiling variant: per-phase s_memtime totals (orbgpu_debug_stamps)
-stamps: $(LIB)/liborbgpu_stamps.so
-$(LIB)/liborbgpu_stamps.so: $(GPU_SRCS) $(GPU_HDRS)
+# STAMPS=1: k_fast_cells (+ pose kernel), STAMPS=2: k_octree
+STAMPS ?= 1
+stamps:
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS -shared -o $@ $(GPU_SRCS)
+	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
 
 .PHONY: all oracle clean stamps

@@ -28,28 +28,46 @@ __constant__ int8_t c_pattern[1024] = {
 // Profiling build only (make stamps): per-phase s_memtime totals.
 #ifdef ORB_STAMPS
 __device__ unsigned long long g_stamps[64 * 16];  // 64 spread copies of 16 counters
-#define STAMP_INIT                                           \
+#define STAMP_ON_INIT                                        \
   unsigned long long st_acc_[16] = {};                       \
   unsigned long long st_prev_ = __builtin_amdgcn_s_memtime()
-#define STAMP(i)                                                     \
+#define STAMP_ON(i)                                                  \
   do {                                                               \
     const unsigned long long st_now_ = __builtin_amdgcn_s_memtime(); \
     st_acc_[i] += st_now_ - st_prev_;                                \
     st_prev_ = st_now_;                                              \
   } while (0)
-#define STAMP_ADD(i, v) (st_acc_[i] += (unsigned long long)(v))
-#define STAMP_END                                                              \
+#define STAMP_ON_ADD(i, v) (st_acc_[i] += (unsigned long long)(v))
+#define STAMP_ON_END                                                           \
   do {                                                                         \
     if ((threadIdx.x & 63) == 0) {                                             \
       _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_)                        \
         if (st_acc_[i_]) atomicAdd(&g_stamps[(blockIdx.x & 63) * 16 + i_], st_acc_[i_]); \
     }                                                                          \
   } while (0)
+#endif
+// ORB_STAMPS=1 instruments k_fast_cells, =2 k_octree (one kernel per build).
+#if defined(ORB_STAMPS) && ORB_STAMPS == 1
+#define STAMP_INIT STAMP_ON_INIT
+#define STAMP(i) STAMP_ON(i)
+#define STAMP_ADD(i, v) STAMP_ON_ADD(i, v)
+#define STAMP_END STAMP_ON_END
 #else
 #define STAMP_INIT (void)0
 #define STAMP(i) (void)0
 #define STAMP_ADD(i, v) (void)0
 #define STAMP_END (void)0
+#endif
+#if defined(ORB_STAMPS) && ORB_STAMPS == 2
+#define OSTAMP_INIT STAMP_ON_INIT
+#define OSTAMP(i) STAMP_ON(i)
+#define OSTAMP_ADD(i, v) STAMP_ON_ADD(i, v)
+#define OSTAMP_END STAMP_ON_END
+#else
+#define OSTAMP_INIT (void)0
+#define OSTAMP(i) (void)0
+#define OSTAMP_ADD(i, v) (void)0
+#define OSTAMP_END (void)0
 #endif
 
 // Row extents of the 31-px circular patch (orb_extractor.cc:452-464; fixed
@@ -652,19 +670,23 @@ struct OctLds {
   unsigned long long* best;
   int* scan_tmp;                     // kOctThreads + 1
   int* scal;                         // block scalars
+  uint32_t* kdl;                     // candidates [0, kcap): packed keypoint
+  int* knl;                          //                        node position
 };
 
 __global__ __launch_bounds__(kOctThreads) void k_octree(
     const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
     const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
     uint32_t* __restrict__ dense, int* __restrict__ knode, uint32_t* __restrict__ oct_out,
-    int* __restrict__ oct_count, int* __restrict__ err) {
+    int* __restrict__ oct_count, int* __restrict__ err, int n_img, int kcap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
   const int L = P->levels;
-  const int img = blockIdx.x / L, l = blockIdx.x - img * L;
+  // level-major block order: the (largest) level-0 blocks are dispatched first
+  const int l = blockIdx.x / n_img, img = blockIdx.x - l * n_img;
   const LevelGeom& g = P->lev[l];
   const int NC = P->node_cap;
   const int t = threadIdx.x;
+  OSTAMP_INIT;
 
   OctLds s;
   {
@@ -684,24 +706,60 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     s.scan_tmp = p;
     p += kOctThreads + 1;
     s.scal = p;
+    p += 16;
+    s.kdl = reinterpret_cast<uint32_t*>(p);  // candidates [0, kcap) live in LDS
+    s.knl = p + kcap;
   }
 
-  // ---- gather this level's candidates in to_dist order (cell-major, raster).
+  // ---- gather this level's candidates in to_dist order (cell-major, raster):
+  // counts and slot offsets of all cells in one round of loads, a scan, then
+  // every candidate load in flight at once (its cell found by binary search).
   const int nc = g.cell_end - g.cell_begin;
   int* cell_off = s.tmp2;  // nc <= NC guaranteed by the planner
-  for (int i = t; i < nc; i += kOctThreads)
+  int* cell_src = s.stay;
+  for (int i = t; i < nc; i += kOctThreads) {
     cell_off[i] = cell_count[(size_t)img * P->n_cells + g.cell_begin + i];
+    cell_src[i] = cells[g.cell_begin + i].slot_off;
+  }
   __syncthreads();
   const int K = block_scan(cell_off, nc, s.scan_tmp);
-  uint32_t* kd = dense + (size_t)img * P->slots + g.slot_begin;
+  uint32_t* kd = dense + (size_t)img * P->slots + g.slot_begin;  // overflow beyond kcap
   int* kn = knode + (size_t)img * P->slots + g.slot_begin;
+  // candidate k: packed x|y<<12|score<<24 and its node; LDS below kcap, HBM above
+  auto KD = [&](int k) -> uint32_t { return k < kcap ? s.kdl[k] : kd[k]; };
+  auto KN = [&](int k) -> int { return k < kcap ? s.knl[k] : kn[k]; };
+  auto set_kd = [&](int k, uint32_t v) {
+    if (k < kcap)
+      s.kdl[k] = v;
+    else
+      kd[k] = v;
+  };
+  auto set_kn = [&](int k, int v) {
+    if (k < kcap)
+      s.knl[k] = v;
+    else
+      kn[k] = v;
+  };
   {
-    const int wave = t >> 6, lane = t & 63;
-    for (int i = wave; i < nc; i += kOctThreads / 64) {
-      const Cell c = cells[g.cell_begin + i];
-      const int n = cell_count[(size_t)img * P->n_cells + g.cell_begin + i];
-      const uint32_t* src = slots + (size_t)img * P->slots + c.slot_off;
-      for (int k = lane; k < n; k += 64) kd[cell_off[i] + k] = src[k];
+    const uint32_t* sl = slots + (size_t)img * P->slots;
+    for (int k0 = 0; k0 < K; k0 += 4 * kOctThreads) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = min(k0 + u * kOctThreads + t, K - 1);
+        int lo = 0, hi = nc - 1;  // last cell with cell_off <= k
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (cell_off[mid] <= k)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        v[u] = sl[cell_src[lo] + (k - cell_off[lo])];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k0 + u * kOctThreads + t < K) set_kd(k0 + u * kOctThreads + t, v[u]);
     }
   }
   uint32_t* out = oct_out + (size_t)img * P->kp_slots + g.out_off;
@@ -711,15 +769,17 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
   }
   __syncthreads();
 
+  OSTAMP(0);
+  OSTAMP_ADD(10 + (l == 0), 1);
   // ---- roots: round(W/H) equal-width columns; empty roots are erased.
   const int R = g.n_roots;
   const float hx = g.root_w;
   for (int i = t; i < R; i += kOctThreads) s.ccnt[i] = 0;
   __syncthreads();
   for (int k = t; k < K; k += kOctThreads) {
-    const float x = (float)(kd[k] & 0xfff);
+    const float x = (float)(KD(k) & 0xfff);
     const int r = (int)(x / hx);
-    kn[k] = r;
+    set_kn(k, r);
     atomicAdd(&s.ccnt[r], 1);
   }
   __syncthreads();
@@ -737,15 +797,17 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
   }
   __syncthreads();
-  for (int k = t; k < K; k += kOctThreads) kn[k] = s.tmp2[kn[k]];
+  for (int k = t; k < K; k += kOctThreads) set_kn(k, s.tmp2[KN(k)]);
   __syncthreads();
 
+  OSTAMP(1);
   const int N = g.budget;
   int phase = 1, n_exp = 0;
   bool finished = false;
   while (!finished) {
     // ---- choose D and its processing order (rank), uniform across the block
     int m;  // |D|
+    OSTAMP_ADD(12 + (phase == 2), 1);
     for (int i = t; i < S; i += kOctThreads) s.rank[i] = -1;
     __syncthreads();
     if (phase == 1) {
@@ -755,22 +817,28 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
       for (int i = t; i < S; i += kOctThreads)
         if (s.cnt[i] >= 2) s.rank[i] = s.tmp2[i];
     } else {
-      // stable sort of exp_list[0..n_exp) by (cnt, x0); processed from the back
+      // stable sort of exp_list[0..n_exp) by (cnt, x0); processed from the back.
+      // Keys (cnt, x0, list index) are unique, so a node's rank is the number
+      // of smaller keys: one LDS read + compare per other node.
+      unsigned long long* key = s.best;  // free until the final selection
       for (int j = t; j < n_exp; j += kOctThreads) {
         const int pj = s.exp_list[j];
-        const int cj = s.cnt[pj], xj = s.x0[pj];
+        key[j] = ((unsigned long long)(uint32_t)s.cnt[pj] << 32) |
+                 ((unsigned long long)(uint32_t)s.x0[pj] << 16) | (unsigned long long)j;
+      }
+      __syncthreads();
+      for (int j = t; j < n_exp; j += kOctThreads) {
+        const unsigned long long kj = key[j];
         int r = 0;
-        for (int i = 0; i < n_exp; ++i) {
-          const int pi = s.exp_list[i];
-          const int ci = s.cnt[pi], xi = s.x0[pi];
-          r += (ci < cj) || (ci == cj && (xi < xj || (xi == xj && i < j)));
-        }
-        s.rank[pj] = n_exp - 1 - r;
+#pragma unroll 8
+        for (int i = 0; i < n_exp; ++i) r += key[i] < kj;
+        s.rank[s.exp_list[j]] = n_exp - 1 - r;
       }
       m = n_exp;
     }
     __syncthreads();
 
+    OSTAMP(4);
     // ---- midlines of D and child point counts
     for (int i = t; i < S; i += kOctThreads) {
       if (s.rank[i] >= 0) {
@@ -781,9 +849,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
     __syncthreads();
     for (int k = t; k < K; k += kOctThreads) {
-      const int n = kn[k];
+      const int n = KN(k);
       if (s.rank[n] >= 0) {
-        const int x = kd[k] & 0xfff, y = (kd[k] >> 12) & 0xfff;
+        const uint32_t e = KD(k);
+        const int x = e & 0xfff, y = (e >> 12) & 0xfff;
         const int q = (x < s.mx[n] ? 0 : 1) + (y < s.my[n] ? 0 : 2);
         atomicAdd(&s.ccnt[4 * n + q], 1);
       }
@@ -797,6 +866,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
     __syncthreads();
 
+    OSTAMP(5);
     // ---- phase 2 stops once the node count reaches the budget
     if (phase == 2) {
       for (int r = t; r < m; r += kOctThreads) s.tmp2[r] = s.pc[r] - 1;
@@ -819,6 +889,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
       }
     }
 
+    OSTAMP(6);
     // ---- push offsets (processing order) and stay offsets (list order)
     const int T = block_scan(s.pc, m, s.scan_tmp);  // s.pc[r] = push offset of rank r
     for (int i = t; i < S; i += kOctThreads) s.stay[i] = s.rank[i] < 0 ? 1 : 0;
@@ -831,6 +902,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
       return;  // uniform
     }
 
+    OSTAMP(7);
     // ---- build the next list
     for (int i = t; i < S; i += kOctThreads) {
       const int r = s.rank[i];
@@ -869,16 +941,18 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
     __syncthreads();
     for (int k = t; k < K; k += kOctThreads) {
-      const int n = kn[k];
+      const int n = KN(k);
       const int r = s.rank[n];
       if (r < 0) {
-        kn[k] = T + s.stay[n];
+        set_kn(k, T + s.stay[n]);
       } else {
-        const int x = kd[k] & 0xfff, y = (kd[k] >> 12) & 0xfff;
+        const uint32_t e = KD(k);
+        const int x = e & 0xfff, y = (e >> 12) & 0xfff;
         const int q = (x < s.mx[n] ? 0 : 1) + (y < s.my[n] ? 0 : 2);
-        kn[k] = s.cpos[4 * n + q];
+        set_kn(k, s.cpos[4 * n + q]);
       }
     }
+    OSTAMP(8);
     // expandable children in push order = positions T-1, T-2, ..., 0
     for (int i = t; i < T; i += kOctThreads) s.pc[i] = s.tmp2[T - 1 - i];
     __syncthreads();
@@ -894,6 +968,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
     __syncthreads();
 
+    OSTAMP(9);
     const int S_prev = S;
     S = S_new;
     n_exp = e;
@@ -904,24 +979,29 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     }
   }
 
+  OSTAMP(2);
   // ---- best response per node, first in to_dist order on ties
   for (int i = t; i < S; i += kOctThreads) s.best[i] = 0ull;
   __syncthreads();
   for (int k = t; k < K; k += kOctThreads) {
     const unsigned long long v =
-        ((unsigned long long)(kd[k] >> 24) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)k);
-    atomicMax(&s.best[kn[k]], v);
+        ((unsigned long long)(KD(k) >> 24) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)k);
+    atomicMax(&s.best[KN(k)], v);
   }
   __syncthreads();
   const int n_out = min(S, g.out_cap);
   for (int i = t; i < n_out; i += kOctThreads) {
     const uint32_t k = 0xffffffffu - (uint32_t)(s.best[i] & 0xffffffffull);
-    out[i] = kd[k];
+    out[i] = KD((int)k);
   }
   if (t == 0) {
     oct_count[img * L + l] = n_out;
     if (S > g.out_cap) atomicOr(err, kErrOutCap);
   }
+  OSTAMP(3);
+  if (l == 0) OSTAMP_ADD(14, st_acc_[0] + st_acc_[1] + st_acc_[2] + st_acc_[3] + st_acc_[4] +
+                               st_acc_[5] + st_acc_[6] + st_acc_[7] + st_acc_[8] + st_acc_[9]);
+  OSTAMP_END;
 }
 
 // --------------------------------------------------------------------------
@@ -1170,8 +1250,9 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                      a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count);
   mark(3);
   hipLaunchKernelGGL(k_octree, dim3(n * H.levels), dim3(kOctThreads), a.octree_lds, st, a.plan,
-                     a.cells, (const uint32_t*)a.slots, (const int*)a.cell_count, a.dense, a.knode,
-                     a.oct_out, a.oct_count, a.err);
+                     a.cells,
+                     (const uint32_t*)a.slots, (const int*)a.cell_count, a.dense, a.knode,
+                     a.oct_out, a.oct_count, a.err, n, kOctreeLdsCand);
   mark(4);
   const long waves = (long)n * H.kp_slots;
   hipLaunchKernelGGL(k_describe, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a.plan, src,

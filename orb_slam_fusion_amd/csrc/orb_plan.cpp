@@ -231,7 +231,7 @@ int fast_cell_lds_bytes(int cols, int rows) {
 
 size_t octree_lds_bytes(const PlanHeader& P) {
   const size_t nc = P.node_cap;
-  return nc * 8 + nc * 17 * 4 + nc * 8 * 4 + (256 + 1) * 4 + 16 * 4;
+  return nc * 8 + nc * 17 * 4 + nc * 8 * 4 + (256 + 1) * 4 + 16 * 4 + (size_t)kOctreeLdsCand * 8;
 }
 
 }  // namespace orbgpu
