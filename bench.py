@@ -204,7 +204,10 @@ def main() -> int:
     pmc = REPO / "profiles" / "pmc_traffic.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get(roof_stage)
+            tj = json.loads(pmc.read_text())  # tools/pmc_traffic.sh: HBM bytes per launch
+            if roof_stage in tj:  # scaled to this run's images per launch
+                per = tj[roof_stage] / tj[roof_stage + "_detail"]["images_per_launch"]
+                traffic = round(per * 2 * Bp)
         except Exception:
             traffic = None
 

@@ -1015,6 +1015,22 @@ constexpr int kRawW = 36, kRawH = 31;   // 31x31 patch + dword alignment slack
 constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slack
 constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
 
+// In-wave integer sum by DPP (row_shr 1,2,4,8 + row_bcast 15/31): lane 63
+// holds the total.
+__device__ __forceinline__ int wave_isum_to_lane63(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
+// One wave per octree output slot (measured against a persistent, software-
+// pipelined variant: the extra registers halved residency and lost, 201 vs
+// 167 us).  The slot's count and keypoint are loaded together; dead slots
+// leave before any patch load (their oct_out entries are stale).
 __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
                                                   const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur,
@@ -1022,9 +1038,10 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
                                                   const int* __restrict__ oct_count,
                                                   float* __restrict__ angle_out,
                                                   uint64_t* __restrict__ desc_out, int n_img) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_all[4 * ((kDescLds + 15) & ~15)];
+  constexpr int kSlice = (kDescLds + 15) & ~15;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[4 * kSlice];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* raw = lds_all + wave * ((kDescLds + 15) & ~15);
+  uint8_t* raw = lds_all + wave * kSlice;
   uint8_t* blp = raw + kRawW * kRawH;
   const long gidx = (long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
   if (gidx >= (long)n_img * P->kp_slots) return;  // wave-uniform
@@ -1033,20 +1050,20 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   int l = 0;
   while (l + 1 < P->levels && slot >= P->lev[l + 1].out_off) ++l;
   const LevelGeom& g = P->lev[l];
-  const int idx = slot - g.out_off;
-  if (idx >= oct_count[img * P->levels + l]) return;  // wave-uniform
+  const int cnt = oct_count[img * P->levels + l];
   const uint32_t kp = oct_out[(size_t)img * P->kp_slots + slot];
+  if (slot - g.out_off >= cnt) return;  // wave-uniform
   const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
 
-  // Stage both patches with independent dword loads (one memory round trip).
+  // Stage both patches with independent dword loads (one memory round trip;
+  // unaligned only when the level-0 stride is not a multiple of 4).
   int sp;
   const uint8_t* img0 = level_plane(P, src, pyr, img, l, sp);
-  const uint8_t* B = blur + (size_t)img * P->blur_bytes + g.blur_off;
   const int rx0 = (cx - 15) & ~3, bx0 = (cx - 18) & ~3;
   const uint8_t* rsrc = img0 + (size_t)(cy - 15) * sp + rx0;
-  const uint8_t* bsrc = B + (size_t)(cy - 18) * g.pitch + bx0;
+  const uint8_t* bsrc = blur + (size_t)img * P->blur_bytes + g.blur_off + (size_t)(cy - 18) * g.pitch + bx0;
   constexpr int nr = kRawH * (kRawW / 4), nb = kBlurH * (kBlurW / 4);
-  if (((((uintptr_t)img0) | (uintptr_t)sp) & 3) == 0) {
+  {
     uint32_t v[(nr + nb + 63) / 64];
 #pragma unroll
     for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
@@ -1063,15 +1080,6 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
     for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
       const int i = 64 * u + lane;
       if (i < nr + nb) reinterpret_cast<uint32_t*>(raw)[i] = v[u];
-    }
-  } else {
-    for (int i = lane; i < kRawH * kRawW; i += 64) {
-      const int r = i / kRawW, q = i - r * kRawW;
-      raw[i] = rsrc[(size_t)r * sp + q];
-    }
-    for (int i = lane; i < nb; i += 64) {
-      const int r = i / (kBlurW / 4), q = i - r * (kBlurW / 4);
-      reinterpret_cast<uint32_t*>(blp)[i] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * g.pitch + 4 * q);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1095,11 +1103,8 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
       m01 += in ? v * val : 0;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    m10 += __shfl_xor(m10, o, 64);
-    m01 += __shfl_xor(m01, o, 64);
-  }
+  m10 = __builtin_amdgcn_readlane(wave_isum_to_lane63(m10), 63);
+  m01 = __builtin_amdgcn_readlane(wave_isum_to_lane63(m01), 63);
   const float angle = dev_fast_atan2((float)m01, (float)m10);
 
   const float ang = angle * (float)(3.14159265358979323846 / 180.0);
