@@ -13,7 +13,7 @@ rm -rf gpurun_out/bench_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/bench_prof -o bench \
   -- python3 bench.py --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1 || { echo "rocprof bench failed"; tail -5 gpurun_out/bench_prof.log; exit 1; }
 f=$(find gpurun_out/bench_prof -name '*kernel_stats.csv' | head -n1)
-cp "$f" profiles/$R/bench_kernel_stats.csv
+cp "$f" gpurun_out/bench_kernel_stats.csv  # copy into profiles/$R/ locally (only gpurun_out/ returns)
 python3 tools/kstats.py "$f" > profiles/$R/bench_kernel_stats.txt
 grep '^{' gpurun_out/bench_prof.log | tail -1 > profiles/$R/bench_under_rocprof.json
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_full.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/bench_full.log; exit 1; }
