@@ -20,6 +20,11 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 POSE_OBS_DTYPE = np.dtype([("Xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
                            ("inv_sigma2", "<f4")])
+LBA_EDGE_DTYPE = np.dtype([("point", "<i4"), ("kf", "<i4"), ("u", "<f4"), ("v", "<f4"),
+                           ("ur", "<f4"), ("inv_sigma2", "<f4")])
+# int reduce(void* user, double* buf, int n, int op)   op: 0 sum, 1 max
+LBA_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                 ctypes.c_int, ctypes.c_int)
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
@@ -47,6 +52,10 @@ def lib() -> ctypes.CDLL:
         "orc_sincosf": (None, [_P, _I, _P, _P]),
         "orc_sincosf_check_libm": (ctypes.c_long, [ctypes.c_uint, ctypes.c_uint]),
         "orc_pose_opt": (_I, [_P, _P, _P, _I, _P, _P, _P]),
+        "orc_lba_edge_linearize": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+        "orc_se3_exp_compose": (None, [_P, _P, _P]),
+        "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, LBA_REDUCE_FN, _P, _P, _P,
+                         _P, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(so, name)
@@ -168,3 +177,58 @@ def pose_opt(cam: np.ndarray, pose_in: np.ndarray, obs: np.ndarray):
     out = np.zeros(max(n, 1), np.uint8)
     inl = lib().orc_pose_opt(_p(cam), _p(pose_in), _p(obs), n, _p(pout), _p(out), _p(pd))
     return inl, pout, out[:n].copy(), pd
+
+
+def lba(problem, iters: int = 10, pt_range=None, reduce=None):
+    """LocalBundleAdjustment restatement on an LbaProblem-like object (cam,
+    poses_init, fixed, pts_init, edges).  pt_range=(begin, end) restricts this
+    call to a point shard; reduce(buf: np.ndarray[float64], op) -> None
+    completes the shard sums in place (op 0 sum, 1 max).  Returns dict with
+    poses [n_kf, 7] f64, pts [n_pts, 3] f64 (shard rows only), outlier [E] u8
+    (shard edges only), stats [6]."""
+    cam = np.ascontiguousarray(problem.cam, np.float32)
+    poses = np.ascontiguousarray(problem.poses_init, np.float32)
+    fixed = np.ascontiguousarray(problem.fixed, np.uint8)
+    pts = np.ascontiguousarray(problem.pts_init, np.float32)
+    edges = np.ascontiguousarray(problem.edges, LBA_EDGE_DTYPE)
+    n_kf, n_pts, ne = len(poses), len(pts), len(edges)
+    b, e = pt_range if pt_range is not None else (0, n_pts)
+    po = np.zeros((n_kf, 7), np.float64)
+    xo = np.zeros((n_pts, 3), np.float64)
+    out = np.zeros(max(ne, 1), np.uint8)
+    st = np.zeros(6, np.float64)
+    if reduce is None:
+        cb = LBA_REDUCE_FN(0)
+    else:
+        def _cb(_user, buf, n, op):
+            try:
+                arr = np.ctypeslib.as_array(buf, shape=(n,))
+                reduce(arr, op)
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as a failed reduce
+                return -1
+        cb = LBA_REDUCE_FN(_cb)
+    rc = lib().orc_lba(_p(cam), n_kf, _p(poses), _p(fixed), n_pts, _p(pts), ne, _p(edges), b, e,
+                       iters, cb, None, _p(po), _p(xo), _p(out), _p(st))
+    if rc != 0:
+        raise RuntimeError(f"orc_lba failed ({rc})")
+    return {"poses": po, "pts": xo, "outlier": out[:ne].copy(), "stats": st}
+
+
+def lba_edge_linearize(cam, pose7, X, edge):
+    """-> (depth_positive, err[3], Jl[3,3], Jp[3,6]) of one LBA edge."""
+    cam = np.ascontiguousarray(cam, np.float32)
+    pose7 = np.ascontiguousarray(pose7, np.float64)
+    X = np.ascontiguousarray(X, np.float64)
+    e = np.ascontiguousarray(np.array([edge], LBA_EDGE_DTYPE))
+    err, jl, jp = np.zeros(3), np.zeros(9), np.zeros(18)
+    d = lib().orc_lba_edge_linearize(_p(cam), _p(pose7), _p(X), _p(e), _p(err), _p(jl), _p(jp))
+    return bool(d), err, jl.reshape(3, 3), jp.reshape(3, 6)
+
+
+def se3_exp_compose(u6, pose7):
+    u6 = np.ascontiguousarray(u6, np.float64)
+    pose7 = np.ascontiguousarray(pose7, np.float64)
+    out = np.zeros(7)
+    lib().orc_se3_exp_compose(_p(u6), _p(pose7), _p(out))
+    return out

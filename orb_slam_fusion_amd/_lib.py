@@ -73,6 +73,13 @@ POSE_OBS_DTYPE = np.dtype(
 )
 assert POSE_OBS_DTYPE.itemsize == 28
 
+# orbgpu_lba_edge: point, kf, u, v, ur (< 0: mono), inv_sigma2
+LBA_EDGE_DTYPE = np.dtype(
+    [("point", "<i4"), ("kf", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+     ("inv_sigma2", "<f4")]
+)
+assert LBA_EDGE_DTYPE.itemsize == 24
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 

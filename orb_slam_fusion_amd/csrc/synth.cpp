@@ -180,3 +180,158 @@ void synth_pose_problem(uint64_t seed, int n, int outlier_pct, float* obs, float
 }
 
 }  // extern "C"
+
+namespace {
+// Rotation matrix (row-major) -> unit quaternion (x, y, z, w), w >= 0.
+void quat_from_matrix(const double R[3][3], double q[4]) {
+  const double tr = R[0][0] + R[1][1] + R[2][2];
+  if (tr > 0) {
+    const double s = std::sqrt(tr + 1.0) * 2;
+    q[3] = 0.25 * s;
+    q[0] = (R[2][1] - R[1][2]) / s;
+    q[1] = (R[0][2] - R[2][0]) / s;
+    q[2] = (R[1][0] - R[0][1]) / s;
+  } else if (R[0][0] > R[1][1] && R[0][0] > R[2][2]) {
+    const double s = std::sqrt(1.0 + R[0][0] - R[1][1] - R[2][2]) * 2;
+    q[3] = (R[2][1] - R[1][2]) / s;
+    q[0] = 0.25 * s;
+    q[1] = (R[0][1] + R[1][0]) / s;
+    q[2] = (R[0][2] + R[2][0]) / s;
+  } else if (R[1][1] > R[2][2]) {
+    const double s = std::sqrt(1.0 + R[1][1] - R[0][0] - R[2][2]) * 2;
+    q[3] = (R[0][2] - R[2][0]) / s;
+    q[0] = (R[0][1] + R[1][0]) / s;
+    q[1] = 0.25 * s;
+    q[2] = (R[1][2] + R[2][1]) / s;
+  } else {
+    const double s = std::sqrt(1.0 + R[2][2] - R[0][0] - R[1][1]) * 2;
+    q[3] = (R[1][0] - R[0][1]) / s;
+    q[0] = (R[0][2] + R[2][0]) / s;
+    q[1] = (R[1][2] + R[2][1]) / s;
+    q[2] = 0.25 * s;
+  }
+  if (q[3] < 0)
+    for (int k = 0; k < 4; ++k) q[k] = -q[k];
+}
+void store_pose(const double q[4], const double t[3], float* o) {
+  double n = 0;
+  for (int k = 0; k < 4; ++k) n += q[k] * q[k];
+  n = std::sqrt(n);
+  for (int k = 0; k < 4; ++k) o[k] = (float)(q[k] / n);
+  for (int k = 0; k < 3; ++k) o[4 + k] = (float)t[k];
+}
+}  // namespace
+
+extern "C" {
+
+// Seeded LocalBundleAdjustment window: n_kf
+// keyframes on a 4 m arc (radius 6 m) all facing a 4 x 3 x 2 m box of n_pts
+// points centred on the world origin; point j is observed by the obs_per_pt
+// consecutive keyframes (j + i) mod n_kf, i < obs_per_pt, in ascending
+// keyframe order; half the observations stereo; octave U{0..7}, pixel noise
+// sigma = 1.2^octave; `outlier_pct` % gross outliers (+-U[20,60] px).  The
+// first n_fixed keyframes are fixed.  Initial guesses: poses perturbed by
+// 5 cm / 1 deg, points by 5 cm.  Poses are Tcw (qx, qy, qz, qw, tx, ty, tz);
+// edges are {point, kf, u, v, ur (< 0: mono), inv_sigma2} (int, int, 4 floats).
+// Returns the number of edges (n_pts * obs_per_pt).
+int synth_lba_problem(uint64_t seed, int n_kf, int n_pts, int obs_per_pt, int n_fixed,
+                      int outlier_pct, float* cam, float* poses_true, float* poses_init,
+                      uint8_t* fixed, float* pts_true, float* pts_init, void* edges) {
+  XorShift64Star rng(seed * 0x9E3779B97F4A7C15ull + 11);
+  const double fx = 458.654, fy = 457.296, cx = 367.215, cy = 248.375, bf = 0.11 * fx;
+  cam[0] = (float)fx;
+  cam[1] = (float)fy;
+  cam[2] = (float)cx;
+  cam[3] = (float)cy;
+  cam[4] = (float)bf;
+  const double radius = 6.0, arc = 4.0;
+  std::vector<double> Rcw((size_t)n_kf * 9), tcw((size_t)n_kf * 3);
+  for (int k = 0; k < n_kf; ++k) {
+    const double th = -0.5 * arc / radius + (n_kf > 1 ? k * (arc / radius) / (n_kf - 1) : 0.0);
+    const double C[3] = {radius * std::sin(th), 0.0, -radius * std::cos(th)};
+    double z[3] = {-C[0], -C[1], -C[2]};
+    const double zn = std::sqrt(z[0] * z[0] + z[1] * z[1] + z[2] * z[2]);
+    for (double& v : z) v /= zn;
+    const double up[3] = {0, -1, 0};  // image rows grow downwards
+    double x[3] = {up[1] * z[2] - up[2] * z[1], up[2] * z[0] - up[0] * z[2], up[0] * z[1] - up[1] * z[0]};
+    const double xn = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    for (double& v : x) v /= xn;
+    const double y[3] = {z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]};
+    double R[3][3];  // rows = camera axes in world coordinates (R_cw)
+    for (int c = 0; c < 3; ++c) {
+      R[0][c] = x[c];
+      R[1][c] = y[c];
+      R[2][c] = z[c];
+    }
+    double t[3];
+    for (int r = 0; r < 3; ++r) t[r] = -(R[r][0] * C[0] + R[r][1] * C[1] + R[r][2] * C[2]);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) Rcw[(size_t)k * 9 + 3 * r + c] = R[r][c];
+    for (int r = 0; r < 3; ++r) tcw[(size_t)k * 3 + r] = t[r];
+    double q[4];
+    quat_from_matrix(R, q);
+    store_pose(q, t, poses_true + 7 * k);
+    // perturbed initial pose: 1 deg about a random axis, 5 cm along a random direction
+    double dq[4], qi[4];
+    quat_from_axis_angle(rng.unit() - 0.5, rng.unit() - 0.5, rng.unit() - 0.5,
+                         3.14159265358979 / 180, dq);
+    quat_mul(dq, q, qi);
+    double dir[3] = {rng.unit() - 0.5, rng.unit() - 0.5, rng.unit() - 0.5};
+    const double dn = std::sqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    double ti[3];
+    for (int r = 0; r < 3; ++r) ti[r] = t[r] + 0.05 * dir[r] / dn;
+    if (k < n_fixed) {
+      store_pose(q, t, poses_init + 7 * k);
+    } else {
+      if (qi[3] < 0)
+        for (double& v : qi) v = -v;
+      store_pose(qi, ti, poses_init + 7 * k);
+    }
+    fixed[k] = k < n_fixed ? 1 : 0;
+  }
+  struct Edge {
+    int32_t point, kf;
+    float u, v, ur, inv_sigma2;
+  };
+  Edge* E = static_cast<Edge*>(edges);
+  int ne = 0;
+  for (int j = 0; j < n_pts; ++j) {
+    const double X[3] = {4.0 * (rng.unit() - 0.5), 3.0 * (rng.unit() - 0.5), 2.0 * (rng.unit() - 0.5)};
+    for (int c = 0; c < 3; ++c) pts_true[3 * j + c] = (float)X[c];
+    double dir[3] = {rng.unit() - 0.5, rng.unit() - 0.5, rng.unit() - 0.5};
+    const double dn = std::sqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    for (int c = 0; c < 3; ++c) pts_init[3 * j + c] = (float)(X[c] + 0.05 * dir[c] / dn);
+    // observing keyframes in ascending index order
+    std::vector<int> kfs;
+    for (int i = 0; i < obs_per_pt && i < n_kf; ++i) kfs.push_back((j + i) % n_kf);
+    for (size_t a = 1; a < kfs.size(); ++a)
+      for (size_t b = a; b > 0 && kfs[b - 1] > kfs[b]; --b) std::swap(kfs[b - 1], kfs[b]);
+    for (int k : kfs) {
+      const double* R = &Rcw[(size_t)k * 9];
+      const double* t = &tcw[(size_t)k * 3];
+      double Xc[3];
+      for (int r = 0; r < 3; ++r) Xc[r] = R[3 * r] * X[0] + R[3 * r + 1] * X[1] + R[3 * r + 2] * X[2] + t[r];
+      const int oct = rng.uniform(0, 7);
+      float s2 = 1.0f;
+      for (int l = 0; l < oct; ++l) s2 = (float)(s2 * 1.2) * 1.0f;
+      const float inv_sigma2 = 1.0f / (s2 * s2);
+      const double sig = s2;
+      const double u_true = fx * Xc[0] / Xc[2] + cx, v_true = fy * Xc[1] / Xc[2] + cy;
+      double uo = u_true + sig * rng.gauss(), vo = v_true + sig * rng.gauss();
+      const bool stereo = rng.unit() < 0.5;
+      double ur = stereo ? u_true - bf / Xc[2] + sig * rng.gauss() : -1.0;
+      if (rng.uniform(0, 99) < outlier_pct) {
+        const double du = (rng.uniform(0, 1) ? 1 : -1) * (20 + 40 * rng.unit());
+        const double dv = (rng.uniform(0, 1) ? 1 : -1) * (20 + 40 * rng.unit());
+        uo += du;
+        vo += dv;
+        if (stereo) ur += du;
+      }
+      if (stereo && ur < 0) ur = 0;
+      E[ne++] = Edge{j, k, (float)uo, (float)vo, (float)ur, inv_sigma2};
+    }
+  }
+  return ne;
+}
+
+}  // extern "C"

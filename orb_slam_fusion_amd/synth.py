@@ -7,10 +7,11 @@ from functools import lru_cache
 
 import numpy as np
 
-from ._lib import LIB_DIR, POSE_OBS_DTYPE
+from ._lib import LBA_EDGE_DTYPE, LIB_DIR, POSE_OBS_DTYPE
 
 FRAME_SEED_BASE = 0x5EED0000
 POSE_SEED = 7
+LBA_SEED = 11
 
 
 @lru_cache(None)
@@ -25,6 +26,8 @@ def _so() -> ctypes.CDLL:
     so.synth_pose_problem.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]
+    so.synth_lba_problem.argtypes = [ctypes.c_uint64] + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 7
+    so.synth_lba_problem.restype = ctypes.c_int
     return so
 
 
@@ -51,3 +54,28 @@ def pose_problem(seed: int = POSE_SEED, n: int = 600, outlier_pct: int = 10):
     _so().synth_pose_problem(seed, n, outlier_pct, obs.ctypes.data, cam.ctypes.data, pt.ctypes.data,
                              pi.ctypes.data)
     return cam, pi, pt, obs
+
+
+class LbaProblem:
+    """A LocalBundleAdjustment window (config C4 by default): cam[5];
+    poses_true / poses_init [n_kf, 7] (Tcw as qx, qy, qz, qw, tx, ty, tz);
+    fixed [n_kf] uint8; pts_true / pts_init [n_pts, 3]; edges LBA_EDGE_DTYPE."""
+
+    def __init__(self, cam, poses_true, poses_init, fixed, pts_true, pts_init, edges):
+        self.cam, self.poses_true, self.poses_init, self.fixed = cam, poses_true, poses_init, fixed
+        self.pts_true, self.pts_init, self.edges = pts_true, pts_init, edges
+
+
+def lba_problem(seed: int = LBA_SEED, n_kf: int = 20, n_pts: int = 3000, obs_per_pt: int = 6,
+                n_fixed: int = 2, outlier_pct: int = 0) -> LbaProblem:
+    cam = np.zeros(5, np.float32)
+    pt = np.zeros((n_kf, 7), np.float32)
+    pi = np.zeros((n_kf, 7), np.float32)
+    fixed = np.zeros(n_kf, np.uint8)
+    xt = np.zeros((n_pts, 3), np.float32)
+    xi = np.zeros((n_pts, 3), np.float32)
+    edges = np.zeros(n_pts * min(obs_per_pt, n_kf), LBA_EDGE_DTYPE)
+    ne = _so().synth_lba_problem(seed, n_kf, n_pts, obs_per_pt, n_fixed, outlier_pct,
+                                 cam.ctypes.data, pt.ctypes.data, pi.ctypes.data, fixed.ctypes.data,
+                                 xt.ctypes.data, xi.ctypes.data, edges.ctypes.data)
+    return LbaProblem(cam, pt, pi, fixed, xt, xi, edges[:ne])
