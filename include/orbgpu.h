@@ -159,6 +159,54 @@ orbgpu_status orbgpu_pose_opt_batch(orbgpu_pose_ctx* c, const orbgpu_camera* cam
                                     orbgpu_pose* d_Tcw_out, uint8_t* d_outlier, int* d_inliers,
                                     double* d_pose_out_d, void* hip_stream);
 
+/* ------------------------------------------------------------------------
+ * LocalBundleAdjustment -- replaces the solve of
+ * Optimizer::LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*, int&,
+ * int&, int&, int&) (optimizer.h:66-68, optimizer.cc:1053-1441): the caller
+ * gathers the window as the reference does (:1057-1124: local keyframes,
+ * their map points, fixed keyframes) and hands over the graph; the library
+ * runs optimize(iterations) (g2o LM, BlockSolver_6_3 Schur complement on the
+ * points, :1359-1360) and the outlier test (:1362-1400); the caller erases
+ * the flagged observations under Map::mMutexMapUpdate and writes poses and
+ * points back (:1402-1441).
+ * ------------------------------------------------------------------------ */
+typedef struct orbgpu_lba_edge {
+  int32_t point;    /* map point index (vertex id MP.id_ + maxKFid + 1 -> 0..n_pts-1)     */
+  int32_t kf;       /* keyframe index (vertex id KF.id_ -> 0..n_kf-1)                      */
+  float u, v;       /* mvKeysUn[leftIndex].pt                                              */
+  float ur;         /* mvuRight[leftIndex]; < 0 -> EdgeSE3ProjectXYZ (mono, :1248-1274),
+                       else g2o::EdgeStereoSE3ProjectXYZ (:1275-1310)                      */
+  float inv_sigma2; /* mvInvLevelSigma2[kpUn.octave]                                       */
+} orbgpu_lba_edge;
+
+typedef struct orbgpu_lba_ctx orbgpu_lba_ctx;
+
+/* Completes a point-sharded reduction across ranks: called on
+ * the host thread with a device buffer of n doubles (stream-synchronized),
+ * op 0 = sum, 1 = max; must leave the reduced values in the buffer before
+ * returning (e.g. an RCCL all-reduce + stream sync).  Returns 0 on success. */
+typedef int (*orbgpu_lba_reduce_fn)(void* user, double* d_buf, int n, int op, void* hip_stream);
+
+orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out);
+void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
+
+/* One window from host buffers.  Keyframe k is fixed iff fixed[k] (the map's
+ * initial keyframe, :1161, and every fixed camera, :1169-1183).  Points
+ * [pt_begin, pt_end) and their edges are this call's shard (the whole window:
+ * 0, n_pts); with reduce == NULL the shard must be the whole window.
+ * *stop_flag (optional) is polled before every LM iteration (pbStopFlag).
+ * Outputs: optimised poses (float, unit quaternion; poses_out_d optional
+ * doubles), pts_out rows of the shard's points, outlier[i] for the shard's
+ * edges (chi2 > 5.991 / 7.815 or depth <= 0), stats (optional, 6 doubles):
+ * initial / final robust chi2, LM iterations, trials, final lambda, outliers. */
+orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* c, const orbgpu_camera* cam, int n_kf,
+                                  const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
+                                  const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
+                                  int pt_begin, int pt_end, int iterations,
+                                  const volatile int* stop_flag, orbgpu_lba_reduce_fn reduce,
+                                  void* user, orbgpu_pose* poses_out, double* poses_out_d,
+                                  float* pts_out, uint8_t* outlier, double* stats);
+
 #ifdef __cplusplus
 }
 #endif

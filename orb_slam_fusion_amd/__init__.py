@@ -8,9 +8,11 @@ mirror of the reference interface over that ABI.
 """
 from ._lib import KEYPOINT_DTYPE, POSE_OBS_DTYPE, OrbGpuError, library_path
 from .extractor import OrbExtractor
+from .lba import LocalBundleAdjuster
 from .optimizer import PoseFrame, PoseOptimizer
 
 __all__ = [
+    "LocalBundleAdjuster",
     "KEYPOINT_DTYPE",
     "POSE_OBS_DTYPE",
     "OrbGpuError",

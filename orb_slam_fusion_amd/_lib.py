@@ -107,7 +107,18 @@ SIGNATURES = {
         _I,
         [_P, ctypes.POINTER(Camera), _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     ),
+    "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
+    "orbgpu_lba_ctx_destroy": (None, [_P]),
+    "orbgpu_lba_optimize": (
+        _I,
+        [_P, ctypes.POINTER(Camera), _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P,
+         _P, _P, _P],
+    ),
 }
+
+# int (*orbgpu_lba_reduce_fn)(void* user, double* d_buf, int n, int op, void* hip_stream)
+LBA_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_void_p)
 
 _lib = None
 

@@ -64,6 +64,10 @@ __device__ __forceinline__ Se3 se3_compose(const Se3& a, const Se3& b) {
   return r;
 }
 
+// kUniform: every lane of the wave evaluates the same exp (PoseOptimization),
+// so the branches are made wave-uniform with readfirstlane; otherwise each
+// lane takes its own branch (LocalBundleAdjustment, one pose per lane).
+template <bool kUniform = true>
 __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   const double w0 = u[0], w1 = u[1], w2 = u[2];
   const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
@@ -75,7 +79,8 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
     for (int j = 0; j < 3; ++j) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
   double R[3][3], V[3][3];
   // all lanes evaluate the same exp: wave-uniform branches (scalar, no exec masking)
-  if (__builtin_amdgcn_readfirstlane(theta < 0.00001 ? 1 : 0)) {
+  const int small = theta < 0.00001 ? 1 : 0;
+  if (kUniform ? __builtin_amdgcn_readfirstlane(small) : small) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -95,8 +100,8 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   Se3 e{0, 0, 0, 1, {0, 0, 0}};
   // Eigen quaternionbase_assign_impl, the three pivot cases written out
   double t = R[0][0] + R[1][1] + R[2][2];
-  const int qcase = __builtin_amdgcn_readfirstlane(
-      t > 0 ? 0 : R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0]) ? 1 : R[1][1] > R[0][0] ? 2 : 3);
+  const int qc = t > 0 ? 0 : R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0]) ? 1 : R[1][1] > R[0][0] ? 2 : 3;
+  const int qcase = kUniform ? __builtin_amdgcn_readfirstlane(qc) : qc;
   if (qcase == 0) {
     t = sqrt(t + 1.0);
     e.qw = 0.5 * t;
