@@ -196,8 +196,8 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
     dsz += (k + 1) & ~(size_t)1;
     return o;
   };
-  const size_t d_err = take(3 * E), d_hpl = take(18 * E), d_hppe = take(27 * E), d_w = take(18 * E),
-               d_wb = take(6 * E), d_hll = take(9 * P), d_bl = take(3 * P), d_dinv = take(9 * P),
+  const size_t d_err = take(3 * E), d_hpl = take(18 * E), d_hppe = take(27 * E),
+               d_hlle = take(12 * E), d_hll = take(9 * P), d_bl = take(3 * P), d_dinv = take(9 * P),
                d_hpp = take(36 * F), d_bp = take(6 * F), d_diag = take(n + 2),
                d_sys = take((size_t)n * n + 2 * n + 2), d_work = take((size_t)n * n + 2),
                d_xp = take(n + 2), d_scal = take(4), d_part = take(nblk), d_out = take(2);
@@ -250,8 +250,7 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   a.err = D + d_err;
   a.hpl = D + d_hpl;
   a.hpp_e = D + d_hppe;
-  a.w = D + d_w;
-  a.wb = D + d_wb;
+  a.hll_e = D + d_hlle;
   a.hll = D + d_hll;
   a.bl = D + d_bl;
   a.dinv = D + d_dinv;

@@ -197,64 +197,78 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_errors(LbaArgs a, const dou
   lba_finish_sum(s, a.partials, a.counter, out);
 }
 
-// ---- buildSystem, point side: one thread per point of the shard.  Hll, bl
-// in edge order; per edge: Hpl (6x3, free poses) and its Hpp / bp terms.
+// ---- buildSystem, edge side: one thread per edge of the shard.  Its
+// Jacobians at the current state and its terms of Hll / bl (point), Hpl and
+// Hpp / bp (free pose) -- summed per point and per pose in fixed order below.
 __global__ __launch_bounds__(kLbaThreads) void k_lba_linearize(LbaArgs a, const double* __restrict__ poses,
                                                                const double* __restrict__ pts) {
+  const int i = blockIdx.x * kLbaThreads + threadIdx.x;
+  if (i >= a.n_edges) return;
+  const LbaEdgeDev e = a.edges[i];
+  const double X[3] = {pts[3 * e.point], pts[3 * e.point + 1], pts[3 * e.point + 2]};
+  const Se3 T = load_pose(poses + 7 * e.kf);
+  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
+  const int D = e.ur < 0.f ? 2 : 3;
+  double Jl[3][3], Jp[3][6];
+  lba_jacobians(e, T, X, a.cam, Jl, Jp);
+  double r0, w;
+  huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
+  const double info = (double)e.inv_sigma2, wi = w * info;
+  double om[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) om[r] = (-info * ev[r]) * w;
+  double* hl = a.hll_e + 12 * (size_t)i;  // 9 Hll terms (row-major), 3 bl terms
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    double g = 0;
+    for (int r = 0; r < D; ++r) g += Jl[r][s] * om[r];
+    hl[9 + s] = g;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      double h = 0;
+      for (int r = 0; r < D; ++r) h += Jl[r][s] * wi * Jl[r][q];
+      hl[3 * s + q] = h;
+    }
+  }
+  if (a.hidx[e.kf] < 0) return;
+  double* hpl = a.hpl + 18 * (size_t)i;
+  double* hp = a.hpp_e + 27 * (size_t)i;  // 21 lower-triangle Hpp terms, then 6 bp terms
+  int hk = 0;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    double g = 0;
+    for (int r = 0; r < D; ++r) g += Jp[r][s] * om[r];
+    hp[21 + s] = g;
+#pragma unroll
+    for (int q = 0; q <= s; ++q) {
+      double h = 0;
+      for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jp[r][q];
+      hp[hk++] = h;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      double h = 0;
+      for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jl[r][q];
+      hpl[3 * s + q] = h;
+    }
+  }
+}
+
+// ---- buildSystem, point side: one thread per point sums its edges' Hll / bl
+// terms in insertion order (as g2o adds them edge by edge).
+__global__ __launch_bounds__(kLbaThreads) void k_lba_point_sum(LbaArgs a) {
   const int p = blockIdx.x * kLbaThreads + threadIdx.x;
   if (p >= a.n_pts) return;
-  const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
-  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+  double H[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = a.pt_begin[p]; i < a.pt_begin[p + 1]; ++i) {
-    const LbaEdgeDev e = a.edges[i];
-    const Se3 T = load_pose(poses + 7 * e.kf);
-    const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
-    const int D = e.ur < 0.f ? 2 : 3;
-    double Jl[3][3], Jp[3][6];
-    lba_jacobians(e, T, X, a.cam, Jl, Jp);
-    double r0, w;
-    huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
-    const double info = (double)e.inv_sigma2, wi = w * info;
-    double om[3];
+    const double* hl = a.hll_e + 12 * (size_t)i;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) om[r] = (-info * ev[r]) * w;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      for (int r = 0; r < D; ++r) b[s] += Jl[r][s] * om[r];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        double h = 0;
-        for (int r = 0; r < D; ++r) h += Jl[r][s] * wi * Jl[r][q];
-        H[3 * s + q] += h;
-      }
-    }
-    if (a.hidx[e.kf] < 0) continue;
-    double* hpl = a.hpl + 18 * (size_t)i;
-    double* hp = a.hpp_e + 27 * (size_t)i;  // 21 lower-triangle Hpp terms, then 6 bp terms
-    int hk = 0;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      double g = 0;
-      for (int r = 0; r < D; ++r) g += Jp[r][s] * om[r];
-      hp[21 + s] = g;
-#pragma unroll
-      for (int q = 0; q <= s; ++q) {
-        double h = 0;
-        for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jp[r][q];
-        hp[hk++] = h;
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        double h = 0;
-        for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jl[r][q];
-        hpl[3 * s + q] = h;
-      }
-    }
+    for (int k = 0; k < 12; ++k) H[k] += hl[k];
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k) a.hll[9 * (size_t)p + k] = H[k];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) a.bl[3 * (size_t)p + k] = b[k];
+  for (int k = 0; k < 3; ++k) a.bl[3 * (size_t)p + k] = H[9 + k];
   atomic_max_pos(a.diag + a.n_sys, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));  // Hll max
 }
 
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_pose_sum(LbaArgs a) {
 }
 
 // ---- Schur, point side (per trial lambda): Dinv = (Hll + lambda I)^-1 by
-// cofactors; per free edge W = Hpl Dinv and W bl.
+// cofactors (Eigen compute_inverse_size3).
 __global__ __launch_bounds__(kLbaThreads) void k_lba_schur_points(LbaArgs a, double lambda) {
   const int p = blockIdx.x * kLbaThreads + threadIdx.x;
   if (p >= a.n_pts) return;
@@ -315,101 +329,187 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_schur_points(LbaArgs a, dou
   const double det = A[0][0] * c00 + A[0][1] * c10 + A[0][2] * c20;
   if (det == 0) a.flags[0] = 1;  // singular landmark block: the trial fails (tmp = DBL_MAX)
   const double id = det != 0 ? 1.0 / det : 0.0;
-  double Di[3][3];
-  Di[0][0] = c00 * id;
-  Di[1][0] = c10 * id;
-  Di[2][0] = c20 * id;
-  Di[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) * id;
-  Di[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) * id;
-  Di[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) * id;
-  Di[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) * id;
-  Di[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) * id;
-  Di[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) * id;
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) a.dinv[9 * (size_t)p + 3 * r + c] = Di[r][c];
-  const double bl[3] = {a.bl[3 * (size_t)p], a.bl[3 * (size_t)p + 1], a.bl[3 * (size_t)p + 2]};
-  for (int i = a.pt_begin[p]; i < a.pt_begin[p + 1]; ++i) {
-    if (a.hidx[a.edges[i].kf] < 0) continue;
-    const double* B = a.hpl + 18 * (size_t)i;
-    double* W = a.w + 18 * (size_t)i;
-    double* wb = a.wb + 6 * (size_t)i;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      double wv[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        wv[c] = B[3 * s] * Di[0][c] + B[3 * s + 1] * Di[1][c] + B[3 * s + 2] * Di[2][c];
-        W[3 * s + c] = wv[c];
-      }
-      wb[s] = wv[0] * bl[0] + wv[1] * bl[1] + wv[2] * bl[2];
-    }
-  }
+  double* Di = a.dinv + 9 * (size_t)p;
+  Di[0] = c00 * id;
+  Di[3] = c10 * id;
+  Di[6] = c20 * id;
+  Di[1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) * id;
+  Di[4] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) * id;
+  Di[7] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) * id;
+  Di[2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) * id;
+  Di[5] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) * id;
+  Di[8] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) * id;
 }
 
-// ---- Schur, pose side: one block per free-pose pair (i <= j) sharing points.
-// S_ij = [i == j] Hpp_i - sum over shared points W_i Hpl_j^T (pair-list order);
+// W = Hpl_e Dinv_point (6 x 3)
+__device__ __forceinline__ void lba_w(const double* __restrict__ B, const double* __restrict__ Di,
+                                      double W[6][3]) {
+#pragma unroll
+  for (int s = 0; s < 6; ++s)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) W[s][c] = B[3 * s] * Di[c] + B[3 * s + 1] * Di[3 + c] + B[3 * s + 2] * Di[6 + c];
+}
+
+// ---- Schur, pose side: one 256-thread block per free-pose pair (i <= j)
+// sharing points.  The pair's (edge of i, edge of j) entries are strided
+// over the threads (each computes W_i Hpl_j^T, W from the point's Dinv),
+// then a fixed tree per entry of the 6 x 6 block:
+//   S_ij = [i == j] Hpp_i - sum W_i Hpl_j^T;
 // diagonal pairs also produce b_s = bp - sum over the pose's edges W bl.
-__global__ __launch_bounds__(64) void k_lba_schur_pairs(LbaArgs a) {
+__global__ __launch_bounds__(kLbaThreads) void k_lba_schur_pairs(LbaArgs a) {
+  __shared__ double red[4 * 42];
   const int pr = blockIdx.x;
   const int fi = a.pair_i[pr], fj = a.pair_j[pr];
   const int n = a.n_sys;
+  double acc[42];
+#pragma unroll
+  for (int k = 0; k < 42; ++k) acc[k] = 0;
+  for (int k = a.pair_begin[pr] + threadIdx.x; k < a.pair_begin[pr + 1]; k += kLbaThreads) {
+    const int ei = a.pair_ei[k], ej = a.pair_ej[k];
+    double W[6][3];
+    lba_w(a.hpl + 18 * (size_t)ei, a.dinv + 9 * (size_t)a.edges[ei].point, W);
+    const double* B = a.hpl + 18 * (size_t)ej;
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) acc[6 * s + q] += W[s][0] * B[3 * q] + W[s][1] * B[3 * q + 1] + W[s][2] * B[3 * q + 2];
+  }
+  if (fi == fj) {
+    for (int j = a.pose_begin[fi] + threadIdx.x; j < a.pose_begin[fi + 1]; j += kLbaThreads) {
+      const int e = a.pose_edges[j];
+      const int p = a.edges[e].point;
+      double W[6][3];
+      lba_w(a.hpl + 18 * (size_t)e, a.dinv + 9 * (size_t)p, W);
+      const double* bl = a.bl + 3 * (size_t)p;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) acc[36 + s] += W[s][0] * bl[0] + W[s][1] * bl[1] + W[s][2] * bl[2];
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 42; ++k) {
+    double v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[42 * wave + k] = v;
+  }
+  __syncthreads();
   const int t = threadIdx.x;
   if (t < 36) {
     const int s = t / 6, q = t - 6 * s;
-    double acc = fi == fj ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0;
-    for (int k = a.pair_begin[pr]; k < a.pair_begin[pr + 1]; ++k) {
-      const double* W = a.w + 18 * (size_t)a.pair_ei[k];
-      const double* B = a.hpl + 18 * (size_t)a.pair_ej[k];
-      acc -= W[3 * s] * B[3 * q] + W[3 * s + 1] * B[3 * q + 1] + W[3 * s + 2] * B[3 * q + 2];
-    }
-    a.sys[(size_t)(6 * fi + s) * n + 6 * fj + q] = acc;
-    a.sys[(size_t)(6 * fj + q) * n + 6 * fi + s] = acc;
+    const double sum = ((red[t] + red[42 + t]) + red[84 + t]) + red[126 + t];
+    const double v = (fi == fj ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
+    a.sys[(size_t)(6 * fi + s) * n + 6 * fj + q] = v;
+    a.sys[(size_t)(6 * fj + q) * n + 6 * fi + s] = v;
   } else if (fi == fj && t < 42) {
     const int s = t - 36;
-    double acc = a.bp[6 * (size_t)fi + s];
-    for (int j = a.pose_begin[fi]; j < a.pose_begin[fi + 1]; ++j) acc -= a.wb[6 * (size_t)a.pose_edges[j] + s];
-    a.sys[(size_t)n * n + 6 * fi + s] = acc;          // b_s
-    a.sys[(size_t)n * n + n + 6 * fi + s] = a.bp[6 * (size_t)fi + s];  // b_p (for the LM scale)
+    const double sum = ((red[t] + red[42 + t]) + red[84 + t]) + red[126 + t];
+    a.sys[(size_t)n * n + 6 * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
+    a.sys[(size_t)n * n + n + 6 * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (LM scale)
   }
 }
 
-// ---- reduced camera system: S + lambda I = L D L^T (right-looking, in LDS
-// when it fits), then x_p; also the pose part of computeScale and the
-// positivity of the pivots.  One block.
+// ---- reduced camera system: S + lambda I = L D L^T by 6 x 6 pose blocks
+// (no pivoting: the same factorisation as the oracle's scalar LDLT up to
+// rounding).  Per block step K: thread 0 factors the diagonal block; every
+// row below solves its panel row (l = v / d, v = a L_KK^-T), v kept in the
+// mirrored upper position; the trailing lower triangle takes the rank-6
+// update.  Then block-column forward / diagonal / backward substitution.
+// One block of 1024 threads, S in LDS when it fits.  Also the pose part of
+// computeScale and the positivity of the pivots.
 __global__ __launch_bounds__(1024) void k_lba_solve(LbaArgs a, double lambda, int in_lds) {
   extern __shared__ double Sl[];
   const int n = a.n_sys, t = threadIdx.x, nt = blockDim.x;
   double* S = in_lds ? Sl : a.work;
   const double* src = a.sys;
-  for (int i = t; i < n * n; i += nt) S[i] = src[i] + ((i / n) == (i % n) ? lambda : 0.0);
+  for (int r = t >> 5; r < n; r += nt >> 5)
+    for (int c = t & 31; c < n; c += 32) S[(size_t)r * n + c] = src[(size_t)r * n + c] + (r == c ? lambda : 0.0);
   double* y = a.xp;
   for (int i = t; i < n; i += nt) y[i] = src[(size_t)n * n + i];  // b_s
   __shared__ int bad;
   if (t == 0) bad = 0;
   __syncthreads();
-  for (int k = 0; k < n; ++k) {
-    const double dk = S[(size_t)k * n + k];
-    if (t == 0 && !(dk > 0)) bad = 1;
-    // v_i = S_ik (= L_ik d_k); L_ik = v_i / d_k -- row k of the upper part keeps v
-    for (int i = k + 1 + t; i < n; i += nt) {
-      const double v = S[(size_t)i * n + k];
-      S[(size_t)k * n + i] = v;
-      S[(size_t)i * n + k] = dk != 0 ? v / dk : 0.0;
+  const int nb = n / 6;
+  for (int K = 0; K < nb; ++K) {
+    const int k0 = 6 * K;
+    if (t == 0) {  // scalar LDLT of the (updated) diagonal block, in registers
+      double B[6][6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) B[r][c] = S[(size_t)(k0 + r) * n + k0 + c];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double d = B[c][c];
+#pragma unroll
+        for (int c2 = 0; c2 < c; ++c2) d -= B[c][c2] * B[c][c2] * B[c2][c2];
+        B[c][c] = d;
+        if (!(d > 0)) bad = 1;
+#pragma unroll
+        for (int r = c + 1; r < 6; ++r) {
+          double v = B[r][c];
+#pragma unroll
+          for (int c2 = 0; c2 < c; ++c2) v -= B[r][c2] * B[c][c2] * B[c2][c2];
+          B[r][c] = d != 0 ? v / d : 0.0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) S[(size_t)(k0 + r) * n + k0 + c] = B[r][c];
     }
     __syncthreads();
-    const int m = n - k - 1;
-    for (int idx = t; idx < m * m; idx += nt) {
-      const int ii = k + 1 + idx / m, jj = k + 1 + idx % m;
-      if (jj <= ii) S[(size_t)ii * n + jj] -= S[(size_t)ii * n + k] * S[(size_t)k * n + jj];
+    for (int i = k0 + 6 + t; i < n; i += nt) {  // panel rows
+      double v[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double x = S[(size_t)i * n + k0 + c];
+        for (int c2 = 0; c2 < c; ++c2) x -= v[c2] * S[(size_t)(k0 + c) * n + k0 + c2];
+        v[c] = x;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const double d = S[(size_t)(k0 + c) * n + k0 + c];
+        S[(size_t)(k0 + c) * n + i] = v[c];
+        S[(size_t)i * n + k0 + c] = d != 0 ? v[c] / d : 0.0;
+      }
+    }
+    __syncthreads();
+    // trailing lower triangle: thread (row group t >> 5, column lane t & 31)
+    for (int ii = k0 + 6 + (t >> 5); ii < n; ii += nt >> 5) {
+      double l[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) l[c] = S[(size_t)ii * n + k0 + c];
+      for (int jj = k0 + 6 + (t & 31); jj <= ii; jj += 32) {
+        double acc = 0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) acc += l[c] * S[(size_t)(k0 + c) * n + jj];
+        S[(size_t)ii * n + jj] -= acc;
+      }
     }
     __syncthreads();
   }
-  // forward (unit lower), diagonal, backward (L^T), column-oriented
-  for (int j = 0; j < n; ++j) {
-    const double yj = y[j];
-    for (int i = j + 1 + t; i < n; i += nt) y[i] -= S[(size_t)i * n + j] * yj;
+  // forward: unit lower L, block columns
+  for (int K = 0; K < nb; ++K) {
+    const int k0 = 6 * K;
+    if (t == 0) {
+      double yy[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) yy[c] = y[k0 + c];
+#pragma unroll
+      for (int c = 1; c < 6; ++c)
+#pragma unroll
+        for (int c2 = 0; c2 < c; ++c2) yy[c] -= S[(size_t)(k0 + c) * n + k0 + c2] * yy[c2];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) y[k0 + c] = yy[c];
+    }
+    __syncthreads();
+    for (int i = k0 + 6 + t; i < n; i += nt) {
+      double acc = 0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) acc += S[(size_t)i * n + k0 + c] * y[k0 + c];
+      y[i] -= acc;
+    }
     __syncthreads();
   }
   for (int i = t; i < n; i += nt) {
@@ -417,9 +517,27 @@ __global__ __launch_bounds__(1024) void k_lba_solve(LbaArgs a, double lambda, in
     y[i] = d != 0 ? y[i] / d : 0.0;
   }
   __syncthreads();
-  for (int j = n - 1; j >= 0; --j) {
-    const double yj = y[j];
-    for (int i = t; i < j; i += nt) y[i] -= S[(size_t)j * n + i] * yj;
+  // backward: L^T, block columns from the last
+  for (int K = nb - 1; K >= 0; --K) {
+    const int k0 = 6 * K;
+    if (t == 0) {
+      double yy[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) yy[c] = y[k0 + c];
+#pragma unroll
+      for (int c = 4; c >= 0; --c)
+#pragma unroll
+        for (int c2 = c + 1; c2 < 6; ++c2) yy[c] -= S[(size_t)(k0 + c2) * n + k0 + c] * yy[c2];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) y[k0 + c] = yy[c];
+    }
+    __syncthreads();
+    for (int r = t; r < k0; r += nt) {
+      double acc = 0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) acc += S[(size_t)(k0 + c) * n + r] * y[k0 + c];
+      y[r] -= acc;
+    }
     __syncthreads();
   }
   if (t == 0) {
@@ -506,9 +624,11 @@ hipError_t lba_errors(const LbaArgs& a, const double* poses, const double* pts, 
 }
 
 hipError_t lba_build(const LbaArgs& a, const double* poses, const double* pts, hipStream_t st) {
-  if (a.n_pts > 0)
-    hipLaunchKernelGGL(k_lba_linearize, dim3(blocks(a.n_pts, kLbaThreads)), dim3(kLbaThreads), 0, st,
+  if (a.n_edges > 0)
+    hipLaunchKernelGGL(k_lba_linearize, dim3(blocks(a.n_edges, kLbaThreads)), dim3(kLbaThreads), 0, st,
                        a, poses, pts);
+  if (a.n_pts > 0)
+    hipLaunchKernelGGL(k_lba_point_sum, dim3(blocks(a.n_pts, kLbaThreads)), dim3(kLbaThreads), 0, st, a);
   if (a.n_free > 0)
     hipLaunchKernelGGL(k_lba_pose_sum, dim3(a.n_free), dim3(kLbaThreads), 0, st, a);
   return hipGetLastError();
@@ -518,7 +638,8 @@ hipError_t lba_schur(const LbaArgs& a, double lambda, hipStream_t st) {
   if (a.n_pts > 0)
     hipLaunchKernelGGL(k_lba_schur_points, dim3(blocks(a.n_pts, kLbaThreads)), dim3(kLbaThreads), 0,
                        st, a, lambda);
-  if (a.n_pairs > 0) hipLaunchKernelGGL(k_lba_schur_pairs, dim3(a.n_pairs), dim3(64), 0, st, a);
+  if (a.n_pairs > 0)
+    hipLaunchKernelGGL(k_lba_schur_pairs, dim3(a.n_pairs), dim3(kLbaThreads), 0, st, a);
   return hipGetLastError();
 }
 

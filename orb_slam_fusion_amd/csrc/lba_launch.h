@@ -31,8 +31,7 @@ struct LbaArgs {
   double* err;       // [3 E] errors of the last computeActiveErrors
   double* hpl;       // [18 E] Hpl = Jp^T W Jl (6 x 3)
   double* hpp_e;     // [27 E] per-edge Hpp (lower, 21) + bp (6) terms
-  double* w;         // [18 E] Hpl Dinv
-  double* wb;        // [6 E]  Hpl Dinv bl
+  double* hll_e;     // [12 E] per-edge Hll (9) + bl (3) terms
   double* hll;       // [9 P]
   double* bl;        // [3 P]
   double* dinv;      // [9 P]
