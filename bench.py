@@ -94,6 +94,7 @@ def main() -> int:
                          "frames of a step split evenly between them)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
     args = ap.parse_args()
 
     import torch
@@ -251,6 +252,13 @@ def main() -> int:
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(frames, probs, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_lba:
+        # SURVEY §8 row c, reported beside the headline metric (not part of it):
+        # C4 LocalBundleAdjustment window, GPU vs the CPU oracle (1 thread)
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_lba import measure  # noqa: E402
+
+        result["lba"] = measure(calls=10, cpu_calls=0 if args.no_cpu_baseline else 3)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()

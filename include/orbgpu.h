@@ -194,7 +194,8 @@ void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
  * initial keyframe, :1161, and every fixed camera, :1169-1183).  Points
  * [pt_begin, pt_end) and their edges are this call's shard (the whole window:
  * 0, n_pts); with reduce == NULL the shard must be the whole window.
- * *stop_flag (optional) is polled before every LM iteration (pbStopFlag).
+ * *stop_flag (optional; the reference's bool, 1 byte, nonzero = stop) is polled
+ * before every LM iteration (pbStopFlag, SparseOptimizer::terminate).
  * Outputs: optimised poses (float, unit quaternion; poses_out_d optional
  * doubles), pts_out rows of the shard's points, outlier[i] for the shard's
  * edges (chi2 > 5.991 / 7.815 or depth <= 0), stats (optional, 6 doubles):
@@ -203,7 +204,7 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* c, const orbgpu_camera* cam, i
                                   const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
                                   const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
                                   int pt_begin, int pt_end, int iterations,
-                                  const volatile int* stop_flag, orbgpu_lba_reduce_fn reduce,
+                                  const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce,
                                   void* user, orbgpu_pose* poses_out, double* poses_out_d,
                                   float* pts_out, uint8_t* outlier, double* stats);
 

@@ -104,7 +104,7 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
                                   const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
                                   const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
                                   int pt_begin, int pt_end, int iterations,
-                                  const volatile int* stop_flag, orbgpu_lba_reduce_fn reduce,
+                                  const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce,
                                   void* user, orbgpu_pose* poses_out, double* poses_out_d,
                                   float* pts_out, uint8_t* outlier, double* stats) {
   if (!h || !cam || n_kf <= 0 || !poses_in || !fixed || n_pts < 0 || n_edges < 0 ||

@@ -64,7 +64,7 @@ class LocalBundleAdjuster:
             pass
 
     def optimize(self, problem, iterations: int = 10, pt_range=None, group=None,
-                 stop_flag: Optional[ctypes.c_int] = None) -> dict:
+                 stop_flag: Optional[ctypes.c_uint8] = None) -> dict:
         """Returns {"poses": float32 [n_kf, 7], "poses_d": float64 [n_kf, 7],
         "pts": float32 [n_pts, 3] (this shard's rows), "outlier": uint8 [E]
         (this shard's edges), "stats": float64 [6]}.  ``group``: a

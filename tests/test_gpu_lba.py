@@ -63,7 +63,7 @@ def test_lba_stop_flag(gpu_available):
     import ctypes
 
     p = synth.lba_problem(seed=5, n_kf=5, n_pts=40, obs_per_pt=3, n_fixed=1)
-    flag = ctypes.c_int(1)
+    flag = ctypes.c_uint8(1)
     got = LocalBundleAdjuster().optimize(p, stop_flag=flag)
     assert got["stats"][2] == 0  # no LM iteration ran
     assert np.allclose(got["poses"], p.poses_init)
