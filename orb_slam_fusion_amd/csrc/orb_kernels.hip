@@ -106,21 +106,69 @@ __device__ __forceinline__ const uint8_t* level_plane(const PlanHeader* P, const
 // --------------------------------------------------------------------------
 // k_resize: cv::resize INTER_LINEAR, 8UC1.  Horizontal
 // taps are (sx, a0, a1) per column, vertical (r0, r1, b0, b1) per row, both
-// precomputed by the planner.  Columns below vec_end use the 128-bit SIMD
+// precomputed by the planner.  Columns below vec8_end use the 128-bit SIMD
 // rounding ((H>>4)*b >> 16 summed, +2 >> 2), the tail the scalar
 // (H0*b0 + H1*b1 + 2^21) >> 22 -- exactly where OpenCV switches.
-// A 256-thread block makes a 256 x 8 output tile: the source window is staged
-// in LDS with dword loads, each thread then produces 8 consecutive pixels
-// (one 8-byte store).
+// A 256-thread block makes a kResizeTileW x kResizeTileH output tile from its
+// source window staged in LDS (dwordx4 loads).  Each wave owns kResizeTileH/4
+// consecutive output rows of it, each lane 4 adjacent columns; the wave
+// streams the source rows once: the horizontal pass of a row (3 LDS dwords,
+// two v_alignbyte_b32, then per column a v_perm_b32 with a per-lane selector
+// and one v_dot2_u32_u16: h = s0*a0 + s1*a1) is kept in registers for the
+// output rows that share it, with the next row's dwords already in flight.
+// Tap weights lie in [0, 2048] and sum to <= 2049, so (h>>4)*b < 2^24 (full-
+// rate v_mul_u32_u24) and every result is <= 255.
 // --------------------------------------------------------------------------
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ ushort2_t as_us2(uint32_t v) {
+  return __builtin_bit_cast(ushort2_t, v);
+}
+
+struct RsRow {  // one source row of a lane's 4 columns: raw bytes
+  uint32_t d[3];
+};
+__device__ __forceinline__ RsRow rs_load(const uint8_t* __restrict__ row, int base4,
+                                         const int (&bi)[4], bool bytewise) {
+  RsRow r;
+  if (!bytewise) {
+    r.d[0] = *reinterpret_cast<const uint32_t*>(row + base4);
+    r.d[1] = *reinterpret_cast<const uint32_t*>(row + base4 + 4);
+    r.d[2] = *reinterpret_cast<const uint32_t*>(row + base4 + 8);
+  } else {  // tap span > 8 bytes (scale factors above 2): the 8 tap bytes
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      r.d[j] = (uint32_t)row[bi[2 * j] & 0xffff] | ((uint32_t)row[bi[2 * j] >> 16] << 8) |
+               ((uint32_t)row[bi[2 * j + 1] & 0xffff] << 16) | ((uint32_t)row[bi[2 * j + 1] >> 16] << 24);
+    r.d[2] = 0;
+  }
+  return r;
+}
+// h[k] = s0*a0 + s1*a1 of column k; hq[k] = h[k] >> 4 (the SIMD path's input)
+__device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t (&sel)[4],
+                                         const uint32_t (&aw)[4], bool bytewise, uint32_t (&h)[4],
+                                         uint32_t (&hq)[4]) {
+  if (!bytewise) {
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(r.d[1], r.d[0], off);
+    const uint32_t w1 = __builtin_amdgcn_alignbyte(r.d[2], r.d[1], off);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      h[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(w1, w0, sel[k])), as_us2(aw[k]), 0u, false);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      h[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(0u, r.d[k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u)),
+                                    as_us2(aw[k]), 0u, false);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hq[k] = h[k] >> 4;
+}
+
 __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
                                                 const int* __restrict__ rs_tab, ImgSrc src,
                                                 uint8_t* __restrict__ pyr, int l) {
-  // Branch-free by construction: every load and LDS store is unconditional
-  // (clamped indices; duplicates write identical bytes), and single-tap
-  // columns (x >= xmax) carry taps (2048, 0) from the planner.
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int RPT = kResizeTileH / 8;  // output rows per thread
+  constexpr int RW = kResizeTileH / 4;  // output rows per wave
   const LevelGeom& g = P->lev[l];
   const int sw = P->lev[l - 1].w;
   const int nb = gridDim.x * gridDim.y * gridDim.z;
@@ -138,14 +186,14 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
 
-  // per-thread taps, fetched up front
-  const int xs = x0 + (threadIdx.x & 31) * 8;
-  int2 xa[8];
+  // taps, fetched up front (before any store, so no wait ever queues behind one)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int x = x0 + 4 * lane;
+  const int ys = y0 + RW * wave;  // wave-uniform first output row
+  int2 xa[4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) xa[k] = xt[min(xs + k, g.w - 1)];
-  int2 yv[RPT];
-#pragma unroll
-  for (int rr = 0; rr < RPT; ++rr) yv[rr] = yt[min(y0 + (int)(threadIdx.x >> 5) + 8 * rr, yl)];
+  for (int k = 0; k < 4; ++k) xa[k] = xt[min(x + k, g.w - 1)];
+  const int2 tl = yt[min(ys + (lane & (RW - 1)), yl)];
 
   if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && c1 < sp) {
     const int nq = ncol >> 4, total = nrow * nq;
@@ -169,46 +217,75 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
       lds[i] = S[(size_t)(rr0 + r) * sp + min(c0 + c, sw - 1)];
     }
   }
-  __syncthreads();
 
-  uint8_t* Dbase = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + xs;
-  const int xoff = -c0;
+  // per-lane column taps -> byte selectors relative to the lane's LDS window
+  int sx[4], sx1[4];
+  uint32_t aw[4], tail_k = 0;
 #pragma unroll
-  for (int rr = 0; rr < RPT; ++rr) {
-    const int r0 = (yv[rr].x & 0xffff) - rr0, r1 = (yv[rr].x >> 16) - rr0;
-    const int b0 = (int)(short)(yv[rr].y & 0xffff), b1 = (int)(short)(yv[rr].y >> 16);
-    const uint8_t* L0 = lds + r0 * ncol + xoff;
-    const uint8_t* L1 = lds + r1 * ncol + xoff;
-    int s00[8], s01[8], s10[8], s11[8];
+  for (int k = 0; k < 4; ++k) {
+    sx[k] = xa[k].x - c0;
+    sx1[k] = min(xa[k].x + 1, c1) - c0;
+    aw[k] = (uint32_t)xa[k].y;
+    if (min(x + k, g.w - 1) >= g.vec8_end) tail_k |= 1u << k;
+  }
+  const int lo = min(min(sx[0], sx[1]), min(sx[2], sx[3]));
+  const int hi = max(max(sx1[0], sx1[1]), max(sx1[2], sx1[3]));
+  const int base4 = lo & ~3, off = lo & 3;
+  uint32_t sel[4];
+  int bi[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {  // 32 independent LDS reads
-      const int sx = xa[k].x, sx1 = min(sx + 1, c1);
-      s00[k] = L0[sx];
-      s01[k] = L0[sx1];
-      s10[k] = L1[sx];
-      s11[k] = L1[sx1];
-    }
-    uint32_t w[2] = {0u, 0u};
+  for (int k = 0; k < 4; ++k) {
+    sel[k] = (uint32_t)(sx[k] - lo) | 0x0c00u | ((uint32_t)(sx1[k] - lo) << 16) | 0x0c000000u;
+    bi[k] = sx[k] | (sx1[k] << 16);
+  }
+  const bool active = x < g.w;
+  const bool bytewise = __builtin_amdgcn_ballot_w64(active && hi - lo > 7) != 0;
+  const bool any_tail = __builtin_amdgcn_ballot_w64(active && tail_k != 0) != 0;
+  __syncthreads();
+  if (ys > yl) return;  // after the barrier: every wave staged its share
+
+  // stream the source rows: hA/qA = row p, hB/qB = row p+1, row p+2 in flight
+  const int last = nrow - 1;
+  auto rowp = [&](int r) { return lds + min(r, last) * ncol; };
+  uint32_t hA[4], hB[4], qA[4], qB[4];
+  RsRow nd;
+  int p = -1000;
+  uint8_t* D = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + x;
+  const int ye = min(ys + RW - 1, yl);
+  for (int y = ys; y <= ye; ++y) {
+    const int tx = __builtin_amdgcn_readlane(tl.x, y - ys), ty = __builtin_amdgcn_readlane(tl.y, y - ys);
+    const int r0 = (tx & 0xffff) - rr0, r1 = (int)((uint32_t)tx >> 16) - rr0;
+    if (r0 < p || r0 > p + 2) {
+      p = r0;
+      rs_horiz(rs_load(rowp(p), base4, bi, bytewise), off, sel, aw, bytewise, hA, qA);
+      rs_horiz(rs_load(rowp(p + 1), base4, bi, bytewise), off, sel, aw, bytewise, hB, qB);
+      nd = rs_load(rowp(p + 2), base4, bi, bytewise);
+    } else {
+      while (p < r0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int a0 = (int)(short)(xa[k].y & 0xffff), a1 = (int)(short)(xa[k].y >> 16);
-      const int h0 = s00[k] * a0 + s01[k] * a1, h1 = s10[k] * a0 + s11[k] * a1;
-      const int m0 = (max(min(h0 >> 4, 32767), -32768) * b0) >> 16;
-      const int m1 = (max(min(h1 >> 4, 32767), -32768) * b1) >> 16;
-      const int vv = (max(min(m0 + m1, 32767), -32768) + 2) >> 2;
-      const int vs = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-      const int v = xs + k < g.vec8_end ? vv : vs;
-      w[k >> 2] |= (uint32_t)min(max(v, 0), 255) << (8 * (k & 3));
-    }
-    const int y = y0 + (int)(threadIdx.x >> 5) + 8 * rr;
-    if (y <= yl && xs < g.w) {
-      uint8_t* D = Dbase + (size_t)y * g.pitch;
-      if (xs + 8 <= g.w) {
-        *reinterpret_cast<uint2*>(D) = make_uint2(w[0], w[1]);
-      } else {
-        for (int k = 0; k < g.w - xs; ++k) D[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        for (int k = 0; k < 4; ++k) hA[k] = hB[k], qA[k] = qB[k];
+        rs_horiz(nd, off, sel, aw, bytewise, hB, qB);
+        ++p;
+        nd = rs_load(rowp(p + 2), base4, bi, bytewise);
       }
     }
+    // r1 is r0 + 1, or r0 at the clamped first / last source row
+    const bool same = r1 == r0;
+    const uint32_t b0 = (uint32_t)ty & 0xffffu, b1 = (uint32_t)ty >> 16;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t q1 = same ? qA[k] : qB[k];
+      v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(q1, b1) >> 16) + 2) >> 2;
+    }
+    if (any_tail) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (tail_k & (1u << k)) v[k] = (hA[k] * b0 + (same ? hA[k] : hB[k]) * b1 + (1u << 21)) >> 22;
+    }
+    // columns past w land in the pitch padding (pitch is a multiple of 16)
+    if (active)
+      *reinterpret_cast<uint32_t*>(D + (size_t)y * g.pitch) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
   }
 }
 
@@ -226,11 +303,6 @@ __device__ __forceinline__ int reflect101(int i, int n) {
   return i >= n ? 2 * n - 2 - i : i;
 }
 
-typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ ushort2_t as_us2(uint32_t v) {
-  return __builtin_bit_cast(ushort2_t, v);
-}
 
 // Every lane owns output columns x..x+3 (x = 4k) of R rows.  It loads the 12
 // source bytes x-4..x+7 of each row as 3 dwords from an in-row offset clamped

@@ -143,7 +143,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         const int r0 = tab[g.rs_y + 2 * ya] & 0xffff, r1 = tab[g.rs_y + 2 * yb] >> 16;
         g.rs_src_rows = std::max(g.rs_src_rows, r1 - r0 + 1);
       }
-      rs_lds = std::max(rs_lds, g.rs_src_cols * g.rs_src_rows);
+      rs_lds = std::max(rs_lds, g.rs_src_cols * g.rs_src_rows + 16);  // + k_resize's 3-dword overreach
       int x = 0;
       for (; x <= g.w - 16; x += 16) {
       }

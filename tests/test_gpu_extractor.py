@@ -61,6 +61,8 @@ def _compare(params, img, lapping=(0, 0)):
     ctx = f"{w}x{h} params={params} lapping={lapping}"
     for lev, lvl in enumerate(ex.img_pyramid_):
         assert np.array_equal(lvl, orc.level(lev)), f"{ctx}: pyramid level {lev} differs"
+        ob = orc.level(lev, blurred=True)
+        assert np.array_equal(_stage(ex, 0, lev).reshape(ob.shape), ob), f"{ctx}: blurred level {lev} differs"
     if len(k) != len(k_ref) or k.tobytes() != k_ref.tobytes() or (
         len(k) and d.tobytes() != d_ref.tobytes()
     ):
@@ -102,6 +104,13 @@ def test_odd_sizes(gpu_available, size):
     full, _ = synth.stereo_frame(20, w=w, h=h)
     L = 8 if min(w, h) >= 300 else 6
     _compare((1000, 1.2, L, 20, 7), full)
+
+
+@pytest.mark.parametrize("params", [(1000, 1.6, 5, 20, 7), (1000, 1.5, 6, 20, 7), (1000, 2.0, 4, 20, 7)])
+def test_large_scale_factors(gpu_available, params):
+    # coarser pyramids: wider resize tap spans, fewer and smaller levels
+    full, _ = synth.stereo_frame(21, w=1024, h=768)
+    _compare(params, full)
 
 
 def test_low_contrast_uses_min_threshold(gpu_available):
