@@ -93,6 +93,38 @@ orbgpu_status orbgpu_extract_batch(orbgpu_extractor* h, const uint8_t* d_imgs, i
                                    const int lapping[2], orbgpu_keypoint* d_kps, uint8_t* d_descs,
                                    int cap_per_image, int* d_n, int* d_mono, void* hip_stream);
 
+/* ------------------------------------------------------------------------ */
+/* Stereo matching (rectified pinhole stereo).
+ * Replaces: void Frame::ComputeStereoMatches() (include/map/frame.h,
+ *   src/map/frame.cc:828-986), called by the stereo Frame constructor after
+ *   both ExtractORB calls (frame.cc:179-189).  Per left keypoint i: uright[i] =
+ *   Frame::mvuRight[i], depth[i] = Frame::mvDepth[i] (-1 when unmatched).
+ *   bf = Frame::bf_ (mbf), mb = Frame::mb (bf / fx); TH_HIGH / TH_LOW =
+ *   100 / 50 (orb_matcher.cc:35-36).  Window reads beyond a level follow the
+ *   reference's reflect-101 padded pyramid storage (orb_extractor.cc:1105-1114).
+ *   A frame whose match list ends up empty is left as matched (the reference
+ *   reads the median of an empty vector there, frame.cc:966).
+ *
+ * Batch: the handle's last orbgpu_extract_batch call took 2 * n_frames images
+ *   ordered [left 0, right 0, left 1, right 1, ...]; d_imgs / stride /
+ *   image_pitch are that call's level-0 planes and d_kps / d_descs /
+ *   cap_per_image / d_n its outputs, all still on the device.  Writes
+ *   d_uright / d_depth as [n_frames][cap_per_image] floats, stream-ordered on
+ *   hip_stream (NULL: the handle's stream). */
+orbgpu_status orbgpu_stereo_match_batch(orbgpu_extractor* h, int n_frames, const uint8_t* d_imgs,
+                                        int stride, size_t image_pitch, const orbgpu_keypoint* d_kps,
+                                        const uint8_t* d_descs, int cap_per_image, const int* d_n,
+                                        float bf, float mb, float* d_uright, float* d_depth,
+                                        void* hip_stream);
+
+/* Host path: `left` / `right` are the Frame's two extractors
+ *   (mpORBextractorLeft / Right) right after their orbgpu_extract calls on the
+ *   frame's images (same parameters and size); their keypoints, descriptors
+ *   and pyramids are used where they lie on the device.  Writes N = the left
+ *   call's keypoint count floats to uright / depth (host), N <= cap. */
+orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* right, float bf,
+                                  float mb, float* uright, float* depth, int cap);
+
 /* Synchronises the handle's last batch and returns the first device-side
  * error (ORBGPU_ERR_CAPACITY when an internal bound was hit), else ORBGPU_OK. */
 orbgpu_status orbgpu_extractor_check(orbgpu_extractor* h);

@@ -54,6 +54,8 @@ def lib() -> ctypes.CDLL:
         "orc_pose_opt": (_I, [_P, _P, _P, _I, _P, _P, _P]),
         "orc_lba_edge_linearize": (_I, [_P, _P, _P, _P, _P, _P, _P]),
         "orc_se3_exp_compose": (None, [_P, _P, _P]),
+        "orc_stereo_match": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
+                                  _P, _P]),
         "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, LBA_REDUCE_FN, _P, _P, _P,
                          _P, _P]),
     }
@@ -232,3 +234,29 @@ def se3_exp_compose(u6, pose7):
     out = np.zeros(7)
     lib().orc_se3_exp_compose(_p(u6), _p(pose7), _p(out))
     return out
+
+
+def stereo_match(kps_l, desc_l, kps_r, desc_r, pyr_l, pyr_r, scale, inv_scale, bf, mb):
+    """Frame::ComputeStereoMatches (frame.cc:828-986) on the oracle: returns
+    (uright, depth, kept).  pyr_l / pyr_r: lists of the level planes."""
+    kl = np.ascontiguousarray(kps_l, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kps_r, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(desc_l, np.uint8)
+    dr = np.ascontiguousarray(desc_r, np.uint8)
+    L = len(pyr_l)
+    pl = [np.ascontiguousarray(a, np.uint8) for a in pyr_l]
+    pr = [np.ascontiguousarray(a, np.uint8) for a in pyr_r]
+    ptr_l = (ctypes.c_void_p * L)(*[a.ctypes.data for a in pl])
+    ptr_r = (ctypes.c_void_p * L)(*[a.ctypes.data for a in pr])
+    lw = np.array([a.shape[1] for a in pl], np.int32)
+    lh = np.array([a.shape[0] for a in pl], np.int32)
+    sl = np.array([a.strides[0] for a in pl], np.int32)
+    sr = np.array([a.strides[0] for a in pr], np.int32)
+    sc = np.ascontiguousarray(scale, np.float32)
+    isc = np.ascontiguousarray(inv_scale, np.float32)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    kept = lib().orc_stereo_match(_p(kl), len(kl), _p(dl), _p(kr), len(kr), _p(dr), _p(sc), _p(isc),
+                                  ctypes.cast(ptr_l, ctypes.c_void_p), ctypes.cast(ptr_r, ctypes.c_void_p),
+                                  _p(lw), _p(lh), _p(sl), _p(sr), float(bf), float(mb), _p(ur), _p(dep))
+    return ur, dep, kept

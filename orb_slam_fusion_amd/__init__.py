@@ -1,8 +1,8 @@
 """orb_slam_fusion_amd -- MI355X (gfx950) ORB front-end and pose optimisation.
 
 Drop-in for the hot path of J094/orb_slam_fusion:
-``ORB_SLAM_FUSION::OrbExtractor::operator()`` and
-``Optimizer::PoseOptimization``.  The compute runs in hand-written HIP kernels
+``ORB_SLAM_FUSION::OrbExtractor::operator()``, ``Optimizer::PoseOptimization``,
+``Optimizer::LocalBundleAdjustment`` and ``Frame::ComputeStereoMatches``.  The compute runs in hand-written HIP kernels
 (csrc/*.hip) behind the C ABI of include/orbgpu.h; this package is the host
 mirror of the reference interface over that ABI.
 """
@@ -10,6 +10,7 @@ from ._lib import KEYPOINT_DTYPE, POSE_OBS_DTYPE, OrbGpuError, library_path
 from .extractor import OrbExtractor
 from .lba import LocalBundleAdjuster
 from .optimizer import PoseFrame, PoseOptimizer
+from .stereo import compute_stereo_matches
 
 __all__ = [
     "LocalBundleAdjuster",
@@ -19,5 +20,6 @@ __all__ = [
     "OrbExtractor",
     "PoseFrame",
     "PoseOptimizer",
+    "compute_stereo_matches",
     "library_path",
 ]

@@ -97,6 +97,11 @@ SIGNATURES = {
         [_P, _P, _I, _I, _I, _I, ctypes.c_size_t, _P, _P, _P, _I, _P, _P, _P],
     ),
     "orbgpu_extractor_check": (_I, [_P]),
+    "orbgpu_stereo_match_batch": (
+        _I,
+        [_P, _I, _P, _I, ctypes.c_size_t, _P, _P, _I, _P, ctypes.c_float, ctypes.c_float, _P, _P, _P],
+    ),
+    "orbgpu_stereo_match": (_I, [_P, _P, ctypes.c_float, ctypes.c_float, _P, _P, _I]),
     "orbgpu_extractor_stage": (_I, [_P, _I, _I, _P, _I]),
     "orbgpu_extractor_profile": (_I, [_P, _I]),
     "orbgpu_extractor_profile_read": (_I, [_P, _P]),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -13,6 +14,7 @@
 #include "../../include/orbgpu.h"
 #include "orb_launch.h"
 #include "orb_plan_host.h"
+#include "stereo_launch.h"
 
 using namespace orbgpu;
 
@@ -66,6 +68,13 @@ struct orbgpu_extractor {
   std::vector<uint8_t> host_pyr;
   bool host_pyr_valid = false;
   int last_w = 0, last_h = 0;
+
+  // stereo matcher scratch (row lists, row ends, window distances) and the
+  // host path's device outputs
+  uint16_t* d_st_lists = nullptr;
+  int *d_st_rowend = nullptr, *d_st_sad = nullptr;
+  float* d_st_out = nullptr;
+  size_t st_lists = 0, st_rowend = 0, st_sad = 0, st_out = 0;
 
   // optional per-stage event profiling of batch calls (a ring of event sets)
   std::vector<hipEvent_t> prof_events;
@@ -182,6 +191,54 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   return a;
 }
 
+// Row-list entries per frame: a right keypoint spans at most
+// 2 * ceil(2 * s_max) + 3 rows (frame.cc:844-849).
+int stereo_list_cap(const HostPlan& p, int cap) {
+  const float smax = p.scale.back();
+  return cap * (2 * (int)std::ceil(2.0f * smax) + 3);
+}
+
+orbgpu_status ensure_stereo(orbgpu_extractor* h, int n_frames, int cap) {
+  const size_t lists = (size_t)n_frames * stereo_list_cap(h->plan, cap);
+  const size_t rowend = (size_t)n_frames * h->plan.hdr.height, sad = (size_t)n_frames * cap;
+  if (lists > h->st_lists) {
+    dfree(h->d_st_lists);
+    if (dalloc(&h->d_st_lists, lists)) return ORBGPU_ERR_NOMEM;
+    h->st_lists = lists;
+  }
+  if (rowend > h->st_rowend) {
+    dfree(h->d_st_rowend);
+    if (dalloc(&h->d_st_rowend, rowend)) return ORBGPU_ERR_NOMEM;
+    h->st_rowend = rowend;
+  }
+  if (sad > h->st_sad) {
+    dfree(h->d_st_sad);
+    if (dalloc(&h->d_st_sad, sad)) return ORBGPU_ERR_NOMEM;
+    h->st_sad = sad;
+  }
+  return ORBGPU_OK;
+}
+
+StereoLaunch make_stereo(orbgpu_extractor* h, int n_frames, int cap, float bf, float mb,
+                         float* uright, float* depth, size_t out_fstride) {
+  StereoLaunch a{};
+  a.plan = h->d_plan;
+  a.n_frames = n_frames;
+  a.cap = cap;
+  a.rows = h->plan.hdr.height;
+  a.list_cap = stereo_list_cap(h->plan, cap);
+  a.bf = bf;
+  a.mb = mb;
+  a.uright = uright;
+  a.depth = depth;
+  a.out_fstride = out_fstride;
+  a.lists = h->d_st_lists;
+  a.row_end = h->d_st_rowend;
+  a.sad = h->d_st_sad;
+  a.err = h->d_err;
+  return a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -243,6 +300,10 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_kps);
   dfree(h->d_descs);
   dfree(h->d_nm);
+  dfree(h->d_st_lists);
+  dfree(h->d_st_rowend);
+  dfree(h->d_st_sad);
+  dfree(h->d_st_out);
   for (hipEvent_t e : h->prof_events) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -445,6 +506,88 @@ int orbgpu_extractor_stage(orbgpu_extractor* h, int which, int level, void* out,
                : -1;
   }
   return -1;
+}
+
+orbgpu_status orbgpu_stereo_match_batch(orbgpu_extractor* h, int n_frames, const uint8_t* d_imgs,
+                                        int stride, size_t image_pitch, const orbgpu_keypoint* d_kps,
+                                        const uint8_t* d_descs, int cap_per_image, const int* d_n,
+                                        float bf, float mb, float* d_uright, float* d_depth,
+                                        void* hip_stream) {
+  if (!h || n_frames <= 0 || !d_imgs || !d_kps || !d_descs || !d_n || !d_uright || !d_depth ||
+      cap_per_image <= 0 || cap_per_image > 4096 || !(mb > 0.0f))
+    return ORBGPU_ERR_INVALID;
+  if (h->plan_w < 0 || h->ws_images < 2 * n_frames) return ORBGPU_ERR_INVALID;  // no batch yet
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu_status st = ensure_stereo(h, n_frames, cap_per_image);
+  if (st != ORBGPU_OK) return st;
+  const PlanHeader& P = h->plan.hdr;
+  StereoLaunch a = make_stereo(h, n_frames, cap_per_image, bf, mb, d_uright, d_depth,
+                               (size_t)cap_per_image);
+  const float* kps = reinterpret_cast<const float*>(d_kps);
+  for (int side = 0; side < 2; ++side) {  // images 2f (left), 2f + 1 (right)
+    StereoSide& s = side ? a.R : a.L;
+    s.img0 = d_imgs + side * image_pitch;
+    s.img_fstride = 2 * image_pitch;
+    s.img_stride = stride;
+    s.pyr = h->d_pyr + (size_t)side * P.pyr_bytes;
+    s.pyr_fstride = 2 * (size_t)P.pyr_bytes;
+    s.kps = kps + (size_t)side * cap_per_image * 7;
+    s.kp_fstride = 2 * (size_t)cap_per_image;
+    s.desc = d_descs + (size_t)side * cap_per_image * 32;
+    s.n = d_n + side;
+    s.n_fstride = 2;
+  }
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+  return launch_stereo(a, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
+orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* right, float bf,
+                                  float mb, float* uright, float* depth, int cap) {
+  if (!left || !right || !uright || !depth || cap < 0 || !(mb > 0.0f)) return ORBGPU_ERR_INVALID;
+  // both handles must hold a host-path extraction of one geometry and parameter set
+  if (left->last_w <= 0 || right->last_w != left->last_w || right->last_h != left->last_h ||
+      std::memcmp(&left->params, &right->params, sizeof(left->params)) != 0 ||
+      left->device != right->device)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(left->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  const PlanHeader& P = left->plan.hdr;
+  const int kcap = P.kp_slots;
+  orbgpu_status st = ensure_stereo(left, 1, kcap);
+  if (st != ORBGPU_OK) return st;
+  if ((size_t)2 * kcap > left->st_out) {
+    dfree(left->d_st_out);
+    if (dalloc(&left->d_st_out, (size_t)2 * kcap)) return ORBGPU_ERR_NOMEM;
+    left->st_out = (size_t)2 * kcap;
+  }
+  StereoLaunch a = make_stereo(left, 1, kcap, bf, mb, left->d_st_out, left->d_st_out + kcap,
+                               (size_t)kcap);
+  for (int side = 0; side < 2; ++side) {
+    orbgpu_extractor* h = side ? right : left;
+    StereoSide& s = side ? a.R : a.L;
+    s.img0 = h->d_img;
+    s.img_stride = h->plan.hdr.lev[0].pitch;
+    s.pyr = h->d_pyr;
+    s.kps = reinterpret_cast<const float*>(h->d_kps);
+    s.desc = h->d_descs;
+    s.n = h->d_nm;
+  }
+  int n = 0, err = 0;
+  if (launch_stereo(a, left->stream) != hipSuccess ||
+      hipMemcpyAsync(&n, left->d_nm, sizeof(int), hipMemcpyDeviceToHost, left->stream) ||
+      hipMemcpyAsync(&err, left->d_err, sizeof(int), hipMemcpyDeviceToHost, left->stream) ||
+      hipStreamSynchronize(left->stream))
+    return ORBGPU_ERR_DEVICE;
+  if (err) {
+    (void)hipMemset(left->d_err, 0, sizeof(int));
+    return ORBGPU_ERR_CAPACITY;
+  }
+  n = std::min(n, kcap);
+  if (n > cap) return ORBGPU_ERR_CAPACITY;
+  if (n > 0 && (hipMemcpy(uright, left->d_st_out, (size_t)n * sizeof(float), hipMemcpyDeviceToHost) ||
+                hipMemcpy(depth, left->d_st_out + kcap, (size_t)n * sizeof(float),
+                          hipMemcpyDeviceToHost)))
+    return ORBGPU_ERR_DEVICE;
+  return ORBGPU_OK;
 }
 
 orbgpu_status orbgpu_extractor_check(orbgpu_extractor* h) {

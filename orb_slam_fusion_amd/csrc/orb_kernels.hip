@@ -21,9 +21,22 @@
 
 namespace orbgpu {
 
-__constant__ int8_t c_pattern[1024] = {
+constexpr int8_t kPattern[1024] = {
 #include "pattern31.inc"
 };
+// bit_pattern_31_ as floats (x0, y0, x1, y1) per test: one dwordx4 per lane
+struct PatternF {
+  float4 p[256];
+};
+constexpr PatternF make_pattern_f() {
+  PatternF t{};
+  for (int i = 0; i < 256; ++i)
+    t.p[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 1], (float)kPattern[4 * i + 2],
+                    (float)kPattern[4 * i + 3]};
+  return t;
+}
+__constant__ PatternF c_pattern_f_tab = make_pattern_f();
+#define c_pattern_f (c_pattern_f_tab.p)
 
 // Profiling build only (make stamps): per-phase s_memtime totals.
 #ifdef ORB_STAMPS
@@ -500,11 +513,15 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     return;
   }
   // LDS (fast_cell_lds_bytes): ROI rows of ls bytes (ROI column x at row byte
-  // lead + x), score map, u16 survivor list (bit 15 = keypoint flag).
+  // lead + x), score map of the detection area with a zero border (row pitch
+  // dw + 2), u16 survivor list.  A survivor is r << 7 | q (detection row,
+  // column; dw < 128, dh < 256 by the planner), bit 15 = keypoint flag.
   const int ls = (c.cols + 6) & ~3;
+  const int sp2 = dw + 2, nsc = sp2 * (dh + 2);
   uint8_t* roi = lds;
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
-  uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nd + 15) & ~15));
+  uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
+  auto sci = [&](int i) { return ((i >> 7) + 1) * sp2 + (i & 127) + 1; };
 
   // ---- ROI -> LDS: raw dwords, all loads in flight before the first store
   int sp;
@@ -513,47 +530,41 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   {
     const uint8_t* Sa = S - lead;  // rows stay dword-aligned iff sp is; else unaligned loads
     const int ndw = (lead + c.cols + 3) >> 2;
-    const uint32_t mg = ((1u << 19) + ndw - 1) / ndw;
-    const int total = c.rows * ndw;
-    auto at = [&](int i, int& r, int& q) {
-      r = (int)(((uint32_t)i * mg) >> 19);
-      q = i - r * ndw;
-    };
-    uint32_t v[kFastPf];
+    if (ndw <= 16) {
+      // 16 lanes per ROI row, 4 rows per step: lane (q, r0) loads dword q of
+      // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight
+      const int q = lane & 15, r0 = lane >> 4;
+      const bool qv = q < ndw;
+      const int qa = min(q, ndw - 1);  // idle lanes re-read an in-ROI dword
+      for (int k0 = 0; 4 * k0 < c.rows; k0 += kFastPf) {
+        uint32_t v[kFastPf];
 #pragma unroll
-    for (int u = 0; u < kFastPf; ++u) {
-      int r, q;
-      at(min(64 * u + lane, total - 1), r, q);
-      v[u] = *reinterpret_cast<const uint32_t*>(Sa + (size_t)r * sp + 4 * q);
-    }
+        for (int u = 0; u < kFastPf; ++u)
+          v[u] = *reinterpret_cast<const uint32_t*>(Sa + (uint32_t)(min(r0 + 4 * (k0 + u), c.rows - 1) * sp + 4 * qa));
 #pragma unroll
-    for (int u = 0; u < kFastPf; ++u) {
-      const int i = 64 * u + lane;
-      if (i < total) {
-        int r, q;
-        at(i, r, q);
-        *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) = v[u];
+        for (int u = 0; u < kFastPf; ++u) {
+          const int r = r0 + 4 * (k0 + u);
+          if (qv && r < c.rows) *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) = v[u];
+        }
+      }
+    } else {
+      for (int i = lane; i < c.rows * ndw; i += 64) {
+        const int r = i / ndw, q = i - r * ndw;
+        *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) =
+            *reinterpret_cast<const uint32_t*>(Sa + (size_t)r * sp + 4 * q);
       }
     }
-    for (int i = 64 * kFastPf + lane; i < total; i += 64) {
-      int r, q;
-      at(i, r, q);
-      *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) =
-          *reinterpret_cast<const uint32_t*>(Sa + (size_t)r * sp + 4 * q);
-    }
   }
-  for (int i = lane; i < ((nd + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
+  for (int i = lane; i < ((nsc + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
   __syncthreads();
   STAMP(6);
   STAMP_ADD(13, 1);
 
-  const uint32_t magic = ((1u << 19) + dw - 1) / dw;  // exact i / dw for i * dw < 2^19
-  auto row_of = [&](int i) { return (int)(((uint32_t)i * magic) >> 19); };
   const uint8_t* base = roi + 3 * ls + lead + 3;  // detection pixel (0, 0)
   const uint64_t lt = (1ull << lane) - 1ull;
   const int gpr = (dw + 3) >> 2;  // 4-pixel groups per detection row
-  const int ng = dh * gpr;
-  const uint32_t gmag = ((1u << 19) + gpr - 1) / gpr;
+  const int g_r0 = lane / gpr, g_q0 = lane - (lane / gpr) * gpr;
+  const int g_dr = 64 / gpr, g_dq = 64 - g_dr * gpr;
 
   // One threshold pass; returns the number of keypoints, leaves the survivor
   // list (raster order, kp flag in bit 15) in sv[0..*n_sv).
@@ -562,10 +573,8 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // of centres q..q+3 starts at row byte lead + q + 3 (wave-uniform shifts)
     const ushort2_t th2 = as_us2((uint32_t)th * 0x10001u);
     int ns = 0;
-    for (int g0 = 0; g0 < ng; g0 += 64) {
-      const int gi = min(g0 + lane, ng - 1);
-      const int r = (int)(((uint32_t)gi * gmag) >> 19), g = gi - r * gpr;
-      const uint8_t* C = roi + (r + 3) * ls + 4 * g;
+    for (int r = g_r0, g = g_q0; __builtin_amdgcn_ballot_w64(r < dh) != 0;) {
+      const uint8_t* C = roi + (min(r, dh - 1) + 3) * ls + 4 * g;
       auto win = [&](const uint8_t* row, int o) {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (o & ~3));
         return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
@@ -578,48 +587,43 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint32_t to = __builtin_bit_cast(
           uint32_t, sub_sat2(compass2(odd_bytes(wv), odd_bytes(wu), odd_bytes(wd), odd_bytes(wl),
                                       odd_bytes(wr)), th2));   // pixels 1, 3
-      const int nv = (g0 + lane < ng) ? min(dw - 4 * g, 4) : 0;  // valid pixels of the group
+      const int nv = r < dh ? min(dw - 4 * g, 4) : 0;  // valid pixels of the group
       const bool f0 = nv > 0 && (te & 0xffffu), f1 = nv > 1 && (to & 0xffffu);
       const bool f2 = nv > 2 && (te >> 16), f3 = nv > 3 && (to >> 16);
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
       int pos = ns + (int)mbcnt64(m3, mbcnt64(m2, mbcnt64(m1, mbcnt64(m0, 0u))));
-      const int i0 = r * dw + 4 * g;
+      const int i0 = (r << 7) | (4 * g);
       if (f0) sv[pos++] = (uint16_t)i0;
       if (f1) sv[pos++] = (uint16_t)(i0 + 1);
       if (f2) sv[pos++] = (uint16_t)(i0 + 2);
       if (f3) sv[pos] = (uint16_t)(i0 + 3);
       ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+      g += g_dq;
+      r += g_dr;
+      if (g >= gpr) g -= gpr, ++r;
     }
     __syncthreads();
     STAMP(0);
     for (int j = lane; j < ns; j += 64) {
       const int i = sv[j];
-      const int r = row_of(i), q = i - r * dw;
-      const int s = fast_score(base + r * ls + q, ls);
-      sc[i] = (uint8_t)(s >= th ? s : 0);
+      const int s = fast_score(base + (i >> 7) * ls + (i & 127), ls);
+      sc[sci(i)] = (uint8_t)(s >= th ? s : 0);
     }
     __syncthreads();
     STAMP(1);
+    // NMS: a corner is kept iff its score beats all 8 neighbours' (0 for
+    // non-corners and for the zero border outside the detection area)
     int nk = 0;
     for (int b0 = 0; b0 < ns; b0 += 64) {
       const int j = b0 + lane;
       bool kp = false;
       if (j < ns) {
         const int i = sv[j];
-        const int s = sc[i];
-        if (s > 0) {
-          const int r = row_of(i), q = i - r * dw;
-          kp = true;
-#pragma unroll
-          for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-              if (dx == 0 && dy == 0) continue;
-              const int rr = r + dy, qq = q + dx;
-              if (rr < 0 || rr >= dh || qq < 0 || qq >= dw) continue;
-              if (s <= sc[rr * dw + qq]) kp = false;
-            }
-        }
+        const uint8_t* m = sc + sci(i);
+        const int s = m[0];
+        const int n = max(max(max(m[-sp2 - 1], m[-sp2]), max(m[-sp2 + 1], m[-1])),
+                          max(max(m[1], m[sp2 - 1]), max(m[sp2], m[sp2 + 1])));
+        kp = s > n;
         if (kp) sv[j] = (uint16_t)(i | 0x8000);
       }
       nk += __popcll(__ballot(kp));
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   STAMP_ADD(12, ns);
   if (nk == 0) {
     STAMP_ADD(10, 1);
-    for (int j = lane; j < ns; j += 64) sc[sv[j] & 0x7fff] = 0;
+    for (int j = lane; j < ns; j += 64) sc[sci(sv[j] & 0x7fff)] = 0;
     __syncthreads();
     STAMP(3);
     nk = pass(P->min_th, &ns);
@@ -652,10 +656,10 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     const uint64_t m = __ballot(k);
     if (k) {
       const int i = e & 0x7fff;
-      const int r = row_of(i), q = i - r * dw;
+      const int r = i >> 7, q = i & 127;
       const int pos = written + __popcll(m & lt);
       if (pos < c.slot_cap)
-        out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)sc[i] << 24);
+        out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)sc[sci(i)] << 24);
     }
     written += __popcll(m);
   }
@@ -1099,10 +1103,47 @@ __device__ __forceinline__ int wave_isum_to_lane63(int v) {
   return v;
 }
 
+// IC_Angle by v_dot4_u32_u8 over the staged 31-row patch: item t = (row
+// t / 9, dword t % 9) of the patch rows; for the patch's alignment offset o =
+// (cx - 15) & 3 the table gives, per item, the byte weights (u + 15) and
+// (v + 15) and a 0/1 mask, each zero outside the circle (|u| <= umax[|v|]),
+// and the item's LDS offset.  Then m10 = A - 15 S, m01 = B - 15 S with
+// A = sum (u+15) val, B = sum (v+15) val, S = sum val.  Items 279..319 are
+// all-zero padding so every lane runs 5 items.
+constexpr int kIcItems = 31 * 9, kIcSlots = 320;
+struct IcTab {
+  uint32_t e[4][kIcSlots][4];  // [o][item] = {W_u, W_v, W_1, lds offset}
+};
+constexpr int kUmaxC[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr IcTab make_ic_tab() {
+  IcTab T{};
+  for (int o = 0; o < 4; ++o)
+    for (int t = 0; t < kIcItems; ++t) {
+      const int rv = t / 9, j = t % 9, v = rv - 15, av = v < 0 ? -v : v;
+      uint32_t wu = 0, wv = 0, w1 = 0;
+      for (int b = 0; b < 4; ++b) {
+        const int u = 4 * j + b - o - 15, au = u < 0 ? -u : u;
+        if (au <= 15 && au <= kUmaxC[av]) {
+          wu |= (uint32_t)(u + 15) << (8 * b);
+          wv |= (uint32_t)(v + 15) << (8 * b);
+          w1 |= 1u << (8 * b);
+        }
+      }
+      T.e[o][t][0] = wu;
+      T.e[o][t][1] = wv;
+      T.e[o][t][2] = w1;
+      T.e[o][t][3] = (uint32_t)(rv * kRawW + 4 * j);
+    }
+  return T;
+}
+__constant__ IcTab c_ic = make_ic_tab();
+
 // One wave per octree output slot (measured against a persistent, software-
 // pipelined variant: the extra registers halved residency and lost, 201 vs
 // 167 us).  The slot's count and keypoint are loaded together; dead slots
-// leave before any patch load (their oct_out entries are stale).
+// leave before any patch load (their oct_out entries are stale).  Slot, level
+// and keypoint are wave-uniform (scalar unit); the patches are staged as
+// fixed row x dword grids so LDS stores take immediate offsets.
 __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
                                                   const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur,
@@ -1112,71 +1153,74 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
                                                   uint64_t* __restrict__ desc_out, int n_img) {
   constexpr int kSlice = (kDescLds + 15) & ~15;
   __shared__ __attribute__((aligned(16))) uint8_t lds_all[4 * kSlice];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* raw = lds_all + wave * kSlice;
   uint8_t* blp = raw + kRawW * kRawH;
-  const long gidx = (long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
-  if (gidx >= (long)n_img * P->kp_slots) return;  // wave-uniform
-  const int img = (int)(gidx / P->kp_slots);
-  const int slot = (int)(gidx - (long)img * P->kp_slots);
+  const int kps = P->kp_slots;
+  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  if (gidx >= n_img * kps) return;  // wave-uniform
+  const int img = gidx / kps;
+  const int slot = gidx - img * kps;
   int l = 0;
   while (l + 1 < P->levels && slot >= P->lev[l + 1].out_off) ++l;
   const LevelGeom& g = P->lev[l];
-  const int cnt = oct_count[img * P->levels + l];
-  const uint32_t kp = oct_out[(size_t)img * P->kp_slots + slot];
+  const int cnt = __builtin_amdgcn_readfirstlane(oct_count[img * P->levels + l]);
+  const uint32_t kp = __builtin_amdgcn_readfirstlane(oct_out[(size_t)img * kps + slot]);
   if (slot - g.out_off >= cnt) return;  // wave-uniform
   const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
 
   // Stage both patches with independent dword loads (one memory round trip;
-  // unaligned only when the level-0 stride is not a multiple of 4).
+  // unaligned only when the level-0 stride is not a multiple of 4):
+  // raw 31 rows x 9 dwords as 7-row steps of 63 lanes, blurred 37 x 10 as
+  // 6-row steps of 60 lanes.
   int sp;
   const uint8_t* img0 = level_plane(P, src, pyr, img, l, sp);
   const int rx0 = (cx - 15) & ~3, bx0 = (cx - 18) & ~3;
   const uint8_t* rsrc = img0 + (size_t)(cy - 15) * sp + rx0;
   const uint8_t* bsrc = blur + (size_t)img * P->blur_bytes + g.blur_off + (size_t)(cy - 18) * g.pitch + bx0;
-  constexpr int nr = kRawH * (kRawW / 4), nb = kBlurH * (kBlurW / 4);
   {
-    uint32_t v[(nr + nb + 63) / 64];
+    constexpr int kRs = 5, kBs = 7;  // steps
+    const int rr = min(lane / 9, 6), rq = lane - (lane / 9) * 9;      // lanes 63: duplicate of 62
+    const int br = min(lane / 10, 5), bq = min(lane - (lane / 10) * 10, 9);
+    uint32_t vr[kRs], vb[kBs];
 #pragma unroll
-    for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
-      const int i = min(64 * u + lane, nr + nb - 1);
-      if (i < nr) {
-        const int r = i / (kRawW / 4), q = i - r * (kRawW / 4);
-        v[u] = *reinterpret_cast<const uint32_t*>(rsrc + (size_t)r * sp + 4 * q);
-      } else {
-        const int j = i - nr, r = j / (kBlurW / 4), q = j - r * (kBlurW / 4);
-        v[u] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * g.pitch + 4 * q);
-      }
-    }
+    for (int k = 0; k < kRs; ++k)
+      vr[k] = *reinterpret_cast<const uint32_t*>(rsrc + (uint32_t)(min(rr + 7 * k, kRawH - 1) * sp + 4 * rq));
 #pragma unroll
-    for (int u = 0; u < (nr + nb + 63) / 64; ++u) {
-      const int i = 64 * u + lane;
-      if (i < nr + nb) reinterpret_cast<uint32_t*>(raw)[i] = v[u];
-    }
+    for (int k = 0; k < kBs; ++k)
+      vb[k] = *reinterpret_cast<const uint32_t*>(bsrc + (uint32_t)(min(br + 6 * k, kBlurH - 1) * g.pitch + 4 * bq));
+    uint32_t* rd = reinterpret_cast<uint32_t*>(raw + rr * kRawW + 4 * rq);
+    uint32_t* bd = reinterpret_cast<uint32_t*>(blp + br * kBlurW + 4 * bq);
+#pragma unroll
+    for (int k = 0; k < kRs; ++k)
+      if (rr + 7 * k < kRawH) rd[k * 7 * kRawW / 4] = vr[k];
+#pragma unroll
+    for (int k = 0; k < kBs; ++k)
+      if (br + 6 * k < kBlurH) bd[k * 6 * kBlurW / 4] = vb[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  // IC_Angle: lanes 0..61 -> (column u, half); rows -15..0 / 1..15.
-  int m10 = 0, m01 = 0;
+  // IC_Angle (see c_ic)
+  int m10, m01;
   {
-    const int ln = min(lane, 61);
-    const int u = ln % 31 - 15, half = ln / 31;
-    const int au = u < 0 ? -u : u;
-    const uint8_t* colp = raw + 15 * kRawW + (cx - rx0) + u;
+    const uint32_t(*tab)[4] = c_ic.e[(cx - 15) & 3];
+    uint32_t A = 0, B = 0, S = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int v = half ? k + 1 : k - 15;
-      const int av = v < 0 ? -v : v;
-      const int val = colp[min(v, 15) * kRawW];
-      const bool in = lane < 62 && v <= 15 && au <= kUmax[min(av, 15)];
-      m10 += in ? u * val : 0;
-      m01 += in ? v * val : 0;
+    for (int k = 0; k < kIcSlots / 64; ++k) {
+      const uint4 w = *reinterpret_cast<const uint4*>(tab[64 * k + lane]);
+      const uint32_t val = *reinterpret_cast<const uint32_t*>(raw + w.w);
+      A = __builtin_amdgcn_udot4(val, w.x, A, false);
+      B = __builtin_amdgcn_udot4(val, w.y, B, false);
+      S = __builtin_amdgcn_udot4(val, w.z, S, false);
     }
+    const int a = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)A), 63);
+    const int b = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)B), 63);
+    const int s = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)S), 63);
+    m10 = a - 15 * s;
+    m01 = b - 15 * s;
   }
-  m10 = __builtin_amdgcn_readlane(wave_isum_to_lane63(m10), 63);
-  m01 = __builtin_amdgcn_readlane(wave_isum_to_lane63(m01), 63);
   const float angle = dev_fast_atan2((float)m01, (float)m10);
 
   const float ang = angle * (float)(3.14159265358979323846 / 180.0);
@@ -1185,13 +1229,14 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   uint64_t words[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
-    const int8_t* pt = c_pattern + 4 * (64 * w + lane);
-    const float x0 = pt[0], y0 = pt[1], x1 = pt[2], y1 = pt[3];
+    const float4 pt = c_pattern_f[64 * w + lane];
+    const float x0 = pt.x, y0 = pt.y, x1 = pt.z, y1 = pt.w;
     const int r0 = dev_round(__builtin_fmaf(x0, b, y0 * a));
     const int q0 = dev_round(__builtin_fmaf(x0, a, -(y0 * b)));
     const int r1 = dev_round(__builtin_fmaf(x1, b, y1 * a));
     const int q1 = dev_round(__builtin_fmaf(x1, a, -(y1 * b)));
-    const int t0 = ctr[r0 * kBlurW + q0], t1 = ctr[r1 * kBlurW + q1];
+    // |r|, |q| <= 18: 24-bit multiplies (full rate)
+    const int t0 = ctr[__mul24(r0, kBlurW) + q0], t1 = ctr[__mul24(r1, kBlurW) + q1];
     words[w] = __ballot(t0 < t1);
   }
   const size_t o = (size_t)img * P->kp_slots + slot;

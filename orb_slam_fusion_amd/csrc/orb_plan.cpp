@@ -83,6 +83,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
     g.w = cv_round((float)W * out.inv_scale[l]);  // :1096
     g.h = cv_round((float)H * out.inv_scale[l]);
     g.scale = out.scale[l];
+    g.inv_scale = out.inv_scale[l];
     g.patch_size = (float)(int)(kPatchSize * out.scale[l]);
     if (g.w - 2 * kFastBorder < 35 || g.h - 2 * kFastBorder < 35)
       return why = "pyramid level too small for the FAST grid", false;
@@ -183,8 +184,8 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         slots += c.slot_cap;
         max_roi = std::max(max_roi, c.cols * c.rows);
         max_roi_lds = std::max(max_roi_lds, fast_cell_lds_bytes(c.cols, c.rows));
-        if (dw > 0 && dh > 0 && dw * dh * dw >= (1 << 19))
-          return why = "FAST cell too large for the magic division", false;
+        if (dw > 127 || dh > 255)  // k_fast_cells survivor encoding r << 7 | q
+          return why = "FAST cell too large", false;
         out.cells.push_back(c);
       }
     }
@@ -221,12 +222,13 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
 }
 
 // LDS of one FAST cell wave (k_fast_cells): ROI staged with 4-aligned rows
-// (+3 lead bytes), a byte score map of the detection area and a u16
-// survivor list.
+// (+3 lead bytes), a byte score map of the detection area with a zero border
+// and a u16 survivor list.
 int fast_cell_lds_bytes(int cols, int rows) {
   const int ls = (cols + 3 + 3) & ~3;
   const int nd = std::max(cols - 6, 0) * std::max(rows - 6, 0);
-  return ((ls * rows + 15) & ~15) + ((nd + 15) & ~15) + 2 * nd + 16;
+  const int nsc = std::max(cols - 4, 0) * std::max(rows - 4, 0);
+  return ((ls * rows + 15) & ~15) + ((nsc + 15) & ~15) + 2 * nd + 16;
 }
 
 size_t octree_lds_bytes(const PlanHeader& P) {

@@ -18,6 +18,7 @@ struct LevelGeom {
   int pyr_off;       // byte offset of this level in an image's pyramid block (levels >= 1)
   int blur_off;      // byte offset in an image's blurred block (all levels)
   float scale;       // scale_factors_[l]
+  float inv_scale;   // inv_scale_factors_[l]
   float patch_size;  // (float)(int)(31 * scale)                                     (:834)
   // resize tables (levels >= 1), offsets into Plan::rs_tab
   int rs_x, rs_y;    // xofs|alpha pairs, yofs|beta pairs

@@ -157,6 +157,22 @@ class OrbExtractor:
             "orbgpu_extract_batch",
         )
 
+    def stereo_match_batch(self, imgs, kps, descs, n, bf: float, mb: float, uright, depth,
+                           stream=None) -> None:
+        """Frame::ComputeStereoMatches (frame.cc:828-986) for the B/2 stereo frames
+        of this handle's last extract_batch call (images [L0, R0, L1, R1, ...]):
+        imgs, kps, descs, n are that call's arguments; uright / depth: float32
+        CUDA tensors [B/2, cap] (-1 = unmatched).  bf = Frame::bf_, mb = Frame::mb."""
+        B = imgs.shape[0]
+        cap = descs.shape[1]
+        check(
+            lib().orbgpu_stereo_match_batch(
+                self._h, B // 2, ptr(imgs), imgs.stride(1), imgs.stride(0), ptr(kps), ptr(descs), cap,
+                ptr(n), float(bf), float(mb), ptr(uright), ptr(depth), _stream_handle(stream),
+            ),
+            "orbgpu_stereo_match_batch",
+        )
+
     STAGES = ("resize", "blur", "fast_cells", "octree", "describe", "assemble")
 
     def profile(self, max_calls: int) -> None:

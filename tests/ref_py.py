@@ -211,3 +211,80 @@ def distribute_octree(kps, min_x, max_x, min_y, max_y, n_feats):
                 best = kp
         out.append(best)
     return out
+
+
+def stereo_match_py(kl, dl, kr, dr, pyr_l, pyr_r, scale, inv_scale, bf, mb):
+    """Frame::ComputeStereoMatches (frame.cc:828-986) restated with numpy float32
+    scalars: per left keypoint the row band candidates, Hamming best (first
+    strict minimum), 11x11 L1 sweep on reflect-101 padded levels, parabola,
+    disparity clamp, then the 1.5 * 1.4 * median filter.  -> (uright, depth)."""
+    f32 = np.float32
+    nl = len(kl)
+    ur = np.full(nl, -1.0, np.float32)
+    dep = np.full(nl, -1.0, np.float32)
+    rows = pyr_l[0].shape[0]
+    bits = np.unpackbits(np.arange(256, dtype=np.uint8)[:, None], axis=1).sum(1)
+    table = [[] for _ in range(rows)]
+    for i in range(len(kr)):
+        y = f32(kr["y"][i])
+        r = f32(2.0) * f32(scale[kr["octave"][i]])
+        for yi in range(int(np.floor(f32(y - r))), int(np.ceil(f32(y + r))) + 1):
+            if 0 <= yi < rows:
+                table[yi].append(i)
+    maxD = f32(f32(bf) / f32(mb))
+    pads = [(np.pad(a, 19, mode="reflect").astype(np.int64), np.pad(b, 19, mode="reflect").astype(np.int64))
+            for a, b in zip(pyr_l, pyr_r)]
+    kept = []
+    for i in range(nl):
+        uL, vL, oct_ = f32(kl["x"][i]), f32(kl["y"][i]), int(kl["octave"][i])
+        row = int(vL)
+        if row >= rows or not table[row]:
+            continue
+        minU = f32(uL - maxD)
+        if uL < 0:
+            continue
+        best, bidx = 100, 0
+        for j in table[row]:
+            if abs(int(kr["octave"][j]) - oct_) > 1:
+                continue
+            uR = f32(kr["x"][j])
+            if minU <= uR <= uL:
+                d = int(bits[np.bitwise_xor(dl[i], dr[j])].sum())
+                if d < best:
+                    best, bidx = d, j
+        if best >= 75:
+            continue
+        inv = f32(inv_scale[oct_])
+        # std::round: half away from zero (coordinates are >= 0)
+        su = f32(np.floor(np.float64(f32(uL * inv)) + 0.5))
+        sv = f32(np.floor(np.float64(f32(vL * inv)) + 0.5))
+        sr = f32(np.floor(np.float64(f32(f32(kr["x"][bidx]) * inv)) + 0.5))
+        if sr < 0 or f32(sr + 11) >= pyr_l[oct_].shape[1]:
+            continue
+        PL, PR = pads[oct_]
+        xl, yl, xr = int(su) + 19, int(sv) + 19, int(sr) + 19
+        wl = PL[yl - 5:yl + 6, xl - 5:xl + 6]
+        ds = [int(np.abs(wl - PR[yl - 5:yl + 6, xr + inc - 5:xr + inc + 6]).sum()) for inc in range(-5, 6)]
+        bi = int(np.argmin(ds))  # first minimum
+        if bi in (0, 10):
+            continue
+        d1, d2, d3 = f32(ds[bi - 1]), f32(ds[bi]), f32(ds[bi + 1])
+        delta = f32(f32(d1 - d3) / f32(f32(2.0) * f32(f32(d1 + d3) - f32(f32(2.0) * d2))))
+        if not (-1 <= delta <= 1):
+            continue
+        bu = f32(f32(scale[oct_]) * f32(f32(sr + f32(bi - 5)) + delta))
+        disp = f32(uL - bu)
+        if f32(0) <= disp < maxD:
+            if disp <= 0:
+                disp = f32(0.01)
+                bu = f32(np.float64(uL) - 0.01)
+            dep[i] = f32(f32(bf) / disp)
+            ur[i] = bu
+            kept.append((ds[bi], i))
+    if kept:
+        kept.sort()
+        th = f32(f32(f32(1.5) * f32(1.4)) * f32(kept[len(kept) // 2][0]))
+        for d, i in kept:
+            if not (f32(d) < th):
+                ur[i] = dep[i] = -1.0
+    return ur, dep
