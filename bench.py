@@ -95,6 +95,7 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
+    ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches side line")
     args = ap.parse_args()
 
     import torch
@@ -259,6 +260,13 @@ def main() -> int:
         from bench_lba import measure  # noqa: E402
 
         result["lba"] = measure(calls=10, cpu_calls=0 if args.no_cpu_baseline else 3)
+    if rank == 0 and world == 1 and not args.no_stereo:
+        # SURVEY §8(f) rank 1, beside the headline metric (not part of it):
+        # Frame::ComputeStereoMatches per frame on resident extractor outputs
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_stereo import measure as measure_stereo  # noqa: E402
+
+        result["stereo"] = measure_stereo(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()
