@@ -51,6 +51,9 @@ class OrbExtractor {
 
   void ComputePyramid(cv::Mat img);
 
+  // The device handle (frame_stereo_gpu.cc matches on its resident outputs).
+  orbgpu_extractor *gpu() const { return gpu_; }
+
  protected:
   int num_feats_;
   double scale_factor_;

@@ -66,7 +66,10 @@ int OrbExtractor::operator()(cv::InputArray img, cv::InputArray /*msk*/,
     desc_buf_.rowRange(0, n).copyTo(descs.getMat());
   }
 
-  // img_pyramid_: host levels inside a REFLECT_101 frame (orb_extractor.cc:1098-1115)
+#ifndef ORBGPU_STEREO
+  // img_pyramid_: host levels inside a REFLECT_101 frame (orb_extractor.cc:1098-1115).
+  // Its only reader is Frame::ComputeStereoMatches; with the GPU stereo matcher
+  // (frame_stereo_gpu.cc, ORBGPU_STEREO) the levels stay on the device.
   for (int l = 0; l < num_levs_; ++l) {
     const uint8_t *data;
     int w, h, s;
@@ -78,6 +81,8 @@ int OrbExtractor::operator()(cv::InputArray img, cv::InputArray /*msk*/,
                        kEdgeThreshold, cv::BORDER_REFLECT_101);
     img_pyramid_[l] = tmp(cv::Rect(kEdgeThreshold, kEdgeThreshold, w, h));
   }
+#endif
+
   return mono;
 }
 
