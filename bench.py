@@ -212,6 +212,20 @@ def main() -> int:
                 traffic = round(per * 2 * Bp)
         except Exception:
             traffic = None
+    # what actually bounds the kernel: VALU-busy fraction of its SIMDs from the
+    # SQ counter passes (tools/profile_round.sh -> profiles/pmc_sq.json):
+    # SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 / (SQ_BUSY_CYCLES
+    # (cycles summed over the 32 shader engines) x 32 SIMDs per engine)
+    valu_busy = None
+    sq = REPO / "profiles" / "pmc_sq.json"
+    kname = {"resize": "k_resize", "blur": "k_blur", "fast_cells": "k_fast_cells", "octree": "k_octree",
+             "describe": "k_describe", "assemble": "k_assemble"}.get(roof_stage)
+    if sq.exists() and kname:
+        try:
+            k = json.loads(sq.read_text())[kname]
+            valu_busy = round(4 * k["SQ_ACTIVE_INST_VALU"] / (32 * k["SQ_BUSY_CYCLES"]), 3)
+        except Exception:
+            valu_busy = None
 
     result = {
         "metric": METRIC,
@@ -247,6 +261,8 @@ def main() -> int:
             "traffic": traffic,
             "algorithmic_bytes_per_launch": int(roof_bytes),
             "avg_launch_ms": round(roof_ms, 5),
+            "valu_busy": valu_busy,
+            "limiter": "valu issue" if valu_busy is not None and valu_busy > 0.6 else None,
         },
         "stage_ms_per_step": {k: round(v, 5) for k, v in stage_avg.items()},
         "dominant_stage": dom,
