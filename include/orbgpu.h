@@ -240,6 +240,137 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* c, const orbgpu_camera* cam, i
                                   void* user, orbgpu_pose* poses_out, double* poses_out_d,
                                   float* pts_out, uint8_t* outlier, double* stats);
 
+/* ------------------------------------------------------------------------
+ * ORBmatcher projection search (pinhole rig, Frame::Nleft == -1), the
+ * matching that feeds PoseOptimization in Tracking::TrackWithMotionModel
+ * (tracking.cc:2163-2216) and Tracking::SearchLocalPoints (:2626-2690).
+ *
+ * The current frame is given as the reference's Frame fields: keypoints
+ * (mvKeysUn, cv::KeyPoint layout), descriptors (mDescriptors, 32 B rows),
+ * uright (mvuRight; NULL = every keypoint monocular) and claimed (optional,
+ * 1 byte per keypoint: mvpMapPoints[i] != NULL && ->Observations() > 0 before
+ * the call).  The frame grid (FRAME_GRID_COLS x ROWS = 64 x 48,
+ * Frame::AssignFeaturesToGrid, frame.cc:438-465) is built on the device.
+ * Output match[i] per keypoint: >= 0 -> mvpMapPoints[i] = that query point;
+ * -1 -> mvpMapPoints[i] untouched; -2 -> set to NULL (rotation-consistency
+ * removal of a match made by this call).  *nmatches = the function's return.
+ * ------------------------------------------------------------------------ */
+#define ORBGPU_MAX_LEVELS 16
+#define ORBGPU_FRAME_GRID_COLS 64 /* frame.h:41 */
+#define ORBGPU_FRAME_GRID_ROWS 48 /* frame.h:40 */
+
+typedef struct orbgpu_frame_geom {
+  float min_x, max_x, min_y, max_y; /* Frame::mnMinX, mnMaxX, mnMinY, mnMaxY (ComputeImageBounds) */
+  int32_t n_levels;                 /* Frame::mnScaleLevels                                       */
+  float log_scale_factor;           /* Frame::mfLogScaleFactor                                   */
+  float scale_factors[ORBGPU_MAX_LEVELS]; /* Frame::mvScaleFactors                              */
+} orbgpu_frame_geom;
+
+/* One LastFrame observation that SearchByProjection(CurrentFrame, LastFrame)
+ * projects: LastFrame.mvpMapPoints[i] != NULL && !LastFrame.mvbOutlier[i], in
+ * increasing i (orb_matcher.cc:1538-1541). */
+typedef struct orbgpu_proj_point {
+  float Xw[3];      /* pMP->GetWorldPos()                                    */
+  int32_t octave;   /* LastFrame.mvKeys[i].octave                            */
+  float angle;      /* LastFrame.mvKeysUn[i].angle (rotation histogram)      */
+  int32_t has_obs;  /* pMP->Observations() > 0: its matches block later ones */
+  uint8_t desc[32]; /* pMP->GetDescriptor()                                  */
+} orbgpu_proj_point;
+
+/* A local map point (Tracking::mvpLocalMapPoints[j]) as Frame::isInFrustum and
+ * SearchByProjection(Frame&, vector<MapPoint*>, ...) read it. */
+#define ORBGPU_MP_SKIP 1    /* isBad() or mnLastFrameSeen == frame id: not projected */
+#define ORBGPU_MP_HAS_OBS 2 /* Observations() > 0                                      */
+typedef struct orbgpu_map_point {
+  float Xw[3];              /* GetWorldPos()                   */
+  float normal[3];          /* GetNormal()                     */
+  float min_dist, max_dist; /* mfMinDistance, mfMaxDistance    */
+  int32_t flags;            /* ORBGPU_MP_*                     */
+  uint8_t desc[32];         /* GetDescriptor()                 */
+} orbgpu_map_point;
+
+/* MapPoint tracking fields written by Frame::isInFrustum (frame.cc:548-603):
+ * in_view = mbTrackInView; proj_x / proj_y = mTrackProjX / Y (-1 when the
+ * projection fails the depth or image-bounds test); level, proj_xr, depth,
+ * view_cos = mnTrackScaleLevel, mTrackProjXR, mTrackDepth, mTrackViewCos, only
+ * meaningful (and only written by the reference) when in_view. */
+typedef struct orbgpu_track_view {
+  int32_t in_view, level;
+  float proj_x, proj_y, proj_xr, depth, view_cos;
+} orbgpu_track_view;
+
+typedef struct orbgpu_matcher orbgpu_matcher;
+
+/* One context per calling thread (own HIP stream and scratch), sized for
+ * frames of up to max_keypoints keypoints and max_points query points. */
+orbgpu_status orbgpu_matcher_create(int device, int max_keypoints, int max_points,
+                                    orbgpu_matcher** out);
+void orbgpu_matcher_destroy(orbgpu_matcher* m);
+
+/* Replaces: int ORBmatcher::SearchByProjection(Frame& CurrentFrame,
+ *   const Frame& LastFrame, const float th, const bool bMono)
+ *   (orb_matcher.h, orb_matcher.cc:1518-1728) with mbCheckOrientation =
+ *   check_orientation (TrackWithMotionModel: ORBmatcher(0.9, true), th = 7
+ *   stereo / 15 otherwise, 2 th on the retry).  Tcw = CurrentFrame.GetPose(),
+ *   Tlw = LastFrame.GetPose(), mb = CurrentFrame.mb; pts as orbgpu_proj_point. */
+orbgpu_status orbgpu_search_by_projection_last(
+    orbgpu_matcher* m, const orbgpu_frame_geom* geom, const orbgpu_camera* cam, float mb,
+    const orbgpu_pose* Tcw, const orbgpu_pose* Tlw, const orbgpu_keypoint* kps,
+    const uint8_t* descs, const float* uright, const uint8_t* claimed, int n,
+    const orbgpu_proj_point* pts, int n_pts, float th, int mono, int check_orientation,
+    int32_t* match, int* nmatches);
+
+/* Device-resident batch of the above: frame f reads d_Tcw[f], d_Tlw[f],
+ * keypoints / descriptors / uright / claimed at f * kp_stride (keypoints),
+ * d_n[f] keypoints, d_pts + f * pt_stride with d_npts[f] points, and writes
+ * d_match + f * kp_stride (d_n[f] entries) and d_nmatches[f].  d_uright /
+ * d_claimed may be NULL.  Asynchronous on hip_stream (NULL: the context's). */
+orbgpu_status orbgpu_search_by_projection_last_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    float mb, const orbgpu_pose* d_Tcw, const orbgpu_pose* d_Tlw, const orbgpu_keypoint* d_kps,
+    const uint8_t* d_descs, const float* d_uright, const uint8_t* d_claimed, const int* d_n,
+    int kp_stride, const orbgpu_proj_point* d_pts, const int* d_npts, int pt_stride, float th,
+    int mono, int check_orientation, int32_t* d_match, int* d_nmatches, void* hip_stream);
+
+/* Replaces: bool Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit)
+ *   (frame.cc:548-603, Nleft == -1) over Tracking::SearchLocalPoints' loop
+ *   (tracking.cc:2644-2661): points flagged ORBGPU_MP_SKIP are not projected
+ *   (in_view = 0).  Rcw / tcw / Ow = the frame's mRcw (row-major), mtcw, mOw. */
+orbgpu_status orbgpu_frustum(orbgpu_matcher* m, const orbgpu_frame_geom* geom,
+                             const orbgpu_camera* cam, const float Rcw[9], const float tcw[3],
+                             const float Ow[3], const orbgpu_map_point* pts, int n_pts,
+                             float view_cos_limit, orbgpu_track_view* views);
+
+/* Replaces: int ORBmatcher::SearchByProjection(Frame& F,
+ *   const vector<MapPoint*>& vpMapPoints, const float th, const bool bFarPoints,
+ *   const float thFarPoints) (orb_matcher.cc:42-206, Nleft == -1) with
+ *   mfNNratio = nn_ratio; views[j] = point j's tracking fields (from
+ *   orbgpu_frustum or the caller). */
+orbgpu_status orbgpu_search_by_projection_local(
+    orbgpu_matcher* m, const orbgpu_frame_geom* geom, const orbgpu_keypoint* kps,
+    const uint8_t* descs, const float* uright, const uint8_t* claimed, int n,
+    const orbgpu_map_point* pts, const orbgpu_track_view* views, int n_pts, float th,
+    float nn_ratio, int far_points, float th_far_points, int32_t* match, int* nmatches);
+
+/* Tracking::SearchLocalPoints' projection + search in one call: isInFrustum
+ * over pts (views written back for the caller's IncreaseVisible /
+ * mmProjectPoints bookkeeping), then the search above. */
+orbgpu_status orbgpu_search_local_points(
+    orbgpu_matcher* m, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    const float Rcw[9], const float tcw[3], const float Ow[3], const orbgpu_keypoint* kps,
+    const uint8_t* descs, const float* uright, const uint8_t* claimed, int n,
+    const orbgpu_map_point* pts, int n_pts, float view_cos_limit, float th, float nn_ratio,
+    int far_points, float th_far_points, orbgpu_track_view* views, int32_t* match,
+    int* nmatches);
+
+/* MapPoint::PredictScale (mappoint.cc:550-563) as used by the kernels: the
+ * level of a ratio mfMaxDistance / dist is the number of thresholds thr[j-1]
+ * (j = 1 .. n_levels - 1) it reaches, thr[j-1] = the smallest float ratio with
+ * ceil(log(ratio) / log_scale_factor) >= j under the host libm.  Writes
+ * ORBGPU_MAX_LEVELS - 1 floats (+inf past n_levels - 1); returns n_levels - 1
+ * or -1 on bad arguments.  Host-only (no device work). */
+int orbgpu_level_thresholds(float log_scale_factor, int n_levels, float* thr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,12 @@ def lib() -> ctypes.CDLL:
                                   _P, _P]),
         "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, LBA_REDUCE_FN, _P, _P, _P,
                          _P, _P]),
+        "orc_search_last": (_I, [_P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _I, _I, _P]),
+        "orc_frustum": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
+        "orc_search_local": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _I, _F, _P]),
+        "orc_predict_scale": (_I, [_F, _F, _F, _I]),
+        "orc_predict_scale_check": (ctypes.c_long, [_F, _I, _P, ctypes.c_uint32, ctypes.c_uint32]),
+        "orc_frame_grid_cells": (None, [_P, _P, _I, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(so, name)
@@ -65,7 +71,11 @@ def lib() -> ctypes.CDLL:
     return so
 
 
-def _p(a: np.ndarray) -> ctypes.c_void_p:
+def _p(a) -> ctypes.c_void_p:
+    if a is None:
+        return ctypes.c_void_p(0)
+    if isinstance(a, ctypes.Structure):
+        return ctypes.cast(ctypes.pointer(a), ctypes.c_void_p)
     return ctypes.c_void_p(a.ctypes.data)
 
 
@@ -260,3 +270,89 @@ def stereo_match(kps_l, desc_l, kps_r, desc_r, pyr_l, pyr_r, scale, inv_scale, b
                                   ctypes.cast(ptr_l, ctypes.c_void_p), ctypes.cast(ptr_r, ctypes.c_void_p),
                                   _p(lw), _p(lh), _p(sl), _p(sr), float(bf), float(mb), _p(ur), _p(dep))
     return ur, dep, kept
+
+
+# --- ORBmatcher projection searches (match_oracle.cc) -----------------------
+PROJ_POINT_DTYPE = np.dtype([("Xw", "<f4", (3,)), ("octave", "<i4"), ("angle", "<f4"),
+                             ("has_obs", "<i4"), ("desc", "u1", (32,))])
+MAP_POINT_DTYPE = np.dtype([("Xw", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_dist", "<f4"),
+                            ("max_dist", "<f4"), ("flags", "<i4"), ("desc", "u1", (32,))])
+TRACK_VIEW_DTYPE = np.dtype([("in_view", "<i4"), ("level", "<i4"), ("proj_x", "<f4"),
+                             ("proj_y", "<f4"), ("proj_xr", "<f4"), ("depth", "<f4"),
+                             ("view_cos", "<f4")])
+
+
+def _geom(g):
+    """orbgpu_frame_geom bytes from a ctypes FrameGeom (or anything with its fields)."""
+    a = np.zeros(22, np.float32)
+    a[0:4] = [g.min_x, g.max_x, g.min_y, g.max_y]
+    a[4:5].view(np.int32)[0] = g.n_levels
+    a[5] = g.log_scale_factor
+    a[6:22] = list(g.scale_factors)
+    return a
+
+
+def _opt(a, dtype):
+    return None if a is None else np.ascontiguousarray(a, dtype)
+
+
+def search_last(geom, cam, mb, Tcw, Tlw, kps, desc, uright, claimed, pts, th, mono, check_ori):
+    """SearchByProjection(CurrentFrame, LastFrame, th, bMono) -> (nmatches, match[N])."""
+    g = _geom(geom)
+    c = np.ascontiguousarray(cam, np.float32)
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    d = np.ascontiguousarray(desc, np.uint8)
+    p = np.ascontiguousarray(pts, PROJ_POINT_DTYPE)
+    ur, cl = _opt(uright, np.float32), _opt(claimed, np.uint8)
+    tc, tl = np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(Tlw, np.float32)
+    match = np.zeros(max(len(k), 1), np.int32)
+    nm = lib().orc_search_last(_p(g), _p(c), float(mb), _p(tc), _p(tl), _p(k), _p(d), _p(ur),
+                               _p(cl), len(k), _p(p), len(p), float(th), int(mono),
+                               int(check_ori), _p(match))
+    return nm, match[:len(k)]
+
+
+def frustum(geom, cam, Rcw, tcw, Ow, pts, cos_limit, views=None):
+    """Frame::isInFrustum over pts -> TRACK_VIEW_DTYPE [n] (fields the reference
+    does not write keep the values of `views`)."""
+    g = _geom(geom)
+    c = np.ascontiguousarray(cam, np.float32)
+    p = np.ascontiguousarray(pts, MAP_POINT_DTYPE)
+    v = np.zeros(len(p), TRACK_VIEW_DTYPE) if views is None else np.array(views, TRACK_VIEW_DTYPE)
+    R, t, O = (np.ascontiguousarray(x, np.float32) for x in (Rcw, tcw, Ow))
+    lib().orc_frustum(_p(g), _p(c), _p(R), _p(t), _p(O), _p(p), len(p), float(cos_limit), _p(v))
+    return v
+
+
+def search_local(geom, kps, desc, uright, claimed, pts, views, th, nn_ratio, far_points=False,
+                 th_far=0.0):
+    """SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints) -> (nmatches, match)."""
+    g = _geom(geom)
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    d = np.ascontiguousarray(desc, np.uint8)
+    p = np.ascontiguousarray(pts, MAP_POINT_DTYPE)
+    v = np.ascontiguousarray(views, TRACK_VIEW_DTYPE)
+    ur, cl = _opt(uright, np.float32), _opt(claimed, np.uint8)
+    match = np.zeros(max(len(k), 1), np.int32)
+    nm = lib().orc_search_local(_p(g), _p(k), _p(d), _p(ur), _p(cl), len(k), _p(p), _p(v), len(p),
+                                float(th), float(nn_ratio), int(far_points), float(th_far),
+                                _p(match))
+    return nm, match[:len(k)]
+
+
+def predict_scale(max_dist, dist, log_scale, n_levels):
+    return lib().orc_predict_scale(float(max_dist), float(dist), float(log_scale), int(n_levels))
+
+
+def predict_scale_check(log_scale, n_levels, thr, lo_bits, hi_bits):
+    t = np.ascontiguousarray(thr, np.float32)
+    return lib().orc_predict_scale_check(float(log_scale), int(n_levels), _p(t), int(lo_bits),
+                                         int(hi_bits))
+
+
+def frame_grid_cells(geom, kps):
+    g = _geom(geom)
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = np.zeros(max(len(k), 1), np.int32)
+    lib().orc_frame_grid_cells(_p(g), _p(k), len(k), _p(out))
+    return out[:len(k)]

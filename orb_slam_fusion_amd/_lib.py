@@ -80,8 +80,50 @@ LBA_EDGE_DTYPE = np.dtype(
 )
 assert LBA_EDGE_DTYPE.itemsize == 24
 
+# orbgpu_proj_point: a LastFrame observation projected by
+# SearchByProjection(CurrentFrame, LastFrame)
+PROJ_POINT_DTYPE = np.dtype(
+    [("Xw", "<f4", (3,)), ("octave", "<i4"), ("angle", "<f4"), ("has_obs", "<i4"),
+     ("desc", "u1", (32,))]
+)
+assert PROJ_POINT_DTYPE.itemsize == 56
+
+# orbgpu_map_point: a local map point (isInFrustum + SearchByProjection(F, vpMapPoints))
+MP_SKIP, MP_HAS_OBS = 1, 2
+MAP_POINT_DTYPE = np.dtype(
+    [("Xw", "<f4", (3,)), ("normal", "<f4", (3,)), ("min_dist", "<f4"), ("max_dist", "<f4"),
+     ("flags", "<i4"), ("desc", "u1", (32,))]
+)
+assert MAP_POINT_DTYPE.itemsize == 68
+
+# orbgpu_track_view: the MapPoint tracking fields isInFrustum writes
+TRACK_VIEW_DTYPE = np.dtype(
+    [("in_view", "<i4"), ("level", "<i4"), ("proj_x", "<f4"), ("proj_y", "<f4"),
+     ("proj_xr", "<f4"), ("depth", "<f4"), ("view_cos", "<f4")]
+)
+assert TRACK_VIEW_DTYPE.itemsize == 28
+
+MAX_LEVELS = 16
+
+
+class FrameGeom(ctypes.Structure):
+    """orbgpu_frame_geom: Frame::mnMinX/mnMaxX/mnMinY/mnMaxY, mnScaleLevels,
+    mfLogScaleFactor, mvScaleFactors."""
+
+    _fields_ = [
+        ("min_x", ctypes.c_float),
+        ("max_x", ctypes.c_float),
+        ("min_y", ctypes.c_float),
+        ("max_y", ctypes.c_float),
+        ("n_levels", ctypes.c_int32),
+        ("log_scale_factor", ctypes.c_float),
+        ("scale_factors", ctypes.c_float * MAX_LEVELS),
+    ]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
+_F = ctypes.c_float
 
 # name -> (restype, argtypes); mirrors include/orbgpu.h
 SIGNATURES = {
@@ -112,6 +154,31 @@ SIGNATURES = {
         _I,
         [_P, ctypes.POINTER(Camera), _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     ),
+    "orbgpu_matcher_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
+    "orbgpu_matcher_destroy": (None, [_P]),
+    "orbgpu_search_by_projection_last": (
+        _I,
+        [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _F, _P, _P, _P, _P, _P, _P, _I, _P,
+         _I, _F, _I, _I, _P, _P],
+    ),
+    "orbgpu_search_by_projection_last_batch": (
+        _I,
+        [_P, _I, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _F, _P, _P, _P, _P, _P, _P, _P,
+         _I, _P, _P, _I, _F, _I, _I, _P, _P, _P],
+    ),
+    "orbgpu_frustum": (
+        _I, [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _I, _F, _P],
+    ),
+    "orbgpu_search_by_projection_local": (
+        _I,
+        [_P, ctypes.POINTER(FrameGeom), _P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _I, _F, _P, _P],
+    ),
+    "orbgpu_search_local_points": (
+        _I,
+        [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _P, _P, _P, _I, _P,
+         _I, _F, _F, _F, _I, _F, _P, _P, _P],
+    ),
+    "orbgpu_level_thresholds": (_I, [_F, _I, _P]),
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (

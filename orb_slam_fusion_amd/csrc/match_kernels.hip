@@ -1,0 +1,563 @@
+// gfx950 kernels of the ORBmatcher projection searches that feed
+// PoseOptimization in tracking (pinhole rig, Frame::Nleft == -1):
+//
+//   k_mt_grid     block / frame: Frame::AssignFeaturesToGrid (frame.cc:438-465)
+//                 -> per-cell index lists (64 x 48 cells, ascending keypoint
+//                 index inside a cell), counting sort in LDS
+//   k_mt_search   wave / query point: projection (SearchByProjection(Frame&,
+//                 const Frame&) orb_matcher.cc:1538-1577, or Frame::isInFrustum
+//                 frame.cc:548-603 + orb_matcher.cc:50-69), then
+//                 GetFeaturesInArea (frame.cc:679-746): lanes own grid cells
+//                 of the window, filter, Hamming distance from 8 v_bcnt, and
+//                 the wave keeps the best and second candidate by the packed
+//                 key (dist, position in the reference's candidate order) --
+//                 first strict minimum = smallest key; the reference's running
+//                 second best = smallest key of the rest
+//   k_mt_resolve  wave / frame: the reference's matches are sequential
+//                 (a match by a point with observations hides that keypoint
+//                 from every later point, orb_matcher.cc:86-87, 1591-1592).
+//                 A query's result can only change if its best or second
+//                 candidate was claimed earlier, so 64 queries are committed
+//                 at once unless one of them is hit (LDS claim bitmap +
+//                 in-batch owner table); a hit query is searched again with the
+//                 claims masked.  Then the rotation histogram
+//                 (orb_matcher.cc:1614-1632, 1708-1725; ComputeThreeMaxima
+//                 :1841-1873) and the mvpMapPoints writes.
+//
+// Float expressions follow the oracle (oracle/match_oracle.cc): every fused
+// multiply-add the reference build performs is an explicit __builtin_fmaf;
+// the file is compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "match_launch.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kThHigh = 100;      // ORBmatcher::TH_HIGH (orb_matcher.cc:35)
+constexpr int kHistoLength = 30;  // ORBmatcher::HISTO_LENGTH (:37)
+constexpr int kKpFloats = 7;      // orbgpu_keypoint
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint64_t kNoKey = ~0ull;
+
+struct V3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ float mul_sub(float a, float b, float c, float d) {
+  return __builtin_fmaf(a, b, -(c * d));
+}
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return {mul_sub(a.y, b.z, a.z, b.y), mul_sub(a.z, b.x, a.x, b.z), mul_sub(a.x, b.y, a.y, b.x)};
+}
+// Sophus::SO3 * p (so3.hpp:359-367)
+__device__ __forceinline__ V3 quat_rotate(float qx, float qy, float qz, float qw, V3 p) {
+  const V3 qv{qx, qy, qz};
+  V3 uv = cross(qv, p);
+  uv = {uv.x + uv.x, uv.y + uv.y, uv.z + uv.z};
+  const V3 c = cross(qv, uv);
+  return {__builtin_fmaf(qw, uv.x, p.x) + c.x, __builtin_fmaf(qw, uv.y, p.y) + c.y,
+          __builtin_fmaf(qw, uv.z, p.z) + c.z};
+}
+__device__ __forceinline__ V3 se3_apply(const orbgpu_pose& T, V3 p) {
+  const V3 r = quat_rotate(T.qx, T.qy, T.qz, T.qw, p);
+  return {r.x + T.tx, r.y + T.ty, r.z + T.tz};
+}
+// Tcw.inverse().translation() with SO3's renormalised conjugate (se3.hpp:208-211)
+__device__ __forceinline__ V3 se3_inverse_translation(const orbgpu_pose& T) {
+  float q0 = -T.qx, q1 = -T.qy, q2 = -T.qz, q3 = T.qw;
+  const float s = (q0 * q0 + q2 * q2) + (q1 * q1 + q3 * q3);
+  const float len = sqrtf(s);
+  q0 /= len, q1 /= len, q2 /= len, q3 /= len;
+  return quat_rotate(q0, q1, q2, q3, V3{-T.tx, -T.ty, -T.tz});
+}
+__device__ __forceinline__ float dot3(V3 a, V3 b) {
+  return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.x, b.x, a.y * b.y));
+}
+
+__device__ __forceinline__ int kp_octave(const float* k) { return __float_as_int(k[5]); }
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint64_t o = __shfl_xor(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// A query as GetFeaturesInArea + the candidate loop see it (wave-uniform).
+struct Query {
+  bool valid;
+  float x, y, r;  // window centre / half-size (factorX = factorY = r)
+  int min_level, max_level;
+  float ur_ref;   // predicted right coordinate (motion: u - bf * invzc; local: mTrackProjXR)
+  uint32_t d[8];  // query descriptor
+};
+
+__device__ __forceinline__ void load_desc(const uint8_t* p, uint32_t d[8]) {
+  // orbgpu_proj_point / orbgpu_map_point descriptors are 4-byte aligned
+  const uint32_t* w = (const uint32_t*)p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d[i] = w[i];
+}
+
+// SearchByProjection(CurrentFrame, LastFrame) query setup (orb_matcher.cc:1529-1577)
+__device__ Query query_last(const MatchLaunch& a, int f, int q) {
+  const MatchParams& p = a.p;
+  Query Q;
+  Q.valid = false;
+  const orbgpu_pose Tcw = a.Tcw[f];
+  const orbgpu_pose Tlw = a.Tlw[f];
+  const V3 twc = se3_inverse_translation(Tcw);
+  const V3 tlc = se3_apply(Tlw, twc);
+  const bool forward = tlc.z > p.mb && !p.mono;
+  const bool backward = -tlc.z > p.mb && !p.mono;
+  const orbgpu_proj_point* P = a.ppts + (size_t)f * a.pt_stride + q;
+  const V3 x3Dc = se3_apply(Tcw, V3{P->Xw[0], P->Xw[1], P->Xw[2]});
+  const float invzc = (float)(1.0 / (double)x3Dc.z);
+  if (invzc < 0) return Q;
+  const float u = p.fx * x3Dc.x / x3Dc.z + p.cx;
+  const float v = p.fy * x3Dc.y / x3Dc.z + p.cy;
+  if (u < p.min_x || u > p.max_x) return Q;
+  if (v < p.min_y || v > p.max_y) return Q;
+  const int oct = P->octave;
+  Q.r = p.th * p.scale[oct];
+  if (forward) Q.min_level = oct, Q.max_level = -1;
+  else if (backward) Q.min_level = 0, Q.max_level = oct;
+  else Q.min_level = oct - 1, Q.max_level = oct + 1;
+  Q.x = u, Q.y = v;
+  Q.ur_ref = __builtin_fmaf(-p.bf, invzc, u);
+  load_desc(P->desc, Q.d);
+  Q.valid = true;
+  return Q;
+}
+
+// Frame::isInFrustum (frame.cc:548-603); fills V only where the reference writes.
+__device__ bool frustum(const MatchParams& p, const float* pose15, const orbgpu_map_point* M,
+                        orbgpu_track_view& V) {
+  V.in_view = 0;
+  if (M->flags & ORBGPU_MP_SKIP) return false;
+  V.proj_x = -1.0f, V.proj_y = -1.0f;
+  const float* R = pose15;
+  const float* t = pose15 + 9;
+  const float* Ow = pose15 + 12;
+  const V3 P{M->Xw[0], M->Xw[1], M->Xw[2]};
+  V3 Pc;
+  Pc.x = __builtin_fmaf(R[2], P.z, __builtin_fmaf(R[0], P.x, R[1] * P.y)) + t[0];
+  Pc.y = __builtin_fmaf(R[5], P.z, __builtin_fmaf(R[3], P.x, R[4] * P.y)) + t[1];
+  Pc.z = __builtin_fmaf(R[8], P.z, __builtin_fmaf(R[6], P.x, R[7] * P.y)) + t[2];
+  const float pc_dist = sqrtf(dot3(Pc, Pc));
+  const float invz = 1.0f / Pc.z;
+  if (Pc.z < 0.0f) return false;
+  const float u = p.fx * Pc.x / Pc.z + p.cx;
+  const float v = p.fy * Pc.y / Pc.z + p.cy;
+  if (u < p.min_x || u > p.max_x) return false;
+  if (v < p.min_y || v > p.max_y) return false;
+  V.proj_x = u, V.proj_y = v;
+  const float maxD = 1.2f * M->max_dist, minD = 0.8f * M->min_dist;
+  const V3 PO{P.x - Ow[0], P.y - Ow[1], P.z - Ow[2]};
+  const float dist = sqrtf(dot3(PO, PO));
+  if (dist < minD || dist > maxD) return false;
+  const float view_cos = dot3(PO, V3{M->normal[0], M->normal[1], M->normal[2]}) / dist;
+  if (view_cos < p.cos_limit) return false;
+  // MapPoint::PredictScale via the host's thresholds of ceil(log(ratio) / lsf)
+  const float ratio = M->max_dist / dist;
+  int level = 0;
+  if (ratio != __builtin_inff())
+    for (int j = 1; j < p.n_levels; ++j) level += ratio >= p.level_thr[j - 1];
+  V.level = level;
+  V.in_view = 1;
+  V.proj_xr = __builtin_fmaf(-p.bf, invz, u);
+  V.depth = pc_dist;
+  V.view_cos = view_cos;
+  return true;
+}
+
+// SearchByProjection(Frame&, vector<MapPoint*>) query setup (orb_matcher.cc:50-69)
+__device__ Query query_local(const MatchParams& p, const orbgpu_map_point* M,
+                             const orbgpu_track_view& V) {
+  Query Q;
+  Q.valid = false;
+  if (!V.in_view) return Q;
+  if (p.far_points && V.depth > p.th_far) return Q;
+  const int level = V.level;
+  float r = (double)V.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:208-213)
+  if (p.th != 1.0f) r *= p.th;
+  Q.r = r * p.scale[level];
+  Q.min_level = level - 1, Q.max_level = level;
+  Q.x = V.proj_x, Q.y = V.proj_y;
+  Q.ur_ref = V.proj_xr;
+  load_desc(M->desc, Q.d);
+  Q.valid = true;
+  return Q;
+}
+
+struct FrameRef {
+  const float* kps;
+  const uint4* desc;
+  const float* uright;
+  const uint8_t* claimed;
+  const int* cell_start;
+  const uint16_t* cell_idx;
+};
+
+__device__ __forceinline__ FrameRef frame_ref(const MatchLaunch& a, int f) {
+  const size_t ko = (size_t)f * a.kp_stride;
+  FrameRef F;
+  F.kps = a.kps + ko * kKpFloats;
+  F.desc = (const uint4*)(a.desc + ko * 32);
+  F.uright = a.uright ? a.uright + ko : nullptr;
+  F.claimed = a.claimed ? a.claimed + ko : nullptr;
+  F.cell_start = a.cell_start + (size_t)f * (kGridCells + 1);
+  F.cell_idx = a.cell_idx + ko;
+  return F;
+}
+
+// GetFeaturesInArea (frame.cc:679-746) + the best / second candidate loop.
+// claims (LDS bitmap, may be null) masks keypoints matched earlier in the call.
+// Returns packed (dist << 16 | idx) best and second, kNone if absent.
+__device__ void wave_search(const MatchParams& p, const FrameRef& F, const Query& Q,
+                            const uint32_t* claims, uint32_t& best, uint32_t& second) {
+  best = second = kNone;
+  if (!Q.valid) return;
+  const float r = Q.r;
+  const int minCx = max(0, (int)floorf((Q.x - p.min_x - r) * p.inv_w));
+  if (minCx >= kGridCols) return;
+  const int maxCx = min(kGridCols - 1, (int)ceilf((Q.x - p.min_x + r) * p.inv_w));
+  if (maxCx < 0) return;
+  const int minCy = max(0, (int)floorf((Q.y - p.min_y - r) * p.inv_h));
+  if (minCy >= kGridRows) return;
+  const int maxCy = min(kGridRows - 1, (int)ceilf((Q.y - p.min_y + r) * p.inv_h));
+  if (maxCy < 0) return;
+  const int ncy = maxCy - minCy + 1;
+  const int ncells = (maxCx - minCx + 1) * ncy;
+  if (ncells <= 0) return;
+  const bool check_levels = Q.min_level >= 0 || Q.max_level >= 0;
+  const int lane = threadIdx.x & 63;
+  uint64_t b1 = kNoKey, b2 = kNoKey;
+  for (int k = lane; k < ncells; k += 64) {
+    const int cx = k / ncy;
+    const int cell = (minCx + cx) * kGridRows + minCy + (k - cx * ncy);
+    const int s = F.cell_start[cell], e = F.cell_start[cell + 1];
+    for (int j = s; j < e; ++j) {
+      const int idx = F.cell_idx[j];
+      const float* kp = F.kps + (size_t)idx * kKpFloats;
+      const int oct = kp_octave(kp);
+      if (check_levels) {
+        if (oct < Q.min_level) continue;
+        if (Q.max_level >= 0 && oct > Q.max_level) continue;
+      }
+      const float dx = kp[0] - Q.x, dy = kp[1] - Q.y;
+      if (!(fabsf(dx) < r && fabsf(dy) < r)) continue;
+      if (F.claimed && F.claimed[idx]) continue;
+      if (claims && ((claims[idx >> 5] >> (idx & 31)) & 1u)) continue;
+      if (F.uright) {
+        const float uR = F.uright[idx];
+        if (uR > 0 && fabsf(Q.ur_ref - uR) > r) continue;
+      }
+      const uint4 d0 = F.desc[2 * idx], d1 = F.desc[2 * idx + 1];
+      const int dist = __popc(d0.x ^ Q.d[0]) + __popc(d0.y ^ Q.d[1]) + __popc(d0.z ^ Q.d[2]) +
+                       __popc(d0.w ^ Q.d[3]) + __popc(d1.x ^ Q.d[4]) + __popc(d1.y ^ Q.d[5]) +
+                       __popc(d1.z ^ Q.d[6]) + __popc(d1.w ^ Q.d[7]);
+      const uint64_t key = ((uint64_t)dist << 40) | ((uint64_t)k << 16) | (uint64_t)idx;
+      if (key < b1) b2 = b1, b1 = key;
+      else if (key < b2) b2 = key;
+    }
+  }
+  const uint64_t m1 = wave_min_u64(b1);
+  const uint64_t m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+  best = m1 == kNoKey ? kNone : (uint32_t)((m1 >> 40) << 16 | (m1 & 0xFFFF));
+  second = m2 == kNoKey ? kNone : (uint32_t)((m2 >> 40) << 16 | (m2 & 0xFFFF));
+}
+
+__device__ __forceinline__ Query make_query(const MatchLaunch& a, int f, int q, bool write_view) {
+  if (a.mode == kModeLast) return query_last(a, f, q);
+  const size_t o = (size_t)f * a.pt_stride + q;
+  const orbgpu_map_point* M = a.mpts + o;
+  orbgpu_track_view V;
+  if (a.mode == kModeLocalFrustum && write_view) {
+    frustum(a.p, a.frustum_pose + 15 * f, M, V);
+    if ((threadIdx.x & 63) == 0) {
+      // only the fields isInFrustum writes change
+      orbgpu_track_view O = a.views_init ? a.views_init[o] : a.views[o];
+      O.in_view = V.in_view;
+      if (!(M->flags & ORBGPU_MP_SKIP)) O.proj_x = V.proj_x, O.proj_y = V.proj_y;
+      if (V.in_view) O.level = V.level, O.proj_xr = V.proj_xr, O.depth = V.depth, O.view_cos = V.view_cos;
+      a.views[o] = O;
+    }
+  } else {
+    V = a.views[o];
+  }
+  return query_local(a.p, M, V);
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mt_grid(MatchLaunch a) {
+  __shared__ int cnt[kGridCells];
+  __shared__ int start[kGridCells];
+  __shared__ uint16_t lidx[kMatchMaxKeypoints];
+  __shared__ int part[256];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int n = a.n[f];
+  if (n > kMatchMaxKeypoints || n > a.kp_stride) {
+    if (t == 0) atomicOr(a.err, 1);
+    return;
+  }
+  const float* kps = a.kps + (size_t)f * a.kp_stride * kKpFloats;
+  for (int c = t; c < kGridCells; c += 256) cnt[c] = 0;
+  __syncthreads();
+  // Frame::PosInGrid (frame.cc:748-759)
+  auto cell_of = [&](int i) -> int {
+    const float* k = kps + (size_t)i * kKpFloats;
+    const int px = (int)roundf((k[0] - a.p.min_x) * a.p.inv_w);
+    const int py = (int)roundf((k[1] - a.p.min_y) * a.p.inv_h);
+    if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
+    return px * kGridRows + py;
+  };
+  for (int i = t; i < n; i += 256) {
+    const int c = cell_of(i);
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+  __syncthreads();
+  constexpr int kPer = kGridCells / 256;  // 12 cells per thread
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) sum += cnt[t * kPer + j];
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the partials
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  int* cs = a.cell_start + (size_t)f * (kGridCells + 1);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int c = t * kPer + j;
+    const int v = cnt[c];
+    start[c] = run;
+    cs[c] = run;
+    cnt[c] = run;  // cursor
+    run += v;
+  }
+  if (t == 255) cs[kGridCells] = part[255];
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const int c = cell_of(i);
+    if (c >= 0) lidx[atomicAdd(&cnt[c], 1)] = (uint16_t)i;
+  }
+  __syncthreads();
+  // ascending keypoint index inside each cell (push_back order, frame.cc:452-464)
+  for (int c = t; c < kGridCells; c += 256) {
+    const int s = start[c], e = cnt[c];
+    for (int i = s + 1; i < e; ++i) {
+      const uint16_t v = lidx[i];
+      int j = i - 1;
+      while (j >= s && lidx[j] > v) lidx[j + 1] = lidx[j], --j;
+      lidx[j + 1] = v;
+    }
+  }
+  __syncthreads();
+  const int total = part[255];
+  uint16_t* out = a.cell_idx + (size_t)f * a.kp_stride;
+  for (int i = t; i < total; i += 256) out[i] = lidx[i];
+}
+
+__global__ __launch_bounds__(256) void k_mt_search(MatchLaunch a) {
+  const int f = blockIdx.y;
+  const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (q >= a.npts[f]) return;
+  const FrameRef F = frame_ref(a, f);
+  const Query Q = make_query(a, f, q, true);
+  uint32_t best, second;
+  wave_search(a.p, F, Q, nullptr, best, second);
+  if ((threadIdx.x & 63) == 0) {
+    uint32_t* r = a.res + 2 * ((size_t)f * a.pt_stride + q);
+    r[0] = best, r[1] = second;
+  }
+}
+
+// accept decision of one query from its (best, second)
+__device__ __forceinline__ bool accept_of(const MatchLaunch& a, const float* kps, uint32_t best,
+                                          uint32_t second) {
+  if (best == kNone) return false;
+  const int d1 = (int)(best >> 16);
+  if (d1 > kThHigh) return false;
+  if (a.mode == kModeLast) return true;
+  // orb_matcher.cc:117-121: reject iff same level and d1 > ratio * d2
+  const int l1 = kp_octave(kps + (size_t)(best & 0xFFFF) * kKpFloats);
+  const int l2 = second == kNone ? -1 : kp_octave(kps + (size_t)(second & 0xFFFF) * kKpFloats);
+  const int d2 = second == kNone ? 256 : (int)(second >> 16);
+  return !(l1 == l2 && (float)d1 > a.p.nn_ratio * (float)d2);
+}
+
+__device__ __forceinline__ bool has_obs(const MatchLaunch& a, int f, int q) {
+  const size_t o = (size_t)f * a.pt_stride + q;
+  return a.mode == kModeLast ? a.ppts[o].has_obs != 0 : (a.mpts[o].flags & ORBGPU_MP_HAS_OBS) != 0;
+}
+
+// rotation bin of a match (orb_matcher.cc:1626-1630)
+__device__ __forceinline__ int rot_bin(const MatchLaunch& a, const float* kps, int f, int q,
+                                       int idx) {
+  const float factor = kHistoLength / 360.0f;
+  float rot = a.ppts[(size_t)f * a.pt_stride + q].angle - kps[(size_t)idx * kKpFloats + 3];
+  if ((double)rot < 0.0) rot += 360.0f;
+  int bin = (int)roundf(rot * factor);
+  if (bin == kHistoLength) bin = 0;
+  return bin;
+}
+
+__global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
+  __shared__ uint32_t owner[kMatchMaxKeypoints];  // in-batch first claiming lane, 64 = none
+  __shared__ uint32_t claims[kMatchMaxKeypoints / 32];
+  __shared__ uint32_t removed[kMatchMaxKeypoints / 32];
+  __shared__ int hist[kHistoLength];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int n = a.n[f], nq = a.npts[f];
+  if (n > kMatchMaxKeypoints) return;  // reported by k_mt_grid
+  const FrameRef F = frame_ref(a, f);
+  const bool rot_check = a.mode == kModeLast && a.p.check_ori;
+  const bool local = a.mode != kModeLast;
+  // mvpMapPoints of this call: the last matching query (later matches
+  // overwrite, orb_matcher.cc:122, 1611), kept with atomicMax in the output
+  int32_t* match = a.match + (size_t)f * a.kp_stride;
+  for (int i = lane; i < n; i += 64) match[i] = -1, owner[i] = 64;
+  for (int i = lane; i < kMatchMaxKeypoints / 32; i += 64) claims[i] = 0, removed[i] = 0;
+  if (lane < kHistoLength) hist[lane] = 0;
+  __syncthreads();
+  const uint32_t* res = a.res + 2 * (size_t)f * a.pt_stride;
+  int32_t* acc = a.acc + (size_t)f * a.pt_stride;
+  int nmatch = 0;
+  auto claimed_bit = [&](uint32_t key) -> bool {
+    if (key == kNone) return false;
+    const int idx = key & 0xFFFF;
+    return (claims[idx >> 5] >> (idx & 31)) & 1u;
+  };
+  for (int base = 0; base < nq; base += 64) {
+    const int q = base + lane;
+    const bool valid = q < nq;
+    const uint32_t best = valid ? res[2 * q] : kNone;
+    const uint32_t second = valid ? res[2 * q + 1] : kNone;
+    const bool acc0 = valid && accept_of(a, F.kps, best, second);
+    // a query whose best is beyond TH_HIGH stays unmatched whatever is claimed
+    const bool need_check = best != kNone && (int)(best >> 16) <= kThHigh;
+    const bool claimer = acc0 && has_obs(a, f, q);
+    if (claimer) atomicMin(&owner[best & 0xFFFF], (uint32_t)lane);
+    __syncthreads();
+    bool conflict = false;
+    if (need_check) {
+      conflict = claimed_bit(best) || owner[best & 0xFFFF] < (uint32_t)lane;
+      if (local && second != kNone)
+        conflict = conflict || claimed_bit(second) || owner[second & 0xFFFF] < (uint32_t)lane;
+    }
+    __syncthreads();
+    if (claimer) owner[best & 0xFFFF] = 64;
+    const uint64_t cmask = __ballot(conflict);
+    const int first = cmask ? __builtin_ctzll(cmask) : 64;
+    // lanes before the first hit commit together
+    if (lane < first && valid) {
+      if (acc0) {
+        const int idx = best & 0xFFFF;
+        atomicMax(&match[idx], q);
+        if (claimer) atomicOr(&claims[idx >> 5], 1u << (idx & 31));
+        int bin = 0;
+        if (rot_check) {
+          bin = rot_bin(a, F.kps, f, q, idx);
+          atomicAdd(&hist[bin], 1);
+        }
+        acc[q] = idx | (bin << 16);
+      } else {
+        acc[q] = -1;
+      }
+    }
+    nmatch += __popcll(__ballot(lane < first && acc0));
+    __syncthreads();
+    // the rest one at a time, in query order
+    for (int l = first; l < 64 && base + l < nq; ++l) {
+      const int ql = base + l;
+      uint32_t b = __builtin_amdgcn_readlane(best, l);
+      uint32_t s2 = __builtin_amdgcn_readlane(second, l);
+      const bool nc = __builtin_amdgcn_readlane((int)need_check, l) != 0;
+      const bool hit = nc && (claimed_bit(b) || (local && claimed_bit(s2)));
+      if (hit) {
+        const Query Q = make_query(a, f, ql, false);
+        wave_search(a.p, F, Q, claims, b, s2);
+      }
+      const bool ok = accept_of(a, F.kps, b, s2);
+      if (lane == 0) {
+        if (ok) {
+          const int idx = b & 0xFFFF;
+          atomicMax(&match[idx], ql);
+          if (has_obs(a, f, ql)) claims[idx >> 5] |= 1u << (idx & 31);
+          int bin = 0;
+          if (rot_check) {
+            bin = rot_bin(a, F.kps, f, ql, idx);
+            hist[bin] += 1;
+          }
+          acc[ql] = idx | (bin << 16);
+        } else {
+          acc[ql] = -1;
+        }
+      }
+      nmatch += ok;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (rot_check) {
+    // ComputeThreeMaxima (orb_matcher.cc:1841-1873), every lane
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < kHistoLength; ++i) {
+      const int s = hist[i];
+      if (s > max1) {
+        max3 = max2, max2 = max1, max1 = s;
+        ind3 = ind2, ind2 = ind1, ind1 = i;
+      } else if (s > max2) {
+        max3 = max2, max2 = s;
+        ind3 = ind2, ind2 = i;
+      } else if (s > max3) {
+        max3 = s, ind3 = i;
+      }
+    }
+    if ((float)max2 < 0.1f * (float)max1) ind2 = ind3 = -1;
+    else if ((float)max3 < 0.1f * (float)max1) ind3 = -1;
+    // every match in another bin is set to NULL (:1716-1724)
+    int dropped = 0;
+    for (int q = lane; q < nq; q += 64) {
+      const int v = acc[q];
+      if (v < 0) continue;
+      const int bin = v >> 16;
+      if (bin != ind1 && bin != ind2 && bin != ind3) {
+        const int idx = v & 0xFFFF;
+        atomicOr(&removed[idx >> 5], 1u << (idx & 31));
+        ++dropped;
+      }
+    }
+    for (int off = 32; off >= 1; off >>= 1) dropped += __shfl_xor(dropped, off, 64);
+    nmatch -= dropped;
+    __syncthreads();
+    for (int i = lane; i < n; i += 64)
+      if ((removed[i >> 5] >> (i & 31)) & 1u) atomicExch(&match[i], -2);
+  }
+  if (lane == 0) a.nmatches[f] = nmatch;
+}
+
+}  // namespace
+
+hipError_t launch_match(const MatchLaunch& a, hipStream_t st) {
+  if (a.n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mt_grid, dim3(a.n_frames), dim3(256), 0, st, a);
+  if (a.max_pts > 0) {
+    hipLaunchKernelGGL(k_mt_search, dim3((unsigned)((a.max_pts + 3) / 4), a.n_frames), dim3(256),
+                       0, st, a);
+  }
+  hipLaunchKernelGGL(k_mt_resolve, dim3(a.n_frames), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,71 @@
+// Launch descriptor of the ORBmatcher projection searches
+// (orb_matcher.cc:42-206, 1518-1728) over a batch of frames.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/orbgpu.h"
+
+namespace orbgpu {
+
+constexpr int kGridCols = ORBGPU_FRAME_GRID_COLS, kGridRows = ORBGPU_FRAME_GRID_ROWS;
+constexpr int kGridCells = kGridCols * kGridRows;
+constexpr int kMatchMaxKeypoints = 8192;  // per frame (LDS-resident claim state)
+constexpr int kMatchMaxPoints = 1 << 20;  // per frame
+
+enum MatchMode : int { kModeLast = 0, kModeLocal = 1, kModeLocalFrustum = 2 };
+
+// Everything scalar the searches read (passed by value).
+struct MatchParams {
+  float min_x, max_x, min_y, max_y;
+  float inv_w, inv_h;  // FRAME_GRID_COLS / (mnMaxX - mnMinX), ROWS / (mnMaxY - mnMinY)
+  int n_levels;
+  float scale[ORBGPU_MAX_LEVELS];
+  // MapPoint::PredictScale as thresholds: level = #{j >= 1 : ratio >= thr[j-1]}
+  // (host-computed from the reference's ::log(double), see match_api.cpp)
+  float level_thr[ORBGPU_MAX_LEVELS];
+  float fx, fy, cx, cy, bf, mb;
+  float th, nn_ratio, th_far, cos_limit;
+  int mono, check_ori, far_points;
+};
+
+struct MatchLaunch {
+  MatchParams p;
+  int mode;
+  int n_frames;
+  // current frames: frame f's arrays start at f * kp_stride (keypoints)
+  const float* kps;  // orbgpu_keypoint rows (7 x 4 bytes)
+  const uint8_t* desc;
+  const float* uright;     // may be null
+  const uint8_t* claimed;  // may be null
+  const int* n;            // keypoints per frame (device)
+  int kp_stride;
+  // queries: frame f's points start at f * pt_stride
+  const orbgpu_proj_point* ppts;  // kModeLast
+  const orbgpu_map_point* mpts;   // kModeLocal*
+  orbgpu_track_view* views;       // kModeLocal*: read (kModeLocal) / written (kModeLocalFrustum)
+  // kModeLocalFrustum: prior field values for the ones isInFrustum does not
+  // write (null: views itself, updated in place)
+  const orbgpu_track_view* views_init;
+  const int* npts;                // points per frame (device)
+  int pt_stride;
+  int max_pts;                    // max over frames of npts (grid sizing)
+  const orbgpu_pose* Tcw;         // kModeLast: [n_frames]
+  const orbgpu_pose* Tlw;
+  // Rcw (row-major), tcw, Ow per frame, 15 floats: kModeLocalFrustum
+  const float* frustum_pose;
+  // scratch
+  int* cell_start;      // [n_frames][kGridCells + 1]
+  uint16_t* cell_idx;   // [n_frames][kp_stride]
+  uint32_t* res;        // [n_frames][pt_stride][2]: (dist << 16 | idx) best, second
+  int32_t* acc;         // [n_frames][pt_stride]: accepted idx | bin << 16, or -1
+  // outputs
+  int32_t* match;       // [n_frames][kp_stride]
+  int* nmatches;        // [n_frames]
+  int* err;
+};
+
+hipError_t launch_match(const MatchLaunch& a, hipStream_t st);
+
+}  // namespace orbgpu

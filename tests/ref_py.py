@@ -288,3 +288,203 @@ def stereo_match_py(kl, dl, kr, dr, pyr_l, pyr_r, scale, inv_scale, bf, mb):
             if not (f32(d) < th):
                 ur[i] = dep[i] = -1.0
     return ur, dep
+
+
+# --- ORBmatcher projection searches (orb_matcher.cc, frame.cc) --------------
+# Float arithmetic in float32 with the reference build's fused multiply-adds;
+# fmaf is emulated in x86 long double (64-bit mantissa: the product of two
+# floats is exact, the sum rounds once before the final float rounding).
+
+def _f(x):
+    return np.float32(x)
+
+
+def _fmaf(a, b, c):
+    return np.float32(np.longdouble(np.float32(a)) * np.longdouble(np.float32(b))
+                      + np.longdouble(np.float32(c)))
+
+
+def _cross(a, b):
+    return [_fmaf(a[1], b[2], -(_f(a[2]) * _f(b[1]))), _fmaf(a[2], b[0], -(_f(a[0]) * _f(b[2]))),
+            _fmaf(a[0], b[1], -(_f(a[1]) * _f(b[0])))]
+
+
+def _qrot(q, p):
+    qv = [q[0], q[1], q[2]]
+    uv = _cross(qv, p)
+    uv = [_f(u + u) for u in uv]
+    c = _cross(qv, uv)
+    return [_f(_fmaf(q[3], uv[i], p[i]) + c[i]) for i in range(3)]
+
+
+def _se3(T, p):
+    r = _qrot([_f(v) for v in T[:4]], [_f(v) for v in p])
+    return [_f(r[i] + _f(T[4 + i])) for i in range(3)]
+
+
+def _round(v):
+    """std::round / roundf: half away from zero."""
+    v = float(v)
+    return int(np.trunc(v + np.copysign(0.5, v)))
+
+
+def _popcount_dist(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+class _PyFrame:
+    def __init__(self, geom, kps, desc, uright, claimed):
+        self.g, self.kps, self.desc, self.ur = geom, kps, desc, uright
+        self.inv_w = _f(_f(64) / _f(_f(geom.max_x) - _f(geom.min_x)))
+        self.inv_h = _f(_f(48) / _f(_f(geom.max_y) - _f(geom.min_y)))
+        n = len(kps)
+        self.holder = [-1] * n
+        self.hobs = [False] * n
+        if claimed is not None:
+            for i in range(n):
+                if claimed[i]:
+                    self.holder[i], self.hobs[i] = -2, True
+        self.grid = {}
+        for i in range(n):
+            px = _round(_f(_f(kps["x"][i]) - _f(geom.min_x)) * self.inv_w)
+            py = _round(_f(_f(kps["y"][i]) - _f(geom.min_y)) * self.inv_h)
+            if 0 <= px < 64 and 0 <= py < 48:
+                self.grid.setdefault((px, py), []).append(i)
+
+    def area(self, x, y, r, lo, hi):
+        x, y, r = _f(x), _f(y), _f(r)
+        g = self.g
+        x0 = max(0, int(np.floor(_f(_f(x - _f(g.min_x)) - r) * self.inv_w)))
+        if x0 >= 64:
+            return []
+        x1 = min(63, int(np.ceil(_f(_f(x - _f(g.min_x)) + r) * self.inv_w)))
+        if x1 < 0:
+            return []
+        y0 = max(0, int(np.floor(_f(_f(y - _f(g.min_y)) - r) * self.inv_h)))
+        if y0 >= 48:
+            return []
+        y1 = min(47, int(np.ceil(_f(_f(y - _f(g.min_y)) + r) * self.inv_h)))
+        if y1 < 0:
+            return []
+        chk = lo >= 0 or hi >= 0
+        out = []
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                for i in self.grid.get((ix, iy), []):
+                    o = int(self.kps["octave"][i])
+                    if chk and (o < lo or (hi >= 0 and o > hi)):
+                        continue
+                    if abs(_f(self.kps["x"][i]) - x) < r and abs(_f(self.kps["y"][i]) - y) < r:
+                        out.append(i)
+        return out
+
+    def blocked(self, i):
+        return self.holder[i] != -1 and self.hobs[i]
+
+
+def search_last_py(geom, cam, mb, Tcw, Tlw, kps, desc, uright, claimed, pts, th, mono, check_ori):
+    """SearchByProjection(CurrentFrame, LastFrame) (orb_matcher.cc:1518-1728)."""
+    F = _PyFrame(geom, kps, desc, uright, claimed)
+    fx, fy, cx, cy, bf = (_f(v) for v in cam)
+    # Tcw.inverse().translation(): conjugate quaternion renormalised, then -t rotated
+    q = [-_f(Tcw[0]), -_f(Tcw[1]), -_f(Tcw[2]), _f(Tcw[3])]
+    s = _f(_f(_f(q[0] * q[0]) + _f(q[2] * q[2])) + _f(_f(q[1] * q[1]) + _f(q[3] * q[3])))
+    ln = np.sqrt(s, dtype=np.float32)
+    q = [_f(c / ln) for c in q]
+    twc = _qrot(q, [-_f(Tcw[4]), -_f(Tcw[5]), -_f(Tcw[6])])
+    tlc = _se3(Tlw, twc)
+    fwd = tlc[2] > _f(mb) and not mono
+    bwd = -tlc[2] > _f(mb) and not mono
+    hist = [[] for _ in range(30)]
+    nm = 0
+    th = _f(th)
+    for j, P in enumerate(pts):
+        X = _se3(Tcw, P["Xw"])
+        invz = _f(1.0 / float(X[2]))
+        if invz < 0:
+            continue
+        u = _f(_f(fx * X[0]) / X[2] + cx)
+        v = _f(_f(fy * X[1]) / X[2] + cy)
+        if u < _f(geom.min_x) or u > _f(geom.max_x) or v < _f(geom.min_y) or v > _f(geom.max_y):
+            continue
+        o = int(P["octave"])
+        rad = _f(th * _f(geom.scale_factors[o]))
+        if fwd:
+            cand = F.area(u, v, rad, o, -1)
+        elif bwd:
+            cand = F.area(u, v, rad, 0, o)
+        else:
+            cand = F.area(u, v, rad, o - 1, o + 1)
+        best, bi = 256, -1
+        for i in cand:
+            if F.blocked(i):
+                continue
+            if uright is not None and uright[i] > 0:
+                ur = _fmaf(-bf, invz, u)
+                if abs(_f(ur - _f(uright[i]))) > rad:
+                    continue
+            d = _popcount_dist(P["desc"], desc[i])
+            if d < best:
+                best, bi = d, i
+        if best <= 100:
+            F.holder[bi], F.hobs[bi] = j, bool(P["has_obs"])
+            nm += 1
+            if check_ori:
+                rot = _f(_f(P["angle"]) - _f(kps["angle"][bi]))
+                if rot < 0:
+                    rot = _f(rot + _f(360))
+                b = _round(_f(rot * _f(_f(30) / _f(360))))
+                hist[0 if b == 30 else b].append(bi)
+    nulled = set()
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        order = sorted(range(30), key=lambda b: (-sizes[b], b))
+        m1 = sizes[order[0]]
+        keep = {order[0]} if m1 > 0 else set()
+        if m1 > 0 and sizes[order[1]] > 0 and not (_f(sizes[order[1]]) < _f(0.1) * _f(m1)):
+            keep.add(order[1])
+            if sizes[order[2]] > 0 and not (_f(sizes[order[2]]) < _f(0.1) * _f(m1)):
+                keep.add(order[2])
+        for b in range(30):
+            if b not in keep:
+                for i in hist[b]:
+                    F.holder[i] = -1
+                    nulled.add(i)
+                    nm -= 1
+    match = np.array([-2 if i in nulled else (h if h >= 0 else -1)
+                      for i, h in enumerate(F.holder)], np.int32)
+    return nm, match
+
+
+def search_local_py(geom, kps, desc, uright, claimed, pts, views, th, nn):
+    """SearchByProjection(F, vpMapPoints, th) (orb_matcher.cc:42-137)."""
+    F = _PyFrame(geom, kps, desc, uright, claimed)
+    nm = 0
+    for j, (P, V) in enumerate(zip(pts, views)):
+        if not V["in_view"]:
+            continue
+        lv = int(V["level"])
+        r = _f(2.5) if float(V["view_cos"]) > 0.998 else _f(4.0)
+        if th != 1.0:
+            r = _f(r * _f(th))
+        rs = _f(r * _f(geom.scale_factors[lv]))
+        cand = F.area(V["proj_x"], V["proj_y"], rs, lv - 1, lv)
+        ranked = []
+        for pos, i in enumerate(cand):
+            if F.blocked(i):
+                continue
+            if uright is not None and uright[i] > 0 and abs(_f(_f(V["proj_xr"]) - _f(uright[i]))) > rs:
+                continue
+            ranked.append((_popcount_dist(P["desc"], desc[i]), pos, i))
+        if not ranked:
+            continue
+        ranked.sort()
+        d1, _, i1 = ranked[0]
+        d2, l2 = (ranked[1][0], int(kps["octave"][ranked[1][2]])) if len(ranked) > 1 else (256, -1)
+        if d1 > 100:
+            continue
+        if int(kps["octave"][i1]) == l2 and _f(d1) > _f(_f(nn) * _f(d2)):
+            continue
+        F.holder[i1], F.hobs[i1] = j, bool(P["flags"] & 2)
+        nm += 1
+    return nm, np.array([h if h >= 0 else -1 for h in F.holder], np.int32)

@@ -1,0 +1,144 @@
+"""CPU tests of the ORBmatcher projection-search oracle (match_oracle.cc):
+independent Python restatement, PredictScale threshold table of the GPU
+library's host code (exhaustive over the ratios tracking produces), the GCC
+contraction pattern the restated float expressions assume, grid cells."""
+import subprocess
+
+import numpy as np
+import pytest
+
+import binding as orc
+from match_cases import CAM, W, H, last_case, local_case, scale_factors
+from orb_slam_fusion_amd.matcher import frame_geom, level_thresholds
+from ref_py import search_last_py, search_local_py
+
+
+@pytest.mark.parametrize("seed,motion,th,ori,stereo,mono", [
+    (1, "none", 7, True, True, False),
+    (2, "forward", 7, True, True, False),
+    (3, "backward", 15, True, True, False),
+    (4, "none", 30, False, False, False),
+    (5, "forward", 15, True, True, True),   # bMono: no forward/backward windows
+])
+def test_search_last_matches_python(seed, motion, th, ori, stereo, mono):
+    c = last_case(seed, n_kp=220, n_pts=150, stereo=stereo, motion=motion)
+    nm, m = orc.search_last(c.geom, c.cam, c.mb, c.Tcw, c.Tlw, c.kps, c.desc, c.uright, c.claimed,
+                            c.pts, th, mono, ori)
+    nm_py, m_py = search_last_py(c.geom, c.cam, c.mb, c.Tcw, c.Tlw, c.kps, c.desc, c.uright,
+                                 c.claimed, c.pts, th, mono, ori)
+    assert nm == nm_py
+    np.testing.assert_array_equal(m, m_py)
+    assert nm > 10
+
+
+@pytest.mark.parametrize("seed,th,stereo", [(11, 1, True), (12, 3, True), (13, 15, False)])
+def test_search_local_matches_python(seed, th, stereo):
+    c = local_case(seed, n_kp=220, n_pts=180, stereo=stereo)
+    v = orc.frustum(c.geom, c.cam, c.Rcw, c.tcw, c.Ow, c.pts, 0.5)
+    assert v["in_view"].sum() > 50
+    nm, m = orc.search_local(c.geom, c.kps, c.desc, c.uright, c.claimed, c.pts, v, th, 0.8)
+    nm_py, m_py = search_local_py(c.geom, c.kps, c.desc, c.uright, c.claimed, c.pts, v, th, 0.8)
+    assert nm == nm_py
+    np.testing.assert_array_equal(m, m_py)
+
+
+def test_far_points_and_empty_inputs():
+    c = local_case(21, n_kp=150, n_pts=120)
+    v = orc.frustum(c.geom, c.cam, c.Rcw, c.tcw, c.Ow, c.pts, 0.5)
+    nm_all, _ = orc.search_local(c.geom, c.kps, c.desc, c.uright, c.claimed, c.pts, v, 3, 0.8)
+    nm_near, _ = orc.search_local(c.geom, c.kps, c.desc, c.uright, c.claimed, c.pts, v, 3, 0.8,
+                                  True, 4.0)
+    assert nm_near < nm_all
+    nm0, m0 = orc.search_local(c.geom, c.kps[:0], c.desc[:0], None, None, c.pts, v, 3, 0.8)
+    assert nm0 == 0 and len(m0) == 0
+    nm1, m1 = orc.search_local(c.geom, c.kps, c.desc, None, None, c.pts[:0], v[:0], 3, 0.8)
+    assert nm1 == 0 and (m1 == -1).all()
+
+
+def test_frustum_fields_and_skip():
+    c = local_case(22, n_kp=100, n_pts=200)
+    init = np.zeros(len(c.pts), orc.TRACK_VIEW_DTYPE)
+    init["level"] = 77
+    init["proj_x"] = 123.0
+    v = orc.frustum(c.geom, c.cam, c.Rcw, c.tcw, c.Ow, c.pts, 0.5, init)
+    skip = (c.pts["flags"] & 1) != 0
+    assert (v["in_view"][skip] == 0).all() and (v["proj_x"][skip] == 123.0).all()
+    out = (v["in_view"] == 0) & ~skip
+    assert (v["level"][out] == 77).all()           # not written by isInFrustum
+    inv = v["in_view"] == 1
+    assert ((v["level"][inv] >= 0) & (v["level"][inv] < 8)).all()
+    # mTrackProjXR = u - bf / z
+    assert np.all(v["proj_xr"][inv] <= v["proj_x"][inv])
+
+
+def test_predict_scale_threshold_table_exhaustive():
+    """The GPU library's thresholds reproduce ceil(log(ratio) / lsf) on every
+    float ratio in [2^-2, 2^6) (isInFrustum admits [1/1.2, 1.25 * 1.2^7 * slack])."""
+    lsf = float(np.log(np.float32(1.2)))
+    thr = level_thresholds(lsf, 8)
+    assert np.all(np.diff(thr[:7]) > 0) and np.isinf(thr[7:]).all()
+    lo = int(np.float32(0.25).view(np.uint32))
+    hi = int(np.float32(64.0).view(np.uint32))
+    assert orc.predict_scale_check(lsf, 8, thr, lo, hi) == 0
+    # other pyramids
+    for scale, L in [(1.5, 4), (2.0, 3), (1.1, 12)]:
+        lsf = float(np.log(np.float32(scale)))
+        thr = level_thresholds(lsf, L)
+        lo = int(np.float32(0.5).view(np.uint32))
+        hi = int(np.float32(4.0 * scale ** L).view(np.uint32))
+        assert orc.predict_scale_check(lsf, L, thr, lo, hi) == 0
+
+
+def test_predict_scale_values():
+    lsf = float(np.log(np.float32(1.2)))
+    assert orc.predict_scale(1.0, 1.0, lsf, 8) == 0
+    assert orc.predict_scale(1.2, 1.0, lsf, 8) in (0, 1)  # on the boundary: libm decides
+    assert orc.predict_scale(1.21, 1.0, lsf, 8) == 2
+    assert orc.predict_scale(100.0, 1.0, lsf, 8) == 7
+    assert orc.predict_scale(1.0, 3.0, lsf, 8) == 0
+    assert orc.predict_scale(1.0, 0.0, lsf, 8) == 0   # inf ratio -> cvttsd2si INT_MIN -> 0
+
+
+def test_grid_cells_match_pos_in_grid():
+    c = last_case(31, n_kp=300, n_pts=1)
+    cells = orc.frame_grid_cells(c.geom, c.kps)
+    fx = ((c.kps["x"] - np.float32(0)) * np.float32(64 / np.float32(W))).astype(np.float64)
+    fy = ((c.kps["y"] - np.float32(0)) * np.float32(48 / np.float32(H))).astype(np.float64)
+    px = np.trunc(fx + 0.5).astype(int)  # std::round on non-negatives
+    py = np.trunc(fy + 0.5).astype(int)
+    ok = (px >= 0) & (px < 64) & (py >= 0) & (py < 48)
+    np.testing.assert_array_equal(cells[ok], px[ok] * 48 + py[ok])
+    assert (cells[~ok] == -1).all()
+
+
+SNIPPET = r"""
+float mv(float r0,float r1,float r2,float x,float y,float z,float t){ return r0*x + r1*y + r2*z + t; }
+float sq(float x,float y,float z){ return x*x + y*y + z*z; }
+float ab(float a,float b,float c,float d){ return a*b - c*d; }
+float rc(float p, float w, float u, float c){ return p + w*u + c; }
+float ur(float u, float bf, float iz){ return u - bf*iz; }
+"""
+
+
+def test_gcc_contraction_pattern(tmp_path):
+    """The restated Eigen/Sophus expressions assume GCC's fusion of the FIRST
+    product of a sum (the reference builds -O2 -march=native C++, where
+    contraction is on): checked on GCC 11 output for the scalar forms."""
+    src = tmp_path / "c.cc"
+    src.write_text(SNIPPET)
+    asm = subprocess.run(["g++", "-std=c++11", "-O2", "-march=haswell", "-S", "-o", "-", str(src)],
+                         capture_output=True, text=True, check=True).stdout
+    fn = {}
+    cur = None
+    for line in asm.splitlines():
+        if line.startswith("_Z") and line.endswith(":"):
+            cur = line[:-1]
+            fn[cur] = []
+        elif cur and line.strip().startswith("v"):
+            fn[cur].append(line.split()[0])
+    mv = fn["_Z2mvfffffff"]
+    assert mv == ["vmulss", "vfmadd132ss", "vfmadd132ss", "vaddss"]  # r1*y; fma(r0,x,.); fma(r2,z,.); +t
+    assert fn["_Z2sqfff"] == ["vmulss", "vfmadd132ss", "vfmadd231ss"]
+    assert fn["_Z2abffff"] == ["vmulss", "vfmsub132ss"]             # fma(a, b, -(c*d))
+    assert fn["_Z2rcffff"] == ["vfmadd132ss", "vaddss"]             # fma(w, u, p) + c
+    assert fn["_Z2urfff"] == ["vfnmadd231ss"]                       # fma(-bf, iz, u)
