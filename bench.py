@@ -96,6 +96,10 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches side line")
+    ap.add_argument("--no-match", action="store_true",
+                    help="skip the SearchByProjection (motion-model search) side line")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the per-frame host-path latency side line")
     args = ap.parse_args()
 
     import torch
@@ -283,6 +287,20 @@ def main() -> int:
         from bench_stereo import measure as measure_stereo  # noqa: E402
 
         result["stereo"] = measure_stereo(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+    if rank == 0 and world == 1 and not args.no_match:
+        # SURVEY §8(f) rank 2, beside the headline metric (not part of it):
+        # SearchByProjection(CurrentFrame, LastFrame) on resident frame outputs
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_match import measure as measure_match  # noqa: E402
+
+        result["match"] = measure_match(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+    if rank == 0 and world == 1 and not args.no_latency:
+        # north_star's per-frame target: one stereo frame at a time through the
+        # host ABI (2-thread extraction + PoseOptimization) vs the CPU oracle
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_latency import measure as measure_latency  # noqa: E402
+
+        result["latency"] = measure_latency(frames=40, cpu_frames=0 if args.no_cpu_baseline else 8)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()

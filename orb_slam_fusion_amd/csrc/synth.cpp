@@ -31,15 +31,12 @@ struct XorShift64Star {
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-// Stereo pair from one canvas of width w + disparity: left(x) = canvas(x),
-// right(x) = canvas(x + disparity).  Canvas = vertical gradient 40..200, 300
-// axis-aligned rectangles (sides U[4,60], grey U[0,255]), 150 discs (radius
-// U[3,25]), then per-pixel U[-6,6] noise, clamped.  seed = 0x5EED0000 + frame.
-void synth_stereo_frame(uint64_t seed, int w, int h, int disparity, uint8_t* left,
-                        uint8_t* right) {
-  const int cw = w + disparity;
+// Canvas = vertical gradient 40..200, 300 axis-aligned rectangles (sides
+// U[4,60], grey U[0,255]), 150 discs (radius U[3,25]), then per-pixel U[-6,6]
+// noise, clamped.
+std::vector<int> make_canvas(uint64_t seed, int cw, int h) {
   std::vector<int> c((size_t)cw * h);
   XorShift64Star rng(seed);
   for (int y = 0; y < h; ++y)
@@ -63,11 +60,41 @@ void synth_stereo_frame(uint64_t seed, int w, int h, int disparity, uint8_t* lef
     int v = c[i] + rng.uniform(-6, 6);
     c[i] = v < 0 ? 0 : v > 255 ? 255 : v;
   }
+  return c;
+}
+
+void crop(const std::vector<int>& c, int cw, int w, int h, int x0, uint8_t* out) {
+  if (!out) return;
   for (int y = 0; y < h; ++y)
-    for (int x = 0; x < w; ++x) {
-      if (left) left[(size_t)y * w + x] = (uint8_t)c[(size_t)y * cw + x];
-      if (right) right[(size_t)y * w + x] = (uint8_t)c[(size_t)y * cw + x + disparity];
-    }
+    for (int x = 0; x < w; ++x) out[(size_t)y * w + x] = (uint8_t)c[(size_t)y * cw + x + x0];
+}
+
+}  // namespace
+
+extern "C" {
+
+// Stereo pair from one canvas of width w + disparity: left(x) = canvas(x),
+// right(x) = canvas(x + disparity).  seed = 0x5EED0000 + frame.
+void synth_stereo_frame(uint64_t seed, int w, int h, int disparity, uint8_t* left,
+                        uint8_t* right) {
+  const int cw = w + disparity;
+  const std::vector<int> c = make_canvas(seed, cw, h);
+  crop(c, cw, w, h, 0, left);
+  crop(c, cw, w, h, disparity, right);
+}
+
+// Two consecutive stereo frames of a camera translating along x over the
+// fronto-parallel canvas plane (depth bf / disparity): last(x) = canvas(x +
+// shift), current(x) = canvas(x), so every feature moves +shift px from the
+// last frame to the current one.  Canvas width w + disparity + shift.
+void synth_track_pair(uint64_t seed, int w, int h, int disparity, int shift, uint8_t* last_l,
+                      uint8_t* last_r, uint8_t* cur_l, uint8_t* cur_r) {
+  const int cw = w + disparity + shift;
+  const std::vector<int> c = make_canvas(seed, cw, h);
+  crop(c, cw, w, h, shift, last_l);
+  crop(c, cw, w, h, shift + disparity, last_r);
+  crop(c, cw, w, h, 0, cur_l);
+  crop(c, cw, w, h, disparity, cur_r);
 }
 
 // Plain noise image (stress case: dense FAST responses, large octree input).

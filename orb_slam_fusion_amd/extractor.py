@@ -17,6 +17,7 @@ src/cam/orb_feature/orb_extractor.cc:407-465, 1011-1117):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Optional, Sequence, Tuple
 
@@ -148,14 +149,14 @@ class OrbExtractor:
         B, H, W = imgs.shape
         cap = descs_out.shape[1]
         lap = (ctypes.c_int * 2)(int(lapping_areas[0]), int(lapping_areas[1]))
-        s = _stream_handle(stream)
-        check(
-            lib().orbgpu_extract_batch(
-                self._h, ptr(imgs), B, W, H, imgs.stride(1), imgs.stride(0), lap, ptr(kps_out),
-                ptr(descs_out), cap, ptr(n_out), ptr(mono_out), s,
-            ),
-            "orbgpu_extract_batch",
-        )
+        with launch_stream(stream) as s:
+            check(
+                lib().orbgpu_extract_batch(
+                    self._h, ptr(imgs), B, W, H, imgs.stride(1), imgs.stride(0), lap, ptr(kps_out),
+                    ptr(descs_out), cap, ptr(n_out), ptr(mono_out), s,
+                ),
+                "orbgpu_extract_batch",
+            )
 
     def stereo_match_batch(self, imgs, kps, descs, n, bf: float, mb: float, uright, depth,
                            stream=None) -> None:
@@ -165,13 +166,14 @@ class OrbExtractor:
         CUDA tensors [B/2, cap] (-1 = unmatched).  bf = Frame::bf_, mb = Frame::mb."""
         B = imgs.shape[0]
         cap = descs.shape[1]
-        check(
-            lib().orbgpu_stereo_match_batch(
-                self._h, B // 2, ptr(imgs), imgs.stride(1), imgs.stride(0), ptr(kps), ptr(descs), cap,
-                ptr(n), float(bf), float(mb), ptr(uright), ptr(depth), _stream_handle(stream),
-            ),
-            "orbgpu_stereo_match_batch",
-        )
+        with launch_stream(stream) as s:
+            check(
+                lib().orbgpu_stereo_match_batch(
+                    self._h, B // 2, ptr(imgs), imgs.stride(1), imgs.stride(0), ptr(kps), ptr(descs),
+                    cap, ptr(n), float(bf), float(mb), ptr(uright), ptr(depth), s,
+                ),
+                "orbgpu_stereo_match_batch",
+            )
 
     STAGES = ("resize", "blur", "fast_cells", "octree", "describe", "assemble")
 
@@ -203,11 +205,34 @@ class OrbExtractor:
             pass
 
 
-def _stream_handle(stream) -> ctypes.c_void_p:
-    if stream is None:
-        import torch
+_side_streams = {}
 
-        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+@contextlib.contextmanager
+def launch_stream(stream):
+    """Stream handle for a batch launch, ordered with torch's work.
+
+    ``stream``: None -> torch's current stream; a torch stream; or a raw int
+    handle (0 = the library handle's own stream, unordered: the caller
+    synchronises).  The ABI reads a NULL handle as "the library handle's own
+    stream", so torch's legacy default stream (handle 0) cannot be named
+    through it: the launch then goes to a side stream that first waits for the
+    default stream and that the default stream waits for afterwards, keeping
+    torch's allocations, fills and copies ordered with the kernels."""
     if isinstance(stream, int):
-        return ctypes.c_void_p(stream)
-    return ctypes.c_void_p(stream.cuda_stream)
+        yield ctypes.c_void_p(stream)
+        return
+    import torch
+
+    cur = torch.cuda.current_stream() if stream is None else stream
+    if cur.cuda_stream != 0:
+        yield ctypes.c_void_p(cur.cuda_stream)
+        return
+    side = _side_streams.get(cur.device)
+    if side is None:
+        side = _side_streams[cur.device] = torch.cuda.Stream(device=cur.device)
+    side.wait_stream(cur)
+    try:
+        yield ctypes.c_void_p(side.cuda_stream)
+    finally:
+        cur.wait_stream(side)

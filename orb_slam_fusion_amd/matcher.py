@@ -28,7 +28,7 @@ import numpy as np
 
 from ._lib import (KEYPOINT_DTYPE, MAP_POINT_DTYPE, MAX_LEVELS, PROJ_POINT_DTYPE,
                    TRACK_VIEW_DTYPE, Camera, FrameGeom, check, lib, ptr)
-from .extractor import _stream_handle
+from .extractor import launch_stream
 
 TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30  # orb_matcher.cc:35-37
 
@@ -115,11 +115,12 @@ class ORBmatcher:
         nmatches int32 [B]."""
         B, K = kps.shape[0], kps.shape[1]
         c = Camera(*[float(v) for v in cam])
-        check(lib().orbgpu_search_by_projection_last_batch(
-            self._h, B, ctypes.byref(geom), ctypes.byref(c), float(mb), ptr(Tcw), ptr(Tlw),
-            ptr(kps), ptr(desc), ptr(uright), ptr(claimed), ptr(n), K, ptr(pts), ptr(npts),
-            pts.shape[1], float(th), int(bMono), int(self.mbCheckOrientation), ptr(match),
-            ptr(nmatches), _stream_handle(stream)), "orbgpu_search_by_projection_last_batch")
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_search_by_projection_last_batch(
+                self._h, B, ctypes.byref(geom), ctypes.byref(c), float(mb), ptr(Tcw), ptr(Tlw),
+                ptr(kps), ptr(desc), ptr(uright), ptr(claimed), ptr(n), K, ptr(pts), ptr(npts),
+                pts.shape[1], float(th), int(bMono), int(self.mbCheckOrientation), ptr(match),
+                ptr(nmatches), s), "orbgpu_search_by_projection_last_batch")
 
     # -- Frame::isInFrustum ---------------------------------------------------
     def is_in_frustum(self, F: MatchFrame, points: np.ndarray, viewingCosLimit: float,

@@ -15,7 +15,7 @@ from typing import Optional
 import numpy as np
 
 from ._lib import POSE_OBS_DTYPE, Camera, check, lib, ptr
-from .extractor import _stream_handle
+from .extractor import launch_stream
 
 
 @dataclass
@@ -64,14 +64,14 @@ class PoseOptimizer:
         pose_out_d optional float64 [P, 7]."""
         P, stride = obs.shape[0], obs.shape[1]
         c = Camera(*[float(v) for v in cam])
-        check(
-            lib().orbgpu_pose_opt_batch(
-                self._h, ctypes.byref(c), ptr(pose_in), ptr(obs), ptr(nobs), stride, P,
-                ptr(pose_out), ptr(outlier), ptr(inliers), ptr(pose_out_d),
-                _stream_handle(stream),
-            ),
-            "orbgpu_pose_opt_batch",
-        )
+        with launch_stream(stream) as s:
+            check(
+                lib().orbgpu_pose_opt_batch(
+                    self._h, ctypes.byref(c), ptr(pose_in), ptr(obs), ptr(nobs), stride, P,
+                    ptr(pose_out), ptr(outlier), ptr(inliers), ptr(pose_out_d), s,
+                ),
+                "orbgpu_pose_opt_batch",
+            )
 
     def close(self) -> None:
         if self._h:

@@ -22,6 +22,8 @@ def _so() -> ctypes.CDLL:
     so = ctypes.CDLL(str(path))
     so.synth_stereo_frame.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p]
+    so.synth_track_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int] + [ctypes.c_void_p] * 4
     so.synth_noise_image.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     so.synth_pose_problem.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -37,6 +39,16 @@ def stereo_frame(frame_idx: int, w: int = 752, h: int = 480, disparity: int = 24
     _so().synth_stereo_frame(FRAME_SEED_BASE + frame_idx, w, h, disparity, left.ctypes.data,
                              right.ctypes.data)
     return left, right
+
+
+def track_pair(frame_idx: int, shift: int = 6, w: int = 752, h: int = 480, disparity: int = 24):
+    """Two consecutive stereo frames of a camera translating along x over the
+    canvas plane: features move +shift px from the last frame to the current
+    one.  Returns (last_left, last_right, cur_left, cur_right)."""
+    ims = [np.zeros((h, w), np.uint8) for _ in range(4)]
+    _so().synth_track_pair(FRAME_SEED_BASE + 0x10000 + frame_idx, w, h, disparity, shift,
+                           *[im.ctypes.data for im in ims])
+    return tuple(ims)
 
 
 def noise_image(seed: int, w: int, h: int) -> np.ndarray:

@@ -22,6 +22,14 @@ FX, BASE = 435.2, 0.11
 def measure(frames: int = 64, calls: int = 20, cpu_frames: int = 4) -> dict:
     import torch
 
+    # every allocation, copy and launch on one non-default stream
+    with torch.cuda.stream(torch.cuda.Stream()):
+        return _measure(frames, calls, cpu_frames)
+
+
+def _measure(frames: int, calls: int, cpu_frames: int) -> dict:
+    import torch
+
     from orb_slam_fusion_amd import OrbExtractor, synth
 
     B = frames
