@@ -122,7 +122,7 @@ orbgpu_status fill_params(orbgpu_matcher* m, const orbgpu_frame_geom* g, const o
 orbgpu_status ensure_scratch(orbgpu_matcher* m, int n_frames, int kp_stride, int pt_stride) {
   if (grow(&m->d_cell_start, m->cap_cells, (size_t)n_frames * (kGridCells + 1)) ||
       grow(&m->d_cell_idx, m->cap_idx, (size_t)n_frames * kp_stride) ||
-      grow(&m->d_res, m->cap_res, (size_t)n_frames * pt_stride * 2) ||
+      grow(&m->d_res, m->cap_res, (size_t)n_frames * pt_stride * orbgpu::kMatchResWords) ||
       grow(&m->d_acc, m->cap_acc, (size_t)n_frames * pt_stride))
     return ORBGPU_ERR_NOMEM;
   return ORBGPU_OK;

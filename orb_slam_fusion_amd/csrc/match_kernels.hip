@@ -16,11 +16,13 @@
 //   k_mt_resolve  wave / frame: the reference's matches are sequential
 //                 (a match by a point with observations hides that keypoint
 //                 from every later point, orb_matcher.cc:86-87, 1591-1592).
-//                 A query's result can only change if its best or second
-//                 candidate was claimed earlier, so 64 queries are committed
-//                 at once unless one of them is hit (LDS claim bitmap +
-//                 in-batch owner table); a hit query is searched again with the
-//                 claims masked.  Then the rotation histogram
+//                 Each query carries its top-4 candidates: under the claims
+//                 so far its result is the first (and second) unclaimed entry.
+//                 64 queries at a time, in rounds: the queries before the first
+//                 one whose pick an earlier pending query claims commit
+//                 together (LDS claim bitmap + owner table); a query whose list
+//                 runs out is searched again with the claims masked.  Then the
+//                 rotation histogram
 //                 (orb_matcher.cc:1614-1632, 1708-1725; ComputeThreeMaxima
 //                 :1841-1873) and the mvpMapPoints writes.
 //
@@ -216,12 +218,17 @@ __device__ __forceinline__ FrameRef frame_ref(const MatchLaunch& a, int f) {
   return F;
 }
 
-// GetFeaturesInArea (frame.cc:679-746) + the best / second candidate loop.
-// claims (LDS bitmap, may be null) masks keypoints matched earlier in the call.
-// Returns packed (dist << 16 | idx) best and second, kNone if absent.
-__device__ void wave_search(const MatchParams& p, const FrameRef& F, const Query& Q,
-                            const uint32_t* claims, uint32_t& best, uint32_t& second) {
-  best = second = kNone;
+// GetFeaturesInArea (frame.cc:679-746) + the candidate loop: the kMatchTopK
+// smallest keys (dist, position in the reference's candidate order) as packed
+// (dist << 16 | idx), kNone-padded, and the number of candidates.  The
+// reference's running best = top[0]; its running second best = top[1] (the
+// smallest key of the rest).  claims (LDS bitmap, may be null) masks
+// keypoints matched earlier in the call.
+__device__ void wave_topk(const MatchParams& p, const FrameRef& F, const Query& Q,
+                          const uint32_t* claims, uint32_t top[kMatchTopK], int& count) {
+#pragma unroll
+  for (int i = 0; i < kMatchTopK; ++i) top[i] = kNone;
+  count = 0;
   if (!Q.valid) return;
   const float r = Q.r;
   const int minCx = max(0, (int)floorf((Q.x - p.min_x - r) * p.inv_w));
@@ -237,7 +244,10 @@ __device__ void wave_search(const MatchParams& p, const FrameRef& F, const Query
   if (ncells <= 0) return;
   const bool check_levels = Q.min_level >= 0 || Q.max_level >= 0;
   const int lane = threadIdx.x & 63;
-  uint64_t b1 = kNoKey, b2 = kNoKey;
+  uint64_t b[kMatchTopK];  // this lane's smallest keys, ascending
+#pragma unroll
+  for (int i = 0; i < kMatchTopK; ++i) b[i] = kNoKey;
+  int local = 0;
   for (int k = lane; k < ncells; k += 64) {
     const int cx = k / ncy;
     const int cell = (minCx + cx) * kGridRows + minCy + (k - cx * ncy);
@@ -262,15 +272,30 @@ __device__ void wave_search(const MatchParams& p, const FrameRef& F, const Query
       const int dist = __popc(d0.x ^ Q.d[0]) + __popc(d0.y ^ Q.d[1]) + __popc(d0.z ^ Q.d[2]) +
                        __popc(d0.w ^ Q.d[3]) + __popc(d1.x ^ Q.d[4]) + __popc(d1.y ^ Q.d[5]) +
                        __popc(d1.z ^ Q.d[6]) + __popc(d1.w ^ Q.d[7]);
-      const uint64_t key = ((uint64_t)dist << 40) | ((uint64_t)k << 16) | (uint64_t)idx;
-      if (key < b1) b2 = b1, b1 = key;
-      else if (key < b2) b2 = key;
+      uint64_t key = ((uint64_t)dist << 40) | ((uint64_t)k << 16) | (uint64_t)idx;
+      ++local;
+#pragma unroll
+      for (int i = 0; i < kMatchTopK; ++i) {  // insertion into the sorted registers
+        const uint64_t lo = key < b[i] ? key : b[i];
+        key = key < b[i] ? b[i] : key;
+        b[i] = lo;
+      }
     }
   }
-  const uint64_t m1 = wave_min_u64(b1);
-  const uint64_t m2 = wave_min_u64(b1 == m1 ? b2 : b1);
-  best = m1 == kNoKey ? kNone : (uint32_t)((m1 >> 40) << 16 | (m1 & 0xFFFF));
-  second = m2 == kNoKey ? kNone : (uint32_t)((m2 >> 40) << 16 | (m2 & 0xFFFF));
+  int total = local;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) total += __shfl_xor(total, off, 64);
+  count = total;
+#pragma unroll
+  for (int i = 0; i < kMatchTopK; ++i) {
+    const uint64_t m = wave_min_u64(b[0]);
+    top[i] = m == kNoKey ? kNone : (uint32_t)((m >> 40) << 16 | (m & 0xFFFF));
+    if (b[0] == m && m != kNoKey) {  // the owning lane pops its head
+#pragma unroll
+      for (int j = 0; j + 1 < kMatchTopK; ++j) b[j] = b[j + 1];
+      b[kMatchTopK - 1] = kNoKey;
+    }
+  }
 }
 
 __device__ __forceinline__ Query make_query(const MatchLaunch& a, int f, int q, bool write_view) {
@@ -374,11 +399,14 @@ __global__ __launch_bounds__(256) void k_mt_search(MatchLaunch a) {
   if (q >= a.npts[f]) return;
   const FrameRef F = frame_ref(a, f);
   const Query Q = make_query(a, f, q, true);
-  uint32_t best, second;
-  wave_search(a.p, F, Q, nullptr, best, second);
+  uint32_t top[kMatchTopK];
+  int count;
+  wave_topk(a.p, F, Q, nullptr, top, count);
   if ((threadIdx.x & 63) == 0) {
-    uint32_t* r = a.res + 2 * ((size_t)f * a.pt_stride + q);
-    r[0] = best, r[1] = second;
+    uint32_t* r = a.res + (size_t)kMatchResWords * ((size_t)f * a.pt_stride + q);
+#pragma unroll
+    for (int i = 0; i < kMatchTopK; ++i) r[i] = top[i];
+    r[kMatchTopK] = (uint32_t)count;
   }
 }
 
@@ -413,7 +441,7 @@ __device__ __forceinline__ int rot_bin(const MatchLaunch& a, const float* kps, i
 }
 
 __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
-  __shared__ uint32_t owner[kMatchMaxKeypoints];  // in-batch first claiming lane, 64 = none
+  __shared__ uint32_t owner[kMatchMaxKeypoints];  // in-round first claiming lane, 64 = none
   __shared__ uint32_t claims[kMatchMaxKeypoints / 32];
   __shared__ uint32_t removed[kMatchMaxKeypoints / 32];
   __shared__ int hist[kHistoLength];
@@ -430,82 +458,88 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   for (int i = lane; i < kMatchMaxKeypoints / 32; i += 64) claims[i] = 0, removed[i] = 0;
   if (lane < kHistoLength) hist[lane] = 0;
   __syncthreads();
-  const uint32_t* res = a.res + 2 * (size_t)f * a.pt_stride;
+  const uint32_t* res = a.res + (size_t)kMatchResWords * f * a.pt_stride;
   int32_t* acc = a.acc + (size_t)f * a.pt_stride;
   int nmatch = 0;
-  auto claimed_bit = [&](uint32_t key) -> bool {
-    if (key == kNone) return false;
+  auto is_claimed = [&](uint32_t key) -> bool {
     const int idx = key & 0xFFFF;
     return (claims[idx >> 5] >> (idx & 31)) & 1u;
   };
   for (int base = 0; base < nq; base += 64) {
     const int q = base + lane;
     const bool valid = q < nq;
-    const uint32_t best = valid ? res[2 * q] : kNone;
-    const uint32_t second = valid ? res[2 * q + 1] : kNone;
-    const bool acc0 = valid && accept_of(a, F.kps, best, second);
-    // a query whose best is beyond TH_HIGH stays unmatched whatever is claimed
-    const bool need_check = best != kNone && (int)(best >> 16) <= kThHigh;
-    const bool claimer = acc0 && has_obs(a, f, q);
-    if (claimer) atomicMin(&owner[best & 0xFFFF], (uint32_t)lane);
-    __syncthreads();
-    bool conflict = false;
-    if (need_check) {
-      conflict = claimed_bit(best) || owner[best & 0xFFFF] < (uint32_t)lane;
-      if (local && second != kNone)
-        conflict = conflict || claimed_bit(second) || owner[second & 0xFFFF] < (uint32_t)lane;
-    }
-    __syncthreads();
-    if (claimer) owner[best & 0xFFFF] = 64;
-    const uint64_t cmask = __ballot(conflict);
-    const int first = cmask ? __builtin_ctzll(cmask) : 64;
-    // lanes before the first hit commit together
-    if (lane < first && valid) {
-      if (acc0) {
-        const int idx = best & 0xFFFF;
-        atomicMax(&match[idx], q);
-        if (claimer) atomicOr(&claims[idx >> 5], 1u << (idx & 31));
-        int bin = 0;
-        if (rot_check) {
-          bin = rot_bin(a, F.kps, f, q, idx);
-          atomicAdd(&hist[bin], 1);
+    uint32_t top[kMatchTopK];
+    int count = 0;
+#pragma unroll
+    for (int i = 0; i < kMatchTopK; ++i) top[i] = valid ? res[(size_t)kMatchResWords * q + i] : kNone;
+    if (valid) count = (int)res[(size_t)kMatchResWords * q + kMatchTopK];
+    const bool obs = valid && has_obs(a, f, q);
+    bool done = !valid;
+    // Rounds: every pending query takes its best / second unclaimed entries;
+    // the queries before the first one that an earlier pending claimer hits
+    // (or whose list ran out) are final and commit together.
+    while (true) {
+      uint32_t b = kNone, s2 = kNone;
+      int found = 0;
+#pragma unroll
+      for (int i = 0; i < kMatchTopK; ++i) {
+        if (top[i] != kNone && !is_claimed(top[i])) {
+          if (found == 0) b = top[i];
+          else if (found == 1) s2 = top[i];
+          ++found;
         }
-        acc[q] = idx | (bin << 16);
-      } else {
-        acc[q] = -1;
       }
-    }
-    nmatch += __popcll(__ballot(lane < first && acc0));
-    __syncthreads();
-    // the rest one at a time, in query order
-    for (int l = first; l < 64 && base + l < nq; ++l) {
-      const int ql = base + l;
-      uint32_t b = __builtin_amdgcn_readlane(best, l);
-      uint32_t s2 = __builtin_amdgcn_readlane(second, l);
-      const bool nc = __builtin_amdgcn_readlane((int)need_check, l) != 0;
-      const bool hit = nc && (claimed_bit(b) || (local && claimed_bit(s2)));
-      if (hit) {
-        const Query Q = make_query(a, f, ql, false);
-        wave_search(a.p, F, Q, claims, b, s2);
+      // a best beyond TH_HIGH can only get worse as claims accumulate
+      const bool hopeless = b != kNone && (int)(b >> 16) > kThHigh;
+      const int need = local ? 2 : 1;
+      const bool exhausted = !done && !hopeless && found < need && count > kMatchTopK;
+      const bool ok = !done && !exhausted && accept_of(a, F.kps, b, s2);
+      const bool claimer = ok && obs;
+      if (claimer) atomicMin(&owner[b & 0xFFFF], (uint32_t)lane);
+      __syncthreads();
+      bool hit = false;
+      if (!done && !exhausted && b != kNone && !hopeless) {
+        hit = owner[b & 0xFFFF] < (uint32_t)lane;
+        if (local && s2 != kNone) hit = hit || owner[s2 & 0xFFFF] < (uint32_t)lane;
       }
-      const bool ok = accept_of(a, F.kps, b, s2);
-      if (lane == 0) {
+      __syncthreads();
+      if (claimer) owner[b & 0xFFFF] = 64;
+      const uint64_t stop_mask = __ballot(hit || exhausted);
+      const int stop = stop_mask ? __builtin_ctzll(stop_mask) : 64;
+      const bool commit = !done && lane < stop;
+      if (commit) {
         if (ok) {
           const int idx = b & 0xFFFF;
-          atomicMax(&match[idx], ql);
-          if (has_obs(a, f, ql)) claims[idx >> 5] |= 1u << (idx & 31);
+          atomicMax(&match[idx], q);
+          if (claimer) atomicOr(&claims[idx >> 5], 1u << (idx & 31));
           int bin = 0;
           if (rot_check) {
-            bin = rot_bin(a, F.kps, f, ql, idx);
-            hist[bin] += 1;
+            bin = rot_bin(a, F.kps, f, q, idx);
+            atomicAdd(&hist[bin], 1);
           }
-          acc[ql] = idx | (bin << 16);
+          acc[q] = idx | (bin << 16);
         } else {
-          acc[ql] = -1;
+          acc[q] = -1;
+        }
+        done = true;
+      }
+      nmatch += __popcll(__ballot(commit && ok));
+      __syncthreads();
+      if (stop == 64) break;
+      // the first stopped query: hit by a claim now committed (its next round
+      // sees it), or its list ran out -> full search with the claims masked
+      const bool ex_stop = (stop_mask >> stop) & 1 && __builtin_amdgcn_readlane((int)exhausted, stop);
+      if (ex_stop) {
+        const Query Q = make_query(a, f, base + stop, false);
+        uint32_t t2[kMatchTopK];
+        int c2;
+        wave_topk(a.p, F, Q, claims, t2, c2);
+        if (lane == stop) {
+#pragma unroll
+          for (int i = 0; i < kMatchTopK; ++i) top[i] = t2[i];
+          count = c2;
         }
       }
-      nmatch += ok;
-      __syncthreads();
     }
   }
   __syncthreads();

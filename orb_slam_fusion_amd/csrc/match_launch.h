@@ -13,6 +13,11 @@ constexpr int kGridCols = ORBGPU_FRAME_GRID_COLS, kGridRows = ORBGPU_FRAME_GRID_
 constexpr int kGridCells = kGridCols * kGridRows;
 constexpr int kMatchMaxKeypoints = 8192;  // per frame (LDS-resident claim state)
 constexpr int kMatchMaxPoints = 1 << 20;  // per frame
+// Per query the search keeps its kMatchTopK best candidates (in the
+// reference's order) plus the candidate count: claims by earlier queries are
+// then resolved from the list, a full re-search only when it runs out.
+constexpr int kMatchTopK = 4;
+constexpr int kMatchResWords = kMatchTopK + 1;
 
 enum MatchMode : int { kModeLast = 0, kModeLocal = 1, kModeLocalFrustum = 2 };
 
@@ -58,7 +63,7 @@ struct MatchLaunch {
   // scratch
   int* cell_start;      // [n_frames][kGridCells + 1]
   uint16_t* cell_idx;   // [n_frames][kp_stride]
-  uint32_t* res;        // [n_frames][pt_stride][2]: (dist << 16 | idx) best, second
+  uint32_t* res;        // [n_frames][pt_stride][kMatchResWords]: top-K (dist << 16 | idx), count
   int32_t* acc;         // [n_frames][pt_stride]: accepted idx | bin << 16, or -1
   // outputs
   int32_t* match;       // [n_frames][kp_stride]
