@@ -363,6 +363,49 @@ orbgpu_status orbgpu_search_local_points(
     int far_points, float th_far_points, orbgpu_track_view* views, int32_t* match,
     int* nmatches);
 
+/* ------------------------------------------------------------------------
+ * DBoW2 bag-of-words conversion (3rdparty/DBoW2, ORBVocabulary =
+ * TemplatedVocabulary<FORB::TDescriptor, FORB>): Frame::ComputeBoW
+ * (frame.cc:761-766) and KeyFrame::ComputeBoW (keyframe.cc:202-208) call
+ * transform(descriptors, mBowVec, mFeatVec, 4).
+ * ------------------------------------------------------------------------ */
+typedef struct orbgpu_vocab orbgpu_vocab;
+
+/* Replaces: bool TemplatedVocabulary::loadFromTextFile(const std::string&)
+ *   (TemplatedVocabulary.h:1248-1327), text format "k L scoring weighting" then
+ *   one "parent isLeaf d0 .. d31 weight" line per node; the tree goes to
+ *   `device`.  ORBGPU_ERR_INVALID for a header outside the reference's bounds
+ *   (k in [0, 20], L in [1, 10], scoring in [0, 5], weighting in [0, 3]). */
+orbgpu_status orbgpu_vocab_load_text(int device, const char* path, orbgpu_vocab** out);
+void orbgpu_vocab_destroy(orbgpu_vocab* v);
+/* info[0..5] = k, L, scoring (DBoW2::ScoringType), weighting (WeightingType),
+ * nodes (root included), words. */
+orbgpu_status orbgpu_vocab_info(const orbgpu_vocab* v, int info[6]);
+
+/* Replaces: void TemplatedVocabulary::transform(const vector<TDescriptor>&
+ *   features, BowVector& v, FeatureVector& fv, int levelsup) const
+ *   (TemplatedVocabulary.h:1057-1118, per feature :1140-1179).  descs: n x 32
+ *   bytes (mDescriptors rows).  BowVector (std::map<WordId, WordValue>) comes
+ *   back as *n_words ascending word ids + weights; FeatureVector
+ *   (std::map<NodeId, vector<unsigned>>) as *n_nodes ascending node ids, the
+ *   feature indices of node j in fv_features[fv_offsets[j] .. fv_offsets[j+1]).
+ *   Capacities: bow_* and fv_nodes / fv_features n entries, fv_offsets n + 1. */
+orbgpu_status orbgpu_bow_transform(orbgpu_vocab* v, const uint8_t* descs, int n, int levelsup,
+                                   uint32_t* bow_words, double* bow_weights, int* n_words,
+                                   uint32_t* fv_nodes, int32_t* fv_offsets, uint32_t* fv_features,
+                                   int* n_nodes);
+
+/* Device-resident batch: frame f's descriptors at d_descs + f * stride * 32,
+ * d_n[f] of them; outputs at f * stride (fv_offsets at f * (stride + 1)),
+ * counts in d_n_words[f] / d_n_nodes[f].  Asynchronous on hip_stream (NULL:
+ * the vocabulary's own stream). */
+orbgpu_status orbgpu_bow_transform_batch(orbgpu_vocab* v, int n_frames, const uint8_t* d_descs,
+                                         const int* d_n, int stride, int levelsup,
+                                         uint32_t* d_bow_words, double* d_bow_weights,
+                                         int* d_n_words, uint32_t* d_fv_nodes,
+                                         int32_t* d_fv_offsets, uint32_t* d_fv_features,
+                                         int* d_n_nodes, void* hip_stream);
+
 /* MapPoint::PredictScale (mappoint.cc:550-563) as used by the kernels: the
  * level of a ratio mfMaxDistance / dist is the number of thresholds thr[j-1]
  * (j = 1 .. n_levels - 1) it reaches, thr[j-1] = the smallest float ratio with

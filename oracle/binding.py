@@ -64,6 +64,10 @@ def lib() -> ctypes.CDLL:
         "orc_predict_scale": (_I, [_F, _F, _F, _I]),
         "orc_predict_scale_check": (ctypes.c_long, [_F, _I, _P, ctypes.c_uint32, ctypes.c_uint32]),
         "orc_frame_grid_cells": (None, [_P, _P, _I, _P]),
+        "orc_vocab_load": (_P, [ctypes.c_char_p]),
+        "orc_vocab_free": (None, [_P]),
+        "orc_vocab_info": (None, [_P, _P]),
+        "orc_bow_transform": (None, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(so, name)
@@ -356,3 +360,38 @@ def frame_grid_cells(geom, kps):
     out = np.zeros(max(len(k), 1), np.int32)
     lib().orc_frame_grid_cells(_p(g), _p(k), len(k), _p(out))
     return out[:len(k)]
+
+
+# --- DBoW2 (bow_oracle.cc) ---------------------------------------------------
+class OracleVocab:
+    """TemplatedVocabulary<FORB> restated: loadFromTextFile + transform."""
+
+    def __init__(self, path):
+        self._h = lib().orc_vocab_load(str(path).encode())
+        if not self._h:
+            raise ValueError(f"vocabulary load failed: {path}")
+
+    def info(self):
+        a = np.zeros(6, np.int32)
+        lib().orc_vocab_info(self._h, _p(a))
+        return dict(zip(("k", "L", "scoring", "weighting", "nodes", "words"), a.tolist()))
+
+    def transform(self, descs, levelsup=4):
+        """-> (bow_words, bow_weights, fv_nodes, fv_offsets, fv_features)"""
+        d = np.ascontiguousarray(descs, np.uint8).reshape(-1, 32)
+        n = len(d)
+        S = max(n, 1)
+        bw, bwt = np.zeros(S, np.uint32), np.zeros(S, np.float64)
+        fn, fo, ff = np.zeros(S, np.uint32), np.zeros(S + 1, np.int32), np.zeros(S, np.uint32)
+        nw, nn = ctypes.c_int(), ctypes.c_int()
+        lib().orc_bow_transform(self._h, _p(d), n, int(levelsup), _p(bw), _p(bwt),
+                                ctypes.byref(nw), _p(fn), _p(fo), _p(ff), ctypes.byref(nn))
+        w, k = nw.value, nn.value
+        return bw[:w], bwt[:w], fn[:k], fo[:k + 1], ff[:fo[k]]
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().orc_vocab_free(self._h)
+        except Exception:
+            pass

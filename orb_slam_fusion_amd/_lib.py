@@ -179,6 +179,13 @@ SIGNATURES = {
          _I, _F, _F, _F, _I, _F, _P, _P, _P],
     ),
     "orbgpu_level_thresholds": (_I, [_F, _I, _P]),
+    "orbgpu_vocab_load_text": (_I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "orbgpu_vocab_destroy": (None, [_P]),
+    "orbgpu_vocab_info": (_I, [_P, _P]),
+    "orbgpu_bow_transform": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "orbgpu_bow_transform_batch": (
+        _I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
+    ),
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (

@@ -2,7 +2,10 @@
 // extractor and seeded pose-only problems.  Host-only helper library
 // (liborbsynth.so) shared by tests/ and bench.py so both sides of every parity
 // and timing run see byte-identical inputs.  Not part of the hot path.
+#include <array>
 #include <cmath>
+#include <cstdio>
+#include <string>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -359,6 +362,60 @@ int synth_lba_problem(uint64_t seed, int n_kf, int n_pts, int obs_per_pt, int n_
     }
   }
   return ne;
+}
+
+// DBoW2 text vocabulary (TemplatedVocabulary::saveToTextFile layout,
+// TemplatedVocabulary.h:1333-1353): a full k-ary tree of depth L, nodes in
+// breadth-first order; a child's descriptor is its parent's with each bit
+// flipped with probability 1/4 (so a descent stays coherent), one sibling in
+// 16 duplicates its left neighbour (ties); leaf weights U[0.2, 8] (idf-like),
+// stop_pct percent of them 0 (stopped words); inner nodes weight 0.
+// trailing_newline reproduces the reference writer's final endl.  Returns the
+// number of nodes written (root excluded) or -1.
+int synth_vocab_text(uint64_t seed, int k, int L, int scoring, int weighting, int stop_pct,
+                     int trailing_newline, const char* path) {
+  FILE* f = std::fopen(path, "w");
+  if (!f) return -1;
+  XorShift64Star rng(seed);
+  std::fprintf(f, "%d %d  %d %d\n", k, L, scoring, weighting);
+  std::vector<std::array<uint8_t, 32>> prev(1), cur;
+  for (int i = 0; i < 32; ++i) prev[0][i] = (uint8_t)rng.uniform(0, 255);
+  int written = 0, prev_start = 0;  // id of the first node of the previous level (root: 0)
+  std::string buf;
+  for (int lev = 1; lev <= L; ++lev) {
+    cur.clear();
+    const bool leaf = lev == L;
+    for (size_t p = 0; p < prev.size(); ++p) {
+      for (int c = 0; c < k; ++c) {
+        std::array<uint8_t, 32> d;
+        if (c > 0 && rng.uniform(0, 15) == 0) {
+          d = cur.back();
+        } else {
+          for (int i = 0; i < 32; ++i) {
+            uint8_t flip = 0;
+            for (int b = 0; b < 8; ++b) flip |= (uint8_t)((rng.uniform(0, 3) == 0) << b);
+            d[i] = prev[p][i] ^ flip;
+          }
+        }
+        cur.push_back(d);
+        const int parent = prev_start + (int)p;
+        double w = 0.0;
+        if (leaf) w = rng.uniform(0, 99) < stop_pct ? 0.0 : 0.2 + 7.8 * rng.unit();
+        char line[512];
+        int o = std::snprintf(line, sizeof line, "%d %d ", parent, leaf ? 1 : 0);
+        for (int i = 0; i < 32; ++i) o += std::snprintf(line + o, sizeof line - o, "%d ", d[i]);
+        std::snprintf(line + o, sizeof line - o, " %g", w);
+        if (written > 0) std::fputc('\n', f);
+        std::fputs(line, f);
+        ++written;
+      }
+    }
+    prev_start = written - (int)cur.size() + 1;  // ids are 1 + line index
+    prev.swap(cur);
+  }
+  if (trailing_newline) std::fputc('\n', f);
+  std::fclose(f);
+  return written;
 }
 
 }  // extern "C"

@@ -24,6 +24,8 @@ def _so() -> ctypes.CDLL:
                                       ctypes.c_void_p, ctypes.c_void_p]
     so.synth_track_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int] + [ctypes.c_void_p] * 4
+    so.synth_vocab_text.argtypes = [ctypes.c_uint64] + [ctypes.c_int] * 6 + [ctypes.c_char_p]
+    so.synth_vocab_text.restype = ctypes.c_int
     so.synth_noise_image.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     so.synth_pose_problem.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -49,6 +51,18 @@ def track_pair(frame_idx: int, shift: int = 6, w: int = 752, h: int = 480, dispa
     _so().synth_track_pair(FRAME_SEED_BASE + 0x10000 + frame_idx, w, h, disparity, shift,
                            *[im.ctypes.data for im in ims])
     return tuple(ims)
+
+
+def vocab_text(path, seed: int = 3, k: int = 10, L: int = 6, scoring: int = 0,
+               weighting: int = 0, stop_pct: int = 3, trailing_newline: bool = True) -> int:
+    """Writes a DBoW2 text vocabulary (ORBvoc.txt layout, full k-ary tree of depth
+    L; scoring / weighting as DBoW2's enums, default L1_NORM / TF_IDF like
+    ORB-SLAM's vocabulary).  Returns the node count (root excluded)."""
+    n = _so().synth_vocab_text(seed, k, L, scoring, weighting, stop_pct, int(trailing_newline),
+                               str(path).encode())
+    if n < 0:
+        raise OSError(f"cannot write {path}")
+    return n
 
 
 def noise_image(seed: int, w: int, h: int) -> np.ndarray:

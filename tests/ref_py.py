@@ -488,3 +488,72 @@ def search_local_py(geom, kps, desc, uright, claimed, pts, views, th, nn):
         F.holder[i1], F.hobs[i1] = j, bool(P["flags"] & 2)
         nm += 1
     return nm, np.array([h if h >= 0 else -1 for h in F.holder], np.int32)
+
+
+# --- DBoW2 transform (TemplatedVocabulary.h:1057-1179) -----------------------
+def load_vocab_py(path):
+    """loadFromTextFile restated in Python: nodes as dicts."""
+    lines = open(path).read().split("\n")
+    k, L, sc, wt = (int(x) for x in lines[0].split())
+    nodes = [dict(parent=0, children=[], desc=bytes(32), weight=0.0, word=0)]
+    n_words = 0
+    for line in lines[1:]:  # every getline after the header, the empty last one included
+        tok = line.split()
+        pid = int(tok[0]) if tok else 0
+        leaf = int(tok[1]) if len(tok) > 1 else 0
+        desc = bytes(int(x) & 255 for x in tok[2:34]) if len(tok) >= 34 else bytes(32)
+        w = float(tok[34]) if len(tok) > 34 else 0.0
+        nid = len(nodes)
+        nodes.append(dict(parent=pid, children=[], desc=desc, weight=w, word=0))
+        nodes[pid]["children"].append(nid)
+        if leaf > 0:
+            nodes[nid]["word"] = n_words
+            n_words += 1
+    return dict(k=k, L=L, scoring=sc, weighting=wt, nodes=nodes, words=n_words)
+
+
+def bow_transform_py(V, descs, levelsup):
+    nodes = V["nodes"]
+    bow, fv = {}, {}
+    if V["words"] == 0:
+        return bow, fv
+    tf = V["weighting"] in (0, 1)
+    for i, d in enumerate(np.asarray(descs, np.uint8)):
+        cur, nid, level = 0, 0, 0
+        while True:
+            level += 1
+            ch = nodes[cur]["children"]
+            dists = [int(np.unpackbits(np.bitwise_xor(d, np.frombuffer(nodes[c]["desc"], np.uint8))).sum())
+                     for c in ch]
+            cur = ch[int(np.argmin(dists))]  # argmin: first minimum
+            if level == V["L"] - levelsup:
+                nid = cur
+            if not nodes[cur]["children"]:
+                break
+        w = nodes[cur]["weight"]
+        if not w > 0:
+            continue
+        word = nodes[cur]["word"]
+        if word in bow:
+            if tf:
+                bow[word] += w
+        else:
+            bow[word] = w
+        fv.setdefault(nid, []).append(i)
+    bow = dict(sorted(bow.items()))
+    if V["scoring"] != 5:
+        if V["scoring"] == 1:
+            norm = 0.0
+            for x in bow.values():
+                norm = float(np.longdouble(x) * np.longdouble(x) + np.longdouble(norm))
+            norm = np.sqrt(norm)
+        else:
+            norm = 0.0
+            for x in bow.values():
+                norm += abs(x)
+        if norm > 0:
+            bow = {k: x / norm for k, x in bow.items()}
+    elif tf and bow:
+        nd = float(len(bow))
+        bow = {k: x / nd for k, x in bow.items()}
+    return bow, dict(sorted(fv.items()))
