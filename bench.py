@@ -98,6 +98,7 @@ def main() -> int:
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches side line")
     ap.add_argument("--no-match", action="store_true",
                     help="skip the SearchByProjection (motion-model search) side line")
+    ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform side line")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the per-frame host-path latency side line")
     args = ap.parse_args()
@@ -294,6 +295,13 @@ def main() -> int:
         from bench_match import measure as measure_match  # noqa: E402
 
         result["match"] = measure_match(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+    if rank == 0 and world == 1 and not args.no_bow:
+        # SURVEY §8(f) rank 4, beside the headline metric (not part of it):
+        # DBoW2 transform (Frame::ComputeBoW) on resident extractor descriptors
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_bow import measure as measure_bow  # noqa: E402
+
+        result["bow"] = measure_bow(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_latency:
         # north_star's per-frame target: one stereo frame at a time through the
         # host ABI (2-thread extraction + PoseOptimization) vs the CPU oracle

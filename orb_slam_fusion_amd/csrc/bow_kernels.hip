@@ -91,14 +91,37 @@ __device__ void bitonic_sort(uint64_t* keys, int m) {
   }
 }
 
+// exclusive scan of one int per thread over the 256-thread block; returns the
+// thread's offset, *total the sum (tmp: 4 ints of LDS)
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) tmp[w] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += tmp[i];
+  *total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return base + inc - v;
+}
+
+// keys: m u64, fw: m doubles (dynamic LDS)
 __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
-  __shared__ uint64_t keys[kBowMaxFeatures];
-  __shared__ int scan[257];
+  extern __shared__ __attribute__((aligned(16))) uint8_t bow_lds[];
+  __shared__ int tmp[4];
+  __shared__ double norm_s;
   const int f = blockIdx.x, t = threadIdx.x;
   const int n = a.n[f];
   const size_t o = (size_t)f * a.stride;
   int m = 1;
   while (m < n) m <<= 1;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(bow_lds);
+  double* fw = reinterpret_cast<double*>(bow_lds + 8 * (size_t)a.lds_m);
   const VocabDev& V = a.voc;
   const bool tf = V.weighting == 0 || V.weighting == 1;
   const bool must = V.scoring != 5;
@@ -106,12 +129,16 @@ __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
   // ---- BowVector
   for (int i = t; i < m; i += 256) {
     uint64_t k = kNoKey;
-    if (i < n && !empty && a.f_weight[o + i] > 0) k = ((uint64_t)a.f_word[o + i] << 32) | (uint32_t)i;
+    if (i < n) {
+      const double w = a.f_weight[o + i];
+      fw[i] = w;
+      if (!empty && w > 0) k = ((uint64_t)a.f_word[o + i] << 32) | (uint32_t)i;
+    }
     keys[i] = k;
   }
   __syncthreads();
   bitonic_sort(keys, m);
-  // segment heads -> output slots (block scan over per-thread chunks)
+  // segment heads -> output slots
   const int per = (m + 255) / 256;
   const int b = min(t * per, m), e = min(b + per, m);
   auto head = [&](int i) {
@@ -119,55 +146,58 @@ __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
   };
   int cnt = 0;
   for (int i = b; i < e; ++i) cnt += head(i);
-  scan[t] = cnt;
-  __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int w = 0; w < 256; ++w) {
-      const int c = scan[w];
-      scan[w] = run;
-      run += c;
-    }
-    scan[256] = run;
-  }
-  __syncthreads();
-  const int n_words = scan[256];
+  int n_words;
+  int pos = block_excl_scan(cnt, tmp, &n_words);
   uint32_t* bw = a.bow_words + o;
   double* bwt = a.bow_weights + o;
-  int pos = scan[t];
+  double wsum[16];  // per <= 16 (m <= 4096)
+  int nh = 0;
   for (int i = b; i < e; ++i) {
     if (!head(i)) continue;
-    const uint32_t word = (uint32_t)(keys[i] >> 32);
-    double w = a.f_weight[o + (uint32_t)keys[i]];
-    if (tf)  // addWeight: the later features of the word, in feature order
-      for (int j = i + 1; j < m && keys[j] != kNoKey && (uint32_t)(keys[j] >> 32) == word; ++j)
-        w += a.f_weight[o + (uint32_t)keys[j]];
-    bw[pos] = word;
-    bwt[pos] = w;
-    ++pos;
+    double w = fw[(uint32_t)keys[i]];
+    if (tf) {  // addWeight: the later features of the word, in feature order
+      const uint64_t word = keys[i] >> 32;
+      for (int j = i + 1; j < m && keys[j] != kNoKey && (keys[j] >> 32) == word; ++j)
+        w += fw[(uint32_t)keys[j]];
+    }
+    bw[pos + nh] = (uint32_t)(keys[i] >> 32);
+    wsum[nh++] = w;
   }
+  __syncthreads();  // fw no longer read: it now holds the word weights in word order
+  for (int h = 0; h < nh; ++h) fw[pos + h] = wsum[h];
   __syncthreads();
-  __threadfence_block();
-  if (tf && n_words > 0 && !must) {
-    const double nd = (double)n_words;
-    for (int i = t; i < n_words; i += 256) bwt[i] /= nd;
-  }
   if (must) {
-    __shared__ double norm_s;
-    if (t == 0) {  // BowVector::normalize: summed in word order
+    if (t == 0) {  // BowVector::normalize: summed in word order, one chain
       double norm = 0.0;
+      int i = 0;
       if (V.scoring == 1) {
-        for (int i = 0; i < n_words; ++i) norm = __builtin_fma(bwt[i], bwt[i], norm);
+        for (; i + 8 <= n_words; i += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = fw[i + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) norm = __builtin_fma(v[u], v[u], norm);
+        }
+        for (; i < n_words; ++i) norm = __builtin_fma(fw[i], fw[i], norm);
         norm = sqrt(norm);
       } else {
-        for (int i = 0; i < n_words; ++i) norm += fabs(bwt[i]);
+        for (; i + 8 <= n_words; i += 8) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = fw[i + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) norm += fabs(v[u]);
+        }
+        for (; i < n_words; ++i) norm += fabs(fw[i]);
       }
       norm_s = norm;
     }
     __syncthreads();
     const double norm = norm_s;
-    if (norm > 0.0)
-      for (int i = t; i < n_words; i += 256) bwt[i] /= norm;
+    for (int i = t; i < n_words; i += 256) bwt[i] = norm > 0.0 ? fw[i] / norm : fw[i];
+  } else {
+    const double nd = (double)n_words;
+    for (int i = t; i < n_words; i += 256) bwt[i] = tf ? fw[i] / nd : fw[i];
   }
   __syncthreads();
   // ---- FeatureVector
@@ -179,25 +209,17 @@ __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
   __syncthreads();
   bitonic_sort(keys, m);
   cnt = 0;
-  for (int i = b; i < e; ++i) cnt += head(i);
-  __syncthreads();
-  scan[t] = cnt;
-  __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int w = 0; w < 256; ++w) {
-      const int c = scan[w];
-      scan[w] = run;
-      run += c;
-    }
-    scan[256] = run;
+  int kept = 0;
+  for (int i = b; i < e; ++i) {
+    cnt += head(i);
+    kept += keys[i] != kNoKey;
   }
-  __syncthreads();
-  const int n_nodes = scan[256];
+  int n_nodes, n_kept;
+  pos = block_excl_scan(cnt, tmp, &n_nodes);
+  (void)block_excl_scan(kept, tmp, &n_kept);
   uint32_t* fn = a.fv_nodes + o;
   int32_t* fo = a.fv_offsets + (size_t)f * (a.stride + 1);
   uint32_t* ff = a.fv_features + o;
-  pos = scan[t];
   for (int i = b; i < e; ++i) {
     if (keys[i] == kNoKey) continue;
     ff[i] = (uint32_t)keys[i];  // sorted position = output position
@@ -208,9 +230,7 @@ __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
     }
   }
   if (t == 0) {
-    int kept = 0;
-    while (kept < m && keys[kept] != kNoKey) ++kept;  // keys sorted: kept ones first
-    fo[n_nodes] = kept;
+    fo[n_nodes] = n_kept;
     a.n_words[f] = n_words;
     a.n_nodes[f] = n_nodes;
   }
@@ -222,7 +242,16 @@ hipError_t launch_bow(const BowLaunch& a, hipStream_t st) {
   if (a.n_frames <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bow_descend, dim3((unsigned)((a.stride + 15) / 16), a.n_frames), dim3(256),
                      0, st, a);
-  hipLaunchKernelGGL(k_bow_assemble, dim3(a.n_frames), dim3(256), 0, st, a);
+  const size_t lds = 16 * (size_t)a.lds_m;
+  if (lds > 64 * 1024) {
+    static bool raised = false;  // > 64 KB dynamic LDS needs the opt-in once
+    if (!raised && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bow_assemble),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       16 * kBowMaxFeatures) != hipSuccess)
+      return hipErrorInvalidValue;
+    raised = true;
+  }
+  hipLaunchKernelGGL(k_bow_assemble, dim3(a.n_frames), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 

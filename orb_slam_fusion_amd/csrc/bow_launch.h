@@ -21,6 +21,7 @@ struct VocabDev {
 struct BowLaunch {
   VocabDev voc;
   int n_frames, stride, levelsup;
+  int lds_m;  // next power of two >= stride (assembly LDS sizing)
   const uint8_t* descs;  // [n_frames][stride][32]
   const int* n;          // features per frame
   // per-feature scratch [n_frames][stride]

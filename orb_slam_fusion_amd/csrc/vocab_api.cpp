@@ -98,6 +98,12 @@ bool parse(const char* path, HostTree& T) {
 
 size_t al(size_t v) { return (v + 255) & ~(size_t)255; }
 
+int pow2_at_least(int v) {
+  int m = 1;
+  while (m < v) m <<= 1;
+  return m;
+}
+
 orbgpu_status upload(orbgpu_vocab* v, const HostTree& T) {
   const int N = (int)T.children.size();
   std::vector<int> off(N + 1, 0);
@@ -208,6 +214,7 @@ orbgpu_status orbgpu_bow_transform_batch(orbgpu_vocab* v, int n_frames, const ui
   orbgpu::BowLaunch L{};
   L.voc = v->dev;
   L.n_frames = n_frames, L.stride = stride, L.levelsup = levelsup;
+  L.lds_m = pow2_at_least(stride);
   L.descs = d_descs, L.n = d_n;
   set_feat(v, L, v->feat_cap);
   L.bow_words = d_bow_words, L.bow_weights = d_bow_weights, L.n_words = d_n_words;
@@ -254,6 +261,7 @@ orbgpu_status orbgpu_bow_transform(orbgpu_vocab* v, const uint8_t* descs, int n,
   orbgpu::BowLaunch L{};
   L.voc = v->dev;
   L.n_frames = 1, L.stride = S, L.levelsup = levelsup;
+  L.lds_m = pow2_at_least(S);
   L.descs = d + o_desc;
   L.n = reinterpret_cast<const int*>(d + o_n);
   set_feat(v, L, v->feat_cap);
