@@ -99,6 +99,8 @@ def main() -> int:
     ap.add_argument("--no-match", action="store_true",
                     help="skip the SearchByProjection (motion-model search) side line")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform side line")
+    ap.add_argument("--no-track", action="store_true",
+                    help="skip the device-resident tracking-chain side line")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the per-frame host-path latency side line")
     args = ap.parse_args()
@@ -302,6 +304,13 @@ def main() -> int:
         from bench_bow import measure as measure_bow  # noqa: E402
 
         result["bow"] = measure_bow(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+    if rank == 0 and world == 1 and not args.no_track:
+        # config C3's path on synthetic data: extract + stereo + SearchByProjection
+        # + PoseOptimization chained on the device, vs the oracle chain on the CPU
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_track import measure as measure_track  # noqa: E402
+
+        result["track"] = measure_track(frames=B, calls=10, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_latency:
         # north_star's per-frame target: one stereo frame at a time through the
         # host ABI (2-thread extraction + PoseOptimization) vs the CPU oracle

@@ -332,6 +332,20 @@ orbgpu_status orbgpu_search_by_projection_last_batch(
     int kp_stride, const orbgpu_proj_point* d_pts, const int* d_npts, int pt_stride, float th,
     int mono, int check_orientation, int32_t* d_match, int* d_nmatches, void* hip_stream);
 
+/* The observation list Optimizer::PoseOptimization builds (optimizer.cc:
+ *   806-877) for frames after orbgpu_search_by_projection_last_batch, whose
+ *   mvpMapPoints held no point before the search (TrackWithMotionModel resets
+ *   them, tracking.cc:2187-2188): for every keypoint i with d_match[i] >= 0,
+ *   in increasing i, one orbgpu_pose_obs {Xw of point d_match[i], mvKeysUn[i].pt,
+ *   mvuRight[i] (-1 when d_uright is NULL), mvInvLevelSigma2[octave]};
+ *   d_obs_index (optional) receives i.  Frame f writes d_obs + f * obs_stride
+ *   and d_nobs[f]: the input of orbgpu_pose_opt_batch, all on the device. */
+orbgpu_status orbgpu_matches_to_pose_obs_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_keypoint* d_kps, const float* d_uright,
+    const int32_t* d_match, const int* d_n, int kp_stride, const orbgpu_proj_point* d_pts,
+    int pt_stride, const float* inv_level_sigma2, int n_levels, orbgpu_pose_obs* d_obs,
+    int obs_stride, int* d_nobs, int32_t* d_obs_index, void* hip_stream);
+
 /* Replaces: bool Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit)
  *   (frame.cc:548-603, Nleft == -1) over Tracking::SearchLocalPoints' loop
  *   (tracking.cc:2644-2661): points flagged ORBGPU_MP_SKIP are not projected

@@ -581,7 +581,58 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   if (lane == 0) a.nmatches[f] = nmatch;
 }
 
+// Optimizer::PoseOptimization's observation list (optimizer.cc:806-877) of a
+// frame whose mvpMapPoints hold exactly this call's matches: keypoints with
+// match[i] >= 0 in increasing i.  Block / frame, 256 keypoints per step.
+__global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
+  __shared__ int wsum[4];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = a.n[f];
+  const size_t ko = (size_t)f * a.kp_stride;
+  const float* kps = a.kps + ko * kKpFloats;
+  orbgpu_pose_obs* obs = a.obs + (size_t)f * a.obs_stride;
+  int32_t* index = a.obs_index ? a.obs_index + (size_t)f * a.obs_stride : nullptr;
+  int base = 0;
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    const int i = i0 + t;
+    const int q = i < n ? a.match[ko + i] : -1;
+    const bool take = q >= 0;
+    const uint64_t bal = __ballot(take);
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (take) {
+      const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+      if (pos < a.obs_stride) {
+        const orbgpu_proj_point& P = a.pts[(size_t)f * a.pt_stride + q];
+        const float* k = kps + (size_t)i * kKpFloats;
+        orbgpu_pose_obs o;
+        o.Xw[0] = P.Xw[0], o.Xw[1] = P.Xw[1], o.Xw[2] = P.Xw[2];
+        o.u = k[0], o.v = k[1];
+        o.ur = a.uright ? a.uright[ko + i] : -1.0f;
+        o.inv_sigma2 = a.inv_sigma2[kp_octave(k)];
+        obs[pos] = o;
+        if (index) index[pos] = i;
+      }
+    }
+    base += total;
+    __syncthreads();
+  }
+  if (t == 0) {
+    a.nobs[f] = min(base, a.obs_stride);
+    if (base > a.obs_stride) atomicOr(a.err, 2);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st) {
+  if (a.n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mt_pose_obs, dim3(a.n_frames), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_match(const MatchLaunch& a, hipStream_t st) {
   if (a.n_frames <= 0) return hipSuccess;

@@ -73,4 +73,24 @@ struct MatchLaunch {
 
 hipError_t launch_match(const MatchLaunch& a, hipStream_t st);
 
+// matches -> PoseOptimization observations (optimizer.cc:806-877)
+struct ObsLaunch {
+  int n_frames;
+  const float* kps;       // orbgpu_keypoint rows, frame f at f * kp_stride
+  const float* uright;    // may be null (every edge monocular)
+  const int32_t* match;   // [n_frames][kp_stride]
+  const int* n;
+  int kp_stride;
+  const orbgpu_proj_point* pts;
+  int pt_stride;
+  float inv_sigma2[ORBGPU_MAX_LEVELS];  // Frame::mvInvLevelSigma2
+  orbgpu_pose_obs* obs;   // [n_frames][obs_stride]
+  int obs_stride;
+  int* nobs;
+  int32_t* obs_index;     // may be null
+  int* err;
+};
+
+hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st);
+
 }  // namespace orbgpu

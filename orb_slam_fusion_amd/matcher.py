@@ -122,6 +122,20 @@ class ORBmatcher:
                 pts.shape[1], float(th), int(bMono), int(self.mbCheckOrientation), ptr(match),
                 ptr(nmatches), s), "orbgpu_search_by_projection_last_batch")
 
+    def matches_to_pose_obs_batch(self, kps, uright, match, n, pts, inv_level_sigma2, obs, nobs,
+                                  obs_index=None, stream=None) -> None:
+        """PoseOptimization's observation list from this call's matches, on the device:
+        kps [B, K, 7]; uright float32 [B, K] or None; match int32 [B, K]; n int32 [B];
+        pts uint8 [B, P, 56]; obs float32 [B, S, 7] (POSE_OBS layout); nobs int32 [B];
+        obs_index int32 [B, S] or None."""
+        B, K = kps.shape[0], kps.shape[1]
+        isg = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_matches_to_pose_obs_batch(
+                self._h, B, ptr(kps), ptr(uright), ptr(match), ptr(n), K, ptr(pts),
+                pts.shape[1], ptr(isg), len(isg), ptr(obs), obs.shape[1], ptr(nobs),
+                ptr(obs_index), s), "orbgpu_matches_to_pose_obs_batch")
+
     # -- Frame::isInFrustum ---------------------------------------------------
     def is_in_frustum(self, F: MatchFrame, points: np.ndarray, viewingCosLimit: float,
                       views: Optional[np.ndarray] = None) -> np.ndarray:
