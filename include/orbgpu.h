@@ -428,6 +428,111 @@ orbgpu_status orbgpu_bow_transform_batch(orbgpu_vocab* v, int n_frames, const ui
  * or -1 on bad arguments.  Host-only (no device work). */
 int orbgpu_level_thresholds(float log_scale_factor, int n_levels, float* thr);
 
+/* ---- Inertial tracking optimisation -----------------
+ * Optimizer::PoseInertialOptimizationLastFrame (optimizer.cc:4762-5160) and
+ * Optimizer::PoseInertialOptimizationLastKeyFrame (:4394-4760): g2o
+ * Gauss-Newton (optimization_algorithm_gauss_newton.cpp), dense LDLT over the
+ * free vertices, 4 rounds x 10 iterations with outlier classification.
+ * Pinhole left camera only (Frame::Nleft == -1; the fisheye right-camera
+ * edges are out of scope).  Matrices are row-major. */
+
+/* A frame's (or key frame's) IMU state: the estimates of VertexPose
+ * (ImuCamPose(Frame*), g2o_types.cc:74-118), VertexVelocity, VertexGyroBias,
+ * VertexAccBias (g2o_types.cc:448-470). */
+typedef struct orbgpu_imu_state {
+  float Rwb[9], twb[3]; /* GetImuRotation / GetImuPosition */
+  float Rcw[9], tcw[3]; /* GetPose() (current frame only; ignored for the previous one) */
+  float v[3];           /* GetVelocity */
+  float bg[3], ba[3];   /* mImuBias (bwx..bwz), (bax..baz) */
+} orbgpu_imu_state;
+
+/* IMU::Preintegrated between the previous and the current frame
+ * (imu_types.h) plus the information matrices the edges derive from it:
+ * info = EdgeInertial's (C.block<9,9>(0,0) inverse, symmetrised, eigenvalues
+ * below 1e-12 zeroed, g2o_types.cc:472-492), info_g / info_a =
+ * C.block<3,3>(9,9) / (12,12) inverses (optimizer.cc:4933-4944). */
+typedef struct orbgpu_imu_preint {
+  float dT;
+  float dR[9], dV[3], dP[3];
+  float JRg[9], JVg[9], JVa[9], JPg[9], JPa[9];
+  float bg[3], ba[3]; /* the linearisation bias b */
+  float pad_;
+  double info[81];
+  double info_g[9], info_a[9];
+} orbgpu_imu_preint;
+
+/* ConstraintPoseImu of the previous frame (mpcpi), as its constructor left
+ * it (H symmetrised and eigen-cleaned, imu_types / g2o_types.h:664-685).
+ * LastFrame mode only. */
+typedef struct orbgpu_imu_prior {
+  double Rwb[9], twb[3], vwb[3], bg[3], ba[3];
+  double H[225];
+} orbgpu_imu_prior;
+
+/* Camera intrinsics (Pinhole params_) + bf + mImuCalib mTcb / mTbc. */
+typedef struct orbgpu_imu_calib {
+  float fx, fy, cx, cy, bf;
+  float Rcb[9], tcb[3];
+  float Rbc[9], tbc[3];
+} orbgpu_imu_calib;
+
+/* One EdgeMonoOnlyPose / EdgeStereoOnlyPose, in frame keypoint order:
+ * mvKeysUn[i].pt, mvuRight[i] (< 0: monocular), mvInvLevelSigma2[octave] /
+ * Uncertainty2, close = (mTrackDepth < 10). */
+typedef struct orbgpu_inertial_obs {
+  float Xw[3];
+  float u, v, ur;
+  float inv_sigma2;
+  int32_t close;
+} orbgpu_inertial_obs;
+
+/* Results: SetImuPoseVelocity(Rwb, twb, v) and mImuBias (float casts), the
+ * double estimates and the 15x15 H (VP, VV, VG, VA order) the reference passes
+ * to `new ConstraintPoseImu(...)` (LastFrame: after Marginalize(H, 0, 14);
+ * LastKeyFrame: the current-frame Hessian), and the return value
+ * nInitialCorrespondences - nBad. */
+typedef struct orbgpu_inertial_result {
+  float Rwb[9], twb[3], v[3], bg[3], ba[3];
+  int32_t n_good;
+  int32_t n_inliers;
+  double Rwb_d[9], twb_d[3], v_d[3], bg_d[3], ba_d[3];
+  double H[225];
+} orbgpu_inertial_result;
+
+#define ORBGPU_INERTIAL_LAST_FRAME 0
+#define ORBGPU_INERTIAL_LAST_KEYFRAME 1
+
+typedef struct orbgpu_inertial_ctx orbgpu_inertial_ctx;
+
+orbgpu_status orbgpu_inertial_ctx_create(int device, int max_problems, int max_obs,
+                                         orbgpu_inertial_ctx** out);
+void orbgpu_inertial_ctx_destroy(orbgpu_inertial_ctx* c);
+
+/* Replaces: int Optimizer::PoseInertialOptimizationLastFrame(Frame*, bool
+ *   bRecInit) (mode ORBGPU_INERTIAL_LAST_FRAME: previous frame free, prior
+ *   edge, marginalisation) and PoseInertialOptimizationLastKeyFrame (mode
+ *   ORBGPU_INERTIAL_LAST_KEYFRAME: last key frame fixed, `prior` unused).  One
+ *   problem from host buffers; outlier[i] = mvbOutlier of observation i. */
+orbgpu_status orbgpu_pose_inertial(orbgpu_inertial_ctx* c, int mode, const orbgpu_imu_calib* calib,
+                                   const orbgpu_imu_state* cur, const orbgpu_imu_state* prev,
+                                   const orbgpu_imu_preint* preint, const orbgpu_imu_prior* prior,
+                                   const orbgpu_inertial_obs* obs, int n_obs, int rec_init,
+                                   orbgpu_inertial_result* res, uint8_t* outlier);
+
+/* Device-resident batch: problem p reads d_cur[p], d_prev[p], d_preint[p],
+ * d_prior[p] (LastFrame), d_obs[p * obs_stride .. + d_nobs[p]); one shared
+ * calibration.  Asynchronous on hip_stream (NULL: the context's stream). */
+orbgpu_status orbgpu_pose_inertial_batch(orbgpu_inertial_ctx* c, int mode,
+                                         const orbgpu_imu_calib* calib, int n_problems,
+                                         const orbgpu_imu_state* d_cur,
+                                         const orbgpu_imu_state* d_prev,
+                                         const orbgpu_imu_preint* d_preint,
+                                         const orbgpu_imu_prior* d_prior,
+                                         const orbgpu_inertial_obs* d_obs, const int* d_nobs,
+                                         int obs_stride, int rec_init,
+                                         orbgpu_inertial_result* d_res, uint8_t* d_outlier,
+                                         void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,10 @@ def lib() -> ctypes.CDLL:
         "orc_vocab_free": (None, [_P]),
         "orc_vocab_info": (None, [_P, _P]),
         "orc_bow_transform": (None, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+        "orc_pose_inertial": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
+        "orc_inertial_system": (None, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
+        "orc_pose_inertial_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
+        "orc_sym_pinv": (None, [_P, _I, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(so, name)
@@ -395,3 +399,41 @@ class OracleVocab:
                 lib().orc_vocab_free(self._h)
         except Exception:
             pass
+
+
+def pose_inertial(case: dict, rec_init: bool = False, with_prev: bool = False):
+    """PoseInertialOptimizationLastFrame (mode 0) / LastKeyFrame (mode 1) on a
+    case of tests/inertial_cases.py: returns (result record, outlier uint8[n])
+    [, the previous frame's final double state]."""
+    from orb_slam_fusion_amd._lib import INERTIAL_RESULT_DTYPE
+
+    obs = case["obs"]
+    n = len(obs)
+    res = np.zeros((), INERTIAL_RESULT_DTYPE)
+    out = np.zeros(max(n, 1), np.uint8)
+    prev_out = np.zeros(21)
+    prior = case.get("prior")
+    lib().orc_pose_inertial_ex(case["mode"], _p(case["calib"]), _p(case["cur"]),
+                               _p(case["prev"]), _p(case["preint"]), _p(prior), _p(obs), n,
+                               int(rec_init), _p(res), _p(out), _p(prev_out))
+    return (res, out[:n].copy(), prev_out) if with_prev else (res, out[:n].copy())
+
+
+def inertial_system(case: dict, cur21: np.ndarray, prev21: np.ndarray, kernels: bool = False):
+    """The oracle's Gauss-Newton (H, b) at double states [Rwb(9) twb v bg ba]."""
+    n = 30 if case["mode"] == 0 else 15
+    H = np.zeros((n, n))
+    b = np.zeros(n)
+    cur21 = np.ascontiguousarray(cur21, np.float64)
+    prev21 = np.ascontiguousarray(prev21, np.float64)
+    lib().orc_inertial_system(case["mode"], _p(case["calib"]), _p(cur21), _p(prev21),
+                              _p(case["preint"]), _p(case.get("prior")), _p(case["obs"]),
+                              len(case["obs"]), int(kernels), _p(H), _p(b))
+    return H, b
+
+
+def sym_pinv(A: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.float64)
+    out = np.zeros_like(A)
+    lib().orc_sym_pinv(_p(A), A.shape[0], _p(out))
+    return out

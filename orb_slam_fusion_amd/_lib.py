@@ -105,6 +105,30 @@ assert TRACK_VIEW_DTYPE.itemsize == 28
 
 MAX_LEVELS = 16
 
+# PoseInertialOptimization inputs/outputs (orbgpu_imu_* in include/orbgpu.h)
+_F9, _F3, _D9, _D3 = ("<f4", (9,)), ("<f4", (3,)), ("<f8", (9,)), ("<f8", (3,))
+IMU_STATE_DTYPE = np.dtype([("Rwb",) + _F9, ("twb",) + _F3, ("Rcw",) + _F9, ("tcw",) + _F3,
+                            ("v",) + _F3, ("bg",) + _F3, ("ba",) + _F3], align=True)
+IMU_PREINT_DTYPE = np.dtype(
+    [("dT", "<f4"), ("dR",) + _F9, ("dV",) + _F3, ("dP",) + _F3, ("JRg",) + _F9, ("JVg",) + _F9,
+     ("JVa",) + _F9, ("JPg",) + _F9, ("JPa",) + _F9, ("bg",) + _F3, ("ba",) + _F3, ("pad_", "<f4"),
+     ("info", "<f8", (81,)), ("info_g",) + _D9, ("info_a",) + _D9], align=True)
+IMU_PRIOR_DTYPE = np.dtype([("Rwb",) + _D9, ("twb",) + _D3, ("vwb",) + _D3, ("bg",) + _D3,
+                            ("ba",) + _D3, ("H", "<f8", (225,))], align=True)
+IMU_CALIB_DTYPE = np.dtype([("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                            ("bf", "<f4"), ("Rcb",) + _F9, ("tcb",) + _F3, ("Rbc",) + _F9,
+                            ("tbc",) + _F3], align=True)
+INERTIAL_OBS_DTYPE = np.dtype([("Xw", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"),
+                               ("inv_sigma2", "<f4"), ("close", "<i4")], align=True)
+INERTIAL_RESULT_DTYPE = np.dtype(
+    [("Rwb",) + _F9, ("twb",) + _F3, ("v",) + _F3, ("bg",) + _F3, ("ba",) + _F3,
+     ("n_good", "<i4"), ("n_inliers", "<i4"), ("Rwb_d",) + _D9, ("twb_d",) + _D3, ("v_d",) + _D3,
+     ("bg_d",) + _D3, ("ba_d",) + _D3, ("H", "<f8", (225,))], align=True)
+assert (IMU_STATE_DTYPE.itemsize, IMU_PREINT_DTYPE.itemsize, IMU_PRIOR_DTYPE.itemsize,
+        IMU_CALIB_DTYPE.itemsize, INERTIAL_OBS_DTYPE.itemsize,
+        INERTIAL_RESULT_DTYPE.itemsize) == (132, 1064, 1968, 116, 32, 2064)
+INERTIAL_LAST_FRAME, INERTIAL_LAST_KEYFRAME = 0, 1
+
 
 class FrameGeom(ctypes.Structure):
     """orbgpu_frame_geom: Frame::mnMinX/mnMaxX/mnMinY/mnMaxY, mnScaleLevels,
