@@ -10,6 +10,7 @@ LIB      := orb_slam_fusion_amd/lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off -Wall
 GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels.hip \
             $(CSRC)/stereo_kernels.hip $(CSRC)/match_kernels.hip $(CSRC)/bow_kernels.hip \
+            $(CSRC)/inertial_kernels.hip $(CSRC)/inertial_api.cpp \
             $(CSRC)/orb_plan.cpp $(CSRC)/orb_api.cpp $(CSRC)/pose_api.cpp $(CSRC)/lba_api.cpp \
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
 GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h

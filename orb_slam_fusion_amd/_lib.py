@@ -213,6 +213,12 @@ SIGNATURES = {
     "orbgpu_bow_transform_batch": (
         _I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
+    "orbgpu_inertial_ctx_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
+    "orbgpu_inertial_ctx_destroy": (None, [_P]),
+    "orbgpu_pose_inertial": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
+    "orbgpu_pose_inertial_batch": (
+        _I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P],
+    ),
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (

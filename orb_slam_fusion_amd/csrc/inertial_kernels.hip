@@ -1,0 +1,1179 @@
+// gfx950 PoseInertialOptimizationLastFrame / LastKeyFrame: one workgroup per
+// problem runs the whole call -- 4 outlier-rejection rounds x 10 g2o
+// Gauss-Newton iterations over the current frame's pose / velocity / bias
+// vertices (and, LastFrame, the previous frame's, tied by the prior), the
+// inlier classification, and the Hessian (marginalised, LastFrame) for the
+// next ConstraintPoseImu.  Reference: optimizer.cc:4394-5160, g2o_types.cc,
+// imu_types.cc:283-310 (see oracle/inertial_oracle.cc for the restatement).
+//
+// Roles inside the workgroup (5 waves):
+//   wave 0     the IMU edges -- EdgeInertial (LogSO3, right Jacobians, the
+//              bias-corrected preintegration in float), EdgeGyroRW/AccRW and
+//              EdgePriorPoseImu -- their errors and Jacobians into LDS, then
+//              the dense LDLT of the n x n system (n = 30 / 15) and the
+//              vertex updates;
+//   waves 1-4  the visual edges (EdgeMono/StereoOnlyPose): errors, Huber
+//              weights, body-frame Jacobians, the 6x6 block + gradient,
+//              reduced by a fixed tree.
+// Between them every thread assembles the system, each owning whole entries
+// (all edge contributions to an entry summed by one thread: no atomics).
+// Everything stays in LDS; observations are read once from HBM.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbgpu.h"
+
+namespace orbgpu {
+
+constexpr int kInWaves = 5;
+constexpr int kInThreads = 64 * kInWaves;
+constexpr int kVisThreads = kInThreads - 64;
+constexpr int kInLdsObs = 2048;  // observations staged in LDS (the rest re-read)
+constexpr int kLd = 31;          // padded row stride of the n x n system
+
+struct CalibD {
+  double fx, fy, cx, cy, bf;
+  double Rcb[9], tcb[3], Rbc[9], tbc[3];
+};
+
+struct StateD {
+  double Rwb[9], twb[3], Rcw[9], tcw[3], v[3], bg[3], ba[3];
+};
+
+// ---- 3x3 helpers (row-major) ------------------------------------------------
+__device__ __forceinline__ void m3_mul(const double* A, const double* B, double* C) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+__device__ __forceinline__ void m3_tr(const double* A, double* C) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * j + i];
+}
+__device__ __forceinline__ void m3_mv(const double* A, const double* v, double* o) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) o[i] = A[3 * i] * v[0] + A[3 * i + 1] * v[1] + A[3 * i + 2] * v[2];
+}
+__device__ __forceinline__ void m3_hat(const double* w, double* W) {
+  W[0] = 0;
+  W[1] = -w[2];
+  W[2] = w[1];
+  W[3] = w[2];
+  W[4] = 0;
+  W[5] = -w[0];
+  W[6] = -w[1];
+  W[7] = w[0];
+  W[8] = 0;
+}
+
+// NormalizeRotation: orthogonal polar factor, 3 Newton steps X <- (X + X^-T)/2
+__device__ __forceinline__ void polar3(double* X) {
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    double C[9];
+    C[0] = X[4] * X[8] - X[5] * X[7];
+    C[1] = X[5] * X[6] - X[3] * X[8];
+    C[2] = X[3] * X[7] - X[4] * X[6];
+    C[3] = X[2] * X[7] - X[1] * X[8];
+    C[4] = X[0] * X[8] - X[2] * X[6];
+    C[5] = X[1] * X[6] - X[0] * X[7];
+    C[6] = X[1] * X[5] - X[2] * X[4];
+    C[7] = X[2] * X[3] - X[0] * X[5];
+    C[8] = X[0] * X[4] - X[1] * X[3];
+    const double rdet = 1.0 / (X[0] * C[0] + X[1] * C[1] + X[2] * C[2]);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) X[i] = 0.5 * (X[i] + C[i] * rdet);
+  }
+}
+
+// ExpSO3 (g2o_types.cc:783-796)
+__device__ __forceinline__ void exp_so3(const double* w, double* R) {
+  const double d2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  const double d = sqrt(d2);
+  double W[9], WW[9];
+  m3_hat(w, W);
+  m3_mul(W, W, WW);
+  double s, c;
+  if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) {
+    s = 1.0;
+    c = 0.5;
+  } else {
+    double sn, cs;
+    sincos(d, &sn, &cs);
+    s = sn / d;
+    c = (1.0 - cs) / d2;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + W[i] * s + WW[i] * c;
+  polar3(R);
+}
+
+// LogSO3 (g2o_types.cc:798-811)
+__device__ __forceinline__ void log_so3(const double* R, double* w) {
+  const double t = R[0] + R[4] + R[8];
+  w[0] = (R[7] - R[5]) / 2;
+  w[1] = (R[2] - R[6]) / 2;
+  w[2] = (R[3] - R[1]) / 2;
+  const double ct = (t - 1.0) * 0.5;
+  if (__builtin_amdgcn_readfirstlane(ct > 1 || ct < -1 ? 1 : 0)) return;
+  const double th = acos(ct);
+  const double s = sin(th);
+  if (__builtin_amdgcn_readfirstlane(fabs(s) < 1e-5 ? 1 : 0)) return;
+  const double f = th / s;
+  w[0] *= f;
+  w[1] *= f;
+  w[2] *= f;
+}
+
+// InverseRightJacobianSO3 (kInv) / RightJacobianSO3 (g2o_types.cc:817-848)
+template <bool kInv>
+__device__ __forceinline__ void right_j(const double* v, double* J) {
+  const double d2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const double d = sqrt(d2);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) J[i] = i % 4 == 0 ? 1.0 : 0.0;
+  if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) return;
+  double W[9], WW[9], sn, cs;
+  m3_hat(v, W);
+  m3_mul(W, W, WW);
+  sincos(d, &sn, &cs);
+  double a, b;
+  if (kInv) {
+    a = 0.5;
+    b = 1.0 / d2 - (1.0 + cs) / (2.0 * d * sn);
+  } else {
+    a = -(1.0 - cs) / d2;
+    b = (d - sn) / (d2 * d);
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) J[i] += W[i] * a + WW[i] * b;
+}
+
+// ---- float side of IMU::Preintegrated ---------------------------------------
+// Preintegrated::GetDeltaRotation(b) (imu_types.cc:289-294): Sophus SO3f::exp
+// of JRg * dbg (so3.hpp:584-618, unnormalised quaternion -> matrix), dR * it,
+// NormalizeRotation (polar factor), cast to double.
+__device__ __forceinline__ void delta_rotation(const orbgpu_imu_preint& p, const float* dbg,
+                                               double* out) {
+  float w[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) w[i] = p.JRg[3 * i] * dbg[0] + p.JRg[3 * i + 1] * dbg[1] + p.JRg[3 * i + 2] * dbg[2];
+  const float th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  float imag, real;
+  if (__builtin_amdgcn_readfirstlane(th2 < 1e-5f * 1e-5f ? 1 : 0)) {
+    const float po4 = th2 * th2;
+    imag = 0.5f - (float)(1.0 / 48.0) * th2 + (float)(1.0 / 3840.0) * po4;
+    real = 1.f - (float)(1.0 / 8.0) * th2 + (float)(1.0 / 384.0) * po4;
+  } else {
+    const float th = sqrtf(th2);
+    const float half = 0.5f * th;
+    imag = sinf(half) / th;
+    real = cosf(half);
+  }
+  const float qx = imag * w[0], qy = imag * w[1], qz = imag * w[2], qw = real;
+  const float tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+  const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+  const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+  const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+  const float E[9] = {1.f - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1.f - (txx + tzz),
+                      tyz - twx, txz - twy, tyz + twx, 1.f - (txx + tyy)};
+  double M[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      M[3 * i + j] = (double)(p.dR[3 * i] * E[j] + p.dR[3 * i + 1] * E[3 + j] + p.dR[3 * i + 2] * E[6 + j]);
+  polar3(M);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) out[i] = (double)(float)M[i];
+}
+
+__device__ __forceinline__ void delta_lin(const float* d0, const float* Jg, const float* Ja,
+                                          const float* dbg, const float* dba, double* out) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float g = Jg[3 * i] * dbg[0] + Jg[3 * i + 1] * dbg[1] + Jg[3 * i + 2] * dbg[2];
+    const float a = Ja[3 * i] * dba[0] + Ja[3 * i + 1] * dba[1] + Ja[3 * i + 2] * dba[2];
+    out[i] = (double)(d0[i] + g + a);
+  }
+}
+
+// ---- LDS ----------------------------------------------------------------------
+struct InShared {
+  StateD cur, prev;
+  double ev_Rcw[9], ev_tcw[3];  // current camera pose at the last computeActiveErrors
+  CalibD cal;
+  double H[30 * kLd];           // the system (full, row-major, padded)
+  double b[30];
+  double x[30];                 // solver x, persists over the call
+  double Ji[9 * 24], ei[9];     // EdgeInertial Jacobian / error
+  double OJ[9 * 24], Oe[9];     // info * Ji, -info * ei
+  double Jp[15 * 15], epr[15];  // EdgePriorPoseImu
+  double OJp[15 * 15], Oep[15];
+  double wp;                    // prior Huber weight
+  double vis[27];               // visual 6x6 (lower, 21) + gradient (6)
+  double red[kInWaves * 27];
+  double temp[32];
+  double pinv[15 * 16];
+  double V[256];                // Jacobi eigenvectors (16 x 16)
+  double HM[30 * kLd];          // final Hessian (LastFrame: 30 x 30 in EdgeInertial order)
+  int perm[30];
+  int ired[kInWaves * 2];
+  int ok;
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum63(double v) {  // lane 63 holds the sum
+  v += dpp_d<0x111, 0xf>(v);
+  v += dpp_d<0x112, 0xf>(v);
+  v += dpp_d<0x114, 0xf>(v);
+  v += dpp_d<0x118, 0xf>(v);
+  v += dpp_d<0x142, 0xa>(v);
+  v += dpp_d<0x143, 0xc>(v);
+  return v;
+}
+__device__ __forceinline__ double bcast(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+
+// ---- visual edges -------------------------------------------------------------
+struct VisObs {  // == orbgpu_inertial_obs
+  float Xw[3];
+  float u, v, ur;
+  float inv_sigma2;
+  int32_t close;
+};
+
+__device__ __forceinline__ void vis_error(const VisObs& o, const double* Rcw, const double* tcw,
+                                          const CalibD& c, double e[3], double Xc[3]) {
+  const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
+  m3_mv(Rcw, X, Xc);
+  Xc[0] += tcw[0];
+  Xc[1] += tcw[1];
+  Xc[2] += tcw[2];
+  const double u = c.fx * Xc[0] / Xc[2] + c.cx;
+  const double v = c.fy * Xc[1] / Xc[2] + c.cy;
+  e[0] = (double)o.u - u;
+  e[1] = (double)o.v - v;
+  e[2] = o.ur >= 0.f ? (double)o.ur - (u - c.bf * (1 / Xc[2])) : 0.0;
+}
+
+__device__ __forceinline__ double vis_chi2(const double e[3], double info, bool stereo) {
+  double s = e[0] * info * e[0] + e[1] * info * e[1];
+  if (stereo) s += e[2] * info * e[2];
+  return s;
+}
+
+// proj_jac * Rcb * SE3deriv(Xb) (g2o_types.cc:361-446)
+__device__ __forceinline__ void vis_jacobian(const double Xc[3], const CalibD& c, bool stereo,
+                                             double J[3][6]) {
+  double Xb[3];
+  m3_mv(c.Rbc, Xc, Xb);
+  Xb[0] += c.tbc[0];
+  Xb[1] += c.tbc[1];
+  Xb[2] += c.tbc[2];
+  const double iz = 1.0 / Xc[2];
+  double pj[3][3] = {{c.fx * iz, 0, -c.fx * Xc[0] / (Xc[2] * Xc[2])},
+                     {0, c.fy * iz, -c.fy * Xc[1] / (Xc[2] * Xc[2])},
+                     {0, 0, 0}};
+  if (stereo) {
+    pj[2][0] = pj[0][0];
+    pj[2][1] = pj[0][1];
+    pj[2][2] = pj[0][2] + c.bf * (1.0 / (Xc[2] * Xc[2]));
+  }
+  const double x = Xb[0], y = Xb[1], z = Xb[2];
+  const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    double PR[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) PR[k] = pj[r][0] * c.Rcb[k] + pj[r][1] * c.Rcb[3 + k] + pj[r][2] * c.Rcb[6 + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) J[r][k] = PR[0] * S[0][k] + PR[1] * S[1][k] + PR[2] * S[2][k];
+  }
+}
+
+// Huber (robust_kernel_impl.cpp): rho'(e2)
+__device__ __forceinline__ double huber_w(double e2, double delta) {
+  return e2 <= delta * delta ? 1.0 : delta / sqrt(e2);
+}
+
+// One visual edge's weighted 6x6 (lower, 21) + gradient (6) into acc[0..26].
+__device__ __forceinline__ void vis_accumulate(const VisObs& o, const double* Rcw, const double* tcw,
+                                               const CalibD& c, bool robust, double w_fixed,
+                                               double (&acc)[27]) {
+  double e[3], Xc[3];
+  vis_error(o, Rcw, tcw, c, e, Xc);
+  const bool st = o.ur >= 0.f;
+  const double info = (double)o.inv_sigma2;
+  double w = w_fixed;
+  if (robust) w = huber_w(vis_chi2(e, info, st), st ? (double)(float)sqrt(7.815) : (double)(float)sqrt(5.991));
+  double J[3][6];
+  vis_jacobian(Xc, c, st, J);
+  const double wi = w * info;
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+#pragma unroll
+    for (int q = 0; q <= r; ++q) {
+      double h = J[0][r] * wi * J[0][q] + J[1][r] * wi * J[1][q];
+      if (st) h += J[2][r] * wi * J[2][q];
+      acc[k++] += h;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double g = J[0][r] * (wi * e[0]) + J[1][r] * (wi * e[1]);
+    if (st) g += J[2][r] * (wi * e[2]);
+    acc[21 + r] -= g;
+  }
+}
+
+// ---- the IMU edges (wave 0, every lane the same values; lane 0 stores) ------
+template <int MODE>
+__device__ void imu_edges(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu_imu_prior* pr,
+                          double dt, bool prior_kernel, int lane) {
+  const StateD &s1 = sh.prev, &s2 = sh.cur;
+  float bg[3], ba[3], dbg[3], dba[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    bg[i] = (float)s1.bg[i];
+    ba[i] = (float)s1.ba[i];
+    dbg[i] = bg[i] - pi.bg[i];
+    dba[i] = ba[i] - pi.ba[i];
+  }
+  double dR[9], dV[3], dP[3];
+  delta_rotation(pi, dbg, dR);
+  delta_lin(pi.dV, pi.JVg, pi.JVa, dbg, dba, dV);
+  delta_lin(pi.dP, pi.JPg, pi.JPa, dbg, dba, dP);
+  const double g2 = -(double)9.81f;  // g = (0, 0, -GRAVITY_VALUE)
+  double Rbw1[9], dRt[9], T[9], eR[9];
+  m3_tr(s1.Rwb, Rbw1);
+  m3_tr(dR, dRt);
+  m3_mul(dRt, Rbw1, T);
+  m3_mul(T, s2.Rwb, eR);
+  double er[3];
+  log_so3(eR, er);
+  double dv[3], dp[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dv[i] = s2.v[i] - s1.v[i] - (i == 2 ? g2 * dt : 0.0);
+    dp[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? g2 * dt * dt / 2 : 0.0);
+  }
+  double rv[3], rp[3];
+  m3_mv(Rbw1, dv, rv);
+  m3_mv(Rbw1, dp, rp);
+  double e[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    e[i] = er[i];
+    e[3 + i] = rv[i] - dV[i];
+    e[6 + i] = rp[i] - dP[i];
+  }
+  // Jacobian blocks (g2o_types.cc:523-578)
+  double invJr[9], A[9], B[9], Rt2[9];
+  right_j<true>(er, invJr);
+  m3_tr(s2.Rwb, Rt2);
+  m3_mul(invJr, Rt2, A);
+  double J0r[9];
+  m3_mul(A, s1.Rwb, J0r);  // -invJr * Rwb2^T * Rwb1
+  double dp2[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) dp2[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? 0.5 * g2 * dt * dt : 0.0);
+  double hv[9], hp[9], rp2[3];
+  m3_hat(rv, hv);
+  m3_mv(Rbw1, dp2, rp2);
+  m3_hat(rp2, hp);
+  double JRg[9], jd[3], RJ[9], eRt[9], Gb[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) JRg[i] = pi.JRg[i];
+  const double dbgd[3] = {dbg[0], dbg[1], dbg[2]};
+  m3_mv(JRg, dbgd, jd);
+  right_j<false>(jd, RJ);
+  m3_tr(eR, eRt);
+  m3_mul(invJr, eRt, A);
+  m3_mul(A, RJ, B);
+  m3_mul(B, JRg, Gb);  // -invJr * eR^T * Jr(JRg dbg) * JRg
+  double R12[9];
+  m3_mul(Rbw1, s2.Rwb, R12);
+  if (lane == 0) {
+    double* J = sh.Ji;
+#pragma unroll
+    for (int i = 0; i < 9 * 24; ++i) J[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        J[i * 24 + j] = -J0r[3 * i + j];
+        J[(3 + i) * 24 + j] = hv[3 * i + j];
+        J[(6 + i) * 24 + j] = hp[3 * i + j];
+        J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
+        J[(3 + i) * 24 + 6 + j] = -Rbw1[3 * i + j];
+        J[(6 + i) * 24 + 6 + j] = -Rbw1[3 * i + j] * dt;
+        J[i * 24 + 9 + j] = -Gb[3 * i + j];
+        J[(3 + i) * 24 + 9 + j] = -(double)pi.JVg[3 * i + j];
+        J[(6 + i) * 24 + 9 + j] = -(double)pi.JPg[3 * i + j];
+        J[(3 + i) * 24 + 12 + j] = -(double)pi.JVa[3 * i + j];
+        J[(6 + i) * 24 + 12 + j] = -(double)pi.JPa[3 * i + j];
+        J[i * 24 + 15 + j] = invJr[3 * i + j];
+        J[(6 + i) * 24 + 18 + j] = R12[3 * i + j];
+        J[(3 + i) * 24 + 21 + j] = Rbw1[3 * i + j];
+      }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) sh.ei[i] = e[i];
+  }
+  if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {  // EdgePriorPoseImu (g2o_types.cc:739-764)
+    double PRt[9], Q[9], epr[15], dt3[3], et[3];
+    m3_tr(pr->Rwb, PRt);
+    m3_mul(PRt, s1.Rwb, Q);
+    log_so3(Q, epr);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dt3[i] = s1.twb[i] - pr->twb[i];
+    m3_mv(PRt, dt3, et);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      epr[3 + i] = et[i];
+      epr[6 + i] = s1.v[i] - pr->vwb[i];
+      epr[9 + i] = s1.bg[i] - pr->bg[i];
+      epr[12 + i] = s1.ba[i] - pr->ba[i];
+    }
+    double ijr[9];
+    right_j<true>(epr, ijr);
+    // chi2 = e^T H e, lane-parallel over rows
+    double part = 0;
+    if (lane < 15) {
+      double t = 0;
+#pragma unroll
+      for (int q = 0; q < 15; ++q) t += pr->H[lane * 15 + q] * epr[q];
+      double el = 0;
+#pragma unroll
+      for (int q = 0; q < 15; ++q) el = lane == q ? epr[q] : el;
+      part = el * t;
+    }
+    const double chi2 = bcast(wave_sum63(part), 63);
+    if (lane == 0) {
+      double* J = sh.Jp;
+#pragma unroll
+      for (int i = 0; i < 225; ++i) J[i] = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          J[i * 15 + j] = ijr[3 * i + j];
+          J[(3 + i) * 15 + 3 + j] = Q[3 * i + j];
+        }
+#pragma unroll
+      for (int i = 6; i < 15; ++i) J[i * 15 + i] = 1.0;
+#pragma unroll
+      for (int i = 0; i < 15; ++i) sh.epr[i] = epr[i];
+      sh.wp = prior_kernel ? huber_w(chi2, 5.0) : 1.0;
+    }
+  }
+}
+
+// Solver index -> EdgeInertial column (-1: not on the edge) and prior column.
+template <int MODE>
+__device__ __forceinline__ int ei_col(int s) {
+  if (s < 6) return 15 + s;      // VP
+  if (s < 9) return 21 + s - 6;  // VV
+  if (s < 15) return -1;         // VG, VA
+  return MODE == ORBGPU_INERTIAL_LAST_FRAME ? s - 15 : -1;  // VPk VVk VGk VAk
+}
+
+// The n x n system from the edge pieces: thread-owned entries.
+template <int MODE>
+__device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu_imu_prior* pr,
+                         int t) {
+  constexpr int n = MODE == ORBGPU_INERTIAL_LAST_FRAME ? 30 : 15;
+  // pass 1: Omega * J and -Omega * e
+  for (int k = t; k < 9 * 24 + 9; k += kInThreads) {
+    if (k < 9 * 24) {
+      const int r = k / 24, c = k % 24;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      sh.OJ[k] = s;
+    } else {
+      const int r = k - 9 * 24;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.ei[q];
+      sh.Oe[r] = -s;
+    }
+  }
+  if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
+    for (int k = t; k < 225 + 15; k += kInThreads) {
+      const double w = sh.wp;
+      if (k < 225) {
+        const int r = k / 15, c = k % 15;
+        double s = 0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) s += (w * pr->H[r * 15 + q]) * sh.Jp[q * 15 + c];
+        sh.OJp[k] = s;
+      } else {
+        const int r = k - 225;
+        double s = 0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) s += pr->H[r * 15 + q] * sh.epr[q];
+        sh.Oep[r] = -s * w;
+      }
+    }
+  }
+  __syncthreads();
+  // pass 2: entry (i, j) = visual + EdgeInertial + random walks + prior
+  for (int k = t; k < n * n + n; k += kInThreads) {
+    const bool isb = k >= n * n;
+    const int i = isb ? k - n * n : k / n, j = isb ? 0 : k % n;
+    double s = 0;
+    if (!isb) {
+      if (i < 6 && j < 6) s += sh.vis[i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i];
+      const int ci = ei_col<MODE>(i), cj = ei_col<MODE>(j);
+      if (ci >= 0 && cj >= 0) {
+        double h = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) h += sh.Ji[r * 24 + ci] * sh.OJ[r * 24 + cj];
+        s += h;
+      }
+      // random walks: VG (9..11) <-> VGk (24..26), VA (12..14) <-> VAk (27..29)
+      const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
+      const int rj = (j >= 9 && j < 15) ? j - 9 : (j >= 24 ? j - 24 : -1);
+      if (ri >= 0 && rj >= 0 && ri / 3 == rj / 3) {
+        const double* Om = ri < 3 ? pi.info_g : pi.info_a;
+        const double sg = ((i < 15) == (j < 15)) ? 1.0 : -1.0;
+        s += sg * Om[(ri % 3) * 3 + rj % 3];
+      }
+      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15 && j >= 15) {
+        double h = 0;
+#pragma unroll
+        for (int r = 0; r < 15; ++r) h += sh.Jp[r * 15 + i - 15] * sh.OJp[r * 15 + j - 15];
+        s += h;
+      }
+      sh.H[i * kLd + j] = s;
+    } else {
+      if (i < 6) s += sh.vis[21 + i];
+      const int ci = ei_col<MODE>(i);
+      if (ci >= 0) {
+        double h = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) h += sh.Ji[r * 24 + ci] * sh.Oe[r];
+        s += h;
+      }
+      const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
+      if (ri >= 0) {  // b = -J^T Omega e with J = -I (previous) / +I (current), e = x2 - x1
+        const double* Om = ri < 3 ? pi.info_g : pi.info_a;
+        const double* x2 = ri < 3 ? sh.cur.bg : sh.cur.ba;
+        const double* x1 = ri < 3 ? sh.prev.bg : sh.prev.ba;
+        const int rr = ri % 3;
+        double oe = 0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) oe += Om[rr * 3 + q] * (x2[q] - x1[q]);
+        s += i < 15 ? -oe : oe;
+      }
+      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15) {
+        double h = 0;
+#pragma unroll
+        for (int r = 0; r < 15; ++r) h += sh.Jp[r * 15 + i - 15] * sh.Oep[r];
+        s += h;
+      }
+      sh.b[i] = s;
+    }
+  }
+}
+
+// Eigen LDLT (diagonal pivoting on the not-yet-updated diagonal, lower
+// triangle) of sh.H and the solve into sh.x when positive: wave 0, lane i
+// owns row i.  Returns isPositive().
+template <int n>
+__device__ bool ldlt_wave(InShared& sh, int lane) {
+  double* A = sh.H;
+  bool neg = false;
+  for (int k = 0; k < n; ++k) {
+    // pivot: first index of the largest |diagonal| in [k, n)
+    double v = (lane >= k && lane < n) ? fabs(A[lane * kLd + lane]) : -1.0;
+    int idx = lane;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double ov = __shfl_xor(v, o, 64);
+      const int oi = __shfl_xor(idx, o, 64);
+      if (ov > v || (ov == v && oi < idx)) {
+        v = ov;
+        idx = oi;
+      }
+    }
+    const int p = __builtin_amdgcn_readfirstlane(idx);
+    if (lane == 0) sh.perm[k] = p;
+    if (p != k) {  // symmetric transposition, lower triangle only
+      const int l = lane;
+      if (l < k) {
+        const double s = A[k * kLd + l];
+        A[k * kLd + l] = A[p * kLd + l];
+        A[p * kLd + l] = s;
+      }
+      if (l > p && l < n) {
+        const double s = A[l * kLd + k];
+        A[l * kLd + k] = A[l * kLd + p];
+        A[l * kLd + p] = s;
+      }
+      if (l == 0) {
+        const double s = A[k * kLd + k];
+        A[k * kLd + k] = A[p * kLd + p];
+        A[p * kLd + p] = s;
+      }
+      if (l > k && l < p) {
+        const double s = A[l * kLd + k];
+        A[l * kLd + k] = A[p * kLd + l];
+        A[p * kLd + l] = s;
+      }
+      wave_sync();
+    }
+    if (k > 0) {
+      if (lane < k) sh.temp[lane] = A[lane * kLd + lane] * A[k * kLd + lane];
+      wave_sync();
+      if (lane >= k && lane < n) {
+        double s0 = 0, s1 = 0;
+        int j = 0;
+        for (; j + 1 < k; j += 2) {
+          s0 += A[lane * kLd + j] * sh.temp[j];
+          s1 += A[lane * kLd + j + 1] * sh.temp[j + 1];
+        }
+        if (j < k) s0 += A[lane * kLd + j] * sh.temp[j];
+        A[lane * kLd + k] -= s0 + s1;
+      }
+      wave_sync();
+    }
+    const double akk = A[k * kLd + k];
+    if (lane > k && lane < n && fabs(akk) > 0) A[lane * kLd + k] /= akk;
+    if (akk < 0) neg = true;
+    wave_sync();
+  }
+  if (neg) return false;
+  // solve: permute b, L y = b, D, L^T x = y, permute back; lane i holds x[i]
+  double x = lane < n ? sh.b[lane] : 0.0;
+  for (int k = 0; k < n; ++k) {
+    const int p = sh.perm[k];
+    const double xk = bcast(x, k), xp = bcast(x, p);
+    if (lane == k) x = xp;
+    if (lane == p) x = xk;
+  }
+  for (int j = 0; j < n; ++j) {
+    const double xj = bcast(x, j);
+    if (lane > j && lane < n) x -= A[lane * kLd + j] * xj;
+  }
+  if (lane < n) {
+    const double d = A[lane * kLd + lane];
+    x = fabs(d) > 1.0 / 1.79769313486231570815e+308 ? x / d : 0.0;
+  }
+  for (int j = n - 1; j >= 0; --j) {
+    const double xj = bcast(x, j);
+    if (lane < j) x -= A[j * kLd + lane] * xj;
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    const int p = sh.perm[k];
+    const double xk = bcast(x, k), xp = bcast(x, p);
+    if (lane == k) x = xp;
+    if (lane == p) x = xk;
+  }
+  if (lane < n) sh.x[lane] = x;
+  return true;
+}
+
+// ImuCamPose::Update (g2o_types.cc:192-214); the NormalizeRotation there
+// discards its result.
+__device__ __forceinline__ void pose_update(StateD& s, const double* u, const CalibD& c, bool store) {
+  double R[9], E[9], Rn[9], d[3], ut[3] = {u[3], u[4], u[5]};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = s.Rwb[i];
+  m3_mv(R, ut, d);
+  exp_so3(u, E);
+  m3_mul(R, E, Rn);
+  double t[3] = {s.twb[0] + d[0], s.twb[1] + d[1], s.twb[2] + d[2]};
+  double Rbw[9], tbw[3], Rcw[9], tcw[3];
+  m3_tr(Rn, Rbw);
+  m3_mv(Rbw, t, tbw);
+  tbw[0] = -tbw[0];
+  tbw[1] = -tbw[1];
+  tbw[2] = -tbw[2];
+  m3_mul(c.Rcb, Rbw, Rcw);
+  m3_mv(c.Rcb, tbw, tcw);
+  if (store) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      s.Rwb[i] = Rn[i];
+      s.Rcw[i] = Rcw[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      s.twb[i] = t[i];
+      s.tcw[i] = tcw[i] + c.tcb[i];
+    }
+  }
+}
+
+__device__ __forceinline__ void load_state(StateD& s, const orbgpu_imu_state& g) {
+  for (int i = 0; i < 9; ++i) {
+    s.Rwb[i] = g.Rwb[i];
+    s.Rcw[i] = g.Rcw[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    s.twb[i] = g.twb[i];
+    s.tcw[i] = g.tcw[i];
+    s.v[i] = g.v[i];
+    s.bg[i] = g.bg[i];
+    s.ba[i] = g.ba[i];
+  }
+}
+
+// Visual sweep over the active edges (waves 1..), reduced into sh.vis; wave 0
+// meanwhile runs `imu` (its own work).  kind 0: Gauss-Newton system (Huber
+// weights where robust); kind 1: unweighted J^T Omega J of the inlier edges
+// (GetHessian) at the current pose.
+template <typename Imu>
+__device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, const VisObs* gobs,
+                          const uint8_t* glv, int cap, int n, bool robust, int kind, int t,
+                          Imu&& imu) {
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0;
+  const int wave = t >> 6, lane = t & 63;
+  if (wave == 0) {
+    imu();
+  } else {
+    const int tv = t - 64;
+    for (int i = tv; i < n; i += kVisThreads) {
+      const bool in_lds = i < cap;
+      const uint8_t l = in_lds ? lv[i] : glv[i];
+      if (l) continue;
+      const VisObs o = in_lds ? ob[i] : gobs[i];
+      vis_accumulate(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, kind == 0 && robust, 1.0, acc);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = wave_sum63(acc[k]);
+  if (lane == 63)
+#pragma unroll
+    for (int k = 0; k < 27; ++k) sh.red[wave * 27 + k] = acc[k];
+  __syncthreads();
+  if (t < 27) {
+    double s = 0;
+#pragma unroll
+    for (int w = 1; w < kInWaves; ++w) s += sh.red[w * 27 + t];
+    sh.vis[t] = s;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kInThreads) void k_pose_inertial(
+    CalibD cal, const orbgpu_imu_state* __restrict__ g_cur, const orbgpu_imu_state* __restrict__ g_prev,
+    const orbgpu_imu_preint* __restrict__ g_preint, const orbgpu_imu_prior* __restrict__ g_prior,
+    const VisObs* __restrict__ g_obs, const int* __restrict__ g_nobs, int obs_stride, int rec_init,
+    orbgpu_inertial_result* __restrict__ g_res, uint8_t* __restrict__ g_out, int lds_obs) {
+  constexpr int n = MODE == ORBGPU_INERTIAL_LAST_FRAME ? 30 : 15;
+  __shared__ InShared sh;
+  extern __shared__ __attribute__((aligned(16))) uint8_t in_lds[];
+  const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nobs = max(0, min(g_nobs[p], obs_stride));
+  const VisObs* gobs = g_obs + (size_t)p * obs_stride;
+  uint8_t* glv = g_out + (size_t)p * obs_stride;
+  const orbgpu_imu_preint& pi = g_preint[p];
+  const orbgpu_imu_prior* pr = MODE == ORBGPU_INERTIAL_LAST_FRAME ? g_prior + p : nullptr;
+  const double dt = (double)pi.dT;
+  const int cap = min(nobs, lds_obs);
+  VisObs* ob = reinterpret_cast<VisObs*>(in_lds);
+  uint8_t* lv = in_lds + (size_t)lds_obs * sizeof(VisObs);
+  for (int i = t; i < cap; i += kInThreads) {
+    ob[i] = gobs[i];
+    lv[i] = 0;
+  }
+  for (int i = cap + t; i < nobs; i += kInThreads) glv[i] = 0;
+  if (t == 0) {
+    sh.cal = cal;
+    load_state(sh.cur, g_cur[p]);
+    load_state(sh.prev, g_prev[p]);
+  }
+  if (t < 30) sh.x[t] = 0;
+  __syncthreads();
+
+  const float chi2MonoLF[4] = {5.991f, 5.991f, 5.991f, 5.991f};
+  const float chi2MonoKF[4] = {12.f, 7.5f, 5.991f, 5.991f};
+  const float chi2Stereo[4] = {15.6f, 9.8f, 7.815f, 7.815f};
+  const int n_edges = nobs + (MODE == ORBGPU_INERTIAL_LAST_FRAME ? 4 : 3);
+  bool robust = true;
+  int nBad = 0, nInl = 0;
+  for (int it = 0; it < 4; ++it) {
+    for (int iter = 0; iter < 10; ++iter) {
+      // computeActiveErrors + buildSystem
+      vis_sweep(sh, ob, lv, gobs, glv, cap, nobs, robust, 0, t,
+                [&] { imu_edges<MODE>(sh, pi, pr, dt, true, lane); });
+      __syncthreads();
+      assemble<MODE>(sh, pi, pr, t);
+      __syncthreads();
+      if (wave == 0) {
+        const bool ok = ldlt_wave<n>(sh, lane);
+        // g2o applies x even when the solve failed (x then keeps its last value)
+        double xv[30];
+#pragma unroll
+        for (int i = 0; i < 30; ++i) xv[i] = sh.x[i];
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) sh.ev_Rcw[i] = sh.cur.Rcw[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) sh.ev_tcw[i] = sh.cur.tcw[i];
+          sh.ok = ok;
+        }
+        pose_update(sh.cur, xv, sh.cal, lane == 0);
+        if (MODE == ORBGPU_INERTIAL_LAST_FRAME) pose_update(sh.prev, xv + 15, sh.cal, lane == 0);
+        if (lane < 3) {
+          sh.cur.v[lane] += xv[6 + lane];
+          sh.cur.bg[lane] += xv[9 + lane];
+          sh.cur.ba[lane] += xv[12 + lane];
+          if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
+            sh.prev.v[lane] += xv[21 + lane];
+            sh.prev.bg[lane] += xv[24 + lane];
+            sh.prev.ba[lane] += xv[27 + lane];
+          }
+        }
+      }
+      __syncthreads();
+      if (!sh.ok) break;
+    }
+    // classification (optimizer.cc:5002-5057 / 4620-4673)
+    const float cm = MODE == ORBGPU_INERTIAL_LAST_FRAME ? chi2MonoLF[it] : chi2MonoKF[it];
+    const float cclose = 1.5 * cm;
+    int bad = 0, good = 0;
+    for (int i = t; i < nobs; i += kInThreads) {
+      const bool in_lds = i < cap;
+      const VisObs o = in_lds ? ob[i] : gobs[i];
+      const uint8_t l = in_lds ? lv[i] : glv[i];
+      double e[3], Xc[3], Xn[3];
+      vis_error(o, l ? sh.cur.Rcw : sh.ev_Rcw, l ? sh.cur.tcw : sh.ev_tcw, sh.cal, e, Xc);
+      const bool st = o.ur >= 0.f;
+      const float chi2 = (float)vis_chi2(e, (double)o.inv_sigma2, st);
+      bool out;
+      if (!st) {
+        const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
+        m3_mv(sh.cur.Rcw, X, Xn);
+        const bool pos = Xn[2] + sh.cur.tcw[2] > 0.0;
+        out = (chi2 > cm && !o.close) || (o.close && chi2 > cclose) || !pos;
+      } else {
+        out = chi2 > chi2Stereo[it];
+      }
+      if (in_lds)
+        lv[i] = out;
+      else
+        glv[i] = out;
+      bad += out;
+      good += !out;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      bad += __shfl_xor(bad, o, 64);
+      good += __shfl_xor(good, o, 64);
+    }
+    if (lane == 0) {
+      sh.ired[wave * 2] = bad;
+      sh.ired[wave * 2 + 1] = good;
+    }
+    __syncthreads();
+    nBad = nInl = 0;
+#pragma unroll
+    for (int w = 0; w < kInWaves; ++w) {
+      nBad += sh.ired[w * 2];
+      nInl += sh.ired[w * 2 + 1];
+    }
+    __syncthreads();
+    if (it == 2) robust = false;
+    if (n_edges < 10) break;
+  }
+  if (nInl < 30 && !rec_init) {  // recover not too bad points
+    int bad = 0;
+    for (int i = t; i < nobs; i += kInThreads) {
+      const bool in_lds = i < cap;
+      const VisObs o = in_lds ? ob[i] : gobs[i];
+      double e[3], Xc[3];
+      vis_error(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, e, Xc);
+      const bool st = o.ur >= 0.f;
+      const float chi2 = (float)vis_chi2(e, (double)o.inv_sigma2, st);
+      if (chi2 < (st ? 24.f : 18.f)) {
+        if (in_lds)
+          lv[i] = 0;
+        else
+          glv[i] = 0;
+      } else {
+        ++bad;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+    if (lane == 0) sh.ired[wave * 2] = bad;
+    __syncthreads();
+    nBad = 0;
+#pragma unroll
+    for (int w = 0; w < kInWaves; ++w) nBad += sh.ired[w * 2];
+    __syncthreads();
+  }
+
+  // ---- the Hessian for the new ConstraintPoseImu ------------------------------
+  // visual inliers' J^T Omega J (waves 1..) while wave 0 linearises the IMU edges
+  vis_sweep(sh, ob, lv, gobs, glv, cap, nobs, false, 1, t,
+            [&] { imu_edges<MODE>(sh, pi, pr, dt, false, lane); });
+  __syncthreads();
+  orbgpu_inertial_result* res = g_res + p;
+  if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
+    // H (30 x 30, EdgeInertial order: previous 0..14, current 15..29)
+    for (int k = t; k < 9 * 24; k += kInThreads) {
+      const int r = k / 24, c = k % 24;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      sh.OJ[k] = s;
+    }
+    for (int k = t; k < 225; k += kInThreads) {
+      const int r = k / 15, c = k % 15;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 15; ++q) s += pr->H[r * 15 + q] * sh.Jp[q * 15 + c];
+      sh.OJp[k] = s;
+    }
+    __syncthreads();
+    for (int k = t; k < 900; k += kInThreads) {
+      const int i = k / 30, j = k % 30;
+      double s = 0;
+      if (i < 24 && j < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) s += sh.Ji[r * 24 + i] * sh.OJ[r * 24 + j];
+      }
+      // gyro RW on 9..11 / 24..26, acc RW on 12..14 / 27..29
+      const int gi = (i >= 9 && i < 12) ? i - 9 : (i >= 24 && i < 27 ? i - 24 : -1);
+      const int gj = (j >= 9 && j < 12) ? j - 9 : (j >= 24 && j < 27 ? j - 24 : -1);
+      if (gi >= 0 && gj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * pi.info_g[gi * 3 + gj];
+      const int ai = (i >= 12 && i < 15) ? i - 12 : (i >= 27 ? i - 27 : -1);
+      const int aj = (j >= 12 && j < 15) ? j - 12 : (j >= 27 ? j - 27 : -1);
+      if (ai >= 0 && aj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * pi.info_a[ai * 3 + aj];
+      if (i < 15 && j < 15) {
+#pragma unroll
+        for (int r = 0; r < 15; ++r) s += sh.Jp[r * 15 + i] * sh.OJp[r * 15 + j];
+      }
+      if (i >= 15 && i < 21 && j >= 15 && j < 21) {
+        const int a = i - 15, c = j - 15;
+        s += sh.vis[a >= c ? a * (a + 1) / 2 + c : c * (c + 1) / 2 + a];
+      }
+      sh.HM[i * kLd + j] = s;
+    }
+    __syncthreads();
+    // Marginalize(H, 0, 14): pinv of the previous-frame block (wave 0,
+    // parallel cyclic Jacobi on a 16 x 16 padding), then the Schur complement
+    if (wave == 0) {
+      double* A = sh.H;   // 16 x 16 working copy (stride kLd)
+      double* V = sh.V;   // 16 x 16 eigenvectors (stride 16)
+      for (int k = lane; k < 256; k += 64) {
+        const int i = k >> 4, j = k & 15;
+        A[i * kLd + j] = (i < 15 && j < 15) ? sh.HM[i * kLd + j] : 0.0;
+        V[k] = i == j ? 1.0 : 0.0;
+      }
+      wave_sync();
+      for (int sweep = 0; sweep < 30; ++sweep) {
+        double off = 0, dg = 0;
+        for (int k = lane; k < 256; k += 64) {
+          const int i = k >> 4, j = k & 15;
+          const double a = A[i * kLd + j];
+          if (i == j) dg += a * a;
+          if (i < j) off += a * a;
+        }
+        off = bcast(wave_sum63(off), 63);
+        dg = bcast(wave_sum63(dg), 63);
+        if (off <= 1e-32 * dg) break;
+        for (int r = 0; r < 15; ++r) {
+          // round-robin pairing of 16 indices: (15, r) and ((r+k)%15, (r-k+15)%15)
+          double* cs = sh.temp;  // c[8], s[8]
+          if (lane < 8) {
+            int pp = lane == 0 ? r : (r + lane) % 15;
+            int qq = lane == 0 ? 15 : (r - lane + 15) % 15;
+            const double apq = A[pp * kLd + qq];
+            double c = 1.0, s = 0.0;
+            if (apq != 0.0) {
+              const double th = (A[qq * kLd + qq] - A[pp * kLd + pp]) / (2 * apq);
+              const double tt = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+              c = 1 / sqrt(tt * tt + 1);
+              s = tt * c;
+            }
+            cs[lane] = c;
+            cs[8 + lane] = s;
+          }
+          wave_sync();
+          // partner / role of every index this round
+          auto pair_of = [&](int i, int& pidx, int& role, int& mate) {
+            if (i == 15 || i == r) {
+              pidx = 0;
+              role = i == r ? 0 : 1;
+              mate = i == r ? 15 : r;
+            } else {
+              const int k1 = (i - r + 15) % 15;  // i = (r + k1) % 15 -> role p of pair k1
+              if (k1 <= 7) {
+                pidx = k1;
+                role = 0;
+                mate = (r - k1 + 15) % 15;
+              } else {
+                pidx = 15 - k1;
+                role = 1;
+                mate = (r + 15 - k1) % 15;
+              }
+            }
+          };
+          // A' = G^T A G with G[p][p] = c, G[q][p] = -s, G[p][q] = s, G[q][q] = c
+          double nv[4], vv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int k = lane + 64 * u, i = k >> 4, j = k & 15;
+            int pi_, ri, mi, pj_, rj, mj;
+            pair_of(i, pi_, ri, mi);
+            pair_of(j, pj_, rj, mj);
+            const double ci = cs[pi_], si = cs[8 + pi_], cj = cs[pj_], sj = cs[8 + pj_];
+            // column i of G: G[i][i] = c, G[mate][i] = role p ? -s : s
+            const double gii = ci, gmi = ri == 0 ? -si : si;
+            const double gjj = cj, gmj = rj == 0 ? -sj : sj;
+            const double a_ij = A[i * kLd + j], a_im = A[i * kLd + mj];
+            const double a_mj = A[mi * kLd + j], a_mm = A[mi * kLd + mj];
+            nv[u] = gii * (a_ij * gjj + a_im * gmj) + gmi * (a_mj * gjj + a_mm * gmj);
+            vv[u] = V[i * 16 + j] * gjj + V[i * 16 + mj] * gmj;
+          }
+          wave_sync();
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int k = lane + 64 * u, i = k >> 4, j = k & 15;
+            A[i * kLd + j] = nv[u];
+            V[i * 16 + j] = vv[u];
+          }
+          wave_sync();
+        }
+      }
+      // pinv = sum over |lambda| > 1e-6 of v v^T / lambda
+      for (int k = lane; k < 225; k += 64) {
+        const int i = k / 15, j = k % 15;
+        double s = 0;
+        for (int m = 0; m < 15; ++m) {
+          const double l = A[m * kLd + m];
+          if (fabs(l) > 1e-6) s += V[i * 16 + m] * V[j * 16 + m] / l;
+        }
+        sh.pinv[i * 16 + j] = s;
+      }
+    }
+    __syncthreads();
+    // T = Hcb pinv (into sh.H rows), then H15 = Hcc - T Hbc
+    for (int k = t; k < 225; k += kInThreads) {
+      const int i = k / 15, j = k % 15;
+      double s = 0;
+#pragma unroll
+      for (int m = 0; m < 15; ++m) s += sh.HM[(15 + i) * kLd + m] * sh.pinv[m * 16 + j];
+      sh.Jp[k] = s;
+    }
+    __syncthreads();
+    for (int k = t; k < 225; k += kInThreads) {
+      const int i = k / 15, j = k % 15;
+      double s = 0;
+#pragma unroll
+      for (int m = 0; m < 15; ++m) s += sh.Jp[i * 15 + m] * sh.HM[m * kLd + 15 + j];
+      res->H[k] = sh.HM[(15 + i) * kLd + 15 + j] - s;
+    }
+  } else {
+    // H (15 x 15): EdgeInertial::GetHessian2 (VP2, VV2), the random walks'
+    // GetHessian2, the visual inliers
+    for (int k = t; k < 9 * 24; k += kInThreads) {
+      const int r = k / 24, c = k % 24;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      sh.OJ[k] = s;
+    }
+    __syncthreads();
+    for (int k = t; k < 225; k += kInThreads) {
+      const int i = k / 15, j = k % 15;
+      double s = 0;
+      if (i < 9 && j < 9) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) s += sh.Ji[r * 24 + 15 + i] * sh.OJ[r * 24 + 15 + j];
+      }
+      if (i >= 9 && i < 12 && j >= 9 && j < 12) s += pi.info_g[(i - 9) * 3 + j - 9];
+      if (i >= 12 && j >= 12) s += pi.info_a[(i - 12) * 3 + j - 12];
+      if (i < 6 && j < 6) s += sh.vis[i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i];
+      res->H[k] = s;
+    }
+  }
+  for (int i = t; i < cap; i += kInThreads) glv[i] = lv[i];
+  if (t == 0) {
+    for (int i = 0; i < 9; ++i) {
+      res->Rwb[i] = (float)sh.cur.Rwb[i];
+      res->Rwb_d[i] = sh.cur.Rwb[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      res->twb[i] = (float)sh.cur.twb[i];
+      res->v[i] = (float)sh.cur.v[i];
+      res->bg[i] = (float)sh.cur.bg[i];
+      res->ba[i] = (float)sh.cur.ba[i];
+      res->twb_d[i] = sh.cur.twb[i];
+      res->v_d[i] = sh.cur.v[i];
+      res->bg_d[i] = sh.cur.bg[i];
+      res->ba_d[i] = sh.cur.ba[i];
+    }
+    res->n_good = nobs - nBad;
+    res->n_inliers = nInl;
+  }
+}
+
+hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_problems,
+                                const orbgpu_imu_state* d_cur, const orbgpu_imu_state* d_prev,
+                                const orbgpu_imu_preint* d_preint, const orbgpu_imu_prior* d_prior,
+                                const orbgpu_inertial_obs* d_obs, const int* d_nobs, int obs_stride,
+                                int rec_init, orbgpu_inertial_result* d_res, uint8_t* d_outlier,
+                                hipStream_t st) {
+  CalibD cd;
+  cd.fx = c.fx;
+  cd.fy = c.fy;
+  cd.cx = c.cx;
+  cd.cy = c.cy;
+  cd.bf = c.bf;
+  for (int i = 0; i < 9; ++i) {
+    cd.Rcb[i] = c.Rcb[i];
+    cd.Rbc[i] = c.Rbc[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    cd.tcb[i] = c.tcb[i];
+    cd.tbc[i] = c.tbc[i];
+  }
+  const int lds_obs = obs_stride < kInLdsObs ? obs_stride : kInLdsObs;
+  const size_t lds = ((size_t)lds_obs * (sizeof(VisObs) + 1) + 15) & ~(size_t)15;
+  const auto* obs = reinterpret_cast<const VisObs*>(d_obs);
+  static bool raised[2] = {false, false};  // > 64 KB of LDS needs the opt-in once
+  if (!raised[mode != ORBGPU_INERTIAL_LAST_FRAME]) {
+    const void* fn = mode == ORBGPU_INERTIAL_LAST_FRAME
+                         ? reinterpret_cast<const void*>(&k_pose_inertial<ORBGPU_INERTIAL_LAST_FRAME>)
+                         : reinterpret_cast<const void*>(&k_pose_inertial<ORBGPU_INERTIAL_LAST_KEYFRAME>);
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
+      return hipErrorInvalidValue;
+    raised[mode != ORBGPU_INERTIAL_LAST_FRAME] = true;
+  }
+  if (mode == ORBGPU_INERTIAL_LAST_FRAME)
+    hipLaunchKernelGGL(k_pose_inertial<ORBGPU_INERTIAL_LAST_FRAME>, dim3(n_problems),
+                       dim3(kInThreads), lds, st, cd, d_cur, d_prev, d_preint, d_prior, obs, d_nobs,
+                       obs_stride, rec_init, d_res, d_outlier, lds_obs);
+  else
+    hipLaunchKernelGGL(k_pose_inertial<ORBGPU_INERTIAL_LAST_KEYFRAME>, dim3(n_problems),
+                       dim3(kInThreads), lds, st, cd, d_cur, d_prev, d_preint, d_prior, obs, d_nobs,
+                       obs_stride, rec_init, d_res, d_outlier, lds_obs);
+  return hipGetLastError();
+}
+
+}  // namespace orbgpu
