@@ -6,13 +6,13 @@
 // next ConstraintPoseImu.  Reference: optimizer.cc:4394-5160, g2o_types.cc,
 // imu_types.cc:283-310 (see oracle/inertial_oracle.cc for the restatement).
 //
-// Roles inside the workgroup (5 waves):
-//   wave 0     the IMU edges -- EdgeInertial (LogSO3, right Jacobians, the
-//              bias-corrected preintegration in float), EdgeGyroRW/AccRW and
-//              EdgePriorPoseImu -- their errors and Jacobians into LDS, then
+// Roles inside the workgroup (6 waves):
+//   wave 0     EdgeInertial (LogSO3, right Jacobians, the bias-corrected
+//              preintegration in float): error and Jacobian into LDS; then
 //              the dense LDLT of the n x n system (n = 30 / 15) and the
-//              vertex updates;
-//   waves 1-4  the visual edges (EdgeMono/StereoOnlyPose): errors, Huber
+//              current frame's vertex updates;
+//   wave 1     EdgePriorPoseImu (LastFrame) and the previous frame's updates;
+//   waves 2-5  the visual edges (EdgeMono/StereoOnlyPose): errors, Huber
 //              weights, body-frame Jacobians, the 6x6 block + gradient,
 //              reduced by a fixed tree.
 // Between them every thread assembles the system, each owning whole entries
@@ -25,9 +25,37 @@
 
 namespace orbgpu {
 
-constexpr int kInWaves = 5;
+// Profiling build only (make stamps): per-phase s_memtime totals of thread 0
+// (wave 0 runs the serial IMU / solve work), flushed once per workgroup.
+#ifdef ORB_STAMPS
+__device__ unsigned long long g_in_stamps[64 * 16];
+#define ISTAMP_INIT                      \
+  unsigned long long ist_acc_[16] = {};  \
+  unsigned long long ist_prev_ = __builtin_amdgcn_s_memtime()
+#define ISTAMP(i)                                                 \
+  do {                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ist_acc_[i] += now_ - ist_prev_;                              \
+    ist_prev_ = now_;                                             \
+  } while (0)
+#define ISTAMP_END                                                                          \
+  do {                                                                                      \
+    if (threadIdx.x == 0)                                                                   \
+      for (int i_ = 0; i_ < 16; ++i_)                                                       \
+        if (ist_acc_[i_]) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + i_], ist_acc_[i_]); \
+  } while (0)
+#define ISTAMP_ADD_ITER (ist_acc_[8] += 1)
+#else
+#define ISTAMP_ADD_ITER (void)0
+#define ISTAMP_INIT (void)0
+#define ISTAMP(i) (void)0
+#define ISTAMP_END (void)0
+#endif
+
+constexpr int kInWaves = 6;
 constexpr int kInThreads = 64 * kInWaves;
-constexpr int kVisThreads = kInThreads - 64;
+constexpr int kVisWave0 = 2;  // waves 0, 1: IMU edges / solve; 2..: visual edges
+constexpr int kVisThreads = kInThreads - 64 * kVisWave0;
 constexpr int kInLdsObs = 2048;  // observations staged in LDS (the rest re-read)
 constexpr int kLd = 31;          // padded row stride of the n x n system
 
@@ -70,10 +98,13 @@ __device__ __forceinline__ void m3_hat(const double* w, double* W) {
   W[8] = 0;
 }
 
-// NormalizeRotation: orthogonal polar factor, 3 Newton steps X <- (X + X^-T)/2
+// NormalizeRotation: orthogonal polar factor by Newton steps X <- (X + X^-T)/2.
+// The inputs here are rotations up to float (preintegration) or double
+// (ExpSO3) rounding, where the iteration converges quadratically: two steps
+// reach double precision (the oracle takes three; same result to rounding).
 __device__ __forceinline__ void polar3(double* X) {
 #pragma unroll
-  for (int it = 0; it < 3; ++it) {
+  for (int it = 0; it < 2; ++it) {
     double C[9];
     C[0] = X[4] * X[8] - X[5] * X[7];
     C[1] = X[5] * X[6] - X[3] * X[8];
@@ -215,6 +246,7 @@ struct InShared {
   double Jp[15 * 15], epr[15];  // EdgePriorPoseImu
   double OJp[15 * 15], Oep[15];
   double wp;                    // prior Huber weight
+  double info[81], info_g[9], info_a[9], pH[225];  // edge informations (LDS copies)
   double vis[27];               // visual 6x6 (lower, 21) + gradient (6)
   double red[kInWaves * 27];
   double temp[32];
@@ -345,10 +377,9 @@ __device__ __forceinline__ void vis_accumulate(const VisObs& o, const double* Rc
   }
 }
 
-// ---- the IMU edges (wave 0, every lane the same values; lane 0 stores) ------
-template <int MODE>
-__device__ void imu_edges(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu_imu_prior* pr,
-                          double dt, bool prior_kernel, int lane) {
+// ---- the IMU edges (one wave each, every lane the same values; lane 0 stores)
+// EdgeInertial::computeError / linearizeOplus (g2o_types.cc:494-578)
+__device__ void inertial_edge(InShared& sh, const orbgpu_imu_preint& pi, double dt, int lane) {
   const StateD &s1 = sh.prev, &s2 = sh.cur;
   float bg[3], ba[3], dbg[3], dba[3];
 #pragma unroll
@@ -386,59 +417,87 @@ __device__ void imu_edges(InShared& sh, const orbgpu_imu_preint& pi, const orbgp
     e[3 + i] = rv[i] - dV[i];
     e[6 + i] = rp[i] - dP[i];
   }
-  // Jacobian blocks (g2o_types.cc:523-578)
-  double invJr[9], A[9], B[9], Rt2[9];
-  right_j<true>(er, invJr);
-  m3_tr(s2.Rwb, Rt2);
-  m3_mul(invJr, Rt2, A);
-  double J0r[9];
-  m3_mul(A, s1.Rwb, J0r);  // -invJr * Rwb2^T * Rwb1
-  double dp2[3];
+  // Jacobian blocks (g2o_types.cc:523-578); the constant ones (-I, -JVg,
+  // -JPg, -JVa, -JPa) and the zeros are in place from inertial_edge_const.
+  // Each block is stored as soon as it is formed (short live ranges).
+  double* J = sh.Ji;
+  auto put = [&](int r0, int c0, const double* m, double sc) {
+    if (lane == 0)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) dp2[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? 0.5 * g2 * dt * dt : 0.0);
-  double hv[9], hp[9], rp2[3];
-  m3_hat(rv, hv);
-  m3_mv(Rbw1, dp2, rp2);
-  m3_hat(rp2, hp);
-  double JRg[9], jd[3], RJ[9], eRt[9], Gb[9];
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-  for (int i = 0; i < 9; ++i) JRg[i] = pi.JRg[i];
-  const double dbgd[3] = {dbg[0], dbg[1], dbg[2]};
-  m3_mv(JRg, dbgd, jd);
-  right_j<false>(jd, RJ);
-  m3_tr(eR, eRt);
-  m3_mul(invJr, eRt, A);
-  m3_mul(A, RJ, B);
-  m3_mul(B, JRg, Gb);  // -invJr * eR^T * Jr(JRg dbg) * JRg
-  double R12[9];
-  m3_mul(Rbw1, s2.Rwb, R12);
-  if (lane == 0) {
-    double* J = sh.Ji;
-#pragma unroll
-    for (int i = 0; i < 9 * 24; ++i) J[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        J[i * 24 + j] = -J0r[3 * i + j];
-        J[(3 + i) * 24 + j] = hv[3 * i + j];
-        J[(6 + i) * 24 + j] = hp[3 * i + j];
-        J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
-        J[(3 + i) * 24 + 6 + j] = -Rbw1[3 * i + j];
-        J[(6 + i) * 24 + 6 + j] = -Rbw1[3 * i + j] * dt;
-        J[i * 24 + 9 + j] = -Gb[3 * i + j];
-        J[(3 + i) * 24 + 9 + j] = -(double)pi.JVg[3 * i + j];
-        J[(6 + i) * 24 + 9 + j] = -(double)pi.JPg[3 * i + j];
-        J[(3 + i) * 24 + 12 + j] = -(double)pi.JVa[3 * i + j];
-        J[(6 + i) * 24 + 12 + j] = -(double)pi.JPa[3 * i + j];
-        J[i * 24 + 15 + j] = invJr[3 * i + j];
-        J[(6 + i) * 24 + 18 + j] = R12[3 * i + j];
-        J[(3 + i) * 24 + 21 + j] = Rbw1[3 * i + j];
-      }
+        for (int j = 0; j < 3; ++j) J[(r0 + i) * 24 + c0 + j] = sc * m[3 * i + j];
+  };
+  if (lane == 0)
 #pragma unroll
     for (int i = 0; i < 9; ++i) sh.ei[i] = e[i];
+  put(3, 6, Rbw1, -1.0);
+  put(6, 6, Rbw1, -dt);
+  put(3, 21, Rbw1, 1.0);
+  {
+    double hv[9];
+    m3_hat(rv, hv);
+    put(3, 0, hv, 1.0);
   }
-  if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {  // EdgePriorPoseImu (g2o_types.cc:739-764)
+  {
+    double dp2[3], rp2[3], hp[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dp2[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? 0.5 * g2 * dt * dt : 0.0);
+    m3_mv(Rbw1, dp2, rp2);
+    m3_hat(rp2, hp);
+    put(6, 0, hp, 1.0);
+  }
+  {
+    double R12[9];
+    m3_mul(Rbw1, s2.Rwb, R12);
+    put(6, 18, R12, 1.0);
+  }
+  double invJr[9];
+  right_j<true>(er, invJr);
+  put(0, 15, invJr, 1.0);
+  {
+    double Rt2[9], A[9], J0r[9];
+    m3_tr(s2.Rwb, Rt2);
+    m3_mul(invJr, Rt2, A);
+    m3_mul(A, s1.Rwb, J0r);
+    put(0, 0, J0r, -1.0);  // -invJr * Rwb2^T * Rwb1
+  }
+  {
+    double JRg[9], jd[3], RJ[9], eRt[9], A[9], B[9], Gb[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) JRg[i] = pi.JRg[i];
+    const double dbgd[3] = {dbg[0], dbg[1], dbg[2]};
+    m3_mv(JRg, dbgd, jd);
+    right_j<false>(jd, RJ);
+    m3_tr(eR, eRt);
+    m3_mul(invJr, eRt, A);
+    m3_mul(A, RJ, B);
+    m3_mul(B, JRg, Gb);
+    put(0, 9, Gb, -1.0);  // -invJr * eR^T * Jr(JRg dbg) * JRg
+  }
+}
+
+// The parts of EdgeInertial's Jacobian that do not depend on the estimates
+// (and the zeros), written once per call.
+__device__ void inertial_edge_const(InShared& sh, const orbgpu_imu_preint& pi, int t) {
+  double* J = sh.Ji;
+  for (int k = t; k < 9 * 24; k += kInThreads) J[k] = 0;
+  __syncthreads();
+  if (t < 9) {
+    const int i = t / 3, j = t % 3;
+    J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
+    J[(3 + i) * 24 + 9 + j] = -(double)pi.JVg[3 * i + j];
+    J[(6 + i) * 24 + 9 + j] = -(double)pi.JPg[3 * i + j];
+    J[(3 + i) * 24 + 12 + j] = -(double)pi.JVa[3 * i + j];
+    J[(6 + i) * 24 + 12 + j] = -(double)pi.JPa[3 * i + j];
+  }
+}
+
+// EdgePriorPoseImu::computeError / linearizeOplus (g2o_types.cc:739-764) on
+// the previous frame's vertices, and its Huber weight (delta 5)
+__device__ void prior_edge(InShared& sh, const orbgpu_imu_prior* pr, bool prior_kernel, int lane) {
+  const StateD& s1 = sh.prev;
+  {
     double PRt[9], Q[9], epr[15], dt3[3], et[3];
     m3_tr(pr->Rwb, PRt);
     m3_mul(PRt, s1.Rwb, Q);
@@ -460,7 +519,7 @@ __device__ void imu_edges(InShared& sh, const orbgpu_imu_preint& pi, const orbgp
     if (lane < 15) {
       double t = 0;
 #pragma unroll
-      for (int q = 0; q < 15; ++q) t += pr->H[lane * 15 + q] * epr[q];
+      for (int q = 0; q < 15; ++q) t += sh.pH[lane * 15 + q] * epr[q];
       double el = 0;
 #pragma unroll
       for (int q = 0; q < 15; ++q) el = lane == q ? epr[q] : el;
@@ -507,13 +566,13 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
       const int r = k / 24, c = k % 24;
       double s = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.Ji[q * 24 + c];
       sh.OJ[k] = s;
     } else {
       const int r = k - 9 * 24;
       double s = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.ei[q];
+      for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.ei[q];
       sh.Oe[r] = -s;
     }
   }
@@ -524,22 +583,29 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
         const int r = k / 15, c = k % 15;
         double s = 0;
 #pragma unroll
-        for (int q = 0; q < 15; ++q) s += (w * pr->H[r * 15 + q]) * sh.Jp[q * 15 + c];
+        for (int q = 0; q < 15; ++q) s += (w * sh.pH[r * 15 + q]) * sh.Jp[q * 15 + c];
         sh.OJp[k] = s;
       } else {
         const int r = k - 225;
         double s = 0;
 #pragma unroll
-        for (int q = 0; q < 15; ++q) s += pr->H[r * 15 + q] * sh.epr[q];
+        for (int q = 0; q < 15; ++q) s += sh.pH[r * 15 + q] * sh.epr[q];
         sh.Oep[r] = -s * w;
       }
     }
   }
   __syncthreads();
   // pass 2: entry (i, j) = visual + EdgeInertial + random walks + prior
-  for (int k = t; k < n * n + n; k += kInThreads) {
-    const bool isb = k >= n * n;
-    const int i = isb ? k - n * n : k / n, j = isb ? 0 : k % n;
+  // the lower triangle (the LDLT reads no other entry) and b
+  constexpr int nl = n * (n + 1) / 2;
+  for (int k = t; k < nl + n; k += kInThreads) {
+    const bool isb = k >= nl;
+    int i = isb ? k - nl : (int)((sqrtf(8.f * k + 1.f) - 1.f) * 0.5f);
+    if (!isb) {  // exact integer triangular root
+      while (i * (i + 1) / 2 > k) --i;
+      while ((i + 1) * (i + 2) / 2 <= k) ++i;
+    }
+    const int j = isb ? 0 : k - i * (i + 1) / 2;
     double s = 0;
     if (!isb) {
       if (i < 6 && j < 6) s += sh.vis[i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i];
@@ -554,7 +620,7 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
       const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
       const int rj = (j >= 9 && j < 15) ? j - 9 : (j >= 24 ? j - 24 : -1);
       if (ri >= 0 && rj >= 0 && ri / 3 == rj / 3) {
-        const double* Om = ri < 3 ? pi.info_g : pi.info_a;
+        const double* Om = ri < 3 ? sh.info_g : sh.info_a;
         const double sg = ((i < 15) == (j < 15)) ? 1.0 : -1.0;
         s += sg * Om[(ri % 3) * 3 + rj % 3];
       }
@@ -576,7 +642,7 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
       }
       const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
       if (ri >= 0) {  // b = -J^T Omega e with J = -I (previous) / +I (current), e = x2 - x1
-        const double* Om = ri < 3 ? pi.info_g : pi.info_a;
+        const double* Om = ri < 3 ? sh.info_g : sh.info_a;
         const double* x2 = ri < 3 ? sh.cur.bg : sh.cur.ba;
         const double* x1 = ri < 3 ? sh.prev.bg : sh.prev.ba;
         const int rr = ri % 3;
@@ -596,100 +662,75 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
   }
 }
 
-// Eigen LDLT (diagonal pivoting on the not-yet-updated diagonal, lower
-// triangle) of sh.H and the solve into sh.x when positive: wave 0, lane i
-// owns row i.  Returns isPositive().
+// Eigen LDLT of sh.H (lower triangle, diagonal pivoting) and the solve into
+// sh.x when it is positive: wave 0, lane i owns row i in registers.  Eigen
+// pivots on the not-yet-updated diagonal (ldlt_inplace::unblocked: the
+// diagonal past k is untouched until its own step), i.e. on the original
+// diagonal: the pivot order is fixed up front (largest |H_ii| first, ties in
+// index order -- Eigen breaks ties by the current position, which only
+// changes rounding) and the permuted matrix is factorised right-looking:
+// step k broadcasts D_k and the column L_jk (v_readlane) and every lane
+// updates its row.  Returns isPositive().
 template <int n>
 __device__ bool ldlt_wave(InShared& sh, int lane) {
-  double* A = sh.H;
-  bool neg = false;
-  for (int k = 0; k < n; ++k) {
-    // pivot: first index of the largest |diagonal| in [k, n)
-    double v = (lane >= k && lane < n) ? fabs(A[lane * kLd + lane]) : -1.0;
-    int idx = lane;
+  const double dl = lane < n ? fabs(sh.H[lane * kLd + lane]) : -1.0;
+  if (lane < n) sh.temp[lane] = dl;
+  wave_sync();
+  int rank = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const double ov = __shfl_xor(v, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ov > v || (ov == v && oi < idx)) {
-        v = ov;
-        idx = oi;
-      }
-    }
-    const int p = __builtin_amdgcn_readfirstlane(idx);
-    if (lane == 0) sh.perm[k] = p;
-    if (p != k) {  // symmetric transposition, lower triangle only
-      const int l = lane;
-      if (l < k) {
-        const double s = A[k * kLd + l];
-        A[k * kLd + l] = A[p * kLd + l];
-        A[p * kLd + l] = s;
-      }
-      if (l > p && l < n) {
-        const double s = A[l * kLd + k];
-        A[l * kLd + k] = A[l * kLd + p];
-        A[l * kLd + p] = s;
-      }
-      if (l == 0) {
-        const double s = A[k * kLd + k];
-        A[k * kLd + k] = A[p * kLd + p];
-        A[p * kLd + p] = s;
-      }
-      if (l > k && l < p) {
-        const double s = A[l * kLd + k];
-        A[l * kLd + k] = A[p * kLd + l];
-        A[p * kLd + l] = s;
-      }
-      wave_sync();
-    }
-    if (k > 0) {
-      if (lane < k) sh.temp[lane] = A[lane * kLd + lane] * A[k * kLd + lane];
-      wave_sync();
-      if (lane >= k && lane < n) {
-        double s0 = 0, s1 = 0;
-        int j = 0;
-        for (; j + 1 < k; j += 2) {
-          s0 += A[lane * kLd + j] * sh.temp[j];
-          s1 += A[lane * kLd + j + 1] * sh.temp[j + 1];
-        }
-        if (j < k) s0 += A[lane * kLd + j] * sh.temp[j];
-        A[lane * kLd + k] -= s0 + s1;
-      }
-      wave_sync();
-    }
-    const double akk = A[k * kLd + k];
-    if (lane > k && lane < n && fabs(akk) > 0) A[lane * kLd + k] /= akk;
-    if (akk < 0) neg = true;
-    wave_sync();
+  for (int j = 0; j < n; ++j) {
+    const double dj = sh.temp[j];
+    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
+  }
+  if (lane < n) sh.perm[rank] = lane;
+  wave_sync();
+  const int pi = lane < n ? sh.perm[lane] : 0;
+  double a[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    const int pj = __builtin_amdgcn_readlane(pi, j);
+    a[j] = sh.H[max(pi, pj) * kLd + min(pi, pj)];
+  }
+  bool neg = false;
+  double dd = 1.0;
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    const double dk = bcast(a[k], k);
+    if (dk < 0) neg = true;
+    if (lane == k) dd = dk;
+    // 1/D_k: v_rcp_f64 + one Newton step (a rounding away from c / D_k); a
+    // zero pivot leaves the column undivided and adds nothing to the rest,
+    // as Eigen's left-looking update (temp = D_j A_kj) does
+    double r = __builtin_amdgcn_rcp(dk);
+    r = fma(r, fma(-dk, r, 1.0), r);
+    const bool nz = fabs(dk) > 0;
+    const double c = a[k];
+    const double lu = nz ? c * r : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < n; ++j) a[j] = fma(-c, bcast(lu, j), a[j]);
+    if (lane > k && nz) a[k] = lu;
   }
   if (neg) return false;
-  // solve: permute b, L y = b, D, L^T x = y, permute back; lane i holds x[i]
-  double x = lane < n ? sh.b[lane] : 0.0;
-  for (int k = 0; k < n; ++k) {
-    const int p = sh.perm[k];
-    const double xk = bcast(x, k), xp = bcast(x, p);
-    if (lane == k) x = xp;
-    if (lane == p) x = xk;
-  }
+  // solve P^T L D L^T P x = b
+  double y = lane < n ? sh.b[pi] : 0.0;
+#pragma unroll
   for (int j = 0; j < n; ++j) {
-    const double xj = bcast(x, j);
-    if (lane > j && lane < n) x -= A[lane * kLd + j] * xj;
+    const double yj = bcast(y, j);
+    y = lane > j ? fma(-a[j], yj, y) : y;
   }
-  if (lane < n) {
-    const double d = A[lane * kLd + lane];
-    x = fabs(d) > 1.0 / 1.79769313486231570815e+308 ? x / d : 0.0;
+  double z = fabs(dd) > 1.0 / 1.79769313486231570815e+308 ? y / dd : 0.0;
+  // L rows to LDS for the transposed solve (column i of L across lanes)
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    if (lane < n && j < lane) sh.H[lane * kLd + j] = a[j];
+  wave_sync();
+#pragma unroll
+  for (int j = n - 1; j > 0; --j) {
+    const double zj = bcast(z, j);
+    const double lji = lane < j ? sh.H[j * kLd + lane] : 0.0;
+    z = fma(-lji, zj, z);
   }
-  for (int j = n - 1; j >= 0; --j) {
-    const double xj = bcast(x, j);
-    if (lane < j) x -= A[j * kLd + lane] * xj;
-  }
-  for (int k = n - 1; k >= 0; --k) {
-    const int p = sh.perm[k];
-    const double xk = bcast(x, k), xp = bcast(x, p);
-    if (lane == k) x = xp;
-    if (lane == p) x = xk;
-  }
-  if (lane < n) sh.x[lane] = x;
+  if (lane < n) sh.x[pi] = z;
   return true;
 }
 
@@ -743,18 +784,23 @@ __device__ __forceinline__ void load_state(StateD& s, const orbgpu_imu_state& g)
 // meanwhile runs `imu` (its own work).  kind 0: Gauss-Newton system (Huber
 // weights where robust); kind 1: unweighted J^T Omega J of the inlier edges
 // (GetHessian) at the current pose.
-template <typename Imu>
+template <typename W0, typename W1>
 __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, const VisObs* gobs,
                           const uint8_t* glv, int cap, int n, bool robust, int kind, int t,
-                          Imu&& imu) {
+                          W0&& w0, W1&& w1) {
   double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0;
   const int wave = t >> 6, lane = t & 63;
+#ifdef ORB_STAMPS
+  const unsigned long long vt0 = __builtin_amdgcn_s_memtime();
+#endif
   if (wave == 0) {
-    imu();
+    w0();
+  } else if (wave == 1) {
+    w1();
   } else {
-    const int tv = t - 64;
+    const int tv = t - 64 * kVisWave0;
     for (int i = tv; i < n; i += kVisThreads) {
       const bool in_lds = i < cap;
       const uint8_t l = in_lds ? lv[i] : glv[i];
@@ -763,16 +809,28 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
       vis_accumulate(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, kind == 0 && robust, 1.0, acc);
     }
   }
+#ifdef ORB_STAMPS
+  const unsigned long long vt1 = __builtin_amdgcn_s_memtime();
+#endif
+  if (wave >= kVisWave0) {
 #pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = wave_sum63(acc[k]);
-  if (lane == 63)
+    for (int k = 0; k < 27; ++k) acc[k] = wave_sum63(acc[k]);
+    if (lane == 63)
 #pragma unroll
-    for (int k = 0; k < 27; ++k) sh.red[wave * 27 + k] = acc[k];
+      for (int k = 0; k < 27; ++k) sh.red[wave * 27 + k] = acc[k];
+  }
+#ifdef ORB_STAMPS
+  if (t == 64 * kVisWave0) {
+    const unsigned long long vt2 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + 10], vt1 - vt0);
+    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + 11], vt2 - vt1);
+  }
+#endif
   __syncthreads();
   if (t < 27) {
     double s = 0;
 #pragma unroll
-    for (int w = 1; w < kInWaves; ++w) s += sh.red[w * 27 + t];
+    for (int w = kVisWave0; w < kInWaves; ++w) s += sh.red[w * 27 + t];
     sh.vis[t] = s;
   }
 }
@@ -807,7 +865,20 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     load_state(sh.prev, g_prev[p]);
   }
   if (t < 30) sh.x[t] = 0;
+  for (int k = t; k < 81 + 18 + 225; k += kInThreads) {
+    if (k < 81)
+      sh.info[k] = pi.info[k];
+    else if (k < 90)
+      sh.info_g[k - 81] = pi.info_g[k - 81];
+    else if (k < 99)
+      sh.info_a[k - 90] = pi.info_a[k - 90];
+    else if (MODE == ORBGPU_INERTIAL_LAST_FRAME)
+      sh.pH[k - 99] = pr->H[k - 99];
+  }
   __syncthreads();
+  inertial_edge_const(sh, pi, t);
+  __syncthreads();
+  ISTAMP_INIT;
 
   const float chi2MonoLF[4] = {5.991f, 5.991f, 5.991f, 5.991f};
   const float chi2MonoKF[4] = {12.f, 7.5f, 5.991f, 5.991f};
@@ -818,17 +889,22 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
   for (int it = 0; it < 4; ++it) {
     for (int iter = 0; iter < 10; ++iter) {
       // computeActiveErrors + buildSystem
-      vis_sweep(sh, ob, lv, gobs, glv, cap, nobs, robust, 0, t,
-                [&] { imu_edges<MODE>(sh, pi, pr, dt, true, lane); });
+      vis_sweep(
+          sh, ob, lv, gobs, glv, cap, nobs, robust, 0, t,
+          [&] {
+            inertial_edge(sh, pi, dt, lane);
+            ISTAMP(6);
+          },
+          [&] {
+            if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, pr, true, lane);
+          });
       __syncthreads();
+      ISTAMP(0);
       assemble<MODE>(sh, pi, pr, t);
       __syncthreads();
+      ISTAMP(1);
       if (wave == 0) {
         const bool ok = ldlt_wave<n>(sh, lane);
-        // g2o applies x even when the solve failed (x then keeps its last value)
-        double xv[30];
-#pragma unroll
-        for (int i = 0; i < 30; ++i) xv[i] = sh.x[i];
         if (lane == 0) {
 #pragma unroll
           for (int i = 0; i < 9; ++i) sh.ev_Rcw[i] = sh.cur.Rcw[i];
@@ -836,20 +912,27 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
           for (int i = 0; i < 3; ++i) sh.ev_tcw[i] = sh.cur.tcw[i];
           sh.ok = ok;
         }
-        pose_update(sh.cur, xv, sh.cal, lane == 0);
-        if (MODE == ORBGPU_INERTIAL_LAST_FRAME) pose_update(sh.prev, xv + 15, sh.cal, lane == 0);
+      }
+      __syncthreads();
+      ISTAMP(2);
+      // g2o applies x even when the solve failed (x then keeps its last
+      // value); the current frame's vertices on wave 0, the previous on wave 1
+      if (wave == 0 || (MODE == ORBGPU_INERTIAL_LAST_FRAME && wave == 1)) {
+        StateD& st = wave == 0 ? sh.cur : sh.prev;
+        const int o = wave == 0 ? 0 : 15;
+        double xv[15];
+#pragma unroll
+        for (int i = 0; i < 15; ++i) xv[i] = sh.x[o + i];
+        pose_update(st, xv, sh.cal, lane == 0);
         if (lane < 3) {
-          sh.cur.v[lane] += xv[6 + lane];
-          sh.cur.bg[lane] += xv[9 + lane];
-          sh.cur.ba[lane] += xv[12 + lane];
-          if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
-            sh.prev.v[lane] += xv[21 + lane];
-            sh.prev.bg[lane] += xv[24 + lane];
-            sh.prev.ba[lane] += xv[27 + lane];
-          }
+          st.v[lane] += xv[6 + lane];
+          st.bg[lane] += xv[9 + lane];
+          st.ba[lane] += xv[12 + lane];
         }
       }
       __syncthreads();
+      ISTAMP(3);
+      ISTAMP_ADD_ITER;
       if (!sh.ok) break;
     }
     // classification (optimizer.cc:5002-5057 / 4620-4673)
@@ -897,6 +980,7 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     }
     __syncthreads();
     if (it == 2) robust = false;
+    ISTAMP(4);
     if (n_edges < 10) break;
   }
   if (nInl < 30 && !rec_init) {  // recover not too bad points
@@ -927,9 +1011,12 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
   }
 
   // ---- the Hessian for the new ConstraintPoseImu ------------------------------
-  // visual inliers' J^T Omega J (waves 1..) while wave 0 linearises the IMU edges
-  vis_sweep(sh, ob, lv, gobs, glv, cap, nobs, false, 1, t,
-            [&] { imu_edges<MODE>(sh, pi, pr, dt, false, lane); });
+  // visual inliers' J^T Omega J (waves 2..) while waves 0, 1 linearise the IMU edges
+  vis_sweep(
+      sh, ob, lv, gobs, glv, cap, nobs, false, 1, t, [&] { inertial_edge(sh, pi, dt, lane); },
+      [&] {
+        if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, pr, false, lane);
+      });
   __syncthreads();
   orbgpu_inertial_result* res = g_res + p;
   if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
@@ -938,14 +1025,14 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       const int r = k / 24, c = k % 24;
       double s = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.Ji[q * 24 + c];
       sh.OJ[k] = s;
     }
     for (int k = t; k < 225; k += kInThreads) {
       const int r = k / 15, c = k % 15;
       double s = 0;
 #pragma unroll
-      for (int q = 0; q < 15; ++q) s += pr->H[r * 15 + q] * sh.Jp[q * 15 + c];
+      for (int q = 0; q < 15; ++q) s += sh.pH[r * 15 + q] * sh.Jp[q * 15 + c];
       sh.OJp[k] = s;
     }
     __syncthreads();
@@ -959,10 +1046,10 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       // gyro RW on 9..11 / 24..26, acc RW on 12..14 / 27..29
       const int gi = (i >= 9 && i < 12) ? i - 9 : (i >= 24 && i < 27 ? i - 24 : -1);
       const int gj = (j >= 9 && j < 12) ? j - 9 : (j >= 24 && j < 27 ? j - 24 : -1);
-      if (gi >= 0 && gj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * pi.info_g[gi * 3 + gj];
+      if (gi >= 0 && gj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * sh.info_g[gi * 3 + gj];
       const int ai = (i >= 12 && i < 15) ? i - 12 : (i >= 27 ? i - 27 : -1);
       const int aj = (j >= 12 && j < 15) ? j - 12 : (j >= 27 ? j - 27 : -1);
-      if (ai >= 0 && aj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * pi.info_a[ai * 3 + aj];
+      if (ai >= 0 && aj >= 0) s += ((i < 15) == (j < 15) ? 1.0 : -1.0) * sh.info_a[ai * 3 + aj];
       if (i < 15 && j < 15) {
 #pragma unroll
         for (int r = 0; r < 15; ++r) s += sh.Jp[r * 15 + i] * sh.OJp[r * 15 + j];
@@ -1095,7 +1182,7 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       const int r = k / 24, c = k % 24;
       double s = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) s += pi.info[r * 9 + q] * sh.Ji[q * 24 + c];
+      for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.Ji[q * 24 + c];
       sh.OJ[k] = s;
     }
     __syncthreads();
@@ -1106,8 +1193,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
 #pragma unroll
         for (int r = 0; r < 9; ++r) s += sh.Ji[r * 24 + 15 + i] * sh.OJ[r * 24 + 15 + j];
       }
-      if (i >= 9 && i < 12 && j >= 9 && j < 12) s += pi.info_g[(i - 9) * 3 + j - 9];
-      if (i >= 12 && j >= 12) s += pi.info_a[(i - 12) * 3 + j - 12];
+      if (i >= 9 && i < 12 && j >= 9 && j < 12) s += sh.info_g[(i - 9) * 3 + j - 9];
+      if (i >= 12 && j >= 12) s += sh.info_a[(i - 12) * 3 + j - 12];
       if (i < 6 && j < 6) s += sh.vis[i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i];
       res->H[k] = s;
     }
@@ -1131,6 +1218,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     res->n_good = nobs - nBad;
     res->n_inliers = nInl;
   }
+  ISTAMP(5);
+  ISTAMP_END;
 }
 
 hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_problems,
@@ -1177,3 +1266,18 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
 }
 
 }  // namespace orbgpu
+
+#ifdef ORB_STAMPS
+extern "C" int orbgpu_debug_inertial_stamps(unsigned long long* out, int n) {
+  if (n > 16) n = 16;
+  static unsigned long long buf[64 * 16];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(orbgpu::g_in_stamps), sizeof(buf)) != hipSuccess) return -1;
+  for (int i = 0; i < n; ++i) {
+    out[i] = 0;
+    for (int c = 0; c < 64; ++c) out[i] += buf[c * 16 + i];
+  }
+  static const unsigned long long z[64 * 16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_in_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
