@@ -99,6 +99,8 @@ def main() -> int:
     ap.add_argument("--no-match", action="store_true",
                     help="skip the SearchByProjection (motion-model search) side line")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform side line")
+    ap.add_argument("--no-inertial", action="store_true",
+                    help="skip the PoseInertialOptimizationLastFrame side line")
     ap.add_argument("--no-track", action="store_true",
                     help="skip the device-resident tracking-chain side line")
     ap.add_argument("--no-latency", action="store_true",
@@ -304,6 +306,14 @@ def main() -> int:
         from bench_bow import measure as measure_bow  # noqa: E402
 
         result["bow"] = measure_bow(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+    if rank == 0 and world == 1 and not args.no_inertial:
+        # PoseInertialOptimizationLastFrame (stereo-inertial
+        # tracking after IMU initialisation), a batch resident in HBM
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_inertial import measure as measure_inertial  # noqa: E402
+
+        result["inertial"] = measure_inertial(problems=B, calls=20, mode=0,
+                                              cpu_problems=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_track:
         # config C3's path on synthetic data: extract + stereo + SearchByProjection
         # + PoseOptimization chained on the device, vs the oracle chain on the CPU

@@ -23,7 +23,7 @@ PMC_GROUPS=tools/pmc_groups_sq2.txt bash tools/pmc_run.sh > "$O/pmc_sq.log" 2>&1
 python3 tools/pmc_summary.py gpurun_out/pmc --json "$O/pmc_sq.json" > "$O/pmc_sq.txt"
 rm -rf gpurun_out/bench_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/bench_prof -o bench \
-  -- python3 bench.py --no-cpu-baseline --no-lba --no-stereo --no-match --no-bow --no-track --no-latency > "$O/bench_prof.log" 2>&1 || { echo "rocprof bench failed"; tail -5 "$O/bench_prof.log"; exit 1; }
+  -- python3 bench.py --no-cpu-baseline --no-lba --no-stereo --no-match --no-bow --no-inertial --no-track --no-latency > "$O/bench_prof.log" 2>&1 || { echo "rocprof bench failed"; tail -5 "$O/bench_prof.log"; exit 1; }
 f=$(find gpurun_out/bench_prof -name '*kernel_stats.csv' | head -n1)
 cp "$f" "$O/bench_kernel_stats.csv"
 python3 tools/kstats.py "$f" > "$O/bench_kernel_stats.txt"
