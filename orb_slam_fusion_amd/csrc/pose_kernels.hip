@@ -372,21 +372,11 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       int q = 0;
       bool accepted = false;
       do {
-        // every lane solves the (identical) 6x6 system: no broadcast barrier
-        double A[6][6], bb[6], x[6];
-        {
-          int hk = 1;
-#pragma unroll
-          for (int r = 0; r < 6; ++r) {
-#pragma unroll
-            for (int c2 = 0; c2 <= r; ++c2) A[r][c2] = A[c2][r] = hb[hk++];
-            bb[r] = hb[22 + r];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 6; ++j) A[j][j] += lambda;
+        // each wave solves the (identical) 6x6 system lane-parallel: no
+        // broadcast barrier
+        double x[6];
         PSTAMP(0);
-        const bool ok = ldlt6_solve(A, bb, x);
+        const bool ok = ldlt6_wave(hb, lambda, x);
         PSTAMP(2);
         const Se3 Tn = se3_compose(se3_exp(x), T);
         PSTAMP(3);

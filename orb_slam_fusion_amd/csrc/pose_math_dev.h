@@ -261,6 +261,78 @@ __device__ __forceinline__ bool ldlt6_solve(double (&A)[6][6], const double (&b)
   return !neg;
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+
+// The same LDLT solve of (H + lambda I) x = b for H = hb[1..21] (lower
+// triangle, row-major) and b = hb[22..27] (LDS), lane-parallel inside each
+// wave: lanes 0..5 own the rows of the pivot-permuted matrix.  Eigen pivots
+// on the not-yet-updated diagonal, i.e. the original one, so the order is
+// fixed up front (ties in index order; Eigen breaks them by position, which
+// only changes rounding) and the factorisation runs right-looking with D_k
+// and the column broadcast by v_readlane.  Every lane returns the full x and
+// isPositive(); the solve is carried out even when a pivot is negative, as
+// ldlt6_solve.
+__device__ __forceinline__ bool ldlt6_wave(const double* hb, double lambda, double (&x)[6]) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane < 6 ? lane : 0;
+  const double dl = lane < 6 ? fabs(hb[1 + li * (li + 1) / 2 + li] + lambda) : -1.0;
+  int rank = 0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double dj = readlane_f64(dl, j);
+    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
+  }
+  // perm[q] = original index at position q: lane q finds the index ranked q
+  int pi = 0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) pi = __builtin_amdgcn_readlane(rank, j) == lane ? j : pi;
+  double a[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int pj = __builtin_amdgcn_readlane(pi, j);
+    const int r = max(pi, pj), c = min(pi, pj);
+    a[j] = hb[1 + r * (r + 1) / 2 + c] + (r == c ? lambda : 0.0);
+  }
+  bool neg = false;
+  double dd = 1.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const double dk = readlane_f64(a[k], k);
+    if (dk < 0) neg = true;
+    if (lane == k) dd = dk;
+    const bool nz = fabs(dk) > 0;
+    const double c = a[k];
+    const double lu = nz ? c / dk : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j) a[j] = fma(-c, readlane_f64(lu, j), a[j]);
+    if (lane > k && nz) a[k] = lu;
+  }
+  double y = hb[22 + pi];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double yj = readlane_f64(y, j);
+    y = lane > j ? fma(-a[j], yj, y) : y;
+  }
+  double z = fabs(dd) > 1.0 / 1.79769313486231570815e+308 ? y / dd : 0.0;
+  // L^T solve: lane i needs L_ji, lane j's a[i]
+#pragma unroll
+  for (int j = 5; j > 0; --j) {
+    const double zj = readlane_f64(z, j);
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (i < j) {
+        const double lji = readlane_f64(a[i], j);
+        z = lane == i ? fma(-lji, zj, z) : z;
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, __builtin_amdgcn_readlane(rank, k));
+  return !neg;
+}
+
 __device__ __forceinline__ void huber_rho(double e2, double delta, double& rho0, double& rho1) {
   const double dsqr = delta * delta;
   if (e2 <= dsqr) {
