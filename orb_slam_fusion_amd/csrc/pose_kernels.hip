@@ -392,7 +392,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
         scale += 1e-3;
         rho /= scale;
         if (rho > 0 && isfinite(tmp)) {
-          double alpha = 1. - pow(2 * rho - 1, 3);
+          double alpha = 1. - cube(2 * rho - 1);
           alpha = fmin(alpha, 2. / 3.);
           lambda *= fmax(1. / 3., alpha);
           ni = 2;

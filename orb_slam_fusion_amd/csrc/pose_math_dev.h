@@ -64,6 +64,15 @@ __device__ __forceinline__ Se3 se3_compose(const Se3& a, const Se3& b) {
   return r;
 }
 
+// x^3 as std::pow(x, 3) returns it (correctly rounded but for double-double
+// ties): the compensated product x*x*x, five instructions instead of the
+// ocml pow routine.
+__device__ __forceinline__ double cube(double x) {
+  const double p = x * x, ep = fma(x, x, -p);
+  const double c = p * x, ec = fma(p, x, -c);
+  return c + fma(ep, x, ec);
+}
+
 // kUniform: every lane of the wave evaluates the same exp (PoseOptimization),
 // so the branches are made wave-uniform with readfirstlane; otherwise each
 // lane takes its own branch (LocalBundleAdjustment, one pose per lane).
@@ -87,7 +96,7 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
       for (int j = 0; j < 3; ++j) R[i][j] = V[i][j] = (i == j ? 1.0 : 0.0) + O[i][j] + O2[i][j];
   } else {
     const double s = sin(theta), c = cos(theta);
-    const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / pow(theta, 3);
+    const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / cube(theta);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
