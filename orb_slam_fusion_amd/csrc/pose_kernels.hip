@@ -15,6 +15,10 @@
 
 #include "pose_math_dev.h"
 
+// fp64 solver arithmetic, parity by tolerance (not bit-exact like the
+// extractor, whose TUs keep -ffp-contract=off): let products fuse into FMAs.
+#pragma clang fp contract(fast)
+
 namespace orbgpu {
 
 // Profiling build only (make stamps): per-phase s_memtime totals, one flush
