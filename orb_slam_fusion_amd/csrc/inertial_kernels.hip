@@ -6,13 +6,13 @@
 // next ConstraintPoseImu.  Reference: optimizer.cc:4394-5160, g2o_types.cc,
 // imu_types.cc:283-310 (see oracle/inertial_oracle.cc for the restatement).
 //
-// Roles inside the workgroup (6 waves):
+// Roles inside the workgroup (8 waves):
 //   wave 0     EdgeInertial (LogSO3, right Jacobians, the bias-corrected
 //              preintegration in float): error and Jacobian into LDS; then
 //              the dense LDLT of the n x n system (n = 30 / 15) and the
 //              current frame's vertex updates;
 //   wave 1     EdgePriorPoseImu (LastFrame) and the previous frame's updates;
-//   waves 2-5  the visual edges (EdgeMono/StereoOnlyPose): errors, Huber
+//   waves 2-7  the visual edges (EdgeMono/StereoOnlyPose): errors, Huber
 //              weights, body-frame Jacobians, the 6x6 block + gradient,
 //              reduced by a fixed tree.
 // Between them every thread assembles the system, each owning whole entries
@@ -56,7 +56,7 @@ __device__ unsigned long long g_in_stamps[64 * 16];
 #define ISTAMP_END (void)0
 #endif
 
-constexpr int kInWaves = 6;
+constexpr int kInWaves = 8;
 constexpr int kInThreads = 64 * kInWaves;
 constexpr int kVisWave0 = 2;  // waves 0, 1: IMU edges / solve; 2..: visual edges
 constexpr int kVisThreads = kInThreads - 64 * kVisWave0;
