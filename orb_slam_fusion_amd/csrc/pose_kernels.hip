@@ -174,6 +174,35 @@ __device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
+// Block-wide sums of NV doubles per thread into LDS (out[0..NV)), fixed tree:
+// DPP row sums (lane 15 of each 16-lane row), the 16 row partials of the
+// block in LDS, then thread k adds value k's partials in row order.  Only
+// LDS consumers need the result (the build sweep's system): no broadcast.
+template <int NV>
+__device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, double* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double x = v[k];
+    x += dpp_f64<0x111, 0xf>(x);
+    x += dpp_f64<0x112, 0xf>(x);
+    x += dpp_f64<0x114, 0xf>(x);
+    x += dpp_f64<0x118, 0xf>(x);
+    v[k] = x;
+  }
+  if ((lane & 15) == 15)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[(wave * 4 + (lane >> 4)) * NV + k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double a = 0;
+#pragma unroll
+    for (int r = 0; r < kPoseWaves * 4; ++r) a += red[r * NV + threadIdx.x];
+    out[threadIdx.x] = a;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ int block_sum_i(int v, int* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -186,7 +215,7 @@ __device__ __forceinline__ int block_sum_i(int v, int* red) {
 }
 
 struct PoseShared {
-  double red[kPoseWaves * 28];
+  double red[kPoseWaves * 4 * 28];
   double hb[28];  // chi2, H (lower, 21), b (6) at the current pose
   int ired[kPoseWaves];
 };
@@ -340,11 +369,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     }
     for (int i = cap + t; i < n; i += kPoseThreads)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
-    block_sum_d<28>(acc, sh.red);
-    if (t == 0)
-#pragma unroll
-      for (int k = 0; k < 28; ++k) sh.hb[k] = acc[k];
-    __syncthreads();
+    block_sum_to_lds<28>(acc, sh.red, sh.hb);
   };
 
   const double* hb = sh.hb;
