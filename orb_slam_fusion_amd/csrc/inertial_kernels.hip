@@ -252,7 +252,7 @@ struct InShared {
   double wp;                    // prior Huber weight
   double info[81], info_g[9], info_a[9], pH[225];  // edge informations (LDS copies)
   double vis[27];               // visual 6x6 (lower, 21) + gradient (6)
-  double red[kInWaves * 27];
+  double red[kInWaves * 4 * 27];
   double temp[32];
   double pinv[15 * 16];
   double V[256];                // Jacobi eigenvectors (16 x 16)
@@ -816,12 +816,19 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
 #ifdef ORB_STAMPS
   const unsigned long long vt1 = __builtin_amdgcn_s_memtime();
 #endif
-  if (wave >= kVisWave0) {
+  if (wave >= kVisWave0) {  // DPP row sums; lane 15 of each row writes its partial
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] = wave_sum63(acc[k]);
-    if (lane == 63)
+    for (int k = 0; k < 27; ++k) {
+      double x = acc[k];
+      x += dpp_d<0x111, 0xf>(x);
+      x += dpp_d<0x112, 0xf>(x);
+      x += dpp_d<0x114, 0xf>(x);
+      x += dpp_d<0x118, 0xf>(x);
+      acc[k] = x;
+    }
+    if ((lane & 15) == 15)
 #pragma unroll
-      for (int k = 0; k < 27; ++k) sh.red[wave * 27 + k] = acc[k];
+      for (int k = 0; k < 27; ++k) sh.red[(wave * 4 + (lane >> 4)) * 27 + k] = acc[k];
   }
 #ifdef ORB_STAMPS
   if (t == 64 * kVisWave0) {
@@ -834,7 +841,7 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
   if (t < 27) {
     double s = 0;
 #pragma unroll
-    for (int w = kVisWave0; w < kInWaves; ++w) s += sh.red[w * 27 + t];
+    for (int r = kVisWave0 * 4; r < kInWaves * 4; ++r) s += sh.red[r * 27 + t];
     sh.vis[t] = s;
   }
 }
