@@ -262,10 +262,12 @@ struct InShared {
   int ok;
 };
 
+// LDS exchange between the lanes of one wave: a wave's LDS instructions
+// execute in order, so it suffices that the compiler keeps program order
+// (memory clobber) and the writes have left the queue (lgkmcnt(0)).
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int CTRL, int ROW_MASK>
