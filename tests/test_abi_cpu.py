@@ -65,6 +65,12 @@ def test_invalid_params_rejected_before_device():
     assert so.orbgpu_extract(None, None, 0, 0, 0, None, None, None, 0, None, None) == \
         _lib.ORBGPU_ERR_INVALID
     assert so.orbgpu_pose_opt(None, None, None, None, 0, None, None, None) == _lib.ORBGPU_ERR_INVALID
+    # inertial entry points: null handle / bad mode / missing prior rejected before any device work
+    assert so.orbgpu_pose_inertial(None, 0, None, None, None, None, None, None, 0, 0, None,
+                                   None) == _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_pose_inertial_batch(None, 0, None, 1, None, None, None, None, None, None, 8,
+                                         0, None, None, None) == _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_inertial_ctx_create(0, 0, 16, ctypes.byref(h)) == _lib.ORBGPU_ERR_INVALID
 
 
 def test_keypoint_struct_is_cv_keypoint_layout():

@@ -119,3 +119,27 @@ def test_batch_matches_oracle(gpu_available, mode):
     for i, c in enumerate(cases):
         ref, ref_out = oracle.pose_inertial(c)
         _check(res[i], outs[i, :len(c["obs"])], ref, ref_out)
+
+
+def test_capacity_and_mode_checks(gpu_available):
+    """Errors come back as status codes: more observations than the context
+    holds (CAPACITY), an unknown mode or a missing prior (INVALID)."""
+    from orb_slam_fusion_amd import _lib
+
+    case = ic.make_case(30, mode=0, n_obs=50)
+    opt = PoseInertialOptimizer(max_obs=10)
+    res = np.zeros((), INERTIAL_RESULT_DTYPE)
+    out = np.zeros(50, np.uint8)
+    so = _lib.lib()
+    p = _lib.ptr
+    args = [p(case["calib"]), p(case["cur"]), p(case["prev"]), p(case["preint"])]
+    assert so.orbgpu_pose_inertial(opt._h, 0, *args, p(case["prior"]), p(case["obs"]), 50, 0,
+                                   p(res), p(out)) == _lib.ORBGPU_ERR_CAPACITY
+    assert so.orbgpu_pose_inertial(opt._h, 7, *args, p(case["prior"]), p(case["obs"]), 5, 0,
+                                   p(res), p(out)) == _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_pose_inertial(opt._h, 0, *args, None, p(case["obs"]), 5, 0, p(res),
+                                   p(out)) == _lib.ORBGPU_ERR_INVALID
+    # LastKeyFrame needs no prior
+    assert so.orbgpu_pose_inertial(opt._h, 1, *args, None, p(case["obs"]), 5, 0, p(res),
+                                   p(out)) == _lib.ORBGPU_OK
+    opt.close()
