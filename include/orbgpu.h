@@ -346,6 +346,11 @@ orbgpu_status orbgpu_matches_to_pose_obs_batch(
     int pt_stride, const float* inv_level_sigma2, int n_levels, orbgpu_pose_obs* d_obs,
     int obs_stride, int* d_nobs, int32_t* d_obs_index, void* hip_stream);
 
+/* The same gather for PoseInertialOptimizationLastFrame / LastKeyFrame
+ *   (optimizer.cc:4816-4900, 4466-4540): orbgpu_inertial_obs rows, with
+ *   close = d_close[point] (MapPoint::mTrackDepth < 10; NULL: 0) and the
+ *   pinhole Uncertainty2 = 1.  Declared with the inertial types below. */
+
 /* Replaces: bool Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit)
  *   (frame.cc:548-603, Nleft == -1) over Tracking::SearchLocalPoints' loop
  *   (tracking.cc:2644-2661): points flagged ORBGPU_MP_SKIP are not projected
@@ -532,6 +537,14 @@ orbgpu_status orbgpu_pose_inertial_batch(orbgpu_inertial_ctx* c, int mode,
                                          int obs_stride, int rec_init,
                                          orbgpu_inertial_result* d_res, uint8_t* d_outlier,
                                          void* hip_stream);
+
+/* orbgpu_matches_to_pose_obs_batch's inertial form (see the comment there). */
+orbgpu_status orbgpu_matches_to_inertial_obs_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_keypoint* d_kps, const float* d_uright,
+    const int32_t* d_match, const int* d_n, int kp_stride, const orbgpu_proj_point* d_pts,
+    const uint8_t* d_close, int pt_stride, const float* inv_level_sigma2, int n_levels,
+    orbgpu_inertial_obs* d_obs, int obs_stride, int* d_nobs, int32_t* d_obs_index,
+    void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -193,6 +193,9 @@ SIGNATURES = {
     "orbgpu_matches_to_pose_obs_batch": (
         _I, [_P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P],
     ),
+    "orbgpu_matches_to_inertial_obs_batch": (
+        _I, [_P, _I, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P],
+    ),
     "orbgpu_frustum": (
         _I, [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _I, _F, _P],
     ),

@@ -396,6 +396,38 @@ orbgpu_status orbgpu_matches_to_pose_obs_batch(
   return orbgpu::launch_pose_obs(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
 }
 
+orbgpu_status orbgpu_matches_to_inertial_obs_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_keypoint* d_kps, const float* d_uright,
+    const int32_t* d_match, const int* d_n, int kp_stride, const orbgpu_proj_point* d_pts,
+    const uint8_t* d_close, int pt_stride, const float* inv_level_sigma2, int n_levels,
+    orbgpu_inertial_obs* d_obs, int obs_stride, int* d_nobs, int32_t* d_obs_index,
+    void* hip_stream) {
+  if (!m || n_frames <= 0 || !d_kps || !d_match || !d_n || kp_stride <= 0 || !d_pts ||
+      pt_stride <= 0 || !inv_level_sigma2 || n_levels <= 0 || n_levels > ORBGPU_MAX_LEVELS ||
+      !d_obs || obs_stride <= 0 || !d_nobs)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu::ObsLaunch L{};
+  L.n_frames = n_frames;
+  L.kps = reinterpret_cast<const float*>(d_kps);
+  L.uright = d_uright;
+  L.match = d_match;
+  L.n = d_n;
+  L.kp_stride = kp_stride;
+  L.pts = d_pts;
+  L.pt_stride = pt_stride;
+  for (int l = 0; l < ORBGPU_MAX_LEVELS; ++l) L.inv_sigma2[l] = l < n_levels ? inv_level_sigma2[l] : 0.0f;
+  L.obs = nullptr;
+  L.iobs = d_obs;
+  L.close = d_close;
+  L.obs_stride = obs_stride;
+  L.nobs = d_nobs;
+  L.obs_index = d_obs_index;
+  L.err = m->d_err;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+  return orbgpu::launch_pose_obs(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
 orbgpu_status orbgpu_frustum(orbgpu_matcher* m, const orbgpu_frame_geom* geom,
                              const orbgpu_camera* cam, const float Rcw[9], const float tcw[3],
                              const float Ow[3], const orbgpu_map_point* pts, int n_pts,

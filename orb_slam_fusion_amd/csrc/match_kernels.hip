@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
   const int n = a.n[f];
   const size_t ko = (size_t)f * a.kp_stride;
   const float* kps = a.kps + ko * kKpFloats;
-  orbgpu_pose_obs* obs = a.obs + (size_t)f * a.obs_stride;
+  orbgpu_pose_obs* obs = a.obs ? a.obs + (size_t)f * a.obs_stride : nullptr;
   int32_t* index = a.obs_index ? a.obs_index + (size_t)f * a.obs_stride : nullptr;
   int base = 0;
   for (int i0 = 0; i0 < n; i0 += 256) {
@@ -608,12 +608,22 @@ __global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
       if (pos < a.obs_stride) {
         const orbgpu_proj_point& P = a.pts[(size_t)f * a.pt_stride + q];
         const float* k = kps + (size_t)i * kKpFloats;
-        orbgpu_pose_obs o;
-        o.Xw[0] = P.Xw[0], o.Xw[1] = P.Xw[1], o.Xw[2] = P.Xw[2];
-        o.u = k[0], o.v = k[1];
-        o.ur = a.uright ? a.uright[ko + i] : -1.0f;
-        o.inv_sigma2 = a.inv_sigma2[kp_octave(k)];
-        obs[pos] = o;
+        if (a.iobs) {  // EdgeMono/StereoOnlyPose rows (optimizer.cc:4816-4900, Uncertainty2 = 1)
+          orbgpu_inertial_obs o;
+          o.Xw[0] = P.Xw[0], o.Xw[1] = P.Xw[1], o.Xw[2] = P.Xw[2];
+          o.u = k[0], o.v = k[1];
+          o.ur = a.uright ? a.uright[ko + i] : -1.0f;
+          o.inv_sigma2 = a.inv_sigma2[kp_octave(k)];
+          o.close = a.close ? (int32_t)a.close[(size_t)f * a.pt_stride + q] : 0;
+          a.iobs[(size_t)f * a.obs_stride + pos] = o;
+        } else {
+          orbgpu_pose_obs o;
+          o.Xw[0] = P.Xw[0], o.Xw[1] = P.Xw[1], o.Xw[2] = P.Xw[2];
+          o.u = k[0], o.v = k[1];
+          o.ur = a.uright ? a.uright[ko + i] : -1.0f;
+          o.inv_sigma2 = a.inv_sigma2[kp_octave(k)];
+          obs[pos] = o;
+        }
         if (index) index[pos] = i;
       }
     }

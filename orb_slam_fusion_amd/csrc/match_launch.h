@@ -84,7 +84,9 @@ struct ObsLaunch {
   const orbgpu_proj_point* pts;
   int pt_stride;
   float inv_sigma2[ORBGPU_MAX_LEVELS];  // Frame::mvInvLevelSigma2
-  orbgpu_pose_obs* obs;   // [n_frames][obs_stride]
+  orbgpu_pose_obs* obs;   // [n_frames][obs_stride] (or, iobs set, unused)
+  orbgpu_inertial_obs* iobs;  // PoseInertialOptimization rows instead of obs
+  const uint8_t* close;       // per point (pt_stride rows), mTrackDepth < 10; may be null
   int obs_stride;
   int* nobs;
   int32_t* obs_index;     // may be null

@@ -136,6 +136,19 @@ class ORBmatcher:
                 pts.shape[1], ptr(isg), len(isg), ptr(obs), obs.shape[1], ptr(nobs),
                 ptr(obs_index), s), "orbgpu_matches_to_pose_obs_batch")
 
+    def matches_to_inertial_obs_batch(self, kps, uright, match, n, pts, close, inv_level_sigma2,
+                                      obs, nobs, obs_index=None, stream=None) -> None:
+        """The same list for PoseInertialOptimizationLastFrame / LastKeyFrame:
+        close uint8 [B, P] (MapPoint::mTrackDepth < 10) or None; obs uint8
+        [B, S, 32] (INERTIAL_OBS layout)."""
+        B, K = kps.shape[0], kps.shape[1]
+        isg = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_matches_to_inertial_obs_batch(
+                self._h, B, ptr(kps), ptr(uright), ptr(match), ptr(n), K, ptr(pts), ptr(close),
+                pts.shape[1], ptr(isg), len(isg), ptr(obs), obs.shape[1], ptr(nobs),
+                ptr(obs_index), s), "orbgpu_matches_to_inertial_obs_batch")
+
     # -- Frame::isInFrustum ---------------------------------------------------
     def is_in_frustum(self, F: MatchFrame, points: np.ndarray, viewingCosLimit: float,
                       views: Optional[np.ndarray] = None) -> np.ndarray:
