@@ -17,9 +17,17 @@ GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
 
 all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so oracle
 
-$(LIB)/liborbgpu.so: $(GPU_SRCS) $(GPU_HDRS)
+OBJDIR   := build/obj
+GPU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(GPU_SRCS))
+
+# one object per translation unit (parallel, incremental), then one link
+$(OBJDIR)/%.o: $(CSRC)/% $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/liborbgpu.so: $(GPU_OBJS)
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_SRCS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_OBJS)
 
 $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 	@mkdir -p $(LIB)
@@ -29,7 +37,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf $(LIB) oracle/_build
+	rm -rf $(LIB) oracle/_build build
 
 # profiling variant: per-phase s_memtime totals (orbgpu_debug_stamps)
 # STAMPS=1: k_fast_cells (+ pose kernel), STAMPS=2: k_octree

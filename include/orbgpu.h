@@ -307,6 +307,14 @@ orbgpu_status orbgpu_matcher_create(int device, int max_keypoints, int max_point
                                     orbgpu_matcher** out);
 void orbgpu_matcher_destroy(orbgpu_matcher* m);
 
+/* Sticky device error word of the context's *_batch calls (the host calls
+ * report it themselves): bit 0 = a frame with more keypoints than kp_stride or
+ * the kernels' bound (the frame was skipped), bit 1 = an observation list
+ * truncated at obs_stride, bit 2 = more query points than pt_stride (only the
+ * first pt_stride searched).  Synchronises the context's stream (and
+ * hip_stream when not NULL); reset != 0 clears the word.  *err = 0 when clean. */
+orbgpu_status orbgpu_matcher_status(orbgpu_matcher* m, void* hip_stream, int reset, int* err);
+
 /* Replaces: int ORBmatcher::SearchByProjection(Frame& CurrentFrame,
  *   const Frame& LastFrame, const float th, const bool bMono)
  *   (orb_matcher.h, orb_matcher.cc:1518-1728) with mbCheckOrientation =

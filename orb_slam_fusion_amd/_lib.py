@@ -180,6 +180,7 @@ SIGNATURES = {
     ),
     "orbgpu_matcher_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
     "orbgpu_matcher_destroy": (None, [_P]),
+    "orbgpu_matcher_status": (_I, [_P, _P, _I, ctypes.POINTER(_I)]),
     "orbgpu_search_by_projection_last": (
         _I,
         [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _F, _P, _P, _P, _P, _P, _P, _I, _P,

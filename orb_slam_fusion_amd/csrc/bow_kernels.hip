@@ -15,6 +15,8 @@
 //                   the norm summed in word order by one lane, then the
 //                   normalisation (BowVector.cpp:30-66, FeatureVector.cpp:28-38)
 #include <hip/hip_runtime.h>
+
+#include "lds_optin.h"
 #include <stdint.h>
 
 #include "bow_launch.h"
@@ -244,12 +246,8 @@ hipError_t launch_bow(const BowLaunch& a, hipStream_t st) {
                      0, st, a);
   const size_t lds = 16 * (size_t)a.lds_m;
   if (lds > 64 * 1024) {
-    static bool raised = false;  // > 64 KB dynamic LDS needs the opt-in once
-    if (!raised && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bow_assemble),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       16 * kBowMaxFeatures) != hipSuccess)
+    if (lds_optin(reinterpret_cast<const void*>(&k_bow_assemble), 16 * kBowMaxFeatures) != hipSuccess)
       return hipErrorInvalidValue;
-    raised = true;
   }
   hipLaunchKernelGGL(k_bow_assemble, dim3(a.n_frames), dim3(256), lds, st, a);
   return hipGetLastError();

@@ -19,6 +19,8 @@
 // (all edge contributions to an entry summed by one thread: no atomics).
 // Everything stays in LDS; observations are read once from HBM.
 #include <hip/hip_runtime.h>
+
+#include "lds_optin.h"
 #include <stdint.h>
 
 #include "../../include/orbgpu.h"
@@ -1261,14 +1263,11 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
   const int lds_obs = obs_stride < kInLdsObs ? obs_stride : kInLdsObs;
   const size_t lds = ((size_t)lds_obs * (sizeof(VisObs) + 1) + 15) & ~(size_t)15;
   const auto* obs = reinterpret_cast<const VisObs*>(d_obs);
-  static bool raised[2] = {false, false};  // > 64 KB of LDS needs the opt-in once
-  if (!raised[mode != ORBGPU_INERTIAL_LAST_FRAME]) {
+  {  // > 64 KB of LDS needs the opt-in (per kernel and device)
     const void* fn = mode == ORBGPU_INERTIAL_LAST_FRAME
                          ? reinterpret_cast<const void*>(&k_pose_inertial<ORBGPU_INERTIAL_LAST_FRAME>)
                          : reinterpret_cast<const void*>(&k_pose_inertial<ORBGPU_INERTIAL_LAST_KEYFRAME>);
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
-      return hipErrorInvalidValue;
-    raised[mode != ORBGPU_INERTIAL_LAST_FRAME] = true;
+    if (lds_optin(fn, 96 * 1024) != hipSuccess) return hipErrorInvalidValue;
   }
   if (mode == ORBGPU_INERTIAL_LAST_FRAME)
     hipLaunchKernelGGL(k_pose_inertial<ORBGPU_INERTIAL_LAST_FRAME>, dim3(n_problems),

@@ -14,6 +14,8 @@
 //   free pose) and, per free-pose pair (i <= j) sharing points, the list of
 //   (edge of i, edge of j) pairs that the Schur complement sums over.
 #include <hip/hip_runtime.h>
+
+#include "lds_optin.h"
 #include <stdint.h>
 
 #include "lba_launch.h"
@@ -647,11 +649,8 @@ hipError_t lba_solve(const LbaArgs& a, double lambda, hipStream_t st) {
   const size_t lds = (size_t)a.n_sys * a.n_sys * sizeof(double);
   const int in_lds = lds <= 150 * 1024 ? 1 : 0;
   if (in_lds && lds > 64 * 1024) {
-    static bool raised = false;
-    if (!raised && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lba_solve),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+    if (lds_optin(reinterpret_cast<const void*>(&k_lba_solve), 150 * 1024) != hipSuccess)
       return hipErrorInvalidValue;
-    raised = true;
   }
   hipLaunchKernelGGL(k_lba_solve, dim3(1), dim3(1024), in_lds ? lds : 0, st, a, lambda, in_lds);
   return hipGetLastError();

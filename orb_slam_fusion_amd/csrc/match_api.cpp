@@ -267,6 +267,7 @@ orbgpu_status orbgpu_matcher_create(int device, int max_keypoints, int max_point
   const size_t pt = sizeof(orbgpu_map_point);
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&m->d_err, sizeof(int)) != hipSuccess ||
+      hipMemset(m->d_err, 0, sizeof(int)) != hipSuccess ||
       arena_reserve(m->in, in_bytes(max_keypoints, max_points, pt)) != ORBGPU_OK ||
       arena_reserve(m->out, out_bytes(max_keypoints, max_points)) != ORBGPU_OK ||
       ensure_scratch(m, 1, max_keypoints, max_points) != ORBGPU_OK) {
@@ -292,6 +293,21 @@ void orbgpu_matcher_destroy(orbgpu_matcher* m) {
   if (m->d_err) (void)hipFree(m->d_err);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
+}
+
+orbgpu_status orbgpu_matcher_status(orbgpu_matcher* m, void* hip_stream, int reset, int* err) {
+  if (!m || !err) return ORBGPU_ERR_INVALID;
+  *err = 0;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (hip_stream && hipStreamSynchronize((hipStream_t)hip_stream) != hipSuccess)
+    return ORBGPU_ERR_DEVICE;
+  int v = 0;
+  if (hipMemcpyAsync(&v, m->d_err, sizeof(int), hipMemcpyDeviceToHost, m->stream) != hipSuccess ||
+      (reset && hipMemsetAsync(m->d_err, 0, sizeof(int), m->stream) != hipSuccess) ||
+      hipStreamSynchronize(m->stream) != hipSuccess)
+    return ORBGPU_ERR_DEVICE;
+  *err = v;
+  return ORBGPU_OK;
 }
 
 orbgpu_status orbgpu_search_by_projection_last(

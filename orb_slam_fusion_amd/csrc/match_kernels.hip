@@ -327,6 +327,7 @@ __global__ __launch_bounds__(256) void k_mt_grid(MatchLaunch a) {
   __shared__ int part[256];
   const int f = blockIdx.x, t = threadIdx.x;
   const int n = a.n[f];
+  if (t == 0 && a.npts[f] > a.pt_stride) atomicOr(a.err, 4);  // searched up to pt_stride only
   if (n > kMatchMaxKeypoints || n > a.kp_stride) {
     if (t == 0) atomicOr(a.err, 1);
     return;
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(256) void k_mt_grid(MatchLaunch a) {
 __global__ __launch_bounds__(256) void k_mt_search(MatchLaunch a) {
   const int f = blockIdx.y;
   const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (q >= a.npts[f]) return;
+  if (q >= min(a.npts[f], a.pt_stride)) return;  // the scratch rows hold pt_stride points
   const FrameRef F = frame_ref(a, f);
   const Query Q = make_query(a, f, q, true);
   uint32_t top[kMatchTopK];
@@ -446,8 +447,8 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   __shared__ uint32_t removed[kMatchMaxKeypoints / 32];
   __shared__ int hist[kHistoLength];
   const int f = blockIdx.x, lane = threadIdx.x;
-  const int n = a.n[f], nq = a.npts[f];
-  if (n > kMatchMaxKeypoints) return;  // reported by k_mt_grid
+  const int n = a.n[f], nq = min(a.npts[f], a.pt_stride);
+  if (n > kMatchMaxKeypoints || n > a.kp_stride) return;  // reported by k_mt_grid
   const FrameRef F = frame_ref(a, f);
   const bool rot_check = a.mode == kModeLast && a.p.check_ori;
   const bool local = a.mode != kModeLast;
@@ -587,7 +588,8 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
 __global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
   __shared__ int wsum[4];
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int n = a.n[f];
+  if (t == 0 && a.n[f] > a.kp_stride) atomicOr(a.err, 1);
+  const int n = min(a.n[f], a.kp_stride);  // the match row holds kp_stride entries
   const size_t ko = (size_t)f * a.kp_stride;
   const float* kps = a.kps + ko * kKpFloats;
   orbgpu_pose_obs* obs = a.obs ? a.obs + (size_t)f * a.obs_stride : nullptr;
@@ -596,7 +598,7 @@ __global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
   for (int i0 = 0; i0 < n; i0 += 256) {
     const int i = i0 + t;
     const int q = i < n ? a.match[ko + i] : -1;
-    const bool take = q >= 0;
+    const bool take = q >= 0 && q < a.pt_stride;
     const uint64_t bal = __ballot(take);
     if (lane == 0) wsum[w] = __popcll(bal);
     __syncthreads();

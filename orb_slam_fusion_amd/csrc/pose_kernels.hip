@@ -11,6 +11,8 @@
 // last computeActiveErrors() (possibly at a rejected trial pose), so the
 // kernel remembers that pose and recomputes -- bit-identical values.
 #include <hip/hip_runtime.h>
+
+#include "lds_optin.h"
 #include <stdint.h>
 
 #include "pose_math_dev.h"
@@ -501,12 +503,8 @@ hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const vo
   const int lds_obs = obs_stride < kPoseLdsObs ? obs_stride : kPoseLdsObs;
   const size_t lds = ((size_t)lds_obs * (sizeof(PoseObsDev) + 1) + 15) & ~(size_t)15;
   if (lds > 64 * 1024) {
-    static bool raised = false;  // > 64 KB dynamic LDS needs the opt-in once
-    if (!raised &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pose_opt),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+    if (lds_optin(reinterpret_cast<const void*>(&k_pose_opt), 150 * 1024) != hipSuccess)
       return hipErrorInvalidValue;
-    raised = true;
   }
   hipLaunchKernelGGL(k_pose_opt, dim3(n_problems), dim3(kPoseThreads), lds, st, c, d_pose_in,
                      reinterpret_cast<const PoseObsDev*>(d_obs), d_nobs, obs_stride, d_pose_out,

@@ -149,6 +149,16 @@ class ORBmatcher:
                 pts.shape[1], ptr(isg), len(isg), ptr(obs), obs.shape[1], ptr(nobs),
                 ptr(obs_index), s), "orbgpu_matches_to_inertial_obs_batch")
 
+    def status(self, reset: bool = True, stream=None) -> int:
+        """Sticky error bits of the *_batch calls (include/orbgpu.h
+        orbgpu_matcher_status): 1 = frame over kp_stride (skipped), 2 = an
+        observation list truncated at obs_stride, 4 = points beyond pt_stride."""
+        err = ctypes.c_int()
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_matcher_status(self._h, s, int(reset), ctypes.byref(err)),
+                  "orbgpu_matcher_status")
+        return err.value
+
     # -- Frame::isInFrustum ---------------------------------------------------
     def is_in_frustum(self, F: MatchFrame, points: np.ndarray, viewingCosLimit: float,
                       views: Optional[np.ndarray] = None) -> np.ndarray:

@@ -11,6 +11,7 @@ import re
 import subprocess
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 from orb_slam_fusion_amd import _lib
@@ -71,6 +72,33 @@ def test_invalid_params_rejected_before_device():
     assert so.orbgpu_pose_inertial_batch(None, 0, None, 1, None, None, None, None, None, None, 8,
                                          0, None, None, None) == _lib.ORBGPU_ERR_INVALID
     assert so.orbgpu_inertial_ctx_create(0, 0, 16, ctypes.byref(h)) == _lib.ORBGPU_ERR_INVALID
+
+
+def test_inertial_mode_and_prior_checked_with_a_handle():
+    """The mode / prior / n_obs checks of inertial_api.cpp run with a non-null
+    handle: they return before the handle is dereferenced or the device is
+    touched, so a dummy address exercises them on the CPU."""
+    so = _lib.lib()
+    dummy = ctypes.c_void_p(0x1000)  # never dereferenced on these paths
+    calib = ctypes.create_string_buffer(256)
+    ctypes.memmove(calib, np.array([1.0, 1.0], np.float32).tobytes(), 8)  # fx, fy > 0
+    cur, prev, pre, prior, res = (ctypes.create_string_buffer(4096) for _ in range(5))
+    obs, out = ctypes.create_string_buffer(64), ctypes.create_string_buffer(8)
+    INV = _lib.ORBGPU_ERR_INVALID
+    # bad mode
+    assert so.orbgpu_pose_inertial(dummy, 5, calib, cur, prev, pre, prior, obs, 1, 0, res, out) == INV
+    assert so.orbgpu_pose_inertial_batch(dummy, 5, calib, 1, cur, prev, pre, prior, obs, obs, 8, 0,
+                                         res, out, None) == INV
+    # LAST_FRAME (mode 0) without a prior
+    assert so.orbgpu_pose_inertial(dummy, 0, calib, cur, prev, pre, None, obs, 1, 0, res, out) == INV
+    assert so.orbgpu_pose_inertial_batch(dummy, 0, calib, 1, cur, prev, pre, None, obs, obs, 8, 0,
+                                         res, out, None) == INV
+    # negative observation count, observations without an outlier buffer
+    assert so.orbgpu_pose_inertial(dummy, 1, calib, cur, prev, pre, None, obs, -1, 0, res, out) == INV
+    assert so.orbgpu_pose_inertial(dummy, 1, calib, cur, prev, pre, None, obs, 1, 0, res, None) == INV
+    # a calibration with fx <= 0
+    zero = ctypes.create_string_buffer(256)
+    assert so.orbgpu_pose_inertial(dummy, 1, zero, cur, prev, pre, None, obs, 1, 0, res, out) == INV
 
 
 def test_keypoint_struct_is_cv_keypoint_layout():
