@@ -15,7 +15,7 @@ GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
 GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
 
-all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so oracle
+all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so build/valu_calib oracle
 
 OBJDIR   := build/obj
 GPU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(GPU_SRCS))
@@ -32,6 +32,11 @@ $(LIB)/liborbgpu.so: $(GPU_OBJS)
 $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 	@mkdir -p $(LIB)
 	$(CXX) -std=c++17 -O2 -fPIC -shared -o $@ $<
+
+# VALU-issue calibration kernel for the SQ counters (tools/profile_round.sh)
+build/valu_calib: tools/valu_calib.hip
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fno-slp-vectorize -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle

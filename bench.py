@@ -2,10 +2,12 @@
 """Throughput bench: ORB extract (stereo, 752x480, 1000 kp, 8 levels) +
 PoseOptimization (600 observations) per frame on MI355X.
 
-A step = one batch of B synthetic stereo frames per GPU: 2B images through
-the gfx950 extractor (orbgpu_extract_batch) and B pose-only problems through
-the gfx950 PoseOptimization (orbgpu_pose_opt_batch) on a second, concurrent
-HIP stream, inputs resident in HBM.  Frames shard across ranks (contiguous
+A step = B distinct synthetic stereo frames per GPU (default 5120, all
+resident in HBM before the timed region), in launch groups of 64 frames: 128
+images through the gfx950 extractor (orbgpu_extract_batch, two pipelines of
+64 images, each its own HIP stream) and 64 pose-only problems through the
+gfx950 PoseOptimization (orbgpu_pose_opt_batch) on a concurrent
+high-priority stream.  Frames shard across ranks (contiguous
 blocks of B frame ids per rank, orb_slam_fusion_amd/dist.py): no
 data-path collective, weak scaling; the max over ranks of the timed region is
 the job time.  Prints one JSON line on rank 0 (contract in the task README).
@@ -33,6 +35,7 @@ W, H = 752, 480
 PARAMS = (1000, 1.2, 8, 20, 7)
 POSE_OBS = 600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PROFILE_ROUND = "r02"  # profiles/<round>/kernels.json (tools/profile_round.sh)
 
 
 def level_sizes(inv_scale):
@@ -40,16 +43,35 @@ def level_sizes(inv_scale):
 
 
 def stage_bytes(sizes, n_kp):
-    """Algorithmic bytes per image for each extractor stage."""
+    """Algorithmic bytes per image for each extractor stage (SURVEY.md §8(d),
+    DESIGN.md §5): the bytes the reference algorithm must read and write once."""
     px = [w * h for w, h in sizes]
     return {
-        "resize": sum(px[l - 1] + px[l] for l in range(1, len(px))),
-        "blur": 2 * sum(px),
-        "fast_cells": sum(px),
-        "octree": 0,  # sequential list rebuilds on a few KB: latency-bound, no HBM claim
-        "describe": n_kp * (749 + 512 + 4 + 32),
-        "assemble": n_kp * (4 + 4 + 32 + 28 + 32),
+        "resize": sum(px[l - 1] + px[l] for l in range(1, len(px))),  # read l-1, write l
+        "blur": 2 * sum(px),                                           # read + write every level
+        "fast_cells": sum(px),                                         # read every level
+        "octree": 0,  # a few KB of candidates per level: latency-bound, no HBM claim
+        "describe": n_kp * (749 + 512),                                # IC_Angle circle + BRIEF samples
+        "assemble": n_kp * (28 + 32),                                  # keypoint record + descriptor
     }
+
+
+STAGE_KERNELS = {"resize": "k_resize", "blur": "k_blur", "fast_cells": "k_fast_cells",
+                 "octree": "k_octree", "describe": "k_describe", "assemble": "k_assemble",
+                 "pose_opt": "k_pose_opt"}
+
+
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
 def cpu_baseline(frames, probs, budget_s: float):
@@ -80,7 +102,21 @@ def cpu_baseline(frames, probs, budget_s: float):
         "kind": "port",
         "sample": f"{done} synthetic 752x480 stereo frames: oracle extract (2 threads, one per "
         f"image) + oracle PoseOptimization ({POSE_OBS} obs, 1 thread), {el:.1f} s",
+        **host_cpu(),
     }
+
+
+def load_profile():
+    """Per-kernel evidence committed under profiles/<round>/ by
+    tools/profile_round.sh: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, separate
+    passes) and calibrated VALU-busy per extractor-stage launch."""
+    f = REPO / "profiles" / PROFILE_ROUND / "kernels.json"
+    if not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text())
+    except ValueError:
+        return None
 
 
 def main() -> int:
@@ -88,10 +124,12 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--frames", type=int, default=64, help="stereo frames per GPU per step")
+    ap.add_argument("--frames", type=int, default=5120,
+                    help="stereo frames per GPU per step (all distinct, resident in HBM)")
+    ap.add_argument("--batch", type=int, default=64, help="stereo frames per launch group")
     ap.add_argument("--pipes", type=int, default=2,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
-                         "frames of a step split evenly between them)")
+                         "each launch group split evenly between them)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
@@ -118,19 +156,27 @@ def main() -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    Bg = args.batch
+    if args.frames % Bg:
+        raise SystemExit(f"--frames {args.frames} not divisible by --batch {Bg}")
+    G = args.frames // Bg  # launch groups per step
+    P = max(1, min(args.pipes, Bg))
+    if Bg % P:
+        raise SystemExit(f"--batch {Bg} not divisible by --pipes {P}")
+    Bp = Bg // P  # stereo frames per pipeline launch
     B = args.frames
-    frames = [synth.stereo_frame(i) for i in dist.frame_indices(rank, world, B)]
-    imgs = np.stack([im for fr in frames for im in fr])  # [2B, H, W]: L0 R0 L1 R1 ...
-    probs = [synth.pose_problem(synth.POSE_SEED + i, POSE_OBS, 10)
-             for i in dist.frame_indices(rank, world, B)]
+    ids = dist.frame_indices(rank, world, B)
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max_workers=16) as pool:  # ctypes releases the GIL
+        frames = list(pool.map(synth.stereo_frame, ids))
+    probs = [synth.pose_problem(synth.POSE_SEED + i, POSE_OBS, 10) for i in ids]
     cam = probs[0][0]
 
-    d_imgs = torch.from_numpy(imgs).to(dev)
-    P = max(1, min(args.pipes, B))
-    if B % P:
-        raise SystemExit(f"--frames {B} not divisible by --pipes {P}")
-    Bp = B // P  # stereo frames per pipeline
-    # one extractor handle per pipeline; each runs on its own library stream
+    d_imgs = torch.empty((2 * B, H, W), dtype=torch.uint8, device=dev)  # L0 R0 L1 R1 ...
+    for k in range(0, B, 256):
+        chunk = np.stack([im for fr in frames[k:k + 256] for im in fr])
+        d_imgs[2 * k:2 * k + len(chunk)].copy_(torch.from_numpy(chunk))
     pipes = [OrbExtractor(*PARAMS, device=local, max_width=W, max_height=H, max_images=2 * Bp)
              for _ in range(P)]
     ex = pipes[0]
@@ -147,28 +193,33 @@ def main() -> int:
     d_pout = torch.zeros((B, 7), dtype=torch.float32, device=dev)
     d_out = torch.zeros((B, POSE_OBS), dtype=torch.uint8, device=dev)
     d_inl = torch.zeros(B, dtype=torch.int32, device=dev)
-    opt = PoseOptimizer(device=local, max_problems=B, max_obs=POSE_OBS)
+    opt = PoseOptimizer(device=local, max_problems=Bg, max_obs=POSE_OBS)
 
-    # Two HIP streams: the extractor's kernel chain and the pose kernel run
-    # concurrently (frame k's pose overlaps frame k+1's extraction in a
-    # pipelined tracker; within a step the B frames are independent).
+    # Two kinds of HIP streams: each extractor pipeline's own, and a
+    # high-priority one for the pose kernel (frame k's pose overlaps frame
+    # k+1's extraction in a pipelined tracker; within a step the frames are
+    # independent).
     s_pose = torch.cuda.Stream(dev, priority=-1)  # high-priority pool: its own HW queue
     pose_ev = []
 
     def step(timed: bool):
-        # the pose kernel (64 long-lived blocks) is queued first so its blocks
-        # take their CUs before the extractor's wide grids fill the device
-        if timed:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(s_pose)
-        opt.batch(cam, d_pin, d_obs, d_nobs, d_pout, d_out, d_inl, stream=s_pose)
-        if timed:
-            e1.record(s_pose)
-            pose_ev.append((e0, e1))
-        for k, e in enumerate(pipes):  # stream=0: the handle's own HIP stream
-            sl = slice(2 * Bp * k, 2 * Bp * (k + 1))
-            e.extract_batch(d_imgs[sl], d_kps[sl], d_desc[sl], d_n[sl], d_mono[sl], stream=0)
+        for g in range(G):
+            f0 = g * Bg
+            # the pose kernel (Bg long-lived blocks) is queued first so its
+            # blocks take their CUs before the extractor's wide grids fill the device
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s_pose)
+            sl = slice(f0, f0 + Bg)
+            opt.batch(cam, d_pin[sl], d_obs[sl], d_nobs[sl], d_pout[sl], d_out[sl], d_inl[sl],
+                      stream=s_pose)
+            if timed:
+                e1.record(s_pose)
+                pose_ev.append((e0, e1))
+            for k, e in enumerate(pipes):  # stream=0: the handle's own HIP stream
+                isl = slice(2 * (f0 + Bp * k), 2 * (f0 + Bp * (k + 1)))
+                e.extract_batch(d_imgs[isl], d_kps[isl], d_desc[isl], d_n[isl], d_mono[isl], stream=0)
 
     for _ in range(args.warmup):
         step(False)
@@ -176,7 +227,7 @@ def main() -> int:
     for e in pipes:
         e.check()
 
-    ex.profile(args.steps)
+    ex.profile(args.steps * G)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -198,44 +249,57 @@ def main() -> int:
     ms_per_step = elapsed / args.steps * 1e3
 
     sizes = level_sizes(ex.GetInverseScaleFactors())
-    per_img = stage_bytes(sizes, int(n_kp.mean()))
-    stage_avg = {k: v / max(calls, 1) for k, v in stage_ms.items()}
+    kp_mean = float(n_kp.mean())
+    per_img = stage_bytes(sizes, kp_mean)
+    bytes_per_frame = 2 * sum(per_img.values())  # 13.76 MB per stereo frame at 1000 kp
+    stage_avg = {k: v / max(calls, 1) for k, v in stage_ms.items()}  # ms per pipeline launch
     stage_avg["pose_opt"] = pose_ms
     dom = max(stage_avg, key=stage_avg.get)
-    if dom == "pose_opt" or per_img.get(dom, 0) == 0:
-        # the dominant kernel is latency-bound; quote the largest HBM-bound stage too
-        hbm_stages = {k: v for k, v in stage_avg.items() if per_img.get(k, 0) > 0}
-        roof_stage = max(hbm_stages, key=hbm_stages.get)
-    else:
-        roof_stage = dom
-    roof_bytes = per_img[roof_stage] * 2 * Bp  # one launch of pipeline 0 covers 2*Bp images
-    roof_ms = stage_avg[roof_stage]
-    achieved = roof_bytes / (roof_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = REPO / "profiles" / "pmc_traffic.json"
-    if pmc.exists():
-        try:
-            tj = json.loads(pmc.read_text())  # tools/pmc_traffic.sh: HBM bytes per launch
-            if roof_stage in tj:  # scaled to this run's images per launch
-                per = tj[roof_stage] / tj[roof_stage + "_detail"]["images_per_launch"]
-                traffic = round(per * 2 * Bp)
-        except Exception:
-            traffic = None
-    # what actually bounds the kernel: VALU-busy fraction of its SIMDs from the
-    # SQ counter passes (tools/profile_round.sh -> profiles/pmc_sq.json):
-    # SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 / (SQ_BUSY_CYCLES
-    # (cycles summed over the 32 shader engines) x 32 SIMDs per engine)
-    valu_busy = None
-    sq = REPO / "profiles" / "pmc_sq.json"
-    kname = {"resize": "k_resize", "blur": "k_blur", "fast_cells": "k_fast_cells", "octree": "k_octree",
-             "describe": "k_describe", "assemble": "k_assemble"}.get(roof_stage)
-    if sq.exists() and kname:
-        try:
-            k = json.loads(sq.read_text())[kname]
-            valu_busy = round(4 * k["SQ_ACTIVE_INST_VALU"] / (32 * k["SQ_BUSY_CYCLES"]), 3)
-        except Exception:
-            valu_busy = None
+    imgs_per_launch = 2 * Bp
+    prof = load_profile()
+    pk = (prof or {}).get("stages", {})
 
+    # headline roofline: the whole extractor pipeline's algorithmic bytes at the
+    # measured frame rate against HBM peak (SURVEY §8(d) aggregate); traffic =
+    # the PMC-measured HBM bytes of the extractor kernels per stereo frame
+    achieved = bytes_per_frame * fps / 1e9
+    traffic = None
+    if all(k in pk and pk[k].get("hbm_bytes_per_image") is not None
+           for k in ("resize", "blur", "fast_cells", "octree", "describe", "assemble")):
+        traffic = round(2 * sum(pk[k]["hbm_bytes_per_image"]
+                                for k in ("resize", "blur", "fast_cells", "octree", "describe",
+                                          "assemble")))
+    kernels = {}
+    for st, ms in stage_avg.items():
+        b = per_img.get(st, 0) * imgs_per_launch if st != "pose_opt" else 0
+        row = {"kernel": STAGE_KERNELS[st], "avg_ms_per_launch": round(ms, 5),
+               "algorithmic_bytes_per_launch": int(b)}
+        if b:
+            row["achieved_GBs"] = round(b / (ms * 1e-3) / 1e9, 2)
+            row["frac"] = round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        p = pk.get(st)
+        if p:
+            if p.get("hbm_bytes_per_image") is not None and st != "pose_opt":
+                row["traffic_per_launch"] = round(p["hbm_bytes_per_image"] * imgs_per_launch)
+            for key in ("valu_busy", "rocprof_avg_ms_per_launch", "bound"):
+                if p.get(key) is not None:
+                    row[key] = p[key]
+        kernels[st] = row
+    roofline = {
+        "bound": "hbm",
+        "scope": "extractor pipeline: SURVEY §8(d) algorithmic bytes per stereo frame x fps",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_unit": "HBM bytes per stereo frame (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/"
+                        f"{PROFILE_ROUND}/kernels.json)",
+        "algorithmic_bytes_per_frame": int(bytes_per_frame),
+        "kernels": kernels,
+        "valu_busy_definition": "kernel SQ_INSTS_VALU per ns / the same counter per ns of a "
+                                "VALU-saturating kernel (tools/valu_calib.hip), same box",
+    }
     result = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -254,26 +318,15 @@ def main() -> int:
             f"+ PoseOptimization ({POSE_OBS} obs, 70% stereo, 10% outliers, fp64 LM)",
             "frames_per_gpu_per_step": B,
             "images_per_gpu_per_step": 2 * B,
+            "launch_groups_per_step": G,
             "parallelism": f"frames sharded over {world} GPU(s), no collective",
-            "streams": f"{P} extractor pipelines ({2 * Bp} images each, own HIP stream) + pose "
-                       "kernel on a high-priority stream, all concurrent",
+            "streams": f"{P} extractor pipelines ({2 * Bp} images per launch, own HIP stream) + "
+                       f"pose kernel ({Bg} problems per launch) on a high-priority stream, all "
+                       "concurrent",
             "keypoints_per_image_mean": float(n_kp.mean()),
             "pose_inliers_mean": float(inl.mean()),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": roof_stage,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": int(roof_bytes),
-            "avg_launch_ms": round(roof_ms, 5),
-            "valu_busy": valu_busy,
-            "limiter": "valu issue" if valu_busy is not None and valu_busy > 0.6 else None,
-        },
-        "stage_ms_per_step": {k: round(v, 5) for k, v in stage_avg.items()},
+        "roofline": roofline,
         "dominant_stage": dom,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -291,28 +344,28 @@ def main() -> int:
         sys.path.insert(0, str(REPO / "tools"))
         from bench_stereo import measure as measure_stereo  # noqa: E402
 
-        result["stereo"] = measure_stereo(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["stereo"] = measure_stereo(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_match:
         # SURVEY §8(f) rank 2, beside the headline metric (not part of it):
         # SearchByProjection(CurrentFrame, LastFrame) on resident frame outputs
         sys.path.insert(0, str(REPO / "tools"))
         from bench_match import measure as measure_match  # noqa: E402
 
-        result["match"] = measure_match(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["match"] = measure_match(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_bow:
         # SURVEY §8(f) rank 4, beside the headline metric (not part of it):
         # DBoW2 transform (Frame::ComputeBoW) on resident extractor descriptors
         sys.path.insert(0, str(REPO / "tools"))
         from bench_bow import measure as measure_bow  # noqa: E402
 
-        result["bow"] = measure_bow(frames=B, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["bow"] = measure_bow(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_inertial:
         # PoseInertialOptimizationLastFrame (stereo-inertial
         # tracking after IMU initialisation), a batch resident in HBM
         sys.path.insert(0, str(REPO / "tools"))
         from bench_inertial import measure as measure_inertial  # noqa: E402
 
-        result["inertial"] = measure_inertial(problems=B, calls=20, mode=0,
+        result["inertial"] = measure_inertial(problems=Bg, calls=20, mode=0,
                                               cpu_problems=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_track:
         # config C3's path on synthetic data: extract + stereo + SearchByProjection
@@ -320,7 +373,7 @@ def main() -> int:
         sys.path.insert(0, str(REPO / "tools"))
         from bench_track import measure as measure_track  # noqa: E402
 
-        result["track"] = measure_track(frames=B, calls=10, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["track"] = measure_track(frames=Bg, calls=10, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_latency:
         # north_star's per-frame target: one stereo frame at a time through the
         # host ABI (2-thread extraction + PoseOptimization) vs the CPU oracle
