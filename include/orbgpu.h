@@ -226,8 +226,15 @@ void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
  * initial keyframe, :1161, and every fixed camera, :1169-1183).  Points
  * [pt_begin, pt_end) and their edges are this call's shard (the whole window:
  * 0, n_pts); with reduce == NULL the shard must be the whole window.
- * *stop_flag (optional; the reference's bool, 1 byte, nonzero = stop) is polled
- * before every LM iteration (pbStopFlag, SparseOptimizer::terminate).
+ * lambda_init > 0 sets g2o's user lambda (setUserLambdaInit: 100.0 when the
+ * map is inertial, :1137); <= 0 = tau * max diag (computeLambdaInit).
+ * *stop_flag (optional; the reference's bool, 1 byte, nonzero = stop) is read
+ * where g2o polls SparseOptimizer::terminate(): before every LM iteration
+ * (sparse_optimizer.cpp:406) and after every trial
+ * (optimization_algorithm_levenberg.cpp:153-154).  The caller returns before
+ * the call when it is already set (optimizer.cc:1356-1357).
+ * The LM loop runs on the device; with reduce == NULL the call synchronises
+ * once, at its end.
  * Outputs: optimised poses (float, unit quaternion; poses_out_d optional
  * doubles), pts_out rows of the shard's points, outlier[i] for the shard's
  * edges (chi2 > 5.991 / 7.815 or depth <= 0), stats (optional, 6 doubles):
@@ -235,7 +242,7 @@ void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
 orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* c, const orbgpu_camera* cam, int n_kf,
                                   const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
                                   const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
-                                  int pt_begin, int pt_end, int iterations,
+                                  int pt_begin, int pt_end, int iterations, double lambda_init,
                                   const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce,
                                   void* user, orbgpu_pose* poses_out, double* poses_out_d,
                                   float* pts_out, uint8_t* outlier, double* stats);

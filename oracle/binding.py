@@ -56,8 +56,8 @@ def lib() -> ctypes.CDLL:
         "orc_se3_exp_compose": (None, [_P, _P, _P]),
         "orc_stereo_match": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
                                   _P, _P]),
-        "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, LBA_REDUCE_FN, _P, _P, _P,
-                         _P, _P]),
+        "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, ctypes.c_double, _I,
+                         LBA_REDUCE_FN, _P, _P, _P, _P, _P]),
         "orc_search_last": (_I, [_P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _I, _I, _P]),
         "orc_frustum": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
         "orc_search_local": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _I, _F, _P]),
@@ -199,11 +199,14 @@ def pose_opt(cam: np.ndarray, pose_in: np.ndarray, obs: np.ndarray):
     return inl, pout, out[:n].copy(), pd
 
 
-def lba(problem, iters: int = 10, pt_range=None, reduce=None):
+def lba(problem, iters: int = 10, pt_range=None, reduce=None, lambda_init: float = 0.0,
+        stop_after_trials: int = -1):
     """LocalBundleAdjustment restatement on an LbaProblem-like object (cam,
     poses_init, fixed, pts_init, edges).  pt_range=(begin, end) restricts this
     call to a point shard; reduce(buf: np.ndarray[float64], op) -> None
-    completes the shard sums in place (op 0 sum, 1 max).  Returns dict with
+    completes the shard sums in place (op 0 sum, 1 max).  lambda_init > 0:
+    setUserLambdaInit; stop_after_trials >= 0: terminate() turns true once
+    that many LM trials have run.  Returns dict with
     poses [n_kf, 7] f64, pts [n_pts, 3] f64 (shard rows only), outlier [E] u8
     (shard edges only), stats [6]."""
     cam = np.ascontiguousarray(problem.cam, np.float32)
@@ -229,7 +232,8 @@ def lba(problem, iters: int = 10, pt_range=None, reduce=None):
                 return -1
         cb = LBA_REDUCE_FN(_cb)
     rc = lib().orc_lba(_p(cam), n_kf, _p(poses), _p(fixed), n_pts, _p(pts), ne, _p(edges), b, e,
-                       iters, cb, None, _p(po), _p(xo), _p(out), _p(st))
+                       iters, float(lambda_init), int(stop_after_trials), cb, None, _p(po), _p(xo),
+                       _p(out), _p(st))
     if rc != 0:
         raise RuntimeError(f"orc_lba failed ({rc})")
     return {"poses": po, "pts": xo, "outlier": out[:ne].copy(), "stats": st}

@@ -152,7 +152,10 @@ bool inv3(const double A[3][3], double Ai[3][3]) {
 }
 
 // Dense LDLT (natural order, lower triangle) of the n x n row-major S, then
-// solve S x = b in place of x.  Returns false on a non-positive pivot.
+// solve S x = b in place of x.  Returns false on a zero pivot: Eigen's
+// SimplicialLDLT (linear_solver_eigen.h:101-104) reports NumericalIssue only
+// for D(k,k) == 0 (SimplicialCholesky_impl.h, the DoLDLT branch); a negative
+// pivot factorises and the LM step is judged by rho.
 bool ldlt_dense(std::vector<double>& S, int n, const double* b, double* x) {
   std::vector<double> d(n);
   bool ok = true;
@@ -160,7 +163,7 @@ bool ldlt_dense(std::vector<double>& S, int n, const double* b, double* x) {
     double dk = S[(size_t)k * n + k];
     for (int j = 0; j < k; ++j) dk -= S[(size_t)k * n + j] * S[(size_t)k * n + j] * d[j];
     d[k] = dk;
-    if (!(dk > 0)) ok = false;
+    if (dk == 0) ok = false;
     for (int i = k + 1; i < n; ++i) {
       double s = S[(size_t)i * n + k];
       for (int j = 0; j < k; ++j) s -= S[(size_t)i * n + j] * S[(size_t)k * n + j] * d[j];
@@ -196,11 +199,17 @@ SE3 pose_from_float(const float* p) {
 // Returns 0, or -1 on invalid input / a failed reduce.  stats (6 doubles):
 // initial robust chi2, final robust chi2, LM iterations, trials, final lambda,
 // edges flagged as outliers (all over this shard's edges except the chi2,
-// which are global).
+// which are global).  lambda_init > 0: setUserLambdaInit (optimizer.cc:1137,
+// 100 for an inertial map).  stop_after_trials >= 0: SparseOptimizer::
+// terminate() (the pbStopFlag) reads true once that many LM trials have run;
+// it is polled where g2o polls it: before every iteration
+// (sparse_optimizer.cpp:406) and after every trial
+// (optimization_algorithm_levenberg.cpp:153-154).
 int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_t* fixed,
                  int n_pts, const float* pts, int n_edges, const LbaEdge* edges, int pt_begin,
-                 int pt_end, int iters, LbaReduceFn reduce, void* user, double* poses_out,
-                 double* pts_out, uint8_t* outlier, double* stats) {
+                 int pt_end, int iters, double lambda_init, int stop_after_trials,
+                 LbaReduceFn reduce, void* user, double* poses_out, double* pts_out,
+                 uint8_t* outlier, double* stats) {
   const Cam c{cam5[0], cam5[1], cam5[2], cam5[3], cam5[4]};
   if (n_kf <= 0 || n_pts < 0 || pt_begin < 0 || pt_end > n_pts || pt_begin > pt_end) return -1;
   auto red = [&](double* buf, int n, int op) { return reduce ? reduce(user, buf, n, op) : 0; };
@@ -300,7 +309,8 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
   std::vector<SE3> Tn(n_kf);
   std::vector<double> Xn(X);
 
-  for (int it = 0; it < iters; ++it) {
+  auto terminate = [&]() { return stop_after_trials >= 0 && trials >= stop_after_trials; };
+  for (int it = 0; it < iters && !terminate(); ++it) {
     if (it > 0) {  // computeActiveErrors at the accepted state (same values as its trial)
       cur = active_chi2(T, X);
       if (red(&cur, 1, 0)) return -1;
@@ -317,7 +327,7 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
       for (int p = pt_begin; p < pt_end; ++p)
         for (int a = 0; a < 3; ++a) ml = std::max(std::fabs(Hll[(size_t)9 * p + 4 * a]), ml);
       if (red(&ml, 1, 1)) return -1;
-      lambda = tau * std::max(mx, ml);
+      lambda = lambda_init > 0 ? lambda_init : tau * std::max(mx, ml);
       ni = 2;
       nbad = 0;
     }
@@ -409,7 +419,7 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
         ni *= 2;
       }
       ++q;
-    } while (rho < 0 && q < 10);
+    } while (rho < 0 && q < 10 && !terminate());
     ++iters_done;
     if (q == 10 || rho == 0) break;
     if ((ini - cur) * 1e3 < ini)
@@ -453,11 +463,13 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
 
 extern "C" int orc_lba(const float* cam5, int n_kf, const float* poses, const uint8_t* fixed,
                        int n_pts, const float* pts, int n_edges, const void* edges, int pt_begin,
-                       int pt_end, int iters, oracle::LbaReduceFn reduce, void* user,
-                       double* poses_out, double* pts_out, uint8_t* outlier, double* stats) {
+                       int pt_end, int iters, double lambda_init, int stop_after_trials,
+                       oracle::LbaReduceFn reduce, void* user, double* poses_out, double* pts_out,
+                       uint8_t* outlier, double* stats) {
   return oracle::lba_optimize(cam5, n_kf, poses, fixed, n_pts, pts, n_edges,
                               static_cast<const oracle::LbaEdge*>(edges), pt_begin, pt_end, iters,
-                              reduce, user, poses_out, pts_out, outlier, stats);
+                              lambda_init, stop_after_trials, reduce, user, poses_out, pts_out,
+                              outlier, stats);
 }
 
 // Edge linearisation probe for the finite-difference tests: error (3),

@@ -227,8 +227,8 @@ SIGNATURES = {
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (
         _I,
-        [_P, ctypes.POINTER(Camera), _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, _P, _P, _P, _P, _P,
-         _P, _P, _P],
+        [_P, ctypes.POINTER(Camera), _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, ctypes.c_double, _P,
+         _P, _P, _P, _P, _P, _P, _P],
     ),
 }
 

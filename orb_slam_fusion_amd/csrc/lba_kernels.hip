@@ -3,29 +3,45 @@
 // SE3 keyframe poses and marginalized XYZ points (BlockSolver_6_3 Schur
 // complement, core/block_solver.hpp:364-514), fp64 throughout.
 //
-// One kernel per stage of an LM trial; the host drives the LM loop
-// (lba_api.cpp) exactly as oracle/lba_oracle.cc does.  Every sum has a fixed
-// order (per-point loops over the point's edges in insertion order, per-pose
-// block reductions with a fixed tree, last-block-done partial sums in block
-// order), so results are reproducible run to run.
+// The LM loop itself runs on the device (lba_launch.h): every kernel reads
+// the LbaCtrl state at entry and returns when its stage is not due, and the
+// single thread that closes a stage (the last block to finish it) takes the
+// LM decision of optimization_algorithm_levenberg.cpp:59-168 in place.  One
+// LM trial is five launches:
 //
-// Layout (per call, this rank's point shard):
-//   edges in point-major order (CSR pt_begin), pose-major index lists (CSR per
-//   free pose) and, per free-pose pair (i <= j) sharing points, the list of
-//   (edge of i, edge of j) pairs that the Schur complement sums over.
+//   k_lba_linearize  thread / edge      Jacobians + per-edge Hessian terms  } once per
+//   k_lba_sums       block / pose,      Hpp / bp and Hll / bl sums,          } iteration
+//                    thread / point     lambda init (computeLambdaInit)      }
+//   k_lba_schur      block / pose pair  S_ij = [i=j]Hpp_i - sum Hpl_i Dinv Hpl_j^T, b_s
+//   k_lba_solve      one block          (S + lambda I) = L D L^T by 16 x 16 tiles:
+//                                       diagonal tile in registers, panel and
+//                                       trailing update as v_mfma_f64_16x16x4
+//   k_lba_trial      thread / edge      back-substitution, trial state, errors,
+//                                       robust chi2 and computeScale -> decision
+//
+// Sums inside a launch have a fixed order (per-thread loops in edge order,
+// fixed trees, block partials summed by the last block in block order), so
+// results are reproducible run to run.  The reduction orders differ from
+// g2o's sequential ones: parity is by tolerance (tests/test_gpu_lba.py).
 #include <hip/hip_runtime.h>
-
-#include "lds_optin.h"
 #include <stdint.h>
 
 #include "lba_launch.h"
+#include "lds_optin.h"
 #include "pose_math_dev.h"
+
+// fp64 solver TU (tolerance parity, not bit parity): products may fuse.
+#pragma clang fp contract(fast)
 
 namespace orbgpu {
 
 namespace {
 
-constexpr int kLbaThreads = 256;
+constexpr int kThreads = 256;
+constexpr int kMaxKfLds = 1024;  // trial poses staged in LDS up to this many keyframes
+constexpr double kTau = 1e-5;    // OptimizationAlgorithmLevenberg _tau
+
+typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ Se3 load_pose(const double* p) {
   Se3 T;
@@ -49,7 +65,8 @@ __device__ __forceinline__ void store_pose(const Se3& T, double* p) {
   p[6] = T.t[2];
 }
 
-// error of one edge (EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ); returns
+// error of one edge (EdgeSE3ProjectXYZ, optimizable_types.h:105-125 /
+// EdgeStereoSE3ProjectXYZ, types_six_dof_expmap.cpp:174-257); returns
 // isDepthPositive on the same state
 __device__ __forceinline__ bool lba_error(const LbaEdgeDev& e, const Se3& T, const double X[3],
                                           const LbaCamDev& c, double err[3]) {
@@ -99,7 +116,7 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
       R[r][2] = c2[r];
     }
   }
-  if (e.ur < 0.f) {
+  if (e.ur < 0.f) {  // optimizable_types.cc:134-155
     const double pj[2][3] = {{-(c.fx / z), 0.0, -(-c.fx * x / (z * z))},
                              {0.0, -(c.fy / z), -(-c.fy * y / (z * z))}};
     const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
@@ -114,7 +131,7 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
     for (int k = 0; k < 3; ++k) Jl[2][k] = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) Jp[2][k] = 0;
-  } else {
+  } else {  // types_six_dof_expmap.cpp:211-257
     const double z_2 = z * z, fx = c.fx, fy = c.fy, bf = c.bf;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -143,195 +160,19 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
   }
 }
 
-// Fixed-tree block sum of one double (256 threads); valid in thread 0.
-__device__ __forceinline__ double lba_block_sum(double v, double* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  const double r = ((red[0] + red[1]) + red[2]) + red[3];
-  __syncthreads();
-  return r;
-}
-
-// Last-block-done finish: block partials summed in block order into *out.
-__device__ __forceinline__ void lba_finish_sum(double partial, volatile double* partials,
-                                               unsigned* counter, double* out) {
-  __shared__ bool last;
-  if (threadIdx.x == 0) {
-    partials[blockIdx.x] = partial;
-    __threadfence();
-    last = atomicAdd(counter, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
-    double s = 0;
-    for (unsigned b = 0; b < gridDim.x; ++b) s += partials[b];
-    *out = s;
-    *counter = 0;
-  }
-}
-
-__device__ __forceinline__ void atomic_max_pos(double* p, double v) {  // v >= 0
-  atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
-}
-
-// ---- computeActiveErrors + robust chi2 over this shard's edges at a state
-__global__ __launch_bounds__(kLbaThreads) void k_lba_errors(LbaArgs a, const double* __restrict__ poses,
-                                                            const double* __restrict__ pts, double* out) {
-  __shared__ double red[4];
-  const int i = blockIdx.x * kLbaThreads + threadIdx.x;
-  double r0 = 0;
-  if (i < a.n_edges) {
-    const LbaEdgeDev e = a.edges[i];
-    const Se3 T = load_pose(poses + 7 * e.kf);
-    const double X[3] = {pts[3 * e.point], pts[3 * e.point + 1], pts[3 * e.point + 2]};
-    double err[3];
-    lba_error(e, T, X, a.cam, err);
-    a.err[3 * i] = err[0];
-    a.err[3 * i + 1] = err[1];
-    a.err[3 * i + 2] = err[2];
-    double w;
-    huber_rho(lba_chi2(e, err), lba_delta(e), r0, w);
-  }
-  const double s = lba_block_sum(r0, red);
-  lba_finish_sum(s, a.partials, a.counter, out);
-}
-
-// ---- buildSystem, edge side: one thread per edge of the shard.  Its
-// Jacobians at the current state and its terms of Hll / bl (point), Hpl and
-// Hpp / bp (free pose) -- summed per point and per pose in fixed order below.
-__global__ __launch_bounds__(kLbaThreads) void k_lba_linearize(LbaArgs a, const double* __restrict__ poses,
-                                                               const double* __restrict__ pts) {
-  const int i = blockIdx.x * kLbaThreads + threadIdx.x;
-  if (i >= a.n_edges) return;
-  const LbaEdgeDev e = a.edges[i];
-  const double X[3] = {pts[3 * e.point], pts[3 * e.point + 1], pts[3 * e.point + 2]};
-  const Se3 T = load_pose(poses + 7 * e.kf);
-  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
-  const int D = e.ur < 0.f ? 2 : 3;
-  double Jl[3][3], Jp[3][6];
-  lba_jacobians(e, T, X, a.cam, Jl, Jp);
-  double r0, w;
-  huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
-  const double info = (double)e.inv_sigma2, wi = w * info;
-  double om[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) om[r] = (-info * ev[r]) * w;
-  double* hl = a.hll_e + 12 * (size_t)i;  // 9 Hll terms (row-major), 3 bl terms
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    double g = 0;
-    for (int r = 0; r < D; ++r) g += Jl[r][s] * om[r];
-    hl[9 + s] = g;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      double h = 0;
-      for (int r = 0; r < D; ++r) h += Jl[r][s] * wi * Jl[r][q];
-      hl[3 * s + q] = h;
-    }
-  }
-  if (a.hidx[e.kf] < 0) return;
-  double* hpl = a.hpl + 18 * (size_t)i;
-  double* hp = a.hpp_e + 27 * (size_t)i;  // 21 lower-triangle Hpp terms, then 6 bp terms
-  int hk = 0;
-#pragma unroll
-  for (int s = 0; s < 6; ++s) {
-    double g = 0;
-    for (int r = 0; r < D; ++r) g += Jp[r][s] * om[r];
-    hp[21 + s] = g;
-#pragma unroll
-    for (int q = 0; q <= s; ++q) {
-      double h = 0;
-      for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jp[r][q];
-      hp[hk++] = h;
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      double h = 0;
-      for (int r = 0; r < D; ++r) h += Jp[r][s] * wi * Jl[r][q];
-      hpl[3 * s + q] = h;
-    }
-  }
-}
-
-// ---- buildSystem, point side: one thread per point sums its edges' Hll / bl
-// terms in insertion order (as g2o adds them edge by edge).
-__global__ __launch_bounds__(kLbaThreads) void k_lba_point_sum(LbaArgs a) {
-  const int p = blockIdx.x * kLbaThreads + threadIdx.x;
-  if (p >= a.n_pts) return;
-  double H[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = a.pt_begin[p]; i < a.pt_begin[p + 1]; ++i) {
-    const double* hl = a.hll_e + 12 * (size_t)i;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) H[k] += hl[k];
-  }
-#pragma unroll
-  for (int k = 0; k < 9; ++k) a.hll[9 * (size_t)p + k] = H[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) a.bl[3 * (size_t)p + k] = H[9 + k];
-  atomic_max_pos(a.diag + a.n_sys, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));  // Hll max
-}
-
-// ---- buildSystem, pose side: one block per free pose, its edges strided over
-// the threads, a fixed tree per term.  -> Hpp (6x6 full) and bp.
-__global__ __launch_bounds__(kLbaThreads) void k_lba_pose_sum(LbaArgs a) {
-  __shared__ double red[4 * 27];
-  const int f = blockIdx.x;
-  double acc[27];
-#pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0;
-  for (int j = a.pose_begin[f] + threadIdx.x; j < a.pose_begin[f + 1]; j += kLbaThreads) {
-    const double* hp = a.hpp_e + 27 * (size_t)a.pose_edges[j];
-#pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] += hp[k];
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-    double v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[27 * wave + k] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 27) {
-    const int k = threadIdx.x;
-    const double v = ((red[k] + red[27 + k]) + red[54 + k]) + red[81 + k];
-    if (k < 21) {
-      // lower-triangle index k -> (s, q)
-      int s = 0, q = k;
-      while (q > s) {
-        q -= s + 1;
-        ++s;
-      }
-      a.hpp[36 * (size_t)f + 6 * s + q] = v;
-      a.hpp[36 * (size_t)f + 6 * q + s] = v;
-      if (s == q) a.diag[6 * f + s] = v;  // this shard's Hpp diagonal (lambda init, summed over ranks)
-    } else {
-      a.bp[6 * (size_t)f + (k - 21)] = v;
-    }
-  }
-}
-
-// ---- Schur, point side (per trial lambda): Dinv = (Hll + lambda I)^-1 by
-// cofactors (Eigen compute_inverse_size3).
-__global__ __launch_bounds__(kLbaThreads) void k_lba_schur_points(LbaArgs a, double lambda) {
-  const int p = blockIdx.x * kLbaThreads + threadIdx.x;
-  if (p >= a.n_pts) return;
+// (Hll + lambda I)^-1 by cofactors (Eigen compute_inverse_size3); returns the
+// determinant (0 = singular landmark block: the trial fails).
+__device__ __forceinline__ double inv3_lambda(const double* __restrict__ h, double lambda, double Di[9]) {
   double A[3][3];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) A[r][c] = a.hll[9 * (size_t)p + 3 * r + c] + (r == c ? lambda : 0.0);
+    for (int c = 0; c < 3; ++c) A[r][c] = h[3 * r + c] + (r == c ? lambda : 0.0);
   const double c00 = A[1][1] * A[2][2] - A[1][2] * A[2][1];
   const double c10 = A[1][2] * A[2][0] - A[1][0] * A[2][2];
   const double c20 = A[1][0] * A[2][1] - A[1][1] * A[2][0];
   const double det = A[0][0] * c00 + A[0][1] * c10 + A[0][2] * c20;
-  if (det == 0) a.flags[0] = 1;  // singular landmark block: the trial fails (tmp = DBL_MAX)
   const double id = det != 0 ? 1.0 / det : 0.0;
-  double* Di = a.dinv + 9 * (size_t)p;
   Di[0] = c00 * id;
   Di[3] = c10 * id;
   Di[6] = c20 * id;
@@ -341,272 +182,833 @@ __global__ __launch_bounds__(kLbaThreads) void k_lba_schur_points(LbaArgs a, dou
   Di[2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) * id;
   Di[5] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) * id;
   Di[8] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) * id;
+  return det;
 }
 
-// W = Hpl_e Dinv_point (6 x 3)
-__device__ __forceinline__ void lba_w(const double* __restrict__ B, const double* __restrict__ Di,
-                                      double W[6][3]) {
-#pragma unroll
-  for (int s = 0; s < 6; ++s)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) W[s][c] = B[3 * s] * Di[c] + B[3 * s + 1] * Di[3 + c] + B[3 * s + 2] * Di[6 + c];
+// DPP lane move of a double (two 32-bit halves); lanes whose source is out of
+// range or whose row is masked off read 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  return __hiloint2double(hi, lo);
 }
 
-// ---- Schur, pose side: one 256-thread block per free-pose pair (i <= j)
-// sharing points.  The pair's (edge of i, edge of j) entries are strided
-// over the threads (each computes W_i Hpl_j^T, W from the point's Dinv),
-// then a fixed tree per entry of the 6 x 6 block:
-//   S_ij = [i == j] Hpp_i - sum W_i Hpl_j^T;
-// diagonal pairs also produce b_s = bp - sum over the pose's edges W bl.
-__global__ __launch_bounds__(kLbaThreads) void k_lba_schur_pairs(LbaArgs a) {
-  __shared__ double red[4 * 42];
+// Fixed-tree sum of K doubles over a 256-thread block; valid in every thread.
+template <int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* red /* 4 * K */) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double x = v[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    v[k] = x;
+  }
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[K * (threadIdx.x >> 6) + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
+  __syncthreads();
+}
+
+// Last-block-done ticket (cdna_hip_programming.md §6 Guideline 16, counter
+// form): every storing wave drains, the block joins, lane 0 releases at agent
+// scope and takes a ticket; the last block acquires before reading the other
+// blocks' stores.  The counter resets itself for the next launch.
+__device__ __forceinline__ bool last_block(unsigned* counter) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// Sum of K per-block partials (partials[K * b + k]) in a fixed tree, by the
+// last block; valid in every thread.
+template <int K>
+__device__ __forceinline__ void sum_partials(const double* partials, int nb, double (&out)[K], double* red) {
+  double v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = 0;
+  for (int b = threadIdx.x; b < nb; b += kThreads)
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += partials[K * b + k];
+  block_sum<K>(v, red);
+#pragma unroll
+  for (int k = 0; k < K; ++k) out[k] = v[k];
+}
+
+__device__ __forceinline__ void publish(const LbaArgs& a, const LbaCtrl& c) {
+  const unsigned long long w = ((unsigned long long)(c.done ? 1u : 0u) << 32) | (unsigned)c.trials;
+  __hip_atomic_store(&a.host->progress, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ int host_stop(const LbaArgs& a) {
+  return __hip_atomic_load(&a.host->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+// ---- the LM decisions (one thread) --------------------------------------
+// start of optimize(): computeActiveErrors at the initial state
+__device__ void ctl_init(const LbaArgs& a, double chi, int stop) {
+  LbaCtrl& c = *a.ctrl;
+  c.cur = chi;
+  c.chi_init = chi;
+  c.ini = chi;
+  c.it = 0;
+  c.q = 0;
+  c.nbad = 0;
+  c.state = 0;
+  c.iters_done = 0;
+  c.trials = 0;
+  c.need_build = 1;
+  c.stopped = stop;
+  // SparseOptimizer::optimize: for (i < iterations && !terminate() ...)
+  c.done = (c.max_iters <= 0 || stop) ? 1 : 0;
+  publish(a, c);
+}
+
+// computeLambdaInit (optimization_algorithm_levenberg.cpp:180-191)
+__device__ void ctl_lambda(const LbaArgs& a, double maxdiag) {
+  LbaCtrl& c = *a.ctrl;
+  c.lambda = c.user_lambda > 0 ? c.user_lambda : kTau * maxdiag;
+  c.ni = 2;
+  c.nbad = 0;
+}
+
+// one trial's verdict (optimization_algorithm_levenberg.cpp:118-167)
+__device__ void ctl_decide(const LbaArgs& a, double chi_trial, double scale_l, int bad, int stop) {
+  LbaCtrl& c = *a.ctrl;
+  double tmp = chi_trial;
+  if (bad) tmp = 1.7976931348623157e308;  // !ok2 -> tempChi = max
+  double rho = c.cur - tmp;
+  const double scale = a.scal[0] + scale_l + 1e-3;
+  rho /= scale;
+  if (rho > 0 && isfinite(tmp)) {
+    double alpha = 1. - cube(2 * rho - 1);
+    alpha = fmin(alpha, 2. / 3.);
+    c.lambda *= fmax(1. / 3., alpha);
+    c.ni = 2;
+    c.cur = tmp;
+    c.state ^= 1;  // discardTop: the trial state becomes current
+  } else {
+    c.lambda *= c.ni;  // pop: the current state stays
+    c.ni *= 2;
+  }
+  ++c.q;
+  ++c.trials;
+  c.stopped = stop;
+  if (!(rho < 0 && c.q < 10 && !stop)) {  // the do-while ends: the iteration is over
+    ++c.iters_done;
+    int done = 0;
+    if (c.q == 10 || rho == 0) {
+      done = 1;  // Terminate
+    } else {
+      if ((c.ini - c.cur) * 1e3 < c.ini)
+        c.nbad++;
+      else
+        c.nbad = 0;
+      if (c.nbad >= 3) done = 1;
+    }
+    ++c.it;
+    if (c.it >= c.max_iters || stop) done = 1;  // the for loop's bound and terminate()
+    c.done = done;
+    c.need_build = done ? 0 : 1;
+  }
+  publish(a, c);
+}
+
+// ---- computeActiveErrors at the initial state ----------------------------
+__global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
+  __shared__ double red[4];
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  double r0 = 0;
+  if (i < a.n_edges) {
+    const LbaEdgeDev e = a.edges[i];
+    const Se3 T = load_pose(a.poses[0] + 7 * e.kf);
+    const double* x = a.pts[0] + 3 * e.point;
+    const double X[3] = {x[0], x[1], x[2]};
+    double err[3];
+    lba_error(e, T, X, a.cam, err);
+    a.err[3 * i] = err[0];
+    a.err[3 * i + 1] = err[1];
+    a.err[3 * i + 2] = err[2];
+    double w;
+    huber_rho(lba_chi2(e, err), lba_delta(e), r0, w);
+  }
+  double v[1] = {r0};
+  block_sum<1>(v, red);
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = v[0];
+  if (!last_block(a.counter + 0)) return;
+  double s[1];
+  sum_partials<1>(a.partials, gridDim.x, s, red);
+  if (threadIdx.x == 0) {
+    const int stop = host_stop(a);
+    if (a.sharded) {
+      a.red[0] = s[0];
+      a.red[1] = stop;
+    } else {
+      ctl_init(a, s[0], stop);
+    }
+  }
+}
+
+// ---- buildSystem, edge side: Jacobians at the current state and each
+// edge's terms of Hll / bl (point), Hpl and Hpp / bp (free pose)
+// (base_binary_edge.hpp:56-119 with the robust weight of base_edge.h:91-97).
+// The row loops run over 3 rows for mono edges too: their third Jacobian
+// row and error are zero, and adding an exact 0 changes no sum (constant
+// trip counts keep the Jacobians in registers, not in scratch).
+__global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done || !c.need_build) return;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n_edges) return;
+  const LbaEdgeDev e = a.edges[i];
+  const double* x = a.pts[c.state] + 3 * e.point;
+  const double X[3] = {x[0], x[1], x[2]};
+  const Se3 T = load_pose(a.poses[c.state] + 7 * e.kf);
+  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
+  double Jl[3][3], Jp[3][6];
+  lba_jacobians(e, T, X, a.cam, Jl, Jp);
+  double r0, w;
+  huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
+  const double info = (double)e.inv_sigma2, wi = w * info;
+  double om[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) om[r] = (-info * ev[r]) * w;
+  double hl[12];  // 9 Hll terms (row-major), 3 bl terms
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    double g = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) g += Jl[r][s] * om[r];
+    hl[9 + s] = g;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      double h = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) h += Jl[r][s] * wi * Jl[r][q];
+      hl[3 * s + q] = h;
+    }
+  }
+  double* hlo = a.hll_e + 12 * (size_t)i;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) hlo[k] = hl[k];
+  if (e.f < 0) return;
+  double hp[27], hpl[18];  // 21 lower-triangle Hpp terms, 6 bp terms; Hpl 6 x 3
+  int hk = 0;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    double g = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) g += Jp[r][s] * om[r];
+    hp[21 + s] = g;
+#pragma unroll
+    for (int q = 0; q <= s; ++q) {
+      double h = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) h += Jp[r][s] * wi * Jp[r][q];
+      hp[hk++] = h;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      double h = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) h += Jp[r][s] * wi * Jl[r][q];
+      hpl[3 * s + q] = h;
+    }
+  }
+  double* hpo = a.hpp_e + 27 * (size_t)i;
+#pragma unroll
+  for (int k = 0; k < 27; ++k) hpo[k] = hp[k];
+  double* hplo = a.hpl + 18 * (size_t)i;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) hplo[k] = hpl[k];
+}
+
+// ---- buildSystem, vertex side.  Blocks [0, n_free): one free pose each,
+// its edges strided over the threads, a fixed tree per term -> Hpp (6 x 6
+// full), bp and the pose diagonal.  Blocks [n_free, ...): one point per
+// thread summing its edges' Hll / bl in insertion order.  The last block
+// opens the iteration: iniChi, and at iteration 0 computeLambdaInit (tau *
+// max |diag| over pose and point blocks).
+__global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
+  __shared__ double red[4 * 27];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done || !c.need_build) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double hmax = 0;
+  if ((int)blockIdx.x < a.n_free) {
+    const int f = blockIdx.x;
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] = 0;
+    const int j0 = a.pose_begin[f], j1 = a.pose_begin[f + 1];
+    for (int jb = j0 + threadIdx.x; jb < j1; jb += 4 * kThreads) {
+      int ei[4];  // four edges' indices in flight before their terms
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ei[u] = jb + u * kThreads < j1 ? a.pslot[jb + u * kThreads].x : -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (ei[u] < 0) continue;
+        const double* hp = a.hpp_e + 27 * (size_t)ei[u];
+#pragma unroll
+        for (int k = 0; k < 27; ++k) acc[k] += hp[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      double v = acc[k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) red[27 * wave + k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 27) {
+      const int k = threadIdx.x;
+      const double v = ((red[k] + red[27 + k]) + red[54 + k]) + red[81 + k];
+      if (k < 21) {
+        int s = 0, q = k;  // lower-triangle index k -> (s, q)
+        while (q > s) {
+          q -= s + 1;
+          ++s;
+        }
+        a.hpp[36 * (size_t)f + 6 * s + q] = v;
+        a.hpp[36 * (size_t)f + 6 * q + s] = v;
+        if (s == q) a.diag[6 * f + s] = v;
+      } else {
+        a.bp[6 * (size_t)f + (k - 21)] = v;
+      }
+    }
+  } else {
+    const int p = (blockIdx.x - a.n_free) * kThreads + threadIdx.x;
+    if (p < a.n_pts) {
+      double H[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      const int i0 = a.pt_begin[p], i1 = a.pt_begin[p + 1];
+      for (int ib = i0; ib < i1; ib += 4) {  // four edges' loads in flight
+        double hl[4][12];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int k = 0; k < 12; ++k) hl[u][k] = ib + u < i1 ? a.hll_e[12 * (size_t)(ib + u) + k] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ib + u < i1)
+#pragma unroll
+            for (int k = 0; k < 12; ++k) H[k] += hl[u][k];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) a.hll[9 * (size_t)p + k] = H[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.bl[3 * (size_t)p + k] = H[9 + k];
+      hmax = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hmax = fmax(hmax, __shfl_xor(hmax, o, 64));
+    if (lane == 0) red[wave] = hmax;
+    __syncthreads();
+    hmax = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  }
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = hmax;
+  if (!last_block(a.counter + 1)) return;
+  // max is order-independent: every reduction order gives the same value
+  double m = 0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) m = fmax(m, a.partials[b]);
+  for (int k = threadIdx.x; k < a.n_sys; k += kThreads) m = fmax(m, fabs(a.diag[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  __syncthreads();
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    LbaCtrl& cw = *a.ctrl;
+    const double mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    if (a.sharded) {
+      // this shard's point maximum; the host max-reduces it and sum-reduces
+      // the pose diagonal, then k_lba_ctl(kCtlLambda) finishes lambda init
+      double hm = 0;
+      for (int b = a.n_free; b < (int)gridDim.x; ++b) hm = fmax(hm, a.partials[b]);
+      a.diag[a.n_sys] = hm;
+    } else if (cw.it == 0) {
+      ctl_lambda(a, mx);
+    }
+    cw.ini = cw.cur;
+    cw.q = 0;
+    cw.need_build = 0;
+  }
+}
+
+// ---- Schur complement of the points at the trial's lambda: one 512-thread
+// block per free-pose pair (fi <= fj).  Threads stride over pose fi's edges
+// (point order); each finds its point's edges to pose fj and adds
+// W_i Hpl_j^T with W_i = Hpl_i (Hll + lambda I)^-1; the diagonal pair also
+// takes b_s = bp - sum W_i bl.  (block_solver.hpp:392-460)  Loads are issued
+// in batches (slot record -> point data + the point's free indices -> the
+// matching Hpl) so each thread waits on three memory round trips.
+constexpr int kSchurThreads = 512;
+constexpr int kSchurWaves = kSchurThreads / 64;
+
+__global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
+  __shared__ double red[kSchurWaves * 4 * 42];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const double lambda = c.lambda;
   const int pr = blockIdx.x;
   const int fi = a.pair_i[pr], fj = a.pair_j[pr];
   const int n = a.n_sys;
+  const bool diag = fi == fj;
   double acc[42];
 #pragma unroll
   for (int k = 0; k < 42; ++k) acc[k] = 0;
-  for (int k = a.pair_begin[pr] + threadIdx.x; k < a.pair_begin[pr + 1]; k += kLbaThreads) {
-    const int ei = a.pair_ei[k], ej = a.pair_ej[k];
+  for (int k = a.pose_begin[fi] + threadIdx.x; k < a.pose_begin[fi + 1]; k += kSchurThreads) {
+    const int4 sl = a.pslot[k];  // {edge, point, first edge of the point, end}
+    const int ei = sl.x, p = sl.y;
+    double hll[9], B[18];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) hll[q] = a.hll[9 * (size_t)p + q];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) B[q] = a.hpl[18 * (size_t)ei + q];
+    double blp[3] = {0, 0, 0};
+    if (diag)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) blp[q] = a.bl[3 * (size_t)p + q];
+    int fs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fs[u] = sl.z + u < sl.w ? a.ef[sl.z + u] : -2;
+    double Di[9];
+    inv3_lambda(hll, lambda, Di);
     double W[6][3];
-    lba_w(a.hpl + 18 * (size_t)ei, a.dinv + 9 * (size_t)a.edges[ei].point, W);
-    const double* B = a.hpl + 18 * (size_t)ej;
 #pragma unroll
     for (int s = 0; s < 6; ++s)
 #pragma unroll
-      for (int q = 0; q < 6; ++q) acc[6 * s + q] += W[s][0] * B[3 * q] + W[s][1] * B[3 * q + 1] + W[s][2] * B[3 * q + 2];
-  }
-  if (fi == fj) {
-    for (int j = a.pose_begin[fi] + threadIdx.x; j < a.pose_begin[fi + 1]; j += kLbaThreads) {
-      const int e = a.pose_edges[j];
-      const int p = a.edges[e].point;
-      double W[6][3];
-      lba_w(a.hpl + 18 * (size_t)e, a.dinv + 9 * (size_t)p, W);
-      const double* bl = a.bl + 3 * (size_t)p;
+      for (int q = 0; q < 3; ++q) W[s][q] = B[3 * s] * Di[q] + B[3 * s + 1] * Di[3 + q] + B[3 * s + 2] * Di[6 + q];
+    for (int base = sl.z;;) {
 #pragma unroll
-      for (int s = 0; s < 6; ++s) acc[36 + s] += W[s][0] * bl[0] + W[s][1] * bl[1] + W[s][2] * bl[2];
+      for (int u = 0; u < 8; ++u) {
+        if (fs[u] != fj) continue;
+        const double* Bj = a.hpl + 18 * (size_t)(base + u);
+#pragma unroll
+        for (int s = 0; s < 6; ++s)
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+            acc[6 * s + q] += W[s][0] * Bj[3 * q] + W[s][1] * Bj[3 * q + 1] + W[s][2] * Bj[3 * q + 2];
+      }
+      base += 8;
+      if (base >= sl.w) break;  // points seen by more than 8 keyframes: next chunk
+#pragma unroll
+      for (int u = 0; u < 8; ++u) fs[u] = base + u < sl.w ? a.ef[base + u] : -2;
     }
+    if (diag)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) acc[36 + s] += W[s][0] * blp[0] + W[s][1] * blp[1] + W[s][2] * blp[2];
   }
+  // fixed tree: DPP row sums (lane 15 of each 16-lane row), then the block's
+  // row partials in row order
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nk = diag ? 42 : 36;
 #pragma unroll
   for (int k = 0; k < 42; ++k) {
-    double v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[42 * wave + k] = v;
+    double x = acc[k];
+    x += dpp_f64<0x111, 0xf>(x);
+    x += dpp_f64<0x112, 0xf>(x);
+    x += dpp_f64<0x114, 0xf>(x);
+    x += dpp_f64<0x118, 0xf>(x);
+    if ((lane & 15) == 15) red[(wave * 4 + (lane >> 4)) * 42 + k] = x;
   }
   __syncthreads();
   const int t = threadIdx.x;
-  if (t < 36) {
-    const int s = t / 6, q = t - 6 * s;
-    const double sum = ((red[t] + red[42 + t]) + red[84 + t]) + red[126 + t];
-    const double v = (fi == fj ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
-    a.sys[(size_t)(6 * fi + s) * n + 6 * fj + q] = v;
-    a.sys[(size_t)(6 * fj + q) * n + 6 * fi + s] = v;
-  } else if (fi == fj && t < 42) {
-    const int s = t - 36;
-    const double sum = ((red[t] + red[42 + t]) + red[84 + t]) + red[126 + t];
-    a.sys[(size_t)n * n + 6 * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
-    a.sys[(size_t)n * n + n + 6 * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (LM scale)
+  if (t < nk) {
+    double sum = 0;
+#pragma unroll 8
+    for (int r = 0; r < kSchurWaves * 4; ++r) sum += red[r * 42 + t];
+    if (t < 36) {
+      const int s = t / 6, q = t - 6 * s;
+      if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
+      const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
+      a.sys[(size_t)(6 * fi + s) * n + 6 * fj + q] = v;
+      a.sys[(size_t)(6 * fj + q) * n + 6 * fi + s] = v;
+    } else {
+      const int s = t - 36;
+      a.sys[(size_t)n * n + 6 * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
+      a.sys[(size_t)n * n + n + 6 * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
+    }
   }
 }
 
-// ---- reduced camera system: S + lambda I = L D L^T by 6 x 6 pose blocks
-// (no pivoting: the same factorisation as the oracle's scalar LDLT up to
-// rounding).  Per block step K: thread 0 factors the diagonal block; every
-// row below solves its panel row (l = v / d, v = a L_KK^-T), v kept in the
-// mirrored upper position; the trailing lower triangle takes the rank-6
-// update.  Then block-column forward / diagonal / backward substitution.
-// One block of 1024 threads, S in LDS when it fits.  Also the pose part of
-// computeScale and the positivity of the pivots.
-__global__ __launch_bounds__(1024) void k_lba_solve(LbaArgs a, double lambda, int in_lds) {
-  extern __shared__ double Sl[];
-  const int n = a.n_sys, t = threadIdx.x, nt = blockDim.x;
-  double* S = in_lds ? Sl : a.work;
-  const double* src = a.sys;
-  for (int r = t >> 5; r < n; r += nt >> 5)
-    for (int c = t & 31; c < n; c += 32) S[(size_t)r * n + c] = src[(size_t)r * n + c] + (r == c ? lambda : 0.0);
-  double* y = a.xp;
-  for (int i = t; i < n; i += nt) y[i] = src[(size_t)n * n + i];  // b_s
+// ---- reduced camera system (S + lambda I) x = b_s: L D L^T by 16 x 16 tiles
+// (linear_solver_eigen.h:93-126 factorises the same matrix with
+// SimplicialLDLT; the factorisation order here is natural, tiled).
+// Per tile step K:
+//   1. wave 0 factors the diagonal tile in registers (lane i owns row i, the
+//      pivot row broadcast by v_readlane) and inverts its unit-lower L_KK;
+//   2. the panel L_IK = A_IK L_KK^-T D_K^-1 -- v_mfma_f64_16x16x4 (A_IK
+//      times L_KK^-T, 4 k-steps), waves over tiles I;
+//   3. the trailing update A_IJ -= L_IK D_K L_JK^T for K < J <= I -- MFMA,
+//      waves over tiles.
+// Then forward / diagonal / backward substitution by tiles with the saved
+// L_KK^-1 (16 x 16 mat-vecs, no serial chains), the pose part of
+// computeScale, and the failure flag (a zero pivot: Eigen's SimplicialLDLT
+// reports NumericalIssue only for D(k,k) == 0).
+// kLds: S (n_pad x (n_pad + 1), odd stride: conflict-free tile columns) and
+// the L_KK^-1 tiles in LDS; else both in a.work.
+template <bool kLds>
+__global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
+  extern __shared__ double smem[];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const double lambda = c.lambda;
+  const int n = a.n_sys, N = a.n_pad, LD = N + 1, T = N >> 4;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 15, lk = lane >> 4;
+  double* S;
+  double* Li;
+  double* Dg;
+  double* y;
+  __shared__ double red[4];
   __shared__ int bad;
+  if constexpr (kLds) {
+    S = smem;
+    Li = smem + (size_t)N * LD;
+    Dg = Li + (size_t)T * 256;
+    y = Dg + N;
+  } else {
+    S = a.work;
+    Li = a.work + (size_t)N * LD;
+    Dg = smem;
+    y = smem + N;
+  }
+  const double* src = a.sys;
+  // S + lambda I with identity padding (D = 1, L = 0): 8 loads in flight per
+  // thread before the LDS writes
+  for (int e0 = t; e0 < N * N; e0 += 8 * kThreads) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kThreads, r = e / N, cc = e - r * N;
+      v[u] = e < N * N && r < n && cc < n ? src[(size_t)r * n + cc] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kThreads, r = e / N, cc = e - r * N;
+      if (e < N * N) S[(size_t)r * LD + cc] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
+    }
+  }
+  for (int r = t; r < N; r += kThreads) y[r] = r < n ? src[(size_t)n * n + r] : 0.0;
   if (t == 0) bad = 0;
   __syncthreads();
-  const int nb = n / 6;
-  for (int K = 0; K < nb; ++K) {
-    const int k0 = 6 * K;
-    if (t == 0) {  // scalar LDLT of the (updated) diagonal block, in registers
-      double B[6][6];
+
+  for (int K = 0; K < T; ++K) {
+    const int k0 = 16 * K;
+    if (wave == 0) {
+      double r[16];
 #pragma unroll
-      for (int r = 0; r < 6; ++r)
+      for (int j = 0; j < 16; ++j) r[j] = S[(size_t)(k0 + li) * LD + k0 + j];
+      double dmine = 0;
+      int zero = 0;
 #pragma unroll
-        for (int c = 0; c <= r; ++c) B[r][c] = S[(size_t)(k0 + r) * n + k0 + c];
+      for (int cI = 0; cI < 16; ++cI) {
+        const double dc = readlane_f64(r[cI], cI);
+        if (li == cI) dmine = dc;
+        zero |= dc == 0.0;
+        const double inv = dc != 0.0 ? 1.0 / dc : 0.0;
+        double rc[16];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double d = B[c][c];
+        for (int j = cI + 1; j < 16; ++j) rc[j] = readlane_f64(r[j], cI);
+        if (li > cI) {
+          const double l = r[cI] * inv;
 #pragma unroll
-        for (int c2 = 0; c2 < c; ++c2) d -= B[c][c2] * B[c][c2] * B[c2][c2];
-        B[c][c] = d;
-        if (!(d > 0)) bad = 1;
-#pragma unroll
-        for (int r = c + 1; r < 6; ++r) {
-          double v = B[r][c];
-#pragma unroll
-          for (int c2 = 0; c2 < c; ++c2) v -= B[r][c2] * B[c][c2] * B[c2][c2];
-          B[r][c] = d != 0 ? v / d : 0.0;
+          for (int j = cI + 1; j < 16; ++j) r[j] -= l * rc[j];
+          r[cI] = l;
         }
       }
+      if (lane < 16) {
 #pragma unroll
-      for (int r = 0; r < 6; ++r)
+        for (int j = 0; j < 16; ++j)
+          if (j < li) S[(size_t)(k0 + li) * LD + k0 + j] = r[j];
+        Dg[k0 + li] = dmine;
+      }
+      __threadfence_block();  // the rows are re-read by the other lanes
+      // L_KK^-1, column li: forward substitution, the rows of L read back
+      // with one address per step (LDS broadcast); this wave wrote them
+      double x[16];
 #pragma unroll
-        for (int c = 0; c <= r; ++c) S[(size_t)(k0 + r) * n + k0 + c] = B[r][c];
+      for (int i = 0; i < 16; ++i) x[i] = i == li ? 1.0 : 0.0;
+#pragma unroll
+      for (int i = 1; i < 16; ++i) {
+        double s = x[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) s -= S[(size_t)(k0 + i) * LD + k0 + k] * x[k];
+        x[i] = s;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Li[(size_t)K * 256 + i * 16 + li] = x[i];
+      }
+      if (lane == 0 && zero) bad = 1;
     }
     __syncthreads();
-    for (int i = k0 + 6 + t; i < n; i += nt) {  // panel rows
-      double v[6];
+    // panel: L_IK = (A_IK L_KK^-T) D_K^-1
+    for (int I = K + 1 + wave; I < T; I += 4) {
+      const int i0 = 16 * I;
+      d4 acc = {0, 0, 0, 0};
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double x = S[(size_t)i * n + k0 + c];
-        for (int c2 = 0; c2 < c; ++c2) x -= v[c2] * S[(size_t)(k0 + c) * n + k0 + c2];
-        v[c] = x;
+      for (int kc = 0; kc < 4; ++kc) {
+        const int kk = 4 * kc + lk;
+        const double av = S[(size_t)(i0 + li) * LD + k0 + kk];
+        const double bv = Li[(size_t)K * 256 + li * 16 + kk];  // (L^-1)^T[kk][li]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
+      const double dinv = 1.0 / Dg[k0 + li];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const double d = S[(size_t)(k0 + c) * n + k0 + c];
-        S[(size_t)(k0 + c) * n + i] = v[c];
-        S[(size_t)i * n + k0 + c] = d != 0 ? v[c] / d : 0.0;
-      }
+      for (int rr = 0; rr < 4; ++rr) S[(size_t)(i0 + lk + 4 * rr) * LD + k0 + li] = acc[rr] * dinv;
     }
     __syncthreads();
-    // trailing lower triangle: thread (row group t >> 5, column lane t & 31)
-    for (int ii = k0 + 6 + (t >> 5); ii < n; ii += nt >> 5) {
-      double l[6];
+    // trailing: A_IJ -= L_IK (D_K L_JK^T), tiles K < J <= I enumerated row-major
+    const int m = T - K - 1;
+    const int ntile = m * (m + 1) / 2;
+    for (int q = wave; q < ntile; q += 4) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= q) ++I;
+      const int J = q - I * (I + 1) / 2;
+      const int i0 = 16 * (K + 1 + I), j0 = 16 * (K + 1 + J);
+      d4 acc;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) l[c] = S[(size_t)ii * n + k0 + c];
-      for (int jj = k0 + 6 + (t & 31); jj <= ii; jj += 32) {
-        double acc = 0;
+      for (int rr = 0; rr < 4; ++rr) acc[rr] = S[(size_t)(i0 + lk + 4 * rr) * LD + j0 + li];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) acc += l[c] * S[(size_t)(k0 + c) * n + jj];
-        S[(size_t)ii * n + jj] -= acc;
+      for (int kc = 0; kc < 4; ++kc) {
+        const int kk = 4 * kc + lk;
+        const double av = -S[(size_t)(i0 + li) * LD + k0 + kk];
+        const double bv = S[(size_t)(j0 + li) * LD + k0 + kk] * Dg[k0 + kk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) S[(size_t)(i0 + lk + 4 * rr) * LD + j0 + li] = acc[rr];
     }
     __syncthreads();
   }
-  // forward: unit lower L, block columns
-  for (int K = 0; K < nb; ++K) {
-    const int k0 = 6 * K;
-    if (t == 0) {
-      double yy[6];
+  // forward: L y = b_s
+  for (int K = 0; K < T; ++K) {
+    const int k0 = 16 * K;
+    if (t < 16) {
+      double s = 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) yy[c] = y[k0 + c];
-#pragma unroll
-      for (int c = 1; c < 6; ++c)
-#pragma unroll
-        for (int c2 = 0; c2 < c; ++c2) yy[c] -= S[(size_t)(k0 + c) * n + k0 + c2] * yy[c2];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) y[k0 + c] = yy[c];
+      for (int k = 0; k < 16; ++k) s += Li[(size_t)K * 256 + t * 16 + k] * y[k0 + k];
+      __builtin_amdgcn_wave_barrier();
+      y[k0 + t] = s;
     }
     __syncthreads();
-    for (int i = k0 + 6 + t; i < n; i += nt) {
-      double acc = 0;
+    for (int r = k0 + 16 + t; r < N; r += kThreads) {
+      double s = 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) acc += S[(size_t)i * n + k0 + c] * y[k0 + c];
-      y[i] -= acc;
+      for (int k = 0; k < 16; ++k) s += S[(size_t)r * LD + k0 + k] * y[k0 + k];
+      y[r] -= s;
     }
     __syncthreads();
   }
-  for (int i = t; i < n; i += nt) {
-    const double d = S[(size_t)i * n + i];
-    y[i] = d != 0 ? y[i] / d : 0.0;
-  }
+  for (int r = t; r < N; r += kThreads) y[r] = Dg[r] != 0.0 ? y[r] / Dg[r] : 0.0;
   __syncthreads();
-  // backward: L^T, block columns from the last
-  for (int K = nb - 1; K >= 0; --K) {
-    const int k0 = 6 * K;
-    if (t == 0) {
-      double yy[6];
+  // backward: L^T x = y
+  for (int K = T - 1; K >= 0; --K) {
+    const int k0 = 16 * K;
+    if (t < 16) {
+      double s = 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) yy[c] = y[k0 + c];
-#pragma unroll
-      for (int c = 4; c >= 0; --c)
-#pragma unroll
-        for (int c2 = c + 1; c2 < 6; ++c2) yy[c] -= S[(size_t)(k0 + c2) * n + k0 + c] * yy[c2];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) y[k0 + c] = yy[c];
+      for (int k = 0; k < 16; ++k) s += Li[(size_t)K * 256 + k * 16 + t] * y[k0 + k];
+      __builtin_amdgcn_wave_barrier();
+      y[k0 + t] = s;
     }
     __syncthreads();
-    for (int r = t; r < k0; r += nt) {
-      double acc = 0;
+    for (int r = t; r < k0; r += kThreads) {
+      double s = 0;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) acc += S[(size_t)(k0 + c) * n + r] * y[k0 + c];
-      y[r] -= acc;
+      for (int k = 0; k < 16; ++k) s += S[(size_t)(k0 + k) * LD + r] * y[k0 + k];
+      y[r] -= s;
     }
     __syncthreads();
   }
+  // x_p and the pose part of computeScale: x . (lambda x + b_p)
+  double sc = 0;
+  for (int r = t; r < n; r += kThreads) {
+    const double xv = y[r];
+    a.xp[r] = xv;
+    sc += xv * (lambda * xv + src[(size_t)n * n + n + r]);
+  }
+  double v[1] = {sc};
+  block_sum<1>(v, red);
   if (t == 0) {
-    double sc = 0;  // x_p . (lambda x_p + b_p)
-    for (int i = 0; i < n; ++i) sc += y[i] * (lambda * y[i] + src[(size_t)n * n + n + i]);
-    a.scal[0] = sc;
-    if (bad) a.flags[0] = 1;
+    a.scal[0] = v[0];
+    a.scal[1] = bad;
   }
 }
 
-// ---- back-substitution and trial state: one thread per point (x_l, trial
-// point, landmark part of computeScale) ...
-__global__ __launch_bounds__(kLbaThreads) void k_lba_backsub(LbaArgs a, double lambda,
-                                                             const double* __restrict__ pts,
-                                                             double* __restrict__ pts_trial) {
-  __shared__ double red[4];
-  const int p = blockIdx.x * kLbaThreads + threadIdx.x;
-  double sl = 0;
-  if (p < a.n_pts) {
-    double cp[3] = {a.bl[3 * (size_t)p], a.bl[3 * (size_t)p + 1], a.bl[3 * (size_t)p + 2]};
-    for (int i = a.pt_begin[p]; i < a.pt_begin[p + 1]; ++i) {
-      const int h = a.hidx[a.edges[i].kf];
-      if (h < 0) continue;
-      const double* B = a.hpl + 18 * (size_t)i;
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int s = 0; s < 6; ++s) cp[c] -= B[3 * s + c] * a.xp[6 * h + s];
-    }
-    const double* Di = a.dinv + 9 * (size_t)p;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const double v = Di[3 * r] * cp[0] + Di[3 * r + 1] * cp[1] + Di[3 * r + 2] * cp[2];
-      pts_trial[3 * (size_t)p + r] = pts[3 * (size_t)p + r] + v;
-      sl += v * (lambda * v + a.bl[3 * (size_t)p + r]);
-    }
-  }
-  const double s = lba_block_sum(sl, red);
-  lba_finish_sum(s, a.partials, a.counter, a.scal + 1);
-}
-
-// ... and one thread per keyframe: T' = exp(x_p) T for free poses.
-__global__ __launch_bounds__(64) void k_lba_pose_update(LbaArgs a, const double* __restrict__ poses,
-                                                        double* __restrict__ poses_trial) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= a.n_kf) return;
+// ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
+__device__ __forceinline__ void trial_pose(const LbaArgs& a, int s0, int k, double* out) {
+  Se3 T = load_pose(a.poses[s0] + 7 * k);
   const int h = a.hidx[k];
-  Se3 T = load_pose(poses + 7 * k);
   if (h >= 0) {
     double u[6];
 #pragma unroll
     for (int s = 0; s < 6; ++s) u[s] = a.xp[6 * h + s];
     T = se3_compose(se3_exp<false>(u), T);
   }
-  store_pose(T, poses_trial + 7 * k);
+  store_pose(T, out);
+}
+
+// windows with more keyframes than the LDS table holds: the trial poses go
+// to the state buffer first
+__global__ __launch_bounds__(kThreads) void k_lba_trial_poses(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  if (k < a.n_kf) trial_pose(a, c.state, k, a.poses[c.state ^ 1] + 7 * k);
+}
+
+// ---- one LM trial, edge side: back-substitution x_l = Dinv (b_l - sum
+// Hpl^T x_p) of the edge's point (recomputed by each of its edges; the first
+// edge writes the point), the edge's error and robust chi2 at the trial state
+// (computeActiveErrors), the landmark part of computeScale; the last block
+// sums the partials in block order and takes the LM decision.
+__global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
+  __shared__ double tp[kMaxKfLds * 7];
+  __shared__ double red[4 * 3];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const double lambda = c.lambda;
+  const int s0 = c.state, s1 = s0 ^ 1;
+  const bool lds_poses = a.n_kf <= kMaxKfLds;
+  if (lds_poses) {
+    for (int k = threadIdx.x; k < a.n_kf; k += kThreads) {
+      trial_pose(a, s0, k, tp + 7 * k);
+      if (blockIdx.x == 0)
+#pragma unroll
+        for (int q = 0; q < 7; ++q) a.poses[s1][7 * k + q] = tp[7 * k + q];
+    }
+    __syncthreads();
+  }
+  const double* tposes = lds_poses ? tp : a.poses[s1];
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  double part[3] = {0, 0, 0};  // robust chi2, landmark scale, singular landmark blocks
+  if (i < a.n_edges) {
+    const LbaEdgeDev e = a.edges[i];
+    const int p = e.point;
+    const int e0 = a.pt_begin[p], e1 = a.pt_begin[p + 1];
+    const double* blp = a.bl + 3 * (size_t)p;
+    double cp[3] = {blp[0], blp[1], blp[2]};
+    for (int base = e0; base < e1; base += 4) {  // four edges' loads in flight
+      int fs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) fs[u] = base + u < e1 ? a.ef[base + u] : -1;
+      double B[4][18], xv[4][6];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 18; ++q) B[u][q] = fs[u] >= 0 ? a.hpl[18 * (size_t)(base + u) + q] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) xv[u][q] = fs[u] >= 0 ? a.xp[6 * fs[u] + q] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (fs[u] >= 0)
+#pragma unroll
+          for (int b2 = 0; b2 < 3; ++b2)
+#pragma unroll
+            for (int s = 0; s < 6; ++s) cp[b2] -= B[u][3 * s + b2] * xv[u][s];
+    }
+    double Di[9];
+    const double det = inv3_lambda(a.hll + 9 * (size_t)p, lambda, Di);
+    const double* X0 = a.pts[s0] + 3 * (size_t)p;
+    double X[3], v[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      v[r] = Di[3 * r] * cp[0] + Di[3 * r + 1] * cp[1] + Di[3 * r + 2] * cp[2];
+      X[r] = X0[r] + v[r];
+    }
+    if (i == e0) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        a.pts[s1][3 * (size_t)p + r] = X[r];
+        part[1] += v[r] * (lambda * v[r] + blp[r]);
+      }
+      part[2] = det == 0 ? 1.0 : 0.0;
+    }
+    const Se3 T = load_pose(tposes + 7 * e.kf);
+    double err[3];
+    lba_error(e, T, X, a.cam, err);
+    a.err[3 * i] = err[0];
+    a.err[3 * i + 1] = err[1];
+    a.err[3 * i + 2] = err[2];
+    double w;
+    huber_rho(lba_chi2(e, err), lba_delta(e), part[0], w);
+  }
+  block_sum<3>(part, red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.partials[3 * blockIdx.x + k] = part[k];
+  if (!last_block(a.counter + 2)) return;
+  double s[3];
+  sum_partials<3>(a.partials, gridDim.x, s, red);
+  if (threadIdx.x == 0) {
+    if (a.n_edgeless > 0) {  // points without edges: (0 + lambda I)^-1
+      const double h0[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      double Di[9];
+      if (inv3_lambda(h0, lambda, Di) == 0) s[2] += 1;
+    }
+    const int stop = host_stop(a);
+    if (a.sharded) {
+      a.red[0] = s[0];
+      a.red[1] = s[1];
+      a.red[2] = s[2];
+      a.red[3] = stop;
+    } else {
+      ctl_decide(a, s[0], s[1], s[2] > 0 || a.scal[1] != 0, stop);
+    }
+  }
+}
+
+// ---- LM decisions of a point-sharded run, after the host's all-reduce
+__global__ void k_lba_ctl(LbaArgs a, int mode) {
+  if (threadIdx.x != 0) return;
+  LbaCtrl& c = *a.ctrl;
+  if (mode == kCtlInit) {
+    ctl_init(a, a.red[0], a.red[1] > 0);
+    return;
+  }
+  if (c.done) return;
+  if (mode == kCtlLambda) {
+    double m = a.diag[a.n_sys];
+    for (int k = 0; k < a.n_sys; ++k) m = fmax(m, fabs(a.diag[k]));
+    if (c.it == 0) ctl_lambda(a, m);
+    return;
+  }
+  ctl_decide(a, a.red[0], a.red[1], a.red[2] > 0 || a.scal[1] != 0, a.red[3] > 0);
 }
 
 // ---- optimizer.cc:1362-1400: chi2 of the last computeActiveErrors, depth at
-// the final estimates.
-__global__ __launch_bounds__(kLbaThreads) void k_lba_classify(LbaArgs a, const double* __restrict__ poses,
-                                                              const double* __restrict__ pts,
-                                                              uint8_t* __restrict__ outlier) {
-  const int i = blockIdx.x * kLbaThreads + threadIdx.x;
+// the final estimates; the final state copied out in one buffer.
+__global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* __restrict__ outlier,
+                                                           double* __restrict__ out) {
+  const int s = a.ctrl->state;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i < 7 * a.n_kf) out[i] = a.poses[s][i];
+  if (i < 3 * a.n_pts) out[7 * (size_t)a.n_kf + i] = a.pts[s][i];
   if (i >= a.n_edges) return;
   const LbaEdgeDev e = a.edges[i];
-  const Se3 T = load_pose(poses + 7 * e.kf);
-  const double X[3] = {pts[3 * e.point], pts[3 * e.point + 1], pts[3 * e.point + 2]};
+  const Se3 T = load_pose(a.poses[s] + 7 * e.kf);
+  const double* x = a.pts[s] + 3 * e.point;
+  const double X[3] = {x[0], x[1], x[2]};
   double tmp[3];
   const bool depth = lba_error(e, T, X, a.cam, tmp);
   const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
@@ -618,58 +1020,65 @@ inline unsigned blocks(long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 }  // namespace
 
-hipError_t lba_errors(const LbaArgs& a, const double* poses, const double* pts, double* out,
-                      hipStream_t st) {
-  hipLaunchKernelGGL(k_lba_errors, dim3(blocks(a.n_edges > 0 ? a.n_edges : 1, kLbaThreads)),
-                     dim3(kLbaThreads), 0, st, a, poses, pts, out);
+size_t lba_solve_lds_bytes(int n_pad) {
+  const size_t T = (size_t)n_pad / 16;
+  return 8 * ((size_t)n_pad * (n_pad + 1) + T * 256 + 2 * (size_t)n_pad);
+}
+
+hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_lba_begin, dim3(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads)), dim3(kThreads),
+                     0, st, a);
   return hipGetLastError();
 }
 
-hipError_t lba_build(const LbaArgs& a, const double* poses, const double* pts, hipStream_t st) {
+hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
   if (a.n_edges > 0)
-    hipLaunchKernelGGL(k_lba_linearize, dim3(blocks(a.n_edges, kLbaThreads)), dim3(kLbaThreads), 0, st,
-                       a, poses, pts);
-  if (a.n_pts > 0)
-    hipLaunchKernelGGL(k_lba_point_sum, dim3(blocks(a.n_pts, kLbaThreads)), dim3(kLbaThreads), 0, st, a);
-  if (a.n_free > 0)
-    hipLaunchKernelGGL(k_lba_pose_sum, dim3(a.n_free), dim3(kLbaThreads), 0, st, a);
+    hipLaunchKernelGGL(k_lba_linearize, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(k_lba_sums, dim3(a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads)),
+                     dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t lba_schur(const LbaArgs& a, double lambda, hipStream_t st) {
-  if (a.n_pts > 0)
-    hipLaunchKernelGGL(k_lba_schur_points, dim3(blocks(a.n_pts, kLbaThreads)), dim3(kLbaThreads), 0,
-                       st, a, lambda);
-  if (a.n_pairs > 0)
-    hipLaunchKernelGGL(k_lba_schur_pairs, dim3(a.n_pairs), dim3(kLbaThreads), 0, st, a);
+hipError_t lba_schur(const LbaArgs& a, hipStream_t st) {
+  if (a.n_pairs > 0) hipLaunchKernelGGL(k_lba_schur, dim3(a.n_pairs), dim3(kSchurThreads), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t lba_solve(const LbaArgs& a, double lambda, hipStream_t st) {
-  const size_t lds = (size_t)a.n_sys * a.n_sys * sizeof(double);
-  const int in_lds = lds <= 150 * 1024 ? 1 : 0;
-  if (in_lds && lds > 64 * 1024) {
-    if (lds_optin(reinterpret_cast<const void*>(&k_lba_solve), 150 * 1024) != hipSuccess)
+hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
+  if (a.solve_lds) {
+    const size_t lds = lba_solve_lds_bytes(a.n_pad);
+    if (lds > 64 * 1024 &&
+        lds_optin(reinterpret_cast<const void*>(&k_lba_solve<true>), (int)lds) != hipSuccess)
       return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_lba_solve<true>, dim3(1), dim3(kThreads), lds, st, a);
+  } else {
+    hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kThreads), 16 * (size_t)a.n_pad, st, a);
   }
-  hipLaunchKernelGGL(k_lba_solve, dim3(1), dim3(1024), in_lds ? lds : 0, st, a, lambda, in_lds);
+  if (a.n_kf > kMaxKfLds)
+    hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL(k_lba_trial, dim3(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads)), dim3(kThreads),
+                     0, st, a);
   return hipGetLastError();
 }
 
-hipError_t lba_trial(const LbaArgs& a, double lambda, const double* poses, const double* pts,
-                     double* poses_trial, double* pts_trial, hipStream_t st) {
-  hipLaunchKernelGGL(k_lba_backsub, dim3(blocks(a.n_pts > 0 ? a.n_pts : 1, kLbaThreads)),
-                     dim3(kLbaThreads), 0, st, a, lambda, pts, pts_trial);
-  hipLaunchKernelGGL(k_lba_pose_update, dim3(blocks(a.n_kf, 64)), dim3(64), 0, st, a, poses,
-                     poses_trial);
+hipError_t lba_step(const LbaArgs& a, hipStream_t st) {
+  hipError_t e = lba_build(a, st);
+  if (e == hipSuccess) e = lba_schur(a, st);
+  if (e == hipSuccess) e = lba_solve_trial(a, st);
+  return e;
+}
+
+hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st) {
+  hipLaunchKernelGGL(k_lba_ctl, dim3(1), dim3(64), 0, st, a, mode);
   return hipGetLastError();
 }
 
-hipError_t lba_classify(const LbaArgs& a, const double* poses, const double* pts, uint8_t* outlier,
-                        hipStream_t st) {
-  if (a.n_edges > 0)
-    hipLaunchKernelGGL(k_lba_classify, dim3(blocks(a.n_edges, kLbaThreads)), dim3(kLbaThreads), 0, st,
-                       a, poses, pts, outlier);
+hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st) {
+  long n = a.n_edges;
+  if (7L * a.n_kf > n) n = 7L * a.n_kf;
+  if (3L * a.n_pts > n) n = 3L * a.n_pts;
+  hipLaunchKernelGGL(k_lba_classify, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0, st, a,
+                     outlier, out);
   return hipGetLastError();
 }
 

@@ -1,13 +1,24 @@
 // Device-side layout of one LocalBundleAdjustment call (lba_kernels.hip) and
 // the host launchers lba_api.cpp drives.
+//
+// The g2o Levenberg-Marquardt loop (optimization_algorithm_levenberg.cpp:59-168)
+// runs on the device: its state (lambda, ni, current chi2, trial / iteration
+// counters, the stop decision) lives in LbaCtrl and every kernel reads it at
+// entry; a kernel whose stage is not due (the optimisation is done, or the
+// system is already built this iteration) returns at once.  The host only
+// queues "steps" (build + one LM trial) a few ahead of the device and stops
+// when the device reports done through a host-mapped word.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace orbgpu {
 
-struct LbaEdgeDev {  // == orbgpu_lba_edge, point index local to the shard
-  int32_t point, kf;
+struct LbaEdgeDev {  // one observation of the shard, point-major (insertion order in a point)
+  int32_t point;     // shard-local point index
+  int32_t kf;        // keyframe index
+  int32_t f;         // free-pose (Hessian) index, -1 = fixed keyframe
+  int32_t pad;
   float u, v, ur, inv_sigma2;
 };
 
@@ -15,46 +26,69 @@ struct LbaCamDev {
   double fx, fy, cx, cy, bf;
 };
 
+// LM state (one per call, device memory).  Written only by the single thread
+// that takes an LM decision (last block of a stage, or k_lba_ctl when sharded).
+struct LbaCtrl {
+  double lambda, ni, cur, ini, chi_init, user_lambda;
+  int it, q, nbad, need_build, done, state, iters_done, trials, max_iters, stopped;
+};
+
+// LM decision points whose inputs a point-sharded run all-reduces first
+enum LbaCtlMode { kCtlInit = 0, kCtlLambda = 1, kCtlDecide = 2 };
+
+// host-mapped progress word: (done << 32) | trials completed
+struct LbaHostWords {
+  unsigned long long progress;
+  uint32_t stop;  // mirror of the caller's *pbStopFlag, read by the device
+  uint32_t pad;
+};
+
 struct LbaArgs {
   LbaCamDev cam;
   int n_kf, n_pts, n_edges, n_free, n_sys, n_pairs;
-  const LbaEdgeDev* edges;   // this shard's edges, point-major (insertion order in a point)
-  const int* pt_begin;       // [n_pts + 1] CSR of edges per point
+  int sharded;               // 1: LM decisions wait for the host's all-reduce (k_lba_ctl)
+  int solve_lds;             // 1: the reduced system is factorised in LDS
+  int n_pad;                 // n_sys rounded up to the 16-wide MFMA tile
+  int n_edgeless;            // points of the shard with no edge (their Hll is 0)
+  const LbaEdgeDev* edges;   // [n_edges]
   const int* hidx;           // [n_kf] free-pose index, -1 = fixed
+  const int* pt_begin;       // [n_pts + 1] CSR of edges per point
   const int* pose_begin;     // [n_free + 1] CSR of edges per free pose
-  const int* pose_edges;     //   edge indices (ascending)
-  const int* pair_i;         // [n_pairs] free-pose pairs (i <= j) sharing points
+  const int4* pslot;         //   {edge, point, point's first edge, end} (edge ascending)
+  const int* ef;             // [n_edges] free-pose index of each edge (edges[i].f, packed)
+  const int* pair_i;         // [n_pairs] free-pose pairs (i <= j), row-major upper triangle
   const int* pair_j;
-  const int* pair_begin;     // [n_pairs + 1] CSR of (edge of i, edge of j) entries
-  const int* pair_ei;
-  const int* pair_ej;
-  double* err;       // [3 E] errors of the last computeActiveErrors
-  double* hpl;       // [18 E] Hpl = Jp^T W Jl (6 x 3)
-  double* hpp_e;     // [27 E] per-edge Hpp (lower, 21) + bp (6) terms
-  double* hll_e;     // [12 E] per-edge Hll (9) + bl (3) terms
-  double* hll;       // [9 P]
-  double* bl;        // [3 P]
-  double* dinv;      // [9 P]
-  double* hpp;       // [36 F] full 6 x 6 per free pose
-  double* bp;        // [6 F]
-  double* diag;      // [n_sys + 1]: Hpp diagonal (sum-reduced), Hll max (max-reduced)
-  double* sys;       // [n_sys^2 + 2 n_sys]: S, b_s, b_p  (the reduced buffer)
-  double* work;      // [n_sys^2] factorisation when S does not fit LDS
-  double* xp;        // [n_sys]
-  double* scal;      // [4]: pose scale part, landmark scale part, chi2 out, spare
-  double* partials;  // block partial sums
-  unsigned* counter; // last-block-done counter (self-resetting)
-  int* flags;        // [1]: solve / landmark-inverse failure of the current trial
+  double* poses[2];          // [7 n_kf] current / trial state (ctrl.state selects)
+  double* pts[2];            // [3 n_pts]
+  double* err;               // [3 E] errors of the last computeActiveErrors
+  double* hpl;               // [18 E] Hpl = Jp^T W Jl (6 x 3), free-pose edges only
+  double* hpp_e;             // [27 E] per-edge Hpp (lower, 21) + bp (6) terms
+  double* hll_e;             // [12 E] per-edge Hll (9) + bl (3) terms
+  double* hll;               // [9 P]
+  double* bl;                // [3 P]
+  double* hpp;               // [36 F] full 6 x 6 per free pose
+  double* bp;                // [6 F]
+  double* diag;              // [n_sys + 1]: Hpp diagonal | Hll max  (lambda init, reduced)
+  double* sys;               // [n_sys^2 + 2 n_sys]: S | b_s | b_p  (reduced per trial)
+  double* work;              // [n_pad (n_pad + 1)] factorisation when S does not fit LDS
+  double* xp;                // [n_sys] pose step
+  double* red;               // [4]: init / trial reduce buffer (chi2, landmark scale, bad, stop)
+  double* scal;              // [2]: pose part of computeScale, solve failure
+  double* partials;          // block partials (2 per block)
+  unsigned* counter;         // last-block-done tickets (self-resetting), one per stage
+  LbaCtrl* ctrl;
+  LbaHostWords* host;        // host-mapped
 };
 
-hipError_t lba_errors(const LbaArgs& a, const double* poses, const double* pts, double* out,
-                      hipStream_t st);
-hipError_t lba_build(const LbaArgs& a, const double* poses, const double* pts, hipStream_t st);
-hipError_t lba_schur(const LbaArgs& a, double lambda, hipStream_t st);
-hipError_t lba_solve(const LbaArgs& a, double lambda, hipStream_t st);
-hipError_t lba_trial(const LbaArgs& a, double lambda, const double* poses, const double* pts,
-                     double* poses_trial, double* pts_trial, hipStream_t st);
-hipError_t lba_classify(const LbaArgs& a, const double* poses, const double* pts, uint8_t* outlier,
-                        hipStream_t st);
+hipError_t lba_begin(const LbaArgs& a, hipStream_t st);   // initial errors + LM state
+hipError_t lba_step(const LbaArgs& a, hipStream_t st);    // build (if due) + one trial
+// sharded pieces (the host all-reduces between them)
+hipError_t lba_build(const LbaArgs& a, hipStream_t st);
+hipError_t lba_schur(const LbaArgs& a, hipStream_t st);
+hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st);
+hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
+// outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles)
+hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st);
+size_t lba_solve_lds_bytes(int n_pad);
 
 }  // namespace orbgpu

@@ -39,7 +39,14 @@ def dist_reduce(group=None):
 
     def reduce(buf, op: int) -> None:
         t = torch.from_numpy(buf) if isinstance(buf, np.ndarray) else buf
-        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM, group=group)
+        rop = dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM
+        if t.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo moves host memory: stage the device buffer through the host
+            h = t.cpu()
+            dist.all_reduce(h, op=rop, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=rop, group=group)
         if t.is_cuda:
             torch.cuda.synchronize(t.device)
 
@@ -64,11 +71,14 @@ class LocalBundleAdjuster:
             pass
 
     def optimize(self, problem, iterations: int = 10, pt_range=None, group=None,
-                 stop_flag: Optional[ctypes.c_uint8] = None) -> dict:
+                 stop_flag: Optional[ctypes.c_uint8] = None, lambda_init: float = 0.0) -> dict:
         """Returns {"poses": float32 [n_kf, 7], "poses_d": float64 [n_kf, 7],
         "pts": float32 [n_pts, 3] (this shard's rows), "outlier": uint8 [E]
         (this shard's edges), "stats": float64 [6]}.  ``group``: a
-        torch.distributed group whose ranks hold the other point shards."""
+        torch.distributed group whose ranks hold the other point shards.
+        ``lambda_init`` > 0: g2o's setUserLambdaInit (100 for an inertial map,
+        optimizer.cc:1137).  ``stop_flag``: the reference's pbStopFlag, read
+        by the device where g2o polls terminate()."""
         cam = Camera(*[float(v) for v in problem.cam])
         poses = np.ascontiguousarray(problem.poses_init, np.float32)
         fixed = np.ascontiguousarray(problem.fixed, np.uint8)
@@ -100,7 +110,7 @@ class LocalBundleAdjuster:
         check(
             lib().orbgpu_lba_optimize(
                 self._h, ctypes.byref(cam), n_kf, ptr(poses), ptr(fixed), n_pts, ptr(pts), ne,
-                ptr(edges), b, e, iterations,
+                ptr(edges), b, e, iterations, float(lambda_init),
                 ctypes.cast(ctypes.byref(stop_flag), ctypes.c_void_p) if stop_flag is not None else None,
                 cb, None, ptr(po), ptr(pd), ptr(xo), ptr(out), ptr(st),
             ),

@@ -124,7 +124,7 @@ void Optimizer::LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap
   static_assert(sizeof(bool) == 1, "pbStopFlag is read as one byte by the ABI");
   if (orbgpu_lba_optimize(lba_thread_ctx(), &cam, (int)kfs.size(), poses.data(), fixed.data(),
                           (int)mps.size(), pts.data(), (int)edges.size(), edges.data(), 0,
-                          (int)mps.size(), 10,
+                          (int)mps.size(), 10, pMap->IsInertial() ? 100.0 : 0.0,  // :1137
                           reinterpret_cast<const volatile uint8_t *>(pbStopFlag), nullptr, nullptr,
                           poses_out.data(), nullptr, pts_out.data(), outlier.data(),
                           nullptr) != ORBGPU_OK)

@@ -1,0 +1,37 @@
+"""Child process of tests/test_gpu_lba.py::test_lba_two_ranks_one_gpu: one
+rank of a point-sharded LocalBundleAdjustment on cuda:0, the
+shard sums completed by the product's reduce hook (lba.dist_reduce) over a
+gloo group.  Started as a fresh interpreter before it touches the GPU.
+
+    python tests/lba_shard_worker.py RANK WORLD PORT OUT_DIR
+"""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+
+def main() -> None:
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], Path(sys.argv[4])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    import torch.distributed as dist
+
+    from orb_slam_fusion_amd import LocalBundleAdjuster, synth
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = synth.lba_problem()  # C4: 20 KF, 3000 MP, 18000 edges
+    n = len(p.pts_init)
+    cut = [0, n // 2 + 13, n]  # uneven shards on purpose
+    r = LocalBundleAdjuster(0).optimize(p, pt_range=(cut[rank], cut[rank + 1]), group=dist.group.WORLD)
+    np.savez(out / f"r{rank}.npz", poses_d=r["poses_d"], pts=r["pts"], outlier=r["outlier"],
+             stats=r["stats"], cut=np.array(cut))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,8 +1,11 @@
 """GPU LocalBundleAdjustment (orbgpu_lba_optimize) vs the oracle on the same
 windows.  Floating point, so parity is by tolerance: the GPU sums in a
-different (fixed) order and factors the reduced camera system right-looking;
-poses and points agree to ~1e-6 relative, the LM path (iterations, trials)
-and the outlier flags away from the thresholds agree exactly."""
+different (fixed) order and factors the reduced camera system by 16 x 16
+MFMA tiles; poses and points agree to ~1e-6 relative, the LM path
+(iterations, trials) and the outlier flags away from the thresholds agree
+exactly.  The LM loop runs on the device (lba_kernels.hip): the stop flag,
+the user lambda, the LDS / global solver paths and the point-sharded
+two-rank run are each checked against the oracle or the one-rank result."""
 import sys
 from pathlib import Path
 
@@ -23,9 +26,9 @@ def _quat_sign(q, ref):
     return q if np.dot(q[:4], ref[:4]) >= 0 else np.concatenate([-q[:4], q[4:]])
 
 
-def _compare(p, iters=10, tol=1e-6):
-    ref = oracle.lba(p, iters=iters)
-    got = LocalBundleAdjuster().optimize(p, iterations=iters)
+def _compare(p, iters=10, tol=1e-6, lambda_init=0.0):
+    ref = oracle.lba(p, iters=iters, lambda_init=lambda_init)
+    got = LocalBundleAdjuster().optimize(p, iterations=iters, lambda_init=lambda_init)
     assert got["stats"][2] == ref["stats"][2]  # LM iterations
     assert got["stats"][3] == ref["stats"][3]  # trials
     assert abs(got["stats"][1] - ref["stats"][1]) <= tol * ref["stats"][1]
@@ -86,3 +89,98 @@ def test_lba_shard_with_identity_reduce_matches(gpu_available):
     odist.finalize()
     assert np.array_equal(got["poses_d"], ref["poses_d"])
     assert np.array_equal(got["pts"], ref["pts"])
+
+
+def test_lba_inertial_map_user_lambda(gpu_available):
+    """setUserLambdaInit(100.0) when the map is inertial (optimizer.cc:1137)."""
+    got, ref = _compare(synth.lba_problem(seed=6, n_kf=10, n_pts=600, obs_per_pt=4, n_fixed=2),
+                        lambda_init=100.0)
+    assert got["stats"][3] == ref["stats"][3]
+
+
+def test_lba_large_window_global_solver(gpu_available):
+    """28 free keyframes: the 168 x 168 reduced system exceeds the LDS budget and
+    is factorised from global memory (k_lba_solve<false>)."""
+    _compare(synth.lba_problem(seed=9, n_kf=30, n_pts=1500, obs_per_pt=5, n_fixed=2))
+
+
+def test_lba_many_fixed_keyframes(gpu_available):
+    """More keyframes than the trial-pose LDS table holds (k_lba_trial_poses)."""
+    _compare(synth.lba_problem(seed=10, n_kf=1100, n_pts=2200, obs_per_pt=3, n_fixed=1092))
+
+
+def test_lba_stop_flag_mid_run(gpu_available):
+    """*pbStopFlag flipped by another thread while optimize runs (LocalMapping's
+    flag, set from Tracking, localmapping.cc:226).  The device reads it where g2o
+    polls terminate(); the state must equal the oracle stopped after the same
+    number of trials."""
+    import ctypes
+    import threading
+    import time
+
+    p = synth.lba_problem(seed=9, n_kf=30, n_pts=1500, obs_per_pt=5, n_fixed=2)
+    lba = LocalBundleAdjuster()
+    full = lba.optimize(p)
+    t0 = time.perf_counter()
+    lba.optimize(p)
+    span = time.perf_counter() - t0
+    seen = set()
+    for frac in np.linspace(0.05, 0.95, 12):
+        flag = ctypes.c_uint8(0)
+        go = threading.Event()
+
+        def flip(delay=frac * span, flag=flag, go=go):
+            go.wait()
+            time.sleep(delay)  # releases the GIL: the main thread is inside the C call
+            flag.value = 1
+
+        th = threading.Thread(target=flip)
+        th.start()
+        go.set()
+        got = lba.optimize(p, stop_flag=flag)
+        th.join()
+        trials = int(got["stats"][3])
+        seen.add(trials)
+        ref = oracle.lba(p, stop_after_trials=trials)
+        assert got["stats"][2] == ref["stats"][2] and got["stats"][3] == ref["stats"][3]
+        for k in range(len(p.poses_init)):
+            g = _quat_sign(got["poses_d"][k], ref["poses"][k])
+            assert np.allclose(g, ref["poses"][k], rtol=1e-6, atol=1e-6), k
+        assert np.allclose(got["pts"], ref["pts"], rtol=1e-5, atol=1e-5)
+    assert any(0 < t < full["stats"][3] for t in seen), (seen, full["stats"][3])
+
+
+def test_lba_two_ranks_one_gpu(gpu_available, tmp_path):
+    """The point-sharded C4 window on two ranks (fresh child processes, both on
+    cuda:0), partial reduced camera systems / chi2 / LM scale summed through
+    lba.dist_reduce over gloo (optimizer.cc:1359-1360, block_solver.hpp:383-460
+    split by points): the same LM path and state as the one-rank GPU run."""
+    import os
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    worker = REPO / "tests" / "lba_shard_worker.py"
+    procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), str(tmp_path)],
+                              env=env) for r in range(2)]
+    for pr in procs:
+        assert pr.wait(timeout=100) == 0
+    r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
+    p = synth.lba_problem()
+    single = LocalBundleAdjuster().optimize(p)
+    cut = r[0]["cut"]
+    assert (r[0]["poses_d"] == r[1]["poses_d"]).all()  # every rank solves the same system
+    for k in range(2):
+        assert (r[k]["stats"][1:5] == r[0]["stats"][1:5]).all()
+    assert r[0]["stats"][2] == single["stats"][2] and r[0]["stats"][3] == single["stats"][3]
+    assert abs(r[0]["stats"][1] - single["stats"][1]) <= 1e-9 * single["stats"][1]
+    assert np.allclose(r[0]["poses_d"], single["poses_d"], rtol=1e-9, atol=1e-12)
+    pts = np.concatenate([r[0]["pts"][cut[0]:cut[1]], r[1]["pts"][cut[1]:cut[2]]])
+    assert np.allclose(pts, single["pts"], rtol=1e-6, atol=1e-6)
+    owner = (p.edges["point"] >= cut[1]).astype(int)
+    outl = np.where(owner == 0, r[0]["outlier"], r[1]["outlier"])
+    assert (outl == single["outlier"]).all()

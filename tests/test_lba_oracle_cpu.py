@@ -188,3 +188,37 @@ def test_sharded_reduce_matches_single():
     own = p.edges["point"] < cut
     outl = np.where(own, res[0]["outlier"], res[1]["outlier"])
     assert (outl == single["outlier"]).all()
+
+
+def test_oracle_stop_after_trials():
+    """terminate() polled before every iteration and after every trial
+    (sparse_optimizer.cpp:406, optimization_algorithm_levenberg.cpp:153-154):
+    stopping after k trials runs exactly min(k, all) trials, and on an
+    iteration boundary equals optimize(k')."""
+    from orb_slam_fusion_amd import synth
+
+    p = synth.lba_problem(seed=3, n_kf=8, n_pts=400, obs_per_pt=4, n_fixed=1, outlier_pct=10)
+    full = oracle.lba(p)
+    zero = oracle.lba(p, stop_after_trials=0)
+    assert zero["stats"][2] == 0 and zero["stats"][3] == 0
+    assert np.allclose(zero["poses"], p.poses_init.astype(np.float64))
+    for k in range(1, int(full["stats"][3]) + 2):
+        r = oracle.lba(p, stop_after_trials=k)
+        assert r["stats"][3] == min(k, full["stats"][3])
+        its = int(r["stats"][2])
+        same = oracle.lba(p, iters=its)
+        if same["stats"][3] == r["stats"][3]:  # the stop fell on an iteration boundary
+            assert np.array_equal(same["poses"], r["poses"]) and np.array_equal(same["pts"], r["pts"])
+
+
+def test_oracle_user_lambda():
+    """setUserLambdaInit(100) (inertial map, optimizer.cc:1137) starts the LM from
+    lambda = 100 instead of tau * max diag and still converges."""
+    from orb_slam_fusion_amd import synth
+
+    p = synth.lba_problem(seed=6, n_kf=10, n_pts=600, obs_per_pt=4, n_fixed=2)
+    a = oracle.lba(p)
+    b = oracle.lba(p, lambda_init=100.0)
+    assert b["stats"][1] < b["stats"][0] and not np.array_equal(a["poses"], b["poses"])
+    one = oracle.lba(p, iters=1, lambda_init=100.0)
+    assert one["stats"][3] >= 1  # the first trial used lambda 100 (final lambda scaled from it)
