@@ -664,19 +664,51 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
 // reports NumericalIssue only for D(k,k) == 0).
 // kLds: S (n_pad x (n_pad + 1), odd stride: conflict-free tile columns) and
 // the L_KK^-1 tiles in LDS; else both in a.work.
+// Phase clocks of the solve (tools/lba_solve_bench.hip builds with
+// LBA_SOLVE_STAMPS): thread 0 adds the s_memtime delta since its previous
+// stamp to bucket k.
+constexpr int kSolveThreads = 512;
+constexpr int kSolveWaves = kSolveThreads / 64;
+
+// 1 / d: v_rcp_f64 and one Newton step (the pivot chain's latency; not the
+// IEEE division sequence)
+__device__ __forceinline__ double rcp_f64(double d) {
+  const double x = __builtin_amdgcn_rcp(d);
+  return fma(x, fma(-d, x, 1.0), x);
+}
+
+#ifdef LBA_SOLVE_STAMPS
+__device__ unsigned long long g_lba_stamps[16];
+#define LBA_STAMP(k)                                                  \
+  do {                                                                \
+    if (t == 0) {                                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+      g_lba_stamps[k] += now_ - stamp_last;                           \
+      stamp_last = now_;                                              \
+    }                                                                 \
+  } while (0)
+#else
+#define LBA_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <bool kLds>
-__global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
+__global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   extern __shared__ double smem[];
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
   const double lambda = c.lambda;
   const int n = a.n_sys, N = a.n_pad, LD = N + 1, T = N >> 4;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 15, lk = lane >> 4;
+#ifdef LBA_SOLVE_STAMPS
+  unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
+#endif
   double* S;
   double* Li;
   double* Dg;
   double* y;
-  __shared__ double red[4];
+  __shared__ double red[kSolveWaves];
   __shared__ int bad;
   if constexpr (kLds) {
     S = smem;
@@ -690,28 +722,32 @@ __global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
     y = smem + N;
   }
   const double* src = a.sys;
-  // S + lambda I with identity padding (D = 1, L = 0): 8 loads in flight per
+  // S + lambda I with identity padding (D = 1, L = 0): 16 loads in flight per
   // thread before the LDS writes
-  for (int e0 = t; e0 < N * N; e0 += 8 * kThreads) {
-    double v[8];
+  for (int e0 = t; e0 < N * N; e0 += 16 * kSolveThreads) {
+    double v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + u * kThreads, r = e / N, cc = e - r * N;
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
       v[u] = e < N * N && r < n && cc < n ? src[(size_t)r * n + cc] : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = e0 + u * kThreads, r = e / N, cc = e - r * N;
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
       if (e < N * N) S[(size_t)r * LD + cc] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
     }
   }
-  for (int r = t; r < N; r += kThreads) y[r] = r < n ? src[(size_t)n * n + r] : 0.0;
+  for (int r = t; r < N; r += kSolveThreads) y[r] = r < n ? src[(size_t)n * n + r] : 0.0;
   if (t == 0) bad = 0;
   __syncthreads();
+  LBA_STAMP(0);
 
   for (int K = 0; K < T; ++K) {
     const int k0 = 16 * K;
     if (wave == 0) {
+      // 1. diagonal tile: lane li owns row li (full symmetric row), right-
+      // looking, the pivot row broadcast by v_readlane; branch-free (rows at
+      // or above the pivot take l = 0)
       double r[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) r[j] = S[(size_t)(k0 + li) * LD + k0 + j];
@@ -720,18 +756,13 @@ __global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
       for (int cI = 0; cI < 16; ++cI) {
         const double dc = readlane_f64(r[cI], cI);
-        if (li == cI) dmine = dc;
+        dmine = li == cI ? dc : dmine;
         zero |= dc == 0.0;
-        const double inv = dc != 0.0 ? 1.0 / dc : 0.0;
-        double rc[16];
+        const double inv = dc != 0.0 ? rcp_f64(dc) : 0.0;
+        const double l = li > cI ? r[cI] * inv : 0.0;
 #pragma unroll
-        for (int j = cI + 1; j < 16; ++j) rc[j] = readlane_f64(r[j], cI);
-        if (li > cI) {
-          const double l = r[cI] * inv;
-#pragma unroll
-          for (int j = cI + 1; j < 16; ++j) r[j] -= l * rc[j];
-          r[cI] = l;
-        }
+        for (int j = cI + 1; j < 16; ++j) r[j] = fma(-l, readlane_f64(r[j], cI), r[j]);
+        r[cI] = li > cI ? l : r[cI];
       }
       if (lane < 16) {
 #pragma unroll
@@ -740,27 +771,36 @@ __global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
         Dg[k0 + li] = dmine;
       }
       __threadfence_block();  // the rows are re-read by the other lanes
-      // L_KK^-1, column li: forward substitution, the rows of L read back
-      // with one address per step (LDS broadcast); this wave wrote them
+      LBA_STAMP(1);
+      // 2. L_KK^-1, column li, column-oriented (one FMA latency per step),
+      // the rows of L read back with one address per step (LDS broadcast)
       double x[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) x[i] = i == li ? 1.0 : 0.0;
 #pragma unroll
-      for (int i = 1; i < 16; ++i) {
-        double s = x[i];
+      for (int k = 0; k < 15; ++k)
 #pragma unroll
-        for (int k = 0; k < i; ++k) s -= S[(size_t)(k0 + i) * LD + k0 + k] * x[k];
-        x[i] = s;
-      }
+        for (int i = k + 1; i < 16; ++i) x[i] = fma(-S[(size_t)(k0 + i) * LD + k0 + k], x[k], x[i]);
       if (lane < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) Li[(size_t)K * 256 + i * 16 + li] = x[i];
       }
+      // 3. this tile's forward substitution y_K = L_KK^-1 y_K: lane li holds
+      // y_li, the solved entries broadcast
+      double yv = y[k0 + li];
+#pragma unroll
+      for (int j = 0; j < 15; ++j) {
+        const double yj = readlane_f64(yv, j);
+        yv = li > j ? fma(-r[j], yj, yv) : yv;
+      }
+      if (lane < 16) y[k0 + li] = yv;
       if (lane == 0 && zero) bad = 1;
     }
     __syncthreads();
-    // panel: L_IK = (A_IK L_KK^-T) D_K^-1
-    for (int I = K + 1 + wave; I < T; I += 4) {
+    LBA_STAMP(2);
+    // 4. panel: L_IK = (A_IK L_KK^-T) D_K^-1 (MFMA), and the rows' forward
+    // substitution y_I -= L_IK y_K (DPP row sums over the tile's columns)
+    for (int I = K + 1 + wave; I < T; I += kSolveWaves) {
       const int i0 = 16 * I;
       d4 acc = {0, 0, 0, 0};
 #pragma unroll
@@ -770,15 +810,27 @@ __global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
         const double bv = Li[(size_t)K * 256 + li * 16 + kk];  // (L^-1)^T[kk][li]
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
-      const double dinv = 1.0 / Dg[k0 + li];
+      const double dinv = rcp_f64(Dg[k0 + li]);
+      const double ykl = y[k0 + li];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) S[(size_t)(i0 + lk + 4 * rr) * LD + k0 + li] = acc[rr] * dinv;
+      for (int rr = 0; rr < 4; ++rr) {
+        const double l = acc[rr] * dinv;
+        S[(size_t)(i0 + lk + 4 * rr) * LD + k0 + li] = l;
+        double p = l * ykl;
+        p += dpp_f64<0x111, 0xf>(p);
+        p += dpp_f64<0x112, 0xf>(p);
+        p += dpp_f64<0x114, 0xf>(p);
+        p += dpp_f64<0x118, 0xf>(p);
+        if (li == 15) y[i0 + lk + 4 * rr] -= p;
+      }
     }
     __syncthreads();
-    // trailing: A_IJ -= L_IK (D_K L_JK^T), tiles K < J <= I enumerated row-major
+    LBA_STAMP(3);
+    // 5. trailing: A_IJ -= L_IK (D_K L_JK^T), tiles K < J <= I enumerated
+    // row-major, v_mfma_f64_16x16x4 over the tile's 16 columns
     const int m = T - K - 1;
     const int ntile = m * (m + 1) / 2;
-    for (int q = wave; q < ntile; q += 4) {
+    for (int q = wave; q < ntile; q += kSolveWaves) {
       int I = 0;
       while ((I + 1) * (I + 2) / 2 <= q) ++I;
       const int J = q - I * (I + 1) / 2;
@@ -797,60 +849,51 @@ __global__ __launch_bounds__(kThreads) void k_lba_solve(LbaArgs a) {
       for (int rr = 0; rr < 4; ++rr) S[(size_t)(i0 + lk + 4 * rr) * LD + j0 + li] = acc[rr];
     }
     __syncthreads();
+    LBA_STAMP(4);
   }
-  // forward: L y = b_s
-  for (int K = 0; K < T; ++K) {
-    const int k0 = 16 * K;
-    if (t < 16) {
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s += Li[(size_t)K * 256 + t * 16 + k] * y[k0 + k];
-      __builtin_amdgcn_wave_barrier();
-      y[k0 + t] = s;
-    }
-    __syncthreads();
-    for (int r = k0 + 16 + t; r < N; r += kThreads) {
-      double s = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s += S[(size_t)r * LD + k0 + k] * y[k0 + k];
-      y[r] -= s;
-    }
-    __syncthreads();
-  }
-  for (int r = t; r < N; r += kThreads) y[r] = Dg[r] != 0.0 ? y[r] / Dg[r] : 0.0;
+  for (int r = t; r < N; r += kSolveThreads) y[r] = y[r] * rcp_f64(Dg[r]);
   __syncthreads();
-  // backward: L^T x = y
+  LBA_STAMP(5);
+  // backward: L^T x = y by tiles from the last (L_KK^-T mat-vec, then the
+  // rows above take the tile's contribution)
   for (int K = T - 1; K >= 0; --K) {
     const int k0 = 16 * K;
     if (t < 16) {
       double s = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += Li[(size_t)K * 256 + k * 16 + t] * y[k0 + k];
+      for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * 256 + k * 16 + t], y[k0 + k], s);
       __builtin_amdgcn_wave_barrier();
       y[k0 + t] = s;
     }
     __syncthreads();
-    for (int r = t; r < k0; r += kThreads) {
+    for (int r = t; r < k0; r += kSolveThreads) {
       double s = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += S[(size_t)(k0 + k) * LD + r] * y[k0 + k];
+      for (int k = 0; k < 16; ++k) s = fma(S[(size_t)(k0 + k) * LD + r], y[k0 + k], s);
       y[r] -= s;
     }
     __syncthreads();
   }
+  LBA_STAMP(6);
   // x_p and the pose part of computeScale: x . (lambda x + b_p)
   double sc = 0;
-  for (int r = t; r < n; r += kThreads) {
+  for (int r = t; r < n; r += kSolveThreads) {
     const double xv = y[r];
     a.xp[r] = xv;
     sc += xv * (lambda * xv + src[(size_t)n * n + n + r]);
   }
-  double v[1] = {sc};
-  block_sum<1>(v, red);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o, 64);
+  if (lane == 0) red[wave] = sc;
+  __syncthreads();
   if (t == 0) {
-    a.scal[0] = v[0];
+    double v = 0;
+#pragma unroll
+    for (int w = 0; w < kSolveWaves; ++w) v += red[w];
+    a.scal[0] = v;
     a.scal[1] = bad;
   }
+  LBA_STAMP(7);
 }
 
 // ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
@@ -1050,9 +1093,9 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
     if (lds > 64 * 1024 &&
         lds_optin(reinterpret_cast<const void*>(&k_lba_solve<true>), (int)lds) != hipSuccess)
       return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_lba_solve<true>, dim3(1), dim3(kThreads), lds, st, a);
+    hipLaunchKernelGGL(k_lba_solve<true>, dim3(1), dim3(kSolveThreads), lds, st, a);
   } else {
-    hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kThreads), 16 * (size_t)a.n_pad, st, a);
+    hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kSolveThreads), 16 * (size_t)a.n_pad, st, a);
   }
   if (a.n_kf > kMaxKfLds)
     hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
