@@ -364,7 +364,13 @@ orbgpu_status orbgpu_matches_to_pose_obs_batch(
 /* The same gather for PoseInertialOptimizationLastFrame / LastKeyFrame
  *   (optimizer.cc:4816-4900, 4466-4540): orbgpu_inertial_obs rows, with
  *   close = d_close[point] (MapPoint::mTrackDepth < 10; NULL: 0) and the
- *   pinhole Uncertainty2 = 1.  Declared with the inertial types below. */
+ *   pinhole Uncertainty2 = 1.  Declared with the inertial types below.
+ *   In the reference these optimisations run in TrackLocalMap
+ *   (tracking.cc:2262-2285) over mvpMapPoints as SearchLocalPoints left them
+ *   (after IMU initialisation TrackWithMotionModel returns after
+ *   PredictStateIMU without searching, :2170-2176): d_match is then
+ *   orbgpu_search_local_points' match array over the local map points, and
+ *   mTrackDepth is the depth its isInFrustum wrote (orbgpu_track_view). */
 
 /* Replaces: bool Frame::isInFrustum(MapPoint* pMP, float viewingCosLimit)
  *   (frame.cc:548-603, Nleft == -1) over Tracking::SearchLocalPoints' loop

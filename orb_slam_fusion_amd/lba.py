@@ -117,3 +117,117 @@ class LocalBundleAdjuster:
             "orbgpu_lba_optimize",
         )
         return {"poses": po, "poses_d": pd, "pts": xo, "outlier": out[:ne].copy(), "stats": st}
+
+
+# ---------------------------------------------------------------------------
+# Optimizer::LocalBundleAdjustment around the solve: the window gather
+# (optimizer.cc:1057-1124), the flat graph handed to the device (:1150-1354)
+# and the write-back (:1362-1441), over duck-typed KeyFrame / MapPoint / Map
+# objects exposing the reference's members: KeyFrame.id_, mnBALocalForKF,
+# mnBAFixedForKF, isBad(), GetMap(), GetVectorCovisibleKeyFrames(),
+# GetMapPointMatches(), GetPose() (qx, qy, qz, qw, tx, ty, tz), mvKeysUn
+# (objects with .x, .y, .octave), mvuRight, mvInvLevelSigma2; MapPoint.id_,
+# mnBALocalForKF, isBad(), GetMap(), GetObservations() (an ordered mapping
+# KeyFrame -> (leftIndex, rightIndex), in the std::map's key order),
+# GetWorldPos(); Map.GetInitKFid().  (The C++ drop-in, shim/
+# optimizer_lba_gpu.cc, is the same code over the real classes.)
+# ---------------------------------------------------------------------------
+class LbaWindow:
+    """One gathered window: the local / fixed keyframes and local map points
+    in the reference's list orders, the out-params, and the LbaProblem the
+    device solves (edges in insertion order: per local point, its
+    observations in map order; pinhole left-index observations only)."""
+
+    def __init__(self, local_kfs, fixed_kfs, local_mps, num_fixedKF, cam, poses, fixed, pts,
+                 edges, edge_refs):
+        self.local_kfs, self.fixed_kfs, self.local_mps = local_kfs, fixed_kfs, local_mps
+        self.num_fixedKF = num_fixedKF
+        self.num_OptKF = len(local_kfs)
+        self.num_edges = len(edges)
+        self.cam, self.poses_init, self.fixed, self.pts_init = cam, poses, fixed, pts
+        self.edges = edges
+        self.edge_refs = edge_refs  # [(KeyFrame, MapPoint)] per edge
+
+
+def gather_window(pKF, pMap, cam) -> Optional[LbaWindow]:
+    """optimizer.cc:1057-1124 then the graph of :1150-1354.  Returns None when
+    the window has no fixed keyframe (the reference prints "LM-LBA: There are
+    0 fixed KF in the optimizations, LBA aborted" and returns, :1119-1124).
+    The mnBALocalForKF / mnBAFixedForKF marks are written exactly as the
+    reference writes them (bad and other-map covisible keyframes are marked
+    local without joining the window; every observer of a local point is
+    marked fixed once, joining only when good and in the current map)."""
+    cur_map = pKF.GetMap()
+    kid = pKF.id_
+    local_kfs = [pKF]
+    pKF.mnBALocalForKF = kid
+    for k in pKF.GetVectorCovisibleKeyFrames():
+        k.mnBALocalForKF = kid
+        if not k.isBad() and k.GetMap() is cur_map:
+            local_kfs.append(k)
+    num_fixed = 0
+    local_mps = []
+    init_id = pMap.GetInitKFid()
+    for k in local_kfs:
+        if k.id_ == init_id:
+            num_fixed = 1
+        for mp in k.GetMapPointMatches():
+            if mp is not None and not mp.isBad() and mp.GetMap() is cur_map \
+                    and mp.mnBALocalForKF != kid:
+                local_mps.append(mp)
+                mp.mnBALocalForKF = kid
+    fixed_kfs = []
+    for mp in local_mps:
+        for k in mp.GetObservations():
+            if k.mnBALocalForKF != kid and k.mnBAFixedForKF != kid:
+                k.mnBAFixedForKF = kid
+                if not k.isBad() and k.GetMap() is cur_map:
+                    fixed_kfs.append(k)
+    num_fixed += len(fixed_kfs)
+    if num_fixed == 0:
+        return None
+    # vertices: local keyframes (fixed iff the map's initial keyframe), fixed
+    # cameras, points; edges per point in observation order (:1150-1310)
+    kfs = local_kfs + fixed_kfs
+    index = {id(k): i for i, k in enumerate(kfs)}
+    poses = np.array([np.asarray(k.GetPose(), np.float32) for k in kfs], np.float32).reshape(-1, 7)
+    fixed = np.array([1 if (i >= len(local_kfs) or k.id_ == init_id) else 0
+                      for i, k in enumerate(kfs)], np.uint8)
+    pts = np.array([np.asarray(mp.GetWorldPos(), np.float32) for mp in local_mps],
+                   np.float32).reshape(-1, 3)
+    rows, refs = [], []
+    for p, mp in enumerate(local_mps):
+        for k, (left, _right) in mp.GetObservations().items():
+            if k.isBad() or k.GetMap() is not cur_map or left == -1:
+                continue
+            i = index.get(id(k))
+            if i is None:  # a stale local mark (the reference would find no vertex)
+                continue
+            kp = k.mvKeysUn[left]
+            ur = float(k.mvuRight[left])
+            rows.append((p, i, kp.x, kp.y, ur if ur >= 0 else -1.0,
+                         k.mvInvLevelSigma2[kp.octave]))
+            refs.append((k, mp))
+    edges = np.array(rows, LBA_EDGE_DTYPE) if rows else np.zeros(0, LBA_EDGE_DTYPE)
+    return LbaWindow(local_kfs, fixed_kfs, local_mps, num_fixed, np.asarray(cam, np.float32),
+                     poses, fixed, pts, edges, refs)
+
+
+def write_back(win: LbaWindow, result: dict):
+    """optimizer.cc:1362-1441 -> (to_erase, kf_poses, mp_positions): the
+    (KeyFrame, MapPoint) observations to erase (mono edges first, then
+    stereo, each in insertion order; points already bad skipped), the new
+    poses of the local keyframes and the new positions of the local points
+    (the caller applies them under Map::mMutexMapUpdate and calls
+    UpdateNormalAndDepth / IncreaseChangeIndex)."""
+    out = result["outlier"]
+    mono = win.edges["ur"] < 0
+    to_erase = []
+    for sel in (np.nonzero(mono)[0], np.nonzero(~mono)[0]):
+        for e in sel:
+            k, mp = win.edge_refs[e]
+            if not mp.isBad() and out[e]:
+                to_erase.append((k, mp))
+    kf_poses = [(k, result["poses"][i]) for i, k in enumerate(win.local_kfs)]
+    mp_pos = [(mp, result["pts"][p]) for p, mp in enumerate(win.local_mps)]
+    return to_erase, kf_poses, mp_pos
