@@ -361,6 +361,23 @@ orbgpu_status orbgpu_matches_to_pose_obs_batch(
     int pt_stride, const float* inv_level_sigma2, int n_levels, orbgpu_pose_obs* d_obs,
     int obs_stride, int* d_nobs, int32_t* d_obs_index, void* hip_stream);
 
+/* Replaces: bool Frame::UnprojectStereo(const int& i, Eigen::Vector3f& x3D)
+ *   (frame.cc:1008-1020) over Tracking::UpdateLastFrame's loop (tracking.cc:
+ *   2099-2160) on the device: frame f's keypoints with mvDepth > 0, in index
+ *   order, become LastFrame points at the frame's pose d_Tcw[f] (Xw = mRwc Xc
+ *   + mOw; octave, angle and descriptor of the keypoint; has_obs = 1), ready
+ *   for orbgpu_search_by_projection_last_batch.  d_npts[f] = the count (at
+ *   most pt_stride; more sets bit 2 of orbgpu_matcher_status).  The
+ *   reference keeps the tracked map points and adds temporal points for the
+ *   closest stereo keypoints; a caller without a map (the synthetic sequence
+ *   runner) takes every stereo keypoint. */
+orbgpu_status orbgpu_unproject_stereo_batch(orbgpu_matcher* m, int n_frames,
+                                           const orbgpu_camera* cam, const orbgpu_pose* d_Tcw,
+                                           const orbgpu_keypoint* d_kps, const uint8_t* d_descs,
+                                           const float* d_depth, const int* d_n, int kp_stride,
+                                           orbgpu_proj_point* d_pts, int pt_stride, int* d_npts,
+                                           void* hip_stream);
+
 /* The same gather for PoseInertialOptimizationLastFrame / LastKeyFrame
  *   (optimizer.cc:4816-4900, 4466-4540): orbgpu_inertial_obs rows, with
  *   close = d_close[point] (MapPoint::mTrackDepth < 10; NULL: 0) and the

@@ -194,6 +194,9 @@ SIGNATURES = {
     "orbgpu_matches_to_pose_obs_batch": (
         _I, [_P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P],
     ),
+    "orbgpu_unproject_stereo_batch": (
+        _I, [_P, _I, ctypes.POINTER(Camera), _P, _P, _P, _P, _P, _I, _P, _I, _P, _P],
+    ),
     "orbgpu_matches_to_inertial_obs_batch": (
         _I, [_P, _I, _P, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P],
     ),

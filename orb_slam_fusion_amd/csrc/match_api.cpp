@@ -412,6 +412,36 @@ orbgpu_status orbgpu_matches_to_pose_obs_batch(
   return orbgpu::launch_pose_obs(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
 }
 
+orbgpu_status orbgpu_unproject_stereo_batch(orbgpu_matcher* m, int n_frames,
+                                           const orbgpu_camera* cam, const orbgpu_pose* d_Tcw,
+                                           const orbgpu_keypoint* d_kps, const uint8_t* d_descs,
+                                           const float* d_depth, const int* d_n, int kp_stride,
+                                           orbgpu_proj_point* d_pts, int pt_stride, int* d_npts,
+                                           void* hip_stream) {
+  if (!m || n_frames <= 0 || !cam || !d_Tcw || !d_kps || !d_descs || !d_depth || !d_n ||
+      kp_stride <= 0 || !d_pts || pt_stride <= 0 || !d_npts)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu::UnprojLaunch L{};
+  L.n_frames = n_frames;
+  L.fx = cam->fx;
+  L.fy = cam->fy;
+  L.cx = cam->cx;
+  L.cy = cam->cy;
+  L.Tcw = d_Tcw;
+  L.kps = reinterpret_cast<const float*>(d_kps);
+  L.desc = d_descs;
+  L.depth = d_depth;
+  L.n = d_n;
+  L.kp_stride = kp_stride;
+  L.pts = d_pts;
+  L.pt_stride = pt_stride;
+  L.npts = d_npts;
+  L.err = m->d_err;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+  return orbgpu::launch_unproject(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
 orbgpu_status orbgpu_matches_to_inertial_obs_batch(
     orbgpu_matcher* m, int n_frames, const orbgpu_keypoint* d_kps, const float* d_uright,
     const int32_t* d_match, const int* d_n, int kp_stride, const orbgpu_proj_point* d_pts,

@@ -638,7 +638,76 @@ __global__ __launch_bounds__(256) void k_mt_pose_obs(ObsLaunch a) {
   }
 }
 
+// Frame::UnprojectStereo (frame.cc:1008-1020) of every keypoint with
+// mvDepth > 0, in index order (one block per frame, ballot compaction):
+// Xc = ((u - cx) z invfx, (v - cy) z invfy, z), Xw = mRwc Xc + mOw with
+// mRwc = Tcw.rotationMatrix()^T (Eigen's quaternion-to-matrix) and mOw =
+// Tcw.inverse().translation(); the point takes the keypoint's octave, angle
+// and descriptor and counts as observed (Tracking::UpdateLastFrame's points).
+__global__ __launch_bounds__(256) void k_mt_unproject(UnprojLaunch a) {
+  __shared__ int wsum[4];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0 && a.n[f] > a.kp_stride) atomicOr(a.err, 1);
+  const int n = min(a.n[f], a.kp_stride);
+  const size_t ko = (size_t)f * a.kp_stride;
+  const orbgpu_pose T = a.Tcw[f];
+  // Eigen QuaternionBase::toRotationMatrix (rows of Rcw)
+  const float tx = 2 * T.qx, ty = 2 * T.qy, tz = 2 * T.qz;
+  const float twx = tx * T.qw, twy = ty * T.qw, twz = tz * T.qw;
+  const float txx = tx * T.qx, txy = ty * T.qx, txz = tz * T.qx;
+  const float tyy = ty * T.qy, tyz = tz * T.qy, tzz = tz * T.qz;
+  const float R[3][3] = {{1 - (tyy + tzz), txy - twz, txz + twy},
+                         {txy + twz, 1 - (txx + tzz), tyz - twx},
+                         {txz - twy, tyz + twx, 1 - (txx + tyy)}};
+  const V3 Ow = se3_inverse_translation(T);
+  const float invfx = 1.0f / a.fx, invfy = 1.0f / a.fy;
+  int base = 0;
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    const int i = i0 + t;
+    const float z = i < n ? a.depth[ko + i] : 0.0f;
+    const bool take = z > 0;
+    const uint64_t bal = __ballot(take);
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (take) {
+      const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+      if (pos < a.pt_stride) {
+        const float* k = a.kps + (ko + i) * kKpFloats;
+        const float x = (k[0] - a.cx) * z * invfx, y = (k[1] - a.cy) * z * invfy;
+        orbgpu_proj_point P;
+        // mRwc * x3Dc + mOw: (Rwc)_rc = R[c][r]
+        P.Xw[0] = __builtin_fmaf(R[2][0], z, __builtin_fmaf(R[1][0], y, R[0][0] * x)) + Ow.x;
+        P.Xw[1] = __builtin_fmaf(R[2][1], z, __builtin_fmaf(R[1][1], y, R[0][1] * x)) + Ow.y;
+        P.Xw[2] = __builtin_fmaf(R[2][2], z, __builtin_fmaf(R[1][2], y, R[0][2] * x)) + Ow.z;
+        P.octave = kp_octave(k);
+        P.angle = k[3];
+        P.has_obs = 1;
+        const uint4* src = reinterpret_cast<const uint4*>(a.desc + (ko + i) * 32);
+        uint4* dst = reinterpret_cast<uint4*>(P.desc);
+        dst[0] = src[0];
+        dst[1] = src[1];
+        a.pts[(size_t)f * a.pt_stride + pos] = P;
+      }
+    }
+    base += total;
+    __syncthreads();
+  }
+  if (t == 0) {
+    a.npts[f] = min(base, a.pt_stride);
+    if (base > a.pt_stride) atomicOr(a.err, 4);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_unproject(const UnprojLaunch& a, hipStream_t st) {
+  if (a.n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mt_unproject, dim3(a.n_frames), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st) {
   if (a.n_frames <= 0) return hipSuccess;

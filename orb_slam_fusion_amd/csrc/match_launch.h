@@ -95,4 +95,22 @@ struct ObsLaunch {
 
 hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st);
 
+// Frame::UnprojectStereo over the frames' stereo keypoints -> LastFrame points
+struct UnprojLaunch {
+  int n_frames;
+  float fx, fy, cx, cy;
+  const orbgpu_pose* Tcw;  // [n_frames]
+  const float* kps;        // orbgpu_keypoint rows, frame f at f * kp_stride
+  const uint8_t* desc;
+  const float* depth;      // mvDepth
+  const int* n;
+  int kp_stride;
+  orbgpu_proj_point* pts;  // [n_frames][pt_stride]
+  int pt_stride;
+  int* npts;
+  int* err;
+};
+
+hipError_t launch_unproject(const UnprojLaunch& a, hipStream_t st);
+
 }  // namespace orbgpu

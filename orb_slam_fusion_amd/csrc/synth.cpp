@@ -39,18 +39,18 @@ namespace {
 // Canvas = vertical gradient 40..200, 300 axis-aligned rectangles (sides
 // U[4,60], grey U[0,255]), 150 discs (radius U[3,25]), then per-pixel U[-6,6]
 // noise, clamped.
-std::vector<int> make_canvas(uint64_t seed, int cw, int h) {
+std::vector<int> make_canvas(uint64_t seed, int cw, int h, int n_rect = 300, int n_disc = 150) {
   std::vector<int> c((size_t)cw * h);
   XorShift64Star rng(seed);
   for (int y = 0; y < h; ++y)
     for (int x = 0; x < cw; ++x) c[(size_t)y * cw + x] = 40 + (160 * y) / (h > 1 ? h - 1 : 1);
-  for (int r = 0; r < 300; ++r) {
+  for (int r = 0; r < n_rect; ++r) {
     const int x0 = rng.uniform(0, cw - 1), y0 = rng.uniform(0, h - 1);
     const int rw = rng.uniform(4, 60), rh = rng.uniform(4, 60), g = rng.uniform(0, 255);
     for (int y = y0; y < y0 + rh && y < h; ++y)
       for (int x = x0; x < x0 + rw && x < cw; ++x) c[(size_t)y * cw + x] = g;
   }
-  for (int d = 0; d < 150; ++d) {
+  for (int d = 0; d < n_disc; ++d) {
     const int x0 = rng.uniform(0, cw - 1), y0 = rng.uniform(0, h - 1);
     const int rad = rng.uniform(3, 25), g = rng.uniform(0, 255);
     for (int y = y0 - rad; y <= y0 + rad; ++y)
@@ -98,6 +98,23 @@ void synth_track_pair(uint64_t seed, int w, int h, int disparity, int shift, uin
   crop(c, cw, w, h, shift + disparity, last_r);
   crop(c, cw, w, h, 0, cur_l);
   crop(c, cw, w, h, disparity, cur_r);
+}
+
+// A stereo sequence of n_frames frames of a camera translating along x over
+// the canvas plane (configs C3 / C5 on synthetic data): frame k crops the
+// canvas at (n_frames - 1 - k) * shift, so every feature moves +shift px
+// per frame; the object counts scale with the canvas width (the density of
+// one 752-px frame).  left_all / right_all: n_frames * w * h bytes.
+void synth_sequence(uint64_t seed, int n_frames, int w, int h, int disparity, int shift,
+                    uint8_t* left_all, uint8_t* right_all) {
+  const int cw = w + disparity + shift * (n_frames - 1);
+  const double k = (double)cw / (double)(w + disparity);
+  const std::vector<int> c = make_canvas(seed, cw, h, (int)(300 * k), (int)(150 * k));
+  for (int f = 0; f < n_frames; ++f) {
+    const int x0 = (n_frames - 1 - f) * shift;
+    crop(c, cw, w, h, x0, left_all + (size_t)f * w * h);
+    crop(c, cw, w, h, x0 + disparity, right_all + (size_t)f * w * h);
+  }
 }
 
 // Plain noise image (stress case: dense FAST responses, large octree input).

@@ -136,6 +136,19 @@ class ORBmatcher:
                 pts.shape[1], ptr(isg), len(isg), ptr(obs), obs.shape[1], ptr(nobs),
                 ptr(obs_index), s), "orbgpu_matches_to_pose_obs_batch")
 
+    def unproject_stereo_batch(self, cam, Tcw, kps, desc, depth, n, pts, npts,
+                               stream=None) -> None:
+        """Frame::UnprojectStereo of every stereo keypoint (mvDepth > 0) on the
+        device -> LastFrame points: Tcw float32 [B, 7]; kps [B, K, 7]; desc uint8
+        [B, K, 32]; depth float32 [B, K]; n int32 [B]; pts uint8 [B, P, 56];
+        npts int32 [B]."""
+        B, K = kps.shape[0], kps.shape[1]
+        c = Camera(*[float(v) for v in cam])
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_unproject_stereo_batch(
+                self._h, B, ctypes.byref(c), ptr(Tcw), ptr(kps), ptr(desc), ptr(depth), ptr(n), K,
+                ptr(pts), pts.shape[1], ptr(npts), s), "orbgpu_unproject_stereo_batch")
+
     def matches_to_inertial_obs_batch(self, kps, uright, match, n, pts, close, inv_level_sigma2,
                                       obs, nobs, obs_index=None, stream=None) -> None:
         """The same list for PoseInertialOptimizationLastFrame / LastKeyFrame:

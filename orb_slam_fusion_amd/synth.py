@@ -24,6 +24,7 @@ def _so() -> ctypes.CDLL:
                                       ctypes.c_void_p, ctypes.c_void_p]
     so.synth_track_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int] + [ctypes.c_void_p] * 4
+    so.synth_sequence.argtypes = [ctypes.c_uint64] + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2
     so.synth_vocab_text.argtypes = [ctypes.c_uint64] + [ctypes.c_int] * 6 + [ctypes.c_char_p]
     so.synth_vocab_text.restype = ctypes.c_int
     so.synth_noise_image.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -51,6 +52,18 @@ def track_pair(frame_idx: int, shift: int = 6, w: int = 752, h: int = 480, dispa
     _so().synth_track_pair(FRAME_SEED_BASE + 0x10000 + frame_idx, w, h, disparity, shift,
                            *[im.ctypes.data for im in ims])
     return tuple(ims)
+
+
+def sequence(seq_idx: int, n_frames: int, shift: int = 6, w: int = 752, h: int = 480,
+             disparity: int = 24):
+    """A stereo sequence (C3 / C5 on synthetic data): n_frames consecutive
+    frames of a camera translating along x, features moving +shift px per
+    frame, depth bf / disparity.  Returns (left [n, h, w], right [n, h, w])."""
+    left = np.zeros((n_frames, h, w), np.uint8)
+    right = np.zeros((n_frames, h, w), np.uint8)
+    _so().synth_sequence(FRAME_SEED_BASE + 0x20000 + seq_idx, n_frames, w, h, disparity, shift,
+                         left.ctypes.data, right.ctypes.data)
+    return left, right
 
 
 def vocab_text(path, seed: int = 3, k: int = 10, L: int = 6, scoring: int = 0,

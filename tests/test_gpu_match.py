@@ -142,3 +142,53 @@ def test_last_batch_matches_single(matcher):
                                     None, c.pts, 7, False, True)
         assert nm[b] == nm_o
         np.testing.assert_array_equal(match[b, :n[b]], m_o)
+
+
+def test_unproject_stereo_batch(matcher):
+    """Frame::UnprojectStereo over the stereo keypoints (frame.cc:1008-1020):
+    compaction in index order, octave / angle / descriptor carried, Xw = mRwc
+    Xc + mOw against a float64 restatement (float32 tolerance)."""
+    import torch
+
+    from orb_slam_fusion_amd._lib import KEYPOINT_DTYPE, PROJ_POINT_DTYPE
+
+    rng = np.random.default_rng(5)
+    B, K = 3, 700
+    kps = np.zeros((B, K), KEYPOINT_DTYPE)
+    kps["x"], kps["y"] = rng.uniform(0, 752, (B, K)), rng.uniform(0, 480, (B, K))
+    kps["angle"], kps["octave"] = rng.uniform(0, 360, (B, K)), rng.integers(0, 8, (B, K))
+    desc = rng.integers(0, 256, (B, K, 32), dtype=np.uint8)
+    depth = np.where(rng.random((B, K)) < 0.6, rng.uniform(0.5, 9, (B, K)), -1).astype(np.float32)
+    n = np.array([K, 500, 0], np.int32)
+    poses = []
+    for f in range(B):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        poses.append(np.concatenate([q, rng.normal(size=3)]).astype(np.float32))
+    Tcw = np.stack(poses)
+    cam = np.array([458.654, 457.296, 367.215, 248.375, 50.0], np.float32)
+    dev = torch.device("cuda", 0)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pts = torch.zeros((B, K, 56), dtype=torch.uint8, device=dev)
+    npts = torch.zeros(B, dtype=torch.int32, device=dev)
+    matcher.unproject_stereo_batch(cam, d(Tcw), d(kps.view(np.float32).reshape(B, K, 7)), d(desc),
+                                   d(depth), d(n), pts, npts)
+    torch.cuda.synchronize()
+    got = pts.cpu().numpy().view(PROJ_POINT_DTYPE).reshape(B, K)
+    gn = npts.cpu().numpy()
+    for f in range(B):
+        sel = np.nonzero(depth[f, :n[f]] > 0)[0]
+        assert gn[f] == len(sel)
+        g = got[f, :len(sel)]
+        assert np.array_equal(g["octave"], kps["octave"][f, sel])
+        assert np.array_equal(g["angle"], kps["angle"][f, sel])
+        assert np.array_equal(g["desc"], desc[f, sel]) and (g["has_obs"] == 1).all()
+        qx, qy, qz, qw = Tcw[f, :4].astype(np.float64)
+        R = np.array([[1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy - qz * qw), 2 * (qx * qz + qy * qw)],
+                      [2 * (qx * qy + qz * qw), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz - qx * qw)],
+                      [2 * (qx * qz - qy * qw), 2 * (qy * qz + qx * qw), 1 - 2 * (qx * qx + qy * qy)]])
+        z = depth[f, sel].astype(np.float64)
+        Xc = np.stack([(kps["x"][f, sel] - cam[2]) * z / cam[0],
+                       (kps["y"][f, sel] - cam[3]) * z / cam[1], z], 1)
+        Xw = Xc @ R + (-(R.T @ Tcw[f, 4:].astype(np.float64)))
+        np.testing.assert_allclose(g["Xw"], Xw, rtol=2e-5, atol=2e-5)

@@ -44,3 +44,17 @@ def test_track_chain_matches_oracle(gpu_available):
         assert int(inl[f]) == o["inliers"]
         np.testing.assert_array_equal(outl[f, :n], o["outlier"])
         assert np.max(np.abs(pose[f] - o["pose"])) <= 1e-5
+
+
+def test_c5_sequence_runner_tracks(gpu_available):
+    """tools/c5_runner.py's chain (one rank, two sequences batched): frame to
+    frame tracking over a synthetic sequence stays on the known motion."""
+    import c5_runner
+
+    c = c5_runner.SequenceChain(0, 2, 12, 0)
+    c.reset()
+    for t in range(12):
+        c.frame(t)
+    nm, inl = c.stats()
+    assert nm > 200 and inl > 200
+    assert c.ate() < 0.01  # metres over 11 frames of 6 px (about 3 cm) each
