@@ -143,6 +143,10 @@ def main() -> int:
                     help="skip the device-resident tracking-chain side line")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the per-frame host-path latency side line")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the synthetic-sequence (C5 layout) side line")
+    ap.add_argument("--no-lba-sharded", action="store_true",
+                    help="skip the 2-rank point-sharded LBA side line")
     args = ap.parse_args()
 
     import torch
@@ -381,6 +385,35 @@ def main() -> int:
         from bench_latency import measure as measure_latency  # noqa: E402
 
         result["latency"] = measure_latency(frames=40, cpu_frames=0 if args.no_cpu_baseline else 8)
+    if rank == 0 and world == 1 and not args.no_c5:
+        # config C5's per-GPU unit on synthetic data: 8 sequences tracked frame to
+        # frame (tools/c5_runner.py), frames/s of the GPU and the drift vs truth
+        sys.path.insert(0, str(REPO / "tools"))
+        import c5_runner  # noqa: E402
+
+        c = c5_runner.SequenceChain(rank, 8, 110, local)
+        c.reset()
+        for t in range(10):
+            c.frame(t)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(10, 110):
+            c.frame(t)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        nm5, inl5 = c.stats()
+        result["c5"] = {"workload": "8 synthetic stereo sequences on this GPU, each tracked frame to "
+                                    "frame (extract, stereo, SearchByProjection at the motion-model "
+                                    "pose, PoseOptimization, UnprojectStereo), 100 timed frames",
+                        "gpu_fps": round(8 * 100 / el, 1), "ms_per_frame_per_seq": round(el / 100 * 1e3, 3),
+                        "matches_per_frame": round(nm5, 1), "pose_inliers_per_frame": round(inl5, 1),
+                        "ate_m": c.ate()}
+        del c
+    if rank == 0 and world == 1 and not args.no_lba_sharded:
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_lba import measure_sharded  # noqa: E402
+
+        result["lba_sharded"] = measure_sharded(calls=10)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()

@@ -164,7 +164,7 @@ def test_lba_two_ranks_one_gpu(gpu_available, tmp_path):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    worker = REPO / "tests" / "lba_shard_worker.py"
+    worker = REPO / "tools" / "lba_shard_worker.py"
     procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), str(tmp_path)],
                               env=env) for r in range(2)]
     for pr in procs:

@@ -41,6 +41,39 @@ def measure(calls: int = 10, cpu_calls: int = 3) -> dict:
     return out
 
 
+def measure_sharded(calls: int = 10) -> dict:
+    """The C4 window point-sharded over 2 ranks on ONE GPU (two fresh child
+    processes, gloo all-reduce of the device buffers through lba.dist_reduce):
+    a capability line (the exchange's cost with both ranks sharing the GPU),
+    not a multi-GPU scaling figure."""
+    import os
+    import socket
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    worker = REPO / "tools" / "lba_shard_worker.py"
+    with tempfile.TemporaryDirectory() as tmp:
+        procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), tmp,
+                                   str(calls)], env=env) for r in range(2)]
+        if any(p.wait(timeout=300) != 0 for p in procs):
+            return {"error": "worker failed"}
+        r = [np.load(Path(tmp) / f"r{k}.npz") for k in range(2)]
+        return {"workload": "C4 LocalBundleAdjustment point-sharded over 2 ranks on 1 GPU "
+                            "(gloo all-reduce of S, b, chi2, scale per LM trial)",
+                "ms_per_call": round(float(max(x["ms_per_call"] for x in r)), 3),
+                "lm_iterations": int(r[0]["stats"][2]), "lm_trials": int(r[0]["stats"][3]),
+                "chi2": float(r[0]["stats"][1]),
+                "ranks_identical_poses": bool((r[0]["poses_d"] == r[1]["poses_d"]).all()),
+                "scaling": "unmeasured (both ranks on one GPU)"}
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=10)
