@@ -576,6 +576,61 @@ orbgpu_status orbgpu_pose_inertial_batch(orbgpu_inertial_ctx* c, int mode,
                                          orbgpu_inertial_result* d_res, uint8_t* d_outlier,
                                          void* hip_stream);
 
+/* ------------------------------------------------------------------------
+ * LocalInertialBA -- replaces the solve of Optimizer::LocalInertialBA(
+ * KeyFrame* pKF, bool* pbStopFlag, Map* pMap, int& num_fixedKF, int&
+ * num_OptKF, int& num_MPs, int& num_edges, bool bLarge, bool bRecInit)
+ * (optimizer.h, optimizer.cc:2329-2902; LocalMapping dispatches it once the
+ * IMU is initialised, localmapping.cc:108-145).  The caller gathers the
+ * temporal window as the reference does (:2340-2436: the last Nd key frames
+ * through mPrevKF, their map points, the key frame before the window and the
+ * other observers as fixed key frames) and hands over the graph
+ * (:2461-2781); the library runs optimize(opt_it) -- g2o LM with the
+ * user lambda (:2448-2459), BlockSolverX with the points marginalised
+ * (Schur complement), fp64 -- and the outlier test (:2796-2826).  The caller
+ * applies the FAIL test (:2832-2836: 2 err < err_end or NaN, unless bLarge),
+ * erases the flagged observations and writes the key frames and points back
+ * (:2838-2901).  *pbStopFlag is attached only after optimize() (:2794), so it
+ * never stops this optimisation: the call takes no stop flag.
+ *
+ * Key frame k: kfs[k] = ImuCamPose(pKF) (Rwb, twb, Rcw, tcw) + the vertex
+ * estimates (v, bg, ba); fixed[k] = VertexPose (and its IMU vertices) fixed;
+ * imu[k] = pKF->bImu (VertexVelocity / GyroBias / AccBias exist).  Every free
+ * key frame must carry IMU vertices.  In the reduced system a free key frame
+ * owns 15 consecutive rows, VP(6) VV(3) VG(3) VA(3) (g2o orders VP ids before
+ * the IMU vertex ids; SimplicialLDLT's AMD ordering makes the order a
+ * rounding matter only).  Visual edges are orbgpu_lba_edge rows read as
+ * EdgeMono / EdgeStereo (cam_idx 0; inv_sigma2 = mvInvLevelSigma2[octave] /
+ * Uncertainty2, 1 for the pinhole camera); close[p] = pMP->mTrackDepth < 10.
+ * ------------------------------------------------------------------------ */
+#define ORBGPU_LIA_ROBUST 1     /* EdgeInertial under RobustKernelHuber(sqrt(16.92)) (:2571-2581) */
+#define ORBGPU_LIA_DOWNWEIGHT 2 /* EdgeInertial information x 1e-2 (i == N - 1, :2579)            */
+
+typedef struct orbgpu_lia_imu_edge {
+  int32_t kf1;   /* pKFi->mPrevKF: VP1 VV1 VG1 VA1                                  */
+  int32_t kf2;   /* pKFi: VP2 VV2 (and EdgeGyroRW / EdgeAccRW's second vertices)   */
+  int32_t flags; /* ORBGPU_LIA_*                                                    */
+  int32_t pad_;
+  orbgpu_imu_preint preint; /* pKFi->mpImuPreintegrated: deltas, Jacobians, EdgeInertial's
+                               information and the random-walk informations (:2587-2599) */
+} orbgpu_lia_imu_edge;
+
+/* Runs on the LocalBundleAdjustment context (its stream and arena).
+ * iterations = opt_it (10, bLarge 4); lambda_init = the user lambda (1e0,
+ * bLarge 1e-2; must be > 0).  Outputs: kfs_out (float casts: SetPose(Tcw)
+ * from Rcw / tcw, SetVelocity, SetNewBias), kfs_out_d (optional, 21 doubles
+ * per key frame: Rwb(9) twb v bg ba), pts_out, outlier[i] per visual edge,
+ * stats (optional, 7 doubles): err = the robust chi2 before optimize()
+ * (:2790-2791), err_end = the robust chi2 of the last computed errors
+ * (:2793), LM iterations, trials, final lambda, outliers, accepted chi2. */
+orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* c, const orbgpu_imu_calib* calib, int n_kf,
+                                  const orbgpu_imu_state* kfs, const uint8_t* fixed,
+                                  const uint8_t* imu, int n_pts, const float* pts_in,
+                                  const uint8_t* close, int n_edges, const orbgpu_lba_edge* edges,
+                                  int n_imu, const orbgpu_lia_imu_edge* imu_edges, int iterations,
+                                  double lambda_init, orbgpu_imu_state* kfs_out, double* kfs_out_d,
+                                  float* pts_out, uint8_t* outlier, double* stats);
+
 /* orbgpu_matches_to_pose_obs_batch's inertial form (see the comment there). */
 orbgpu_status orbgpu_matches_to_inertial_obs_batch(
     orbgpu_matcher* m, int n_frames, const orbgpu_keypoint* d_kps, const float* d_uright,

@@ -72,6 +72,10 @@ def lib() -> ctypes.CDLL:
         "orc_inertial_system": (None, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
         "orc_pose_inertial_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
         "orc_sym_pinv": (None, [_P, _I, _P]),
+        "orc_lia": (_I, [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, ctypes.c_double, _P,
+                         _P, _P, _P]),
+        "orc_lia_system": (_I, [_P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P]),
+        "orc_lia_vis_linearize": (None, [_P, _P, _P, _P, _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(so, name)
@@ -441,3 +445,44 @@ def sym_pinv(A: np.ndarray) -> np.ndarray:
     out = np.zeros_like(A)
     lib().orc_sym_pinv(_p(A), A.shape[0], _p(out))
     return out
+
+
+def lia(pb, iterations=None, lambda_init=None):
+    """LocalInertialBA's solve (oracle/lia_oracle.cc) on a synth.LiaProblem:
+    -> dict(kfs21 float64 [n_kf, 21] (Rwb, twb, v, bg, ba), pts float64
+    [n_pts, 3], outlier uint8 [E], stats float64 [7])."""
+    n_kf, n_p, ne, ni = len(pb.kfs), len(pb.pts_init), len(pb.edges), len(pb.imu_edges)
+    ko = np.zeros((n_kf, 21))
+    po = np.zeros((n_p, 3))
+    out = np.zeros(max(ne, 1), np.uint8)
+    st = np.zeros(7)
+    it = pb.iterations if iterations is None else iterations
+    lam = pb.lambda_init if lambda_init is None else lambda_init
+    r = lib().orc_lia(_p(pb.calib), n_kf, _p(pb.kfs), _p(pb.fixed), _p(pb.imu), n_p,
+                      _p(pb.pts_init), _p(pb.close), ne, _p(pb.edges), ni, _p(pb.imu_edges), it,
+                      float(lam), _p(ko), _p(po), _p(out), _p(st))
+    assert r == 0, "orc_lia rejected the problem"
+    return dict(kfs21=ko, pts=po, outlier=out[:ne].copy(), stats=st)
+
+
+def lia_system(pb):
+    """The full g2o system (H, b) of the window at its initial state: free key
+    frames' 15-blocks (VP VV VG VA) first, then 3 rows per point; Huber
+    weights from the initial errors."""
+    n_kf, n_p, ne, ni = len(pb.kfs), len(pb.pts_init), len(pb.edges), len(pb.imu_edges)
+    n = 15 * int((pb.fixed == 0).sum()) + 3 * n_p
+    H = np.zeros((n, n))
+    b = np.zeros(n)
+    r = lib().orc_lia_system(_p(pb.calib), n_kf, _p(pb.kfs), _p(pb.fixed), _p(pb.imu), n_p,
+                             _p(pb.pts_init), ne, _p(pb.edges), ni, _p(pb.imu_edges), _p(H), _p(b))
+    assert r == 0
+    return H, b
+
+
+def lia_vis_linearize(calib, kf_state, X, edge):
+    """One EdgeMono / EdgeStereo: error (3), Jl (3x3), Jp (3x6)."""
+    X = np.ascontiguousarray(X, np.float64)
+    calib, kf_state, edge = (np.array(a) for a in (calib, kf_state, edge))
+    err, Jl, Jp = np.zeros(3), np.zeros(9), np.zeros(18)
+    lib().orc_lia_vis_linearize(_p(calib), _p(kf_state), _p(X), _p(edge), _p(err), _p(Jl), _p(Jp))
+    return err, Jl.reshape(3, 3), Jp.reshape(3, 6)

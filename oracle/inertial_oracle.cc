@@ -39,21 +39,11 @@
 #include <vector>
 
 #include "g2o_math.h"
+#include "inertial_math.h"
 #include "../include/orbgpu.h"
 
 namespace oracle {
 namespace inertial {
-
-struct M3 {
-  double a[9];
-  double& operator()(int r, int c) { return a[3 * r + c]; }
-  double operator()(int r, int c) const { return a[3 * r + c]; }
-};
-struct V3 {
-  double a[3];
-  double& operator[](int i) { return a[i]; }
-  double operator[](int i) const { return a[i]; }
-};
 
 M3 eye() {
   M3 m{};
@@ -214,18 +204,9 @@ F3x3 so3f_exp(const float w[3]) {
   return m;
 }
 
-struct Preint {
-  const float* dR;
-  const float* dV;
-  const float* dP;
-  const float* JRg;
-  const float* JVg;
-  const float* JVa;
-  const float* JPg;
-  const float* JPa;
-  const float* bg;  // linearisation bias
-  const float* ba;
-};
+Preint preint_view(const orbgpu_imu_preint& p) {
+  return Preint{p.dR, p.dV, p.dP, p.JRg, p.JVg, p.JVa, p.JPg, p.JPa, p.bg, p.ba};
+}
 
 void fmv(const float* A, const float* v, float* o) {
   for (int i = 0; i < 3; ++i) o[i] = A[3 * i] * v[0] + A[3 * i + 1] * v[1] + A[3 * i + 2] * v[2];
@@ -261,17 +242,6 @@ V3 delta_lin(const float* d0, const float* Jg, const float* Ja, const Preint& p,
 }
 
 // ---- problem ---------------------------------------------------------------
-struct Calib {
-  double fx, fy, cx, cy, bf;
-  M3 Rcb, Rbc;
-  V3 tcb, tbc;
-};
-
-struct State {  // one frame's vertices
-  M3 Rwb, Rcw;
-  V3 twb, tcw, v, bg, ba;
-};
-
 void pose_update(State& s, const double* u, const Calib& c) {  // ImuCamPose::Update
   const V3 ut{{u[3], u[4], u[5]}};
   s.twb = add(s.twb, mv(s.Rwb, ut));
@@ -363,18 +333,18 @@ void bias_f(const State& s, float bg[3], float ba[3]) {  // IMU::Bias from doubl
   }
 }
 
-// EdgeInertial::computeError (g2o_types.cc:494-521); vertex 1 = prev, 2 = cur
-void inertial_error(const Problem& P, double e[9]) {
-  const State &s1 = P.prev, &s2 = P.cur;
+// EdgeInertial::computeError (g2o_types.cc:494-521)
+void inertial_edge_error(const State& s1, const State& s2, const Preint& pi, double dt, const V3& g,
+                         double e[9]) {
   float bg[3], ba[3];
   bias_f(s1, bg, ba);
-  const M3 dR = delta_rotation(P.pi, bg);
-  const V3 dV = delta_lin(P.pi.dV, P.pi.JVg, P.pi.JVa, P.pi, bg, ba);
-  const V3 dP = delta_lin(P.pi.dP, P.pi.JPg, P.pi.JPa, P.pi, bg, ba);
+  const M3 dR = delta_rotation(pi, bg);
+  const V3 dV = delta_lin(pi.dV, pi.JVg, pi.JVa, pi, bg, ba);
+  const V3 dP = delta_lin(pi.dP, pi.JPg, pi.JPa, pi, bg, ba);
   const M3 R1t = tr(s1.Rwb);
   const V3 er = LogSO3(mul(mul(tr(dR), R1t), s2.Rwb));
-  const V3 ev = sub(mv(R1t, sub(sub(s2.v, s1.v), scl(P.g, P.dt))), dV);
-  const V3 ep = sub(mv(R1t, sub(sub(sub(s2.twb, s1.twb), scl(s1.v, P.dt)), scl(P.g, P.dt * P.dt / 2))), dP);
+  const V3 ev = sub(mv(R1t, sub(sub(s2.v, s1.v), scl(g, dt))), dV);
+  const V3 ep = sub(mv(R1t, sub(sub(sub(s2.twb, s1.twb), scl(s1.v, dt)), scl(g, dt * dt / 2))), dP);
   for (int i = 0; i < 3; ++i) {
     e[i] = er[i];
     e[3 + i] = ev[i];
@@ -382,40 +352,47 @@ void inertial_error(const Problem& P, double e[9]) {
   }
 }
 
-
 // EdgeInertial::linearizeOplus (g2o_types.cc:523-578): J[9][24], columns in
 // edge-vertex order VP1(6) VV1(3) VG1(3) VA1(3) VP2(6) VV2(3)
-void inertial_jacobian(const Problem& P, double J[9][24]) {
-  const State &s1 = P.prev, &s2 = P.cur;
+void inertial_edge_jacobian(const State& s1, const State& s2, const Preint& pi, double dt,
+                            const V3& g, double J[9][24]) {
   float bg[3], ba[3];
   bias_f(s1, bg, ba);
-  const V3 dbg{{(double)(bg[0] - P.pi.bg[0]), (double)(bg[1] - P.pi.bg[1]),
-                (double)(bg[2] - P.pi.bg[2])}};
+  const V3 dbg{{(double)(bg[0] - pi.bg[0]), (double)(bg[1] - pi.bg[1]), (double)(bg[2] - pi.bg[2])}};
   const M3 Rwb1 = s1.Rwb, Rbw1 = tr(Rwb1), Rwb2 = s2.Rwb;
-  const M3 dR = delta_rotation(P.pi, bg);
+  const M3 dR = delta_rotation(pi, bg);
   const M3 eR = mul(mul(tr(dR), Rbw1), Rwb2);
   const V3 er = LogSO3(eR);
   const M3 invJr = InvRightJ(er);
-  const M3 JRg = from_f(P.pi.JRg);
+  const M3 JRg = from_f(pi.JRg);
   std::memset(J, 0, sizeof(double) * 9 * 24);
   auto put = [&](int r0, int c0, const M3& m, double s) {
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) J[r0 + i][c0 + j] = s * m(i, j);
   };
   put(0, 0, mul(mul(invJr, tr(Rwb2)), Rwb1), -1.0);
-  put(3, 0, hat(mv(Rbw1, sub(sub(s2.v, s1.v), scl(P.g, P.dt)))), 1.0);
-  put(6, 0, hat(mv(Rbw1, sub(sub(sub(s2.twb, s1.twb), scl(s1.v, P.dt)), scl(P.g, 0.5 * P.dt * P.dt)))), 1.0);
+  put(3, 0, hat(mv(Rbw1, sub(sub(s2.v, s1.v), scl(g, dt)))), 1.0);
+  put(6, 0, hat(mv(Rbw1, sub(sub(sub(s2.twb, s1.twb), scl(s1.v, dt)), scl(g, 0.5 * dt * dt)))), 1.0);
   put(6, 3, eye(), -1.0);
   put(3, 6, Rbw1, -1.0);
-  put(6, 6, Rbw1, -P.dt);
+  put(6, 6, Rbw1, -dt);
   put(0, 9, mul(mul(mul(invJr, tr(eR)), RightJ(mv(JRg, dbg))), JRg), -1.0);
-  put(3, 9, from_f(P.pi.JVg), -1.0);
-  put(6, 9, from_f(P.pi.JPg), -1.0);
-  put(3, 12, from_f(P.pi.JVa), -1.0);
-  put(6, 12, from_f(P.pi.JPa), -1.0);
+  put(3, 9, from_f(pi.JVg), -1.0);
+  put(6, 9, from_f(pi.JPg), -1.0);
+  put(3, 12, from_f(pi.JVa), -1.0);
+  put(6, 12, from_f(pi.JPa), -1.0);
   put(0, 15, invJr, 1.0);
   put(6, 18, mul(Rbw1, Rwb2), 1.0);
   put(3, 21, Rbw1, 1.0);
+}
+
+// the tracking problem's EdgeInertial: vertex set 1 = prev, 2 = cur
+void inertial_error(const Problem& P, double e[9]) {
+  inertial_edge_error(P.prev, P.cur, P.pi, P.dt, P.g, e);
+}
+
+void inertial_jacobian(const Problem& P, double J[9][24]) {
+  inertial_edge_jacobian(P.prev, P.cur, P.pi, P.dt, P.g, J);
 }
 
 // EdgePriorPoseImu::computeError / linearizeOplus (g2o_types.cc:739-764) on
@@ -645,24 +622,30 @@ State load_state(const orbgpu_imu_state& s) {
   return o;
 }
 
+Calib load_calib(const orbgpu_imu_calib& cb) {
+  Calib c;
+  c.fx = cb.fx;
+  c.fy = cb.fy;
+  c.cx = cb.cx;
+  c.cy = cb.cy;
+  c.bf = cb.bf;
+  c.Rcb = from_f(cb.Rcb);
+  c.tcb = from_f3(cb.tcb);
+  c.Rbc = from_f(cb.Rbc);
+  c.tbc = from_f3(cb.tbc);
+  return c;
+}
+
 void load_problem(Problem& P, int mode, const orbgpu_imu_calib& cb, const orbgpu_imu_state& cur,
                   const orbgpu_imu_state& prev, const orbgpu_imu_preint& pi,
                   const orbgpu_imu_prior* prior, const orbgpu_inertial_obs* obs, int n) {
   P.mode = mode;
-  P.c.fx = cb.fx;
-  P.c.fy = cb.fy;
-  P.c.cx = cb.cx;
-  P.c.cy = cb.cy;
-  P.c.bf = cb.bf;
-  P.c.Rcb = from_f(cb.Rcb);
-  P.c.tcb = from_f3(cb.tcb);
-  P.c.Rbc = from_f(cb.Rbc);
-  P.c.tbc = from_f3(cb.tbc);
+  P.c = load_calib(cb);
   P.cur = load_state(cur);
   P.prev = load_state(prev);
-  P.pi = Preint{pi.dR, pi.dV, pi.dP, pi.JRg, pi.JVg, pi.JVa, pi.JPg, pi.JPa, pi.bg, pi.ba};
+  P.pi = preint_view(pi);
   P.dt = pi.dT;
-  P.g = V3{{0, 0, -(double)9.81f}};  // IMU::GRAVITY_VALUE (float)
+  P.g = gravity();  // IMU::GRAVITY_VALUE (float)
   std::memcpy(P.info, pi.info, sizeof(P.info));
   std::memcpy(P.info_g, pi.info_g, sizeof(P.info_g));
   std::memcpy(P.info_a, pi.info_a, sizeof(P.info_a));

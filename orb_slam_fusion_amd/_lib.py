@@ -129,6 +129,13 @@ assert (IMU_STATE_DTYPE.itemsize, IMU_PREINT_DTYPE.itemsize, IMU_PRIOR_DTYPE.ite
         INERTIAL_RESULT_DTYPE.itemsize) == (132, 1064, 1968, 116, 32, 2064)
 INERTIAL_LAST_FRAME, INERTIAL_LAST_KEYFRAME = 0, 1
 
+# orbgpu_lia_imu_edge: one temporal link of LocalInertialBA (EdgeInertial +
+# EdgeGyroRW + EdgeAccRW between key frames kf1 = mPrevKF and kf2)
+LIA_IMU_EDGE_DTYPE = np.dtype([("kf1", "<i4"), ("kf2", "<i4"), ("flags", "<i4"), ("pad_", "<i4"),
+                               ("preint", IMU_PREINT_DTYPE)], align=True)
+assert LIA_IMU_EDGE_DTYPE.itemsize == 1080
+LIA_ROBUST, LIA_DOWNWEIGHT = 1, 2
+
 
 class FrameGeom(ctypes.Structure):
     """orbgpu_frame_geom: Frame::mnMinX/mnMaxX/mnMinY/mnMaxY, mnScaleLevels,
@@ -232,6 +239,11 @@ SIGNATURES = {
         _I,
         [_P, ctypes.POINTER(Camera), _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, ctypes.c_double, _P,
          _P, _P, _P, _P, _P, _P, _P],
+    ),
+    "orbgpu_lia_optimize": (
+        _I,
+        [_P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, ctypes.c_double, _P, _P, _P, _P,
+         _P],
     ),
 }
 

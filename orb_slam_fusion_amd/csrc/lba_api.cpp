@@ -105,28 +105,51 @@ void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c) {
   delete c;
 }
 
-orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf,
-                                  const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
-                                  const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
-                                  int pt_begin, int pt_end, int iterations, double lambda_init,
-                                  const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce,
-                                  void* user, orbgpu_pose* poses_out, double* poses_out_d,
-                                  float* pts_out, uint8_t* outlier, double* stats) {
-  if (!h || !cam || n_kf <= 0 || !poses_in || !fixed || n_pts < 0 || n_edges < 0 ||
-      (n_edges > 0 && !edges) || (n_pts > 0 && !pts_in) || pt_begin < 0 || pt_end > n_pts ||
-      pt_begin > pt_end || iterations < 0 || !poses_out || (pt_end > pt_begin && !pts_out) ||
-      (n_edges > 0 && !outlier) || (!reduce && (pt_begin != 0 || pt_end != n_pts)))
-    return ORBGPU_ERR_INVALID;
+}  // extern "C"
+
+namespace {
+
+// What distinguishes the two windows the context solves: the key-frame model
+// and, for LocalInertialBA, the IMU links and the close flags.
+struct ModelIn {
+  int model = kModelSe3;
+  int pdim = 6;
+  int pstride = 7;
+  const double* state0 = nullptr;  // [pstride * n_kf] initial key-frame states
+  LiaCalibDev icb{};
+  const uint8_t* close = nullptr;  // [n_pts]
+  int n_imu = 0;
+  const orbgpu_lia_imu_edge* imu = nullptr;
+};
+
+struct WindowOut {
+  LbaCtrl ctrl;
+  std::vector<double> state;  // [pstride * n_kf]
+  int n_out = 0;
+};
+
+// The shared body of orbgpu_lba_optimize / orbgpu_lia_optimize: layout,
+// one upload, the device LM loop (or the host-in-the-loop sharded form), the
+// outlier classification and one download.
+orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, const uint8_t* fixed,
+                         int n_pts, const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
+                         int pt_begin, int pt_end, int iterations, double lambda_init,
+                         const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce, void* user,
+                         const ModelIn& m, float* pts_out, uint8_t* outlier, WindowOut& wo) {
   if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
   hipStream_t st = h->stream;
+  const bool imu = m.model == kModelImu;
 
   // ---- graph layout of this shard, O(edges): free-pose indices, point-major
   // edges (insertion order kept inside a point), per-pose edge lists, pairs
-  std::vector<int> hidx(n_kf, -1);
+  std::vector<int> hidx(n_kf, -1), free_kf;
   int nf = 0;
   for (int k = 0; k < n_kf; ++k)
-    if (!fixed[k]) hidx[k] = nf++;
-  const int n = 6 * nf;
+    if (!fixed[k]) {
+      hidx[k] = nf++;
+      free_kf.push_back(k);
+    }
+  const int n = m.pdim * nf;
   const int npad = (n + 15) / 16 * 16;
   if (npad > 2048) return ORBGPU_ERR_INVALID;  // reduced system beyond the solver's LDS vectors
   const int np = pt_end - pt_begin;
@@ -145,12 +168,26 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   const int n_pairs = nf * (nf + 1) / 2;
   std::vector<int> gidx(ne);  // shard edge -> caller's edge index
   std::vector<int> pose_cnt(nf + 1, 0);
+  // IMU links incident to each free key frame (link order)
+  std::vector<int> inc(nf + 1, 0), inc_list;
+  if (imu) {
+    std::vector<std::vector<int>> lists(nf);
+    for (int l = 0; l < m.n_imu; ++l)
+      for (int k : {m.imu[l].kf1, m.imu[l].kf2})
+        if (hidx[k] >= 0) lists[hidx[k]].push_back(l);
+    for (int f = 0; f < nf; ++f) {
+      inc[f + 1] = inc[f] + (int)lists[f].size();
+      inc_list.insert(inc_list.end(), lists[f].begin(), lists[f].end());
+    }
+  }
 
   // ---- sizes: upload | download | compute
-  const size_t K7 = 7 * (size_t)n_kf, P3 = 3 * (size_t)std::max(np, 1);
+  const size_t KS = (size_t)m.pstride * n_kf, P3 = 3 * (size_t)std::max(np, 1);
   const size_t E = std::max(ne, 1), P = std::max(np, 1), F = std::max(nf, 1);
+  const size_t NI = std::max(m.n_imu, 1);
   const int nblk = (int)((std::max(std::max(ne, np), 1) + 255) / 256) + nf + 1;
-  const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1);
+  const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
+                        F + (nf + 1) + std::max(inc_list.size(), (size_t)1);
   size_t up = 0;
   const size_t u_ctrl = up;
   up += 128;
@@ -161,11 +198,15 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   const size_t u_ints = up;
   up = align_up(up + sizeof(int) * n_ints, 256);
   const size_t u_state = up;
-  up = align_up(up + sizeof(double) * (2 * K7 + 2 * P3), 256);
-  const size_t d_begin = up;  // download: ctrl copy | poses | pts | outlier
+  up = align_up(up + sizeof(double) * (2 * KS + 2 * P3), 256);
+  const size_t u_imu = up;
+  if (imu) up = align_up(up + sizeof(LiaImuDev) * NI, 256);
+  const size_t u_close = up;
+  if (imu) up = align_up(up + P, 256);
+  const size_t d_begin = up;  // download: ctrl copy | states | pts | outlier
   size_t dn = 128;
   const size_t d_out = dn;
-  dn += sizeof(double) * (K7 + P3);
+  dn += sizeof(double) * (KS + P3);
   const size_t d_outlier = dn;
   dn = align_up(dn + E, 256);
   size_t cz = align_up(d_begin + dn, 256);
@@ -179,7 +220,9 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
                c_hll = take(9 * P), c_bl = take(3 * P), c_hpp = take(36 * F), c_bp = take(6 * F),
                c_diag = take(n + 2), c_sys = take((size_t)n * n + 2 * n + 2),
                c_work = take(solve_lds ? 2 : (size_t)npad * (npad + 1) + (size_t)(npad / 16) * 256),
-               c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk);
+               c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
+               c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
+               c_itot = take(2);
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
@@ -211,6 +254,9 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   int* I_ef = I_pb + (nf + 1);
   int* I_pi = I_ef + E;
   int* I_pj = I_pi + std::max(n_pairs, 1);
+  int* I_fk = I_pj + std::max(n_pairs, 1);
+  int* I_inc = I_fk + F;
+  int* I_incl = I_inc + (nf + 1);
   std::copy(hidx.begin(), hidx.end(), I_hidx);
   std::copy(cnt.begin(), cnt.end(), I_pt);
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
@@ -233,16 +279,20 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
       I_pi[k] = i;
       I_pj[k] = j;
     }
+  std::copy(free_kf.begin(), free_kf.end(), I_fk);
+  std::copy(inc.begin(), inc.end(), I_inc);
+  std::copy(inc_list.begin(), inc_list.end(), I_incl);
   auto* S0 = reinterpret_cast<double*>(U + u_state);
-  for (int k = 0; k < n_kf; ++k) {
-    const orbgpu_pose& q = poses_in[k];
-    const double v[7] = {q.qx, q.qy, q.qz, q.qw, q.tx, q.ty, q.tz};
-    for (int c = 0; c < 7; ++c) S0[7 * (size_t)k + c] = S0[K7 + 7 * (size_t)k + c] = v[c];
-  }
-  double* X0 = S0 + 2 * K7;
+  std::copy(m.state0, m.state0 + KS, S0);
+  std::copy(m.state0, m.state0 + KS, S0 + KS);
+  double* X0 = S0 + 2 * KS;
   for (int p = 0; p < np; ++p)
     for (int c = 0; c < 3; ++c)
       X0[3 * (size_t)p + c] = X0[P3 + 3 * (size_t)p + c] = pts_in[3 * (size_t)(pt_begin + p) + c];
+  if (imu) {
+    std::memcpy(U + u_imu, m.imu, sizeof(LiaImuDev) * m.n_imu);
+    std::memcpy(U + u_close, m.close + pt_begin, np);
+  }
   if (hipMemcpyAsync(h->arena, U, up, hipMemcpyHostToDevice, st) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
 
@@ -271,9 +321,9 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   a.pair_i = dI + (I_pi - I);
   a.pair_j = dI + (I_pj - I);
   a.poses[0] = dp(u_state);
-  a.poses[1] = dp(u_state) + K7;
-  a.pts[0] = dp(u_state) + 2 * K7;
-  a.pts[1] = dp(u_state) + 2 * K7 + P3;
+  a.poses[1] = dp(u_state) + KS;
+  a.pts[0] = dp(u_state) + 2 * KS;
+  a.pts[1] = dp(u_state) + 2 * KS + P3;
   a.err = dp(c_err);
   a.hpl = dp(c_hpl);
   a.hpp_e = dp(c_hppe);
@@ -292,6 +342,24 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   a.counter = reinterpret_cast<unsigned*>(A + u_cnt);
   a.ctrl = reinterpret_cast<LbaCtrl*>(A + u_ctrl);
   a.host = h->host_dev;
+  a.model = m.model;
+  a.pdim = m.pdim;
+  a.pstride = m.pstride;
+  if (imu) {
+    a.icb = m.icb;
+    a.close = reinterpret_cast<const uint8_t*>(A + u_close);
+    a.n_imu = m.n_imu;
+    a.imu = reinterpret_cast<const LiaImuDev*>(A + u_imu);
+    a.free_kf = dI + (I_fk - I);
+    a.imu_inc = dI + (I_inc - I);
+    a.imu_inc_list = dI + (I_incl - I);
+    a.imu_q = dp(c_imuq);
+    a.himu = dp(c_himu);
+    a.imu_tot = dp(c_itot);
+    // the reduced system's IMU rows get no Schur terms: zero once per call
+    if (hipMemsetAsync(a.sys, 0, sizeof(double) * ((size_t)n * n + 2 * n), st) != hipSuccess)
+      return ORBGPU_ERR_DEVICE;
+  }
 
   volatile LbaHostWords* hw = h->host;
   hw->progress = 0;
@@ -350,17 +418,51 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
       hipMemcpyAsync(h->staging, D, dn, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
-  LbaCtrl c;
-  std::memcpy(&c, h->staging, sizeof(c));
+  std::memcpy(&wo.ctrl, h->staging, sizeof(LbaCtrl));
   const auto* out = reinterpret_cast<const double*>(h->staging + d_out);
   const auto* lo = reinterpret_cast<const uint8_t*>(h->staging + d_outlier);
-  int n_out = 0;
+  wo.n_out = 0;
   for (int j = 0; j < ne; ++j) {
     outlier[gidx[j]] = lo[j];
-    n_out += lo[j];
+    wo.n_out += lo[j];
   }
+  wo.state.assign(out, out + KS);
+  const double* xo = out + KS;
+  for (int p = 0; p < np; ++p)
+    for (int q = 0; q < 3; ++q) pts_out[3 * (size_t)(pt_begin + p) + q] = (float)xo[3 * (size_t)p + q];
+  return ORBGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf,
+                                  const orbgpu_pose* poses_in, const uint8_t* fixed, int n_pts,
+                                  const float* pts_in, int n_edges, const orbgpu_lba_edge* edges,
+                                  int pt_begin, int pt_end, int iterations, double lambda_init,
+                                  const volatile uint8_t* stop_flag, orbgpu_lba_reduce_fn reduce,
+                                  void* user, orbgpu_pose* poses_out, double* poses_out_d,
+                                  float* pts_out, uint8_t* outlier, double* stats) {
+  if (!h || !cam || n_kf <= 0 || !poses_in || !fixed || n_pts < 0 || n_edges < 0 ||
+      (n_edges > 0 && !edges) || (n_pts > 0 && !pts_in) || pt_begin < 0 || pt_end > n_pts ||
+      pt_begin > pt_end || iterations < 0 || !poses_out || (pt_end > pt_begin && !pts_out) ||
+      (n_edges > 0 && !outlier) || (!reduce && (pt_begin != 0 || pt_end != n_pts)))
+    return ORBGPU_ERR_INVALID;
+  std::vector<double> s0(7 * (size_t)n_kf);
   for (int k = 0; k < n_kf; ++k) {
-    const double* v = out + 7 * (size_t)k;
+    const orbgpu_pose& q = poses_in[k];
+    const double v[7] = {q.qx, q.qy, q.qz, q.qw, q.tx, q.ty, q.tz};
+    std::copy(v, v + 7, s0.begin() + 7 * (size_t)k);
+  }
+  ModelIn m;
+  m.state0 = s0.data();
+  WindowOut wo;
+  const orbgpu_status r = run_window(h, cam, n_kf, fixed, n_pts, pts_in, n_edges, edges, pt_begin, pt_end,
+                                     iterations, lambda_init, stop_flag, reduce, user, m, pts_out, outlier, wo);
+  if (r != ORBGPU_OK) return r;
+  for (int k = 0; k < n_kf; ++k) {
+    const double* v = wo.state.data() + 7 * (size_t)k;
     if (poses_out_d)
       for (int q = 0; q < 7; ++q) poses_out_d[7 * k + q] = v[q];
     // Sophus::SE3f(rotation().cast<float>(), translation().cast<float>())
@@ -370,16 +472,105 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
     for (int q = 0; q < 4; ++q) f[q] /= qn;
     poses_out[k] = orbgpu_pose{f[0], f[1], f[2], f[3], f[4], f[5], f[6]};
   }
-  const double* xo = out + K7;
-  for (int p = 0; p < np; ++p)
-    for (int q = 0; q < 3; ++q) pts_out[3 * (size_t)(pt_begin + p) + q] = (float)xo[3 * (size_t)p + q];
   if (stats) {
-    stats[0] = c.chi_init;
-    stats[1] = c.cur;
-    stats[2] = c.iters_done;
-    stats[3] = c.trials;
-    stats[4] = c.lambda;
-    stats[5] = n_out;
+    stats[0] = wo.ctrl.chi_init;
+    stats[1] = wo.ctrl.cur;
+    stats[2] = wo.ctrl.iters_done;
+    stats[3] = wo.ctrl.trials;
+    stats[4] = wo.ctrl.lambda;
+    stats[5] = wo.n_out;
+  }
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* h, const orbgpu_imu_calib* calib, int n_kf,
+                                  const orbgpu_imu_state* kfs, const uint8_t* fixed,
+                                  const uint8_t* imu, int n_pts, const float* pts_in,
+                                  const uint8_t* close, int n_edges, const orbgpu_lba_edge* edges,
+                                  int n_imu, const orbgpu_lia_imu_edge* imu_edges, int iterations,
+                                  double lambda_init, orbgpu_imu_state* kfs_out, double* kfs_out_d,
+                                  float* pts_out, uint8_t* outlier, double* stats) {
+  if (!h || !calib || n_kf <= 0 || !kfs || !fixed || !imu || n_pts < 0 || n_edges < 0 ||
+      (n_edges > 0 && !edges) || (n_pts > 0 && (!pts_in || !pts_out || !close)) || n_imu < 0 ||
+      n_imu > kMaxImuLinks || (n_imu > 0 && !imu_edges) || iterations < 0 || !(lambda_init > 0) ||
+      !kfs_out || (n_edges > 0 && !outlier))
+    return ORBGPU_ERR_INVALID;
+  for (int k = 0; k < n_kf; ++k)
+    if (!fixed[k] && !imu[k]) return ORBGPU_ERR_INVALID;  // a free key frame carries its IMU vertices
+  for (int l = 0; l < n_imu; ++l) {
+    const orbgpu_lia_imu_edge& e = imu_edges[l];
+    if (e.kf1 < 0 || e.kf1 >= n_kf || e.kf2 < 0 || e.kf2 >= n_kf || e.kf1 == e.kf2 || !imu[e.kf1] ||
+        !imu[e.kf2])
+      return ORBGPU_ERR_INVALID;
+  }
+  // ImuCamPose(pKF): Rwb, twb, Rcw, tcw (the float pose), and the vertex estimates
+  std::vector<double> s0(kImuStateStride * (size_t)n_kf);
+  for (int k = 0; k < n_kf; ++k) {
+    const orbgpu_imu_state& g = kfs[k];
+    double* d = s0.data() + kImuStateStride * (size_t)k;
+    for (int i = 0; i < 9; ++i) {
+      d[i] = g.Rwb[i];
+      d[12 + i] = g.Rcw[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      d[9 + i] = g.twb[i];
+      d[21 + i] = g.tcw[i];
+      d[24 + i] = g.v[i];
+      d[27 + i] = g.bg[i];
+      d[30 + i] = g.ba[i];
+    }
+  }
+  ModelIn m;
+  m.model = kModelImu;
+  m.pdim = kImuDim;
+  m.pstride = kImuStateStride;
+  m.state0 = s0.data();
+  m.icb = LiaCalibDev{calib->fx, calib->fy, calib->cx, calib->cy, calib->bf, {}, {}, {}, {}};
+  for (int i = 0; i < 9; ++i) {
+    m.icb.Rcb[i] = calib->Rcb[i];
+    m.icb.Rbc[i] = calib->Rbc[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    m.icb.tcb[i] = calib->tcb[i];
+    m.icb.tbc[i] = calib->tbc[i];
+  }
+  m.close = close;
+  m.n_imu = n_imu;
+  m.imu = imu_edges;
+  const orbgpu_camera cam{calib->fx, calib->fy, calib->cx, calib->cy, calib->bf};
+  WindowOut wo;
+  // *pbStopFlag is attached after optimize() (optimizer.cc:2794): no stop flag
+  const orbgpu_status r = run_window(h, &cam, n_kf, fixed, n_pts, pts_in, n_edges, edges, 0, n_pts, iterations,
+                                     lambda_init, nullptr, nullptr, nullptr, m, pts_out, outlier, wo);
+  if (r != ORBGPU_OK) return r;
+  for (int k = 0; k < n_kf; ++k) {
+    const double* d = wo.state.data() + kImuStateStride * (size_t)k;
+    orbgpu_imu_state& o = kfs_out[k];
+    for (int i = 0; i < 9; ++i) {
+      o.Rwb[i] = (float)d[i];
+      o.Rcw[i] = (float)d[12 + i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      o.twb[i] = (float)d[9 + i];
+      o.tcw[i] = (float)d[21 + i];
+      o.v[i] = (float)d[24 + i];
+      o.bg[i] = (float)d[27 + i];
+      o.ba[i] = (float)d[30 + i];
+    }
+    if (kfs_out_d) {
+      double* q = kfs_out_d + 21 * (size_t)k;
+      std::copy(d, d + 12, q);            // Rwb, twb
+      std::copy(d + 24, d + 33, q + 12);  // v, bg, ba
+    }
+  }
+  if (stats) {
+    stats[0] = wo.ctrl.chi_init;
+    stats[1] = wo.ctrl.last;
+    stats[2] = wo.ctrl.iters_done;
+    stats[3] = wo.ctrl.trials;
+    stats[4] = wo.ctrl.lambda;
+    stats[5] = wo.n_out;
+    stats[6] = wo.ctrl.cur;
   }
   return ORBGPU_OK;
 }

@@ -19,6 +19,13 @@
 //   k_lba_trial      thread / edge      back-substitution, trial state, errors,
 //                                       robust chi2 and computeScale -> decision
 //
+// LocalInertialBA (optimizer.cc:2440-2826) runs on the same kernels with the
+// kModelImu key frame (lba_launch.h): ImuCamPose state, body-frame visual
+// Jacobians (EdgeMono / EdgeStereo, g2o_types.cc:334-415), 15 reduced-system
+// rows per free key frame, and the IMU links (EdgeInertial + EdgeGyroRW +
+// EdgeAccRW, no points) evaluated by one workgroup (k_lia_imu) and added to
+// the camera-side system (k_lia_assemble) before the solve.
+//
 // Sums inside a launch have a fixed order (per-thread loops in edge order,
 // fixed trees, block partials summed by the last block in block order), so
 // results are reproducible run to run.  The reduction orders differ from
@@ -32,6 +39,8 @@
 
 // fp64 solver TU (tolerance parity, not bit parity): products may fuse.
 #pragma clang fp contract(fast)
+
+#include "imu_math_dev.h"
 
 namespace orbgpu {
 
@@ -160,6 +169,98 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
   }
 }
 
+// ---- key-frame models --------------------------------------------------------
+static_assert(sizeof(LiaCalibDev) == sizeof(CalibD), "LiaCalibDev == CalibD");
+
+__device__ __forceinline__ CalibD calib_of(const LbaArgs& a) {
+  CalibD c;
+  c.fx = a.icb.fx;
+  c.fy = a.icb.fy;
+  c.cx = a.icb.cx;
+  c.cy = a.icb.cy;
+  c.bf = a.icb.bf;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    c.Rcb[i] = a.icb.Rcb[i];
+    c.Rbc[i] = a.icb.Rbc[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    c.tcb[i] = a.icb.tcb[i];
+    c.tbc[i] = a.icb.tbc[i];
+  }
+  return c;
+}
+
+// camera point Xc = Rcw X + tcw of an ImuCamPose state (Rcw at +12, tcw at +21)
+__device__ __forceinline__ void imu_cam_point(const double* ks, const double X[3], double Xc[3]) {
+  const double* R = ks + 12;
+  const double* t = ks + 21;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) Xc[r] = R[3 * r] * X[0] + R[3 * r + 1] * X[1] + R[3 * r + 2] * X[2] + t[r];
+}
+
+// Visual edge error at key-frame state ks (7 or 33 doubles); returns
+// isDepthPositive on the same state.  kModelImu: EdgeMono / EdgeStereo
+// (ImuCamPose::Project / ProjectStereo, g2o_types.cc:171-190; the stereo
+// invZ in double).
+template <int M>
+__device__ __forceinline__ bool vis_error(const LbaArgs& a, const LbaEdgeDev& e, const double* ks,
+                                          const double X[3], double err[3]) {
+  if constexpr (M == kModelSe3) {
+    return lba_error(e, load_pose(ks), X, a.cam, err);
+  } else {
+    double Xc[3];
+    imu_cam_point(ks, X, Xc);
+    const double u = a.cam.fx * Xc[0] / Xc[2] + a.cam.cx;
+    const double v = a.cam.fy * Xc[1] / Xc[2] + a.cam.cy;
+    err[0] = (double)e.u - u;
+    err[1] = (double)e.v - v;
+    err[2] = e.ur >= 0.f ? (double)e.ur - (u - a.cam.bf * (1 / Xc[2])) : 0.0;
+    return Xc[2] > 0.0;
+  }
+}
+
+// Visual edge Jacobians (point Jl, pose Jp).  kModelImu: Jl = -proj_jac Rcw,
+// Jp = proj_jac Rcb SE3deriv(Xb) (g2o_types.cc:334-415); mono rows 2 = 0.
+template <int M>
+__device__ __forceinline__ void vis_jacobians(const LbaArgs& a, const LbaEdgeDev& e, const double* ks,
+                                              const double X[3], double Jl[3][3], double Jp[3][6]) {
+  if constexpr (M == kModelSe3) {
+    lba_jacobians(e, load_pose(ks), X, a.cam, Jl, Jp);
+  } else {
+    const LiaCalibDev& c = a.icb;
+    double Xc[3];
+    imu_cam_point(ks, X, Xc);
+    const double* R = ks + 12;
+    const bool st = e.ur >= 0.f;
+    double pj[3][3] = {{c.fx / Xc[2], 0, -c.fx * Xc[0] / (Xc[2] * Xc[2])},
+                       {0, c.fy / Xc[2], -c.fy * Xc[1] / (Xc[2] * Xc[2])},
+                       {0, 0, 0}};
+    if (st) {
+      pj[2][0] = pj[0][0];
+      pj[2][1] = pj[0][1];
+      pj[2][2] = pj[0][2] + c.bf * (1.0 / (Xc[2] * Xc[2]));
+    }
+    double Xb[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      Xb[r] = c.Rbc[3 * r] * Xc[0] + c.Rbc[3 * r + 1] * Xc[1] + c.Rbc[3 * r + 2] * Xc[2] + c.tbc[r];
+    const double x = Xb[0], y = Xb[1], z = Xb[2];
+    const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Jl[r][k] = -(pj[r][0] * R[k] + pj[r][1] * R[3 + k] + pj[r][2] * R[6 + k]);
+      double PR[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) PR[k] = pj[r][0] * c.Rcb[k] + pj[r][1] * c.Rcb[3 + k] + pj[r][2] * c.Rcb[6 + k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Jp[r][k] = PR[0] * S[0][k] + PR[1] * S[1][k] + PR[2] * S[2][k];
+    }
+  }
+}
+
 // (Hll + lambda I)^-1 by cofactors (Eigen compute_inverse_size3); returns the
 // determinant (0 = singular landmark block: the trial fails).
 __device__ __forceinline__ double inv3_lambda(const double* __restrict__ h, double lambda, double Di[9]) {
@@ -267,6 +368,7 @@ __device__ void ctl_init(const LbaArgs& a, double chi, int stop) {
   c.cur = chi;
   c.chi_init = chi;
   c.ini = chi;
+  c.last = chi;
   c.it = 0;
   c.q = 0;
   c.nbad = 0;
@@ -291,6 +393,7 @@ __device__ void ctl_lambda(const LbaArgs& a, double maxdiag) {
 // one trial's verdict (optimization_algorithm_levenberg.cpp:118-167)
 __device__ void ctl_decide(const LbaArgs& a, double chi_trial, double scale_l, int bad, int stop) {
   LbaCtrl& c = *a.ctrl;
+  c.last = chi_trial;
   double tmp = chi_trial;
   if (bad) tmp = 1.7976931348623157e308;  // !ok2 -> tempChi = max
   double rho = c.cur - tmp;
@@ -331,17 +434,17 @@ __device__ void ctl_decide(const LbaArgs& a, double chi_trial, double scale_l, i
 }
 
 // ---- computeActiveErrors at the initial state ----------------------------
+template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   __shared__ double red[4];
   const int i = blockIdx.x * kThreads + threadIdx.x;
   double r0 = 0;
   if (i < a.n_edges) {
     const LbaEdgeDev e = a.edges[i];
-    const Se3 T = load_pose(a.poses[0] + 7 * e.kf);
     const double* x = a.pts[0] + 3 * e.point;
     const double X[3] = {x[0], x[1], x[2]};
     double err[3];
-    lba_error(e, T, X, a.cam, err);
+    vis_error<M>(a, e, a.poses[0] + a.pstride * e.kf, X, err);
     a.err[3 * i] = err[0];
     a.err[3 * i + 1] = err[1];
     a.err[3 * i + 2] = err[2];
@@ -354,6 +457,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   if (!last_block(a.counter + 0)) return;
   double s[1];
   sum_partials<1>(a.partials, gridDim.x, s, red);
+  if (M == kModelImu) s[0] += a.imu_tot[0];  // the IMU links at the initial state (k_lia_imu)
   if (threadIdx.x == 0) {
     const int stop = host_stop(a);
     if (a.sharded) {
@@ -371,6 +475,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
 // The row loops run over 3 rows for mono edges too: their third Jacobian
 // row and error are zero, and adding an exact 0 changes no sum (constant
 // trip counts keep the Jacobians in registers, not in scratch).
+template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done || !c.need_build) return;
@@ -379,10 +484,9 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   const LbaEdgeDev e = a.edges[i];
   const double* x = a.pts[c.state] + 3 * e.point;
   const double X[3] = {x[0], x[1], x[2]};
-  const Se3 T = load_pose(a.poses[c.state] + 7 * e.kf);
   const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
   double Jl[3][3], Jp[3][6];
-  lba_jacobians(e, T, X, a.cam, Jl, Jp);
+  vis_jacobians<M>(a, e, a.poses[c.state] + a.pstride * e.kf, X, Jl, Jp);
   double r0, w;
   huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
   const double info = (double)e.inv_sigma2, wi = w * info;
@@ -488,7 +592,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
         }
         a.hpp[36 * (size_t)f + 6 * s + q] = v;
         a.hpp[36 * (size_t)f + 6 * q + s] = v;
-        if (s == q) a.diag[6 * f + s] = v;
+        if (s == q) a.diag[a.pdim * f + s] = v;
       } else {
         a.bp[6 * (size_t)f + (k - 21)] = v;
       }
@@ -638,12 +742,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
       const int s = t / 6, q = t - 6 * s;
       if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
       const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
-      a.sys[(size_t)(6 * fi + s) * n + 6 * fj + q] = v;
-      a.sys[(size_t)(6 * fj + q) * n + 6 * fi + s] = v;
+      const int P = a.pdim;  // the pose block's rows (VP first in a kModelImu key frame)
+      a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
+      a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
     } else {
-      const int s = t - 36;
-      a.sys[(size_t)n * n + 6 * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
-      a.sys[(size_t)n * n + n + 6 * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
+      const int s = t - 36, P = a.pdim;
+      a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
+      a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
     }
   }
 }
@@ -722,6 +827,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     y = smem + N;
   }
   const double* src = a.sys;
+  const double* hm = a.himu;  // kModelImu: the IMU links' part of the system (else NULL)
   // S + lambda I with identity padding (D = 1, L = 0): 16 loads in flight per
   // thread before the LDS writes
   for (int e0 = t; e0 < N * N; e0 += 16 * kSolveThreads) {
@@ -729,7 +835,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
-      v[u] = e < N * N && r < n && cc < n ? src[(size_t)r * n + cc] : 0.0;
+      v[u] = e < N * N && r < n && cc < n ? src[(size_t)r * n + cc] + (hm ? hm[(size_t)r * n + cc] : 0.0)
+                                           : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -737,7 +844,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
       if (e < N * N) S[(size_t)r * LD + cc] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
     }
   }
-  for (int r = t; r < N; r += kSolveThreads) y[r] = r < n ? src[(size_t)n * n + r] : 0.0;
+  for (int r = t; r < N; r += kSolveThreads)
+    y[r] = r < n ? src[(size_t)n * n + r] + (hm ? hm[(size_t)n * n + r] : 0.0) : 0.0;
   if (t == 0) bad = 0;
   __syncthreads();
   LBA_STAMP(0);
@@ -880,7 +988,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   for (int r = t; r < n; r += kSolveThreads) {
     const double xv = y[r];
     a.xp[r] = xv;
-    sc += xv * (lambda * xv + src[(size_t)n * n + n + r]);
+    sc += xv * (lambda * xv + src[(size_t)n * n + n + r] + (hm ? hm[(size_t)n * n + r] : 0.0));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o, 64);
@@ -923,24 +1031,28 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial_poses(LbaArgs a) {
 // edge writes the point), the edge's error and robust chi2 at the trial state
 // (computeActiveErrors), the landmark part of computeScale; the last block
 // sums the partials in block order and takes the LM decision.
+// kModelImu: the trial key-frame states come from k_lia_trial_states.
+template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
-  __shared__ double tp[kMaxKfLds * 7];
   __shared__ double red[4 * 3];
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
   const double lambda = c.lambda;
   const int s0 = c.state, s1 = s0 ^ 1;
-  const bool lds_poses = a.n_kf <= kMaxKfLds;
-  if (lds_poses) {
-    for (int k = threadIdx.x; k < a.n_kf; k += kThreads) {
-      trial_pose(a, s0, k, tp + 7 * k);
-      if (blockIdx.x == 0)
+  const double* tposes = a.poses[s1];
+  if constexpr (M == kModelSe3) {
+    __shared__ double tp[kMaxKfLds * 7];
+    if (a.n_kf <= kMaxKfLds) {
+      for (int k = threadIdx.x; k < a.n_kf; k += kThreads) {
+        trial_pose(a, s0, k, tp + 7 * k);
+        if (blockIdx.x == 0)
 #pragma unroll
-        for (int q = 0; q < 7; ++q) a.poses[s1][7 * k + q] = tp[7 * k + q];
+          for (int q = 0; q < 7; ++q) a.poses[s1][7 * k + q] = tp[7 * k + q];
+      }
+      __syncthreads();
+      tposes = tp;
     }
-    __syncthreads();
   }
-  const double* tposes = lds_poses ? tp : a.poses[s1];
   const int i = blockIdx.x * kThreads + threadIdx.x;
   double part[3] = {0, 0, 0};  // robust chi2, landmark scale, singular landmark blocks
   if (i < a.n_edges) {
@@ -961,7 +1073,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int q = 0; q < 6; ++q) xv[u][q] = fs[u] >= 0 ? a.xp[6 * fs[u] + q] : 0.0;
+        for (int q = 0; q < 6; ++q) xv[u][q] = fs[u] >= 0 ? a.xp[a.pdim * fs[u] + q] : 0.0;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (fs[u] >= 0)
@@ -987,9 +1099,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
       }
       part[2] = det == 0 ? 1.0 : 0.0;
     }
-    const Se3 T = load_pose(tposes + 7 * e.kf);
     double err[3];
-    lba_error(e, T, X, a.cam, err);
+    vis_error<M>(a, e, tposes + a.pstride * e.kf, X, err);
     a.err[3 * i] = err[0];
     a.err[3 * i + 1] = err[1];
     a.err[3 * i + 2] = err[2];
@@ -1003,6 +1114,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   if (!last_block(a.counter + 2)) return;
   double s[3];
   sum_partials<3>(a.partials, gridDim.x, s, red);
+  if (M == kModelImu) s[0] += a.imu_tot[0];  // the IMU links at the trial state (k_lia_imu)
   if (threadIdx.x == 0) {
     if (a.n_edgeless > 0) {  // points without edges: (0 + lambda I)^-1
       const double h0[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1041,22 +1153,275 @@ __global__ void k_lba_ctl(LbaArgs a, int mode) {
 
 // ---- optimizer.cc:1362-1400: chi2 of the last computeActiveErrors, depth at
 // the final estimates; the final state copied out in one buffer.
+// kModelImu: optimizer.cc:2799-2826 -- the float thresholds chi2Mono2 =
+// 5.991f (1.5f * 5.991f for a close point) and chi2Stereo2 = 7.815f, depth
+// only for mono edges.
+template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* __restrict__ outlier,
                                                            double* __restrict__ out) {
   const int s = a.ctrl->state;
   const int i = blockIdx.x * kThreads + threadIdx.x;
-  if (i < 7 * a.n_kf) out[i] = a.poses[s][i];
-  if (i < 3 * a.n_pts) out[7 * (size_t)a.n_kf + i] = a.pts[s][i];
+  if (i < a.pstride * a.n_kf) out[i] = a.poses[s][i];
+  if (i < 3 * a.n_pts) out[(size_t)a.pstride * a.n_kf + i] = a.pts[s][i];
   if (i >= a.n_edges) return;
   const LbaEdgeDev e = a.edges[i];
-  const Se3 T = load_pose(a.poses[s] + 7 * e.kf);
   const double* x = a.pts[s] + 3 * e.point;
   const double X[3] = {x[0], x[1], x[2]};
   double tmp[3];
-  const bool depth = lba_error(e, T, X, a.cam, tmp);
+  const bool depth = vis_error<M>(a, e, a.poses[s] + a.pstride * e.kf, X, tmp);
   const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
   const double chi = lba_chi2(e, ev);
-  outlier[i] = (chi > (e.ur < 0.f ? 5.991 : 7.815) || !depth) ? 1 : 0;
+  if constexpr (M == kModelSe3) {
+    outlier[i] = (chi > (e.ur < 0.f ? 5.991 : 7.815) || !depth) ? 1 : 0;
+  } else {
+    constexpr float chi2Mono2 = 5.991f, chi2Stereo2 = 7.815f;
+    bool bad;
+    if (e.ur < 0.f) {
+      const bool close = a.close[e.point] != 0;
+      bad = (chi > chi2Mono2 && !close) || (chi > 1.5f * chi2Mono2 && close) || !depth;
+    } else {
+      bad = chi > chi2Stereo2;
+    }
+    outlier[i] = bad ? 1 : 0;
+  }
+}
+
+// ---- LocalInertialBA's IMU links ------------------------------------------
+// One workgroup, a wave per link (links strided over the waves): the
+// EdgeInertial error (and, building, its Jacobian) at the current or trial
+// state, every lane computing the same values (inertial_edge_core); the
+// link's robust chi2 (Huber sqrt(16.92) on flagged links, the information
+// x1e-2 on the window's last link) plus EdgeGyroRW / EdgeAccRW.  Building, it
+// writes the link's quadratic form over the 30 dims (kf1 VP VV VG VA | kf2 VP
+// VV VG VA; EdgeInertial's 24 columns are the first 24) and the gradient
+// -J^T W e.  Thread 0 sums the links' chi2 in link order into imu_tot.
+constexpr int kImuThreads = 256;
+constexpr int kImuWaves = kImuThreads / 64;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void load_state(StateD& s, const double* p) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s.Rwb[i] = p[i];
+    s.Rcw[i] = p[12 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.twb[i] = p[9 + i];
+    s.tcw[i] = p[21 + i];
+    s.v[i] = p[24 + i];
+    s.bg[i] = p[27 + i];
+    s.ba[i] = p[30 + i];
+  }
+}
+
+template <bool kBuild>
+__global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done || (kBuild && !c.need_build)) return;
+  __shared__ double sJ[kImuWaves][9 * 24];
+  __shared__ double sOJ[kImuWaves][9 * 24];
+  __shared__ double sE[kImuWaves][9];  // the link's error (inertial_edge_core, lane 0)
+  __shared__ double chis[kMaxImuLinks];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double* st = a.poses[trial ? c.state ^ 1 : c.state];
+  for (int l = wave; l < a.n_imu; l += kImuWaves) {
+    const LiaImuDev& E = a.imu[l];
+    StateD s1, s2;
+    load_state(s1, st + kImuStateStride * E.kf1);
+    load_state(s2, st + kImuStateStride * E.kf2);
+    double* J = sJ[wave];
+    if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
+      for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
+      wave_lds_sync();
+      if (lane < 9) {
+        const int i = lane / 3, j = lane % 3;
+        J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
+        J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
+        J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
+        J[(3 + i) * 24 + 12 + j] = -(double)E.pi.JVa[3 * i + j];
+        J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
+      }
+    }
+    inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sE[wave]);
+    wave_lds_sync();
+    double e[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) e[k] = sE[wave][k];
+    const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
+    // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
+    double part = 0;
+    if (lane < 9) {
+      double t = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) t += (E.pi.info[lane * 9 + q] * isc) * e[q];
+      double el = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
+      part = el * t;
+    }
+    double chi = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) chi += readlane_f64(part, q);
+    double rho0 = chi, w = 1.0;
+    if (E.flags & ORBGPU_LIA_ROBUST) huber_rho(chi, sqrt(16.92), rho0, w);
+    double eg[3], ea[3], Og[3], Oa[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      eg[i] = s2.bg[i] - s1.bg[i];
+      ea[i] = s2.ba[i] - s1.ba[i];
+    }
+    double cg = 0, ca = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Og[i] = E.pi.info_g[3 * i] * eg[0] + E.pi.info_g[3 * i + 1] * eg[1] + E.pi.info_g[3 * i + 2] * eg[2];
+      Oa[i] = E.pi.info_a[3 * i] * ea[0] + E.pi.info_a[3 * i + 1] * ea[1] + E.pi.info_a[3 * i + 2] * ea[2];
+      cg += eg[i] * Og[i];
+      ca += ea[i] * Oa[i];
+    }
+    if (lane == 0) chis[l] = (rho0 + cg) + ca;
+    if (!kBuild) continue;
+    // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
+    for (int k = lane; k < 9 * 24; k += 64) {
+      const int r = k / 24, col = k - 24 * r;
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * (E.pi.info[r * 9 + q] * isc)) * J[q * 24 + col];
+      sOJ[wave][k] = v;
+    }
+    double We[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * (E.pi.info[r * 9 + q] * isc)) * e[q];
+      We[r] = v;
+    }
+    wave_lds_sync();
+    double* Q = a.imu_q + (size_t)kImuPairQ * l;
+    for (int k = lane; k < 900; k += 64) {
+      const int p = k / 30, q = k - 30 * p;
+      double v = 0;
+      if (p < 24 && q < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sOJ[wave][r * 24 + q];
+      }
+      // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
+      const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
+      if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
+        if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
+      const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
+      if ((p >= 12 && p < 15) || (p >= 27))
+        if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
+      Q[k] = v;
+    }
+    if (lane < 30) {
+      const int p = lane;
+      double g = 0;
+      if (p < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
+      }
+      double og = 0, oa = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        og = p - 9 == i || p - 24 == i ? Og[i] : og;
+        oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
+      }
+      if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
+      if (p >= 24 && p < 27) g -= og;
+      if (p >= 12 && p < 15) g += oa;
+      if (p >= 27) g -= oa;
+      Q[900 + p] = g;
+    }
+    wave_lds_sync();  // J / sOJ are rewritten by this wave's next link
+  }
+  if (kBuild) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0;
+    for (int l = 0; l < a.n_imu; ++l) tot += chis[l];
+    a.imu_tot[0] = tot;
+  }
+}
+
+// The links' part of the camera-side system: entry (r, c) of free key frames
+// (fr, fc) sums, over the links incident to fr in link order, the form
+// entries whose dims land on (r, c); the last n entries are the gradient.
+__global__ __launch_bounds__(kThreads) void k_lia_assemble(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done || !c.need_build) return;
+  const int n = a.n_sys;
+  const long idx = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= (long)n * n + n) return;
+  const bool grad = idx >= (long)n * n;
+  const int r = grad ? (int)(idx - (long)n * n) : (int)(idx / n);
+  const int cc = grad ? 0 : (int)(idx - (long)r * n);
+  const int fr = r / kImuDim, dr = r - kImuDim * fr;
+  const int fc = cc / kImuDim, dc = cc - kImuDim * fc;
+  const int kr = a.free_kf[fr], kc = a.free_kf[fc];
+  double v = 0;
+  for (int j = a.imu_inc[fr]; j < a.imu_inc[fr + 1]; ++j) {
+    const int l = a.imu_inc_list[j];
+    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
+    const int sr = k1 == kr ? 0 : 1;
+    const double* Q = a.imu_q + (size_t)kImuPairQ * l;
+    if (grad) {
+      v += Q[900 + kImuDim * sr + dr];
+    } else {
+      const int sc = k1 == kc ? 0 : (k2 == kc ? 1 : -1);
+      if (sc >= 0) v += Q[(kImuDim * sr + dr) * 30 + kImuDim * sc + dc];
+    }
+  }
+  a.himu[idx] = v;
+}
+
+// Trial key-frame states: ImuCamPose::Update of VP (g2o_types.cc:192-216) and
+// the additive VV / VG / VA updates from the reduced solve; one wave per key
+// frame (the SO3 branches are wave-uniform), fixed key frames copied.
+__global__ __launch_bounds__(64) void k_lia_trial_states(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const int k = blockIdx.x, lane = threadIdx.x;
+  const double* src = a.poses[c.state] + kImuStateStride * k;
+  double* dst = a.poses[c.state ^ 1] + kImuStateStride * k;
+  const int h = a.hidx[k];
+  if (h < 0) {
+    if (lane < kImuStateStride) dst[lane] = src[lane];
+    return;
+  }
+  StateD s;
+  load_state(s, src);
+  const double* u = a.xp + kImuDim * h;
+  double up[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) up[i] = u[i];
+  pose_update(s, up, calib_of(a), true);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.v[i] += u[6 + i];
+    s.bg[i] += u[9 + i];
+    s.ba[i] += u[12 + i];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      dst[i] = s.Rwb[i];
+      dst[12 + i] = s.Rcw[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dst[9 + i] = s.twb[i];
+      dst[21 + i] = s.tcw[i];
+      dst[24 + i] = s.v[i];
+      dst[27 + i] = s.bg[i];
+      dst[30 + i] = s.ba[i];
+    }
+  }
 }
 
 inline unsigned blocks(long n, int t) { return (unsigned)((n + t - 1) / t); }
@@ -1069,14 +1434,29 @@ size_t lba_solve_lds_bytes(int n_pad) {
 }
 
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_lba_begin, dim3(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads)), dim3(kThreads),
-                     0, st, a);
+  const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
+  if (a.model == kModelImu) {
+    hipLaunchKernelGGL(k_lia_imu<false>, dim3(1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lba_begin<kModelImu>, g, dim3(kThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_lba_begin<kModelSe3>, g, dim3(kThreads), 0, st, a);
+  }
   return hipGetLastError();
 }
 
 hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
-  if (a.n_edges > 0)
-    hipLaunchKernelGGL(k_lba_linearize, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
+  const bool imu = a.model == kModelImu;
+  if (a.n_edges > 0) {
+    if (imu)
+      hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
+  }
+  if (imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
+    hipLaunchKernelGGL(k_lia_imu<true>, dim3(1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lia_assemble, dim3(blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads)),
+                       dim3(kThreads), 0, st, a);
+  }
   hipLaunchKernelGGL(k_lba_sums, dim3(a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads)),
                      dim3(kThreads), 0, st, a);
   return hipGetLastError();
@@ -1097,10 +1477,16 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   } else {
     hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kSolveThreads), 16 * (size_t)a.n_pad, st, a);
   }
-  if (a.n_kf > kMaxKfLds)
-    hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
-  hipLaunchKernelGGL(k_lba_trial, dim3(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads)), dim3(kThreads),
-                     0, st, a);
+  const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
+  if (a.model == kModelImu) {
+    hipLaunchKernelGGL(k_lia_trial_states, dim3(a.n_kf), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k_lia_imu<false>, dim3(1), dim3(kImuThreads), 0, st, a, 1);
+    hipLaunchKernelGGL(k_lba_trial<kModelImu>, g, dim3(kThreads), 0, st, a);
+  } else {
+    if (a.n_kf > kMaxKfLds)
+      hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(k_lba_trial<kModelSe3>, g, dim3(kThreads), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -1118,10 +1504,14 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st) {
 
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st) {
   long n = a.n_edges;
-  if (7L * a.n_kf > n) n = 7L * a.n_kf;
+  if ((long)a.pstride * a.n_kf > n) n = (long)a.pstride * a.n_kf;
   if (3L * a.n_pts > n) n = 3L * a.n_pts;
-  hipLaunchKernelGGL(k_lba_classify, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0, st, a,
-                     outlier, out);
+  if (a.model == kModelImu)
+    hipLaunchKernelGGL(k_lba_classify<kModelImu>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0,
+                       st, a, outlier, out);
+  else
+    hipLaunchKernelGGL(k_lba_classify<kModelSe3>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0,
+                       st, a, outlier, out);
   return hipGetLastError();
 }
 

@@ -12,7 +12,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/orbgpu.h"
+
 namespace orbgpu {
+
+// Key-frame models: LocalBundleAdjustment's VertexSE3Expmap (7 doubles: unit
+// quaternion + t; 6 reduced-system rows) and LocalInertialBA's ImuCamPose +
+// IMU vertices (StateD, 33 doubles: Rwb twb Rcw tcw v bg ba; 15 rows VP VV
+// VG VA).
+enum LbaModel { kModelSe3 = 0, kModelImu = 1 };
+constexpr int kImuStateStride = 33;
+constexpr int kImuDim = 15;
+constexpr int kImuPairQ = 30 * 30 + 30;  // per IMU link: 30 x 30 form + gradient
+constexpr int kMaxImuLinks = 64;
+
+struct LiaCalibDev {  // == CalibD (imu_math_dev.h)
+  double fx, fy, cx, cy, bf;
+  double Rcb[9], tcb[3], Rbc[9], tbc[3];
+};
+
+struct LiaImuDev {  // == orbgpu_lia_imu_edge
+  int32_t kf1, kf2, flags, pad;
+  orbgpu_imu_preint pi;
+};
+static_assert(sizeof(LiaImuDev) == sizeof(orbgpu_lia_imu_edge), "LiaImuDev layout");
 
 struct LbaEdgeDev {  // one observation of the shard, point-major (insertion order in a point)
   int32_t point;     // shard-local point index
@@ -30,6 +53,7 @@ struct LbaCamDev {
 // that takes an LM decision (last block of a stage, or k_lba_ctl when sharded).
 struct LbaCtrl {
   double lambda, ni, cur, ini, chi_init, user_lambda;
+  double last;  // robust chi2 of the last computeActiveErrors (LocalInertialBA's err_end)
   int it, q, nbad, need_build, done, state, iters_done, trials, max_iters, stopped;
 };
 
@@ -78,8 +102,27 @@ struct LbaArgs {
   unsigned* counter;         // last-block-done tickets (self-resetting), one per stage
   LbaCtrl* ctrl;
   LbaHostWords* host;        // host-mapped
+  // ---- key-frame model (LocalInertialBA: kModelImu)
+  int model;                 // LbaModel
+  int pdim;                  // reduced-system rows per free key frame (6 / 15)
+  int pstride;               // doubles per key-frame state (7 / 33)
+  LiaCalibDev icb;           // kModelImu: camera + mTcb / mTbc
+  const uint8_t* close;      // [n_pts] MapPoint::mTrackDepth < 10 (kModelImu outlier rule)
+  int n_imu;                 // IMU links (EdgeInertial + EdgeGyroRW + EdgeAccRW each)
+  const LiaImuDev* imu;      // [n_imu]
+  const int* free_kf;        // [n_free] key frame of each free index
+  const int* imu_inc;        // [n_free + 1] CSR of the links incident to a free key frame,
+  const int* imu_inc_list;   //   link ids ascending
+  double* imu_q;             // [n_imu * kImuPairQ] per link: form over (kf1 dims, kf2 dims) + gradient
+  double* himu;              // [n_sys^2 + n_sys] the links' part of the camera system | gradient
+  double* imu_tot;           // [1] robust chi2 of the links at the last evaluation
 };
 
+// Every launcher dispatches on a.model.  kModelImu adds, per stage: the IMU
+// links' chi2 at the initial / trial state (lba_begin, lba_solve_trial), their
+// quadratic forms and the camera-side system they add (lba_build), and the
+// trial key-frame states (ImuCamPose::Update + additive IMU vertices) before
+// the edge stage of a trial.
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st);   // initial errors + LM state
 hipError_t lba_step(const LbaArgs& a, hipStream_t st);    // build (if due) + one trial
 // sharded pieces (the host all-reduces between them)

@@ -19,7 +19,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import LBA_EDGE_DTYPE, LBA_REDUCE_FN, Camera, check, lib, ptr
+from ._lib import (IMU_STATE_DTYPE, LBA_EDGE_DTYPE, LBA_REDUCE_FN, LIA_IMU_EDGE_DTYPE, Camera, check,
+                   lib, ptr)
 
 
 class _DeviceDoubles:
@@ -117,6 +118,43 @@ class LocalBundleAdjuster:
             "orbgpu_lba_optimize",
         )
         return {"poses": po, "poses_d": pd, "pts": xo, "outlier": out[:ne].copy(), "stats": st}
+
+    def optimize_inertial(self, problem, iterations: Optional[int] = None,
+                          lambda_init: Optional[float] = None) -> dict:
+        """Optimizer::LocalInertialBA's solve (optimizer.cc:2440-2826) on a
+        window in the C ABI's layout (``calib``, ``kfs`` IMU_STATE_DTYPE,
+        ``fixed``, ``imu``, ``pts_init``, ``close``, ``edges``, ``imu_edges``
+        LIA_IMU_EDGE_DTYPE; ``iterations`` / ``lambda_init`` default to the
+        problem's, i.e. opt_it and the user lambda of :2334-2339,2448-2459).
+        Returns {"kfs": IMU_STATE_DTYPE [n_kf] (float casts), "kfs21": float64
+        [n_kf, 21] (Rwb twb v bg ba), "pts": float32 [n_pts, 3], "outlier":
+        uint8 [E], "stats": float64 [7] (err, err_end, iterations, trials,
+        lambda, outliers, accepted chi2)}."""
+        kfs = np.ascontiguousarray(problem.kfs, IMU_STATE_DTYPE)
+        fixed = np.ascontiguousarray(problem.fixed, np.uint8)
+        imu = np.ascontiguousarray(problem.imu, np.uint8)
+        pts = np.ascontiguousarray(problem.pts_init, np.float32)
+        close = np.ascontiguousarray(problem.close, np.uint8)
+        edges = np.ascontiguousarray(problem.edges, LBA_EDGE_DTYPE)
+        links = np.ascontiguousarray(problem.imu_edges, LIA_IMU_EDGE_DTYPE)
+        calib = np.array(problem.calib)
+        n_kf, n_pts, ne = len(kfs), len(pts), len(edges)
+        it = problem.iterations if iterations is None else iterations
+        lam = problem.lambda_init if lambda_init is None else lambda_init
+        ko = np.zeros(n_kf, IMU_STATE_DTYPE)
+        kd = np.zeros((n_kf, 21), np.float64)
+        xo = np.array(pts, copy=True)
+        out = np.zeros(max(ne, 1), np.uint8)
+        st = np.zeros(7, np.float64)
+        check(
+            lib().orbgpu_lia_optimize(
+                self._h, ptr(calib), n_kf, ptr(kfs), ptr(fixed), ptr(imu), n_pts, ptr(pts),
+                ptr(close), ne, ptr(edges), len(links), ptr(links), int(it), float(lam), ptr(ko),
+                ptr(kd), ptr(xo), ptr(out), ptr(st),
+            ),
+            "orbgpu_lia_optimize",
+        )
+        return {"kfs": ko, "kfs21": kd, "pts": xo, "outlier": out[:ne].copy(), "stats": st}
 
 
 # ---------------------------------------------------------------------------

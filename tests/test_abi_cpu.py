@@ -101,6 +101,50 @@ def test_inertial_mode_and_prior_checked_with_a_handle():
     assert so.orbgpu_pose_inertial(dummy, 1, zero, cur, prev, pre, None, obs, 1, 0, res, out) == INV
 
 
+def test_local_inertial_ba_checked_with_a_handle():
+    """orbgpu_lia_optimize's argument checks (lba_api.cpp) return before the
+    context is dereferenced: a free key frame without IMU vertices, a link to
+    a key frame without them, a self link, more links than the kernel's bound
+    and a non-positive user lambda are all INVALID."""
+    from orb_slam_fusion_amd import synth
+    from orb_slam_fusion_amd.lba import LocalBundleAdjuster
+
+    so = _lib.lib()
+    pb = synth.lia_problem(3, n_opt=3, n_fixed_cov=1, n_pts=20, max_obs=3)
+    adj = LocalBundleAdjuster.__new__(LocalBundleAdjuster)  # no device context
+    adj._h = ctypes.c_void_p(0x1000)  # never dereferenced on these paths
+    INV = _lib.ORBGPU_ERR_INVALID
+
+    def status(**over):
+        import copy
+        q = copy.deepcopy(pb)
+        for k, v in over.items():
+            setattr(q, k, v)
+        try:
+            adj.optimize_inertial(q)
+        except _lib.OrbGpuError as e:
+            return e.status
+        return _lib.ORBGPU_OK
+
+    try:
+        imu = pb.imu.copy()
+        imu[0] = 0  # a free key frame
+        assert status(imu=imu) == INV
+        imu = pb.imu.copy()
+        imu[int((pb.fixed == 0).sum())] = 0  # the key frame before the window (a link's kf1)
+        assert status(imu=imu) == INV
+        links = pb.imu_edges.copy()
+        links[0]["kf1"] = links[0]["kf2"]
+        assert status(imu_edges=links) == INV
+        many = np.repeat(pb.imu_edges, 30)  # 90 links > the 64-link bound
+        assert status(imu_edges=many) == INV
+        assert status(lambda_init=0.0) == INV
+        assert so.orbgpu_lia_optimize(None, None, 0, None, None, None, 0, None, None, 0, None, 0,
+                                      None, 10, 1.0, None, None, None, None, None) == INV
+    finally:
+        adj._h = ctypes.c_void_p()
+
+
 def test_keypoint_struct_is_cv_keypoint_layout():
     assert _lib.KEYPOINT_DTYPE.itemsize == 28
     assert list(_lib.KEYPOINT_DTYPE.names) == ["x", "y", "size", "angle", "response", "octave",

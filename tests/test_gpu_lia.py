@@ -1,0 +1,84 @@
+"""GPU LocalInertialBA (orbgpu_lia_optimize) vs the oracle (oracle/lia_oracle.cc)
+on the same synthetic windows.  Floating point, so parity is by tolerance:
+the GPU sums in different fixed orders and factors the 15-per-key-frame
+reduced system by 16 x 16 MFMA tiles; the LM path (iterations, trials), the
+outlier flags away from the thresholds and err / err_end agree, states to
+~1e-7 relative."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "oracle"))
+sys.path.insert(0, str(REPO))
+
+import binding as oracle  # noqa: E402
+from orb_slam_fusion_amd import LocalBundleAdjuster, synth  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(pb, tol=1e-6):
+    ref = oracle.lia(pb)
+    got = LocalBundleAdjuster().optimize_inertial(pb)
+    gs, rs = got["stats"], ref["stats"]
+    assert gs[2] == rs[2] and gs[3] == rs[3], (gs, rs)  # LM iterations, trials
+    assert abs(gs[0] - rs[0]) <= 1e-8 * rs[0], (gs[0], rs[0])  # err: one evaluation
+    for k in (1, 6):  # err_end, accepted chi2: after the whole LM path
+        assert abs(gs[k] - rs[k]) <= tol * rs[k], (k, gs[k], rs[k])
+    # lambda follows the gain ratio rho = (chi2 - chi2') / scale, a difference
+    # of nearly equal sums: its rounding shows in the last digits of lambda
+    assert abs(gs[4] - rs[4]) <= 1e-3 * rs[4], (gs[4], rs[4])
+    scale = np.maximum(1.0, np.abs(ref["kfs21"]))
+    dk = (np.abs(got["kfs21"] - ref["kfs21"]) / scale).max()
+    print(f"max state diff {dk:.3g}, chi2 rel diff {abs(gs[1] - rs[1]) / rs[1]:.3g}")
+    assert dk <= tol
+    assert np.allclose(got["pts"], ref["pts"], rtol=1e-5, atol=1e-5)
+    diff = (got["outlier"] != ref["outlier"]).sum()
+    assert diff <= max(1, len(pb.edges) // 4000), diff
+    # float outputs are the casts of the double states
+    assert np.array_equal(got["kfs"]["Rwb"], got["kfs21"][:, :9].astype(np.float32))
+    assert np.array_equal(got["kfs"]["ba"], got["kfs21"][:, 18:21].astype(np.float32))
+    for k in range(len(pb.kfs)):
+        if pb.fixed[k]:
+            assert np.array_equal(got["kfs"][k], pb.kfs[k])
+    return got, ref
+
+
+def test_lia_small_window(gpu_available):
+    _compare(synth.lia_problem(5, n_opt=4, n_fixed_cov=2, n_pts=60, max_obs=4))
+
+
+def test_lia_default_window(gpu_available):
+    got, ref = _compare(synth.lia_problem())  # 10 temporal KF, 11 fixed, 2000 MP, ~16k edges
+    assert got["stats"][1] < 0.6 * got["stats"][0]
+
+
+def test_lia_large_mode(gpu_available):
+    # bLarge: maxOpt 25, opt_it 4, user lambda 1e-2 (optimizer.cc:2334-2339, 2448-2452)
+    _compare(synth.lia_problem(9, n_opt=25, n_fixed_cov=6, n_pts=1500, b_large=True))
+
+
+def test_lia_rec_init(gpu_available):
+    # bRecInit: every EdgeInertial robust (optimizer.cc:2571)
+    _compare(synth.lia_problem(10, n_opt=6, n_pts=800, rec_init=True))
+
+
+def test_lia_outlier_heavy(gpu_available):
+    _compare(synth.lia_problem(12, n_opt=8, n_pts=1000, outlier_frac=0.2))
+
+
+def test_lia_then_lba_on_one_context(gpu_available):
+    """Both windows share the context's arena: an LBA call after a LocalInertialBA
+    call (and back) gives the standalone results."""
+    adj = LocalBundleAdjuster()
+    pl = synth.lba_problem(seed=5, n_kf=5, n_pts=40, obs_per_pt=3, n_fixed=1)
+    pi = synth.lia_problem(5, n_opt=4, n_fixed_cov=2, n_pts=60, max_obs=4)
+    a1 = adj.optimize_inertial(pi)
+    b1 = adj.optimize(pl)
+    a2 = adj.optimize_inertial(pi)
+    b2 = LocalBundleAdjuster().optimize(pl)
+    assert np.array_equal(a1["kfs21"], a2["kfs21"]) and np.array_equal(a1["outlier"], a2["outlier"])
+    assert np.array_equal(b1["poses_d"], b2["poses_d"])
