@@ -133,6 +133,7 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
+    ap.add_argument("--no-lia", action="store_true", help="skip the LocalInertialBA side line")
     ap.add_argument("--no-stereo", action="store_true", help="skip the ComputeStereoMatches side line")
     ap.add_argument("--no-match", action="store_true",
                     help="skip the SearchByProjection (motion-model search) side line")
@@ -342,6 +343,13 @@ def main() -> int:
         from bench_lba import measure  # noqa: E402
 
         result["lba"] = measure(calls=10, cpu_calls=0 if args.no_cpu_baseline else 3)
+    if rank == 0 and world == 1 and not args.no_lia:
+        # SURVEY §8(f) rank 3 (LocalMapping after IMU initialisation), beside the
+        # headline metric: LocalInertialBA window, GPU vs the CPU oracle (1 thread)
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_lba import measure_lia  # noqa: E402
+
+        result["lia"] = measure_lia(calls=10, cpu_calls=0 if args.no_cpu_baseline else 3)
     if rank == 0 and world == 1 and not args.no_stereo:
         # SURVEY §8(f) rank 1, beside the headline metric (not part of it):
         # Frame::ComputeStereoMatches per frame on resident extractor outputs

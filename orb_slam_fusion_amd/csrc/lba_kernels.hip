@@ -767,13 +767,18 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
 // L_KK^-1 (16 x 16 mat-vecs, no serial chains), the pose part of
 // computeScale, and the failure flag (a zero pivot: Eigen's SimplicialLDLT
 // reports NumericalIssue only for D(k,k) == 0).
-// kLds: S (n_pad x (n_pad + 1), odd stride: conflict-free tile columns) and
-// the L_KK^-1 tiles in LDS; else both in a.work.
+// kLds: the lower-triangle tiles of S packed in LDS (tile (I, J), J <= I, at
+// (I (I + 1) / 2 + J) x 272 doubles, rows 17 apart: odd stride, conflict-free
+// tile columns -- only the lower triangle is ever read) and the L_KK^-1
+// tiles; up to n_pad = 160 (10 inertial or 26 SE3 key frames).  Else S row-
+// major in a.work (stride n_pad + 1) and the L_KK^-1 tiles after it.
 // Phase clocks of the solve (tools/lba_solve_bench.hip builds with
 // LBA_SOLVE_STAMPS): thread 0 adds the s_memtime delta since its previous
 // stamp to bucket k.
 constexpr int kSolveThreads = 512;
 constexpr int kSolveWaves = kSolveThreads / 64;
+constexpr int kTileLd = 17;             // row stride inside a packed LDS tile
+constexpr int kTileSz = 16 * kTileLd;   // doubles per packed tile
 
 // 1 / d: v_rcp_f64 and one Newton step (the pivot chain's latency; not the
 // IEEE division sequence)
@@ -805,6 +810,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   if (c.done) return;
   const double lambda = c.lambda;
   const int n = a.n_sys, N = a.n_pad, LD = N + 1, T = N >> 4;
+  const int TS = kLds ? kTileLd : LD;  // row stride inside a tile
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 15, lk = lane >> 4;
 #ifdef LBA_SOLVE_STAMPS
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
@@ -817,7 +823,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   __shared__ int bad;
   if constexpr (kLds) {
     S = smem;
-    Li = smem + (size_t)N * LD;
+    Li = smem + (size_t)(T * (T + 1) / 2) * kTileSz;
     Dg = Li + (size_t)T * 256;
     y = Dg + N;
   } else {
@@ -826,6 +832,13 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     Dg = smem;
     y = smem + N;
   }
+  // tile (I, J) of S, J <= I
+  auto tile = [&](int I, int J) -> double* {
+    if constexpr (kLds)
+      return S + (size_t)(I * (I + 1) / 2 + J) * kTileSz;
+    else
+      return S + (size_t)(16 * I) * LD + 16 * J;
+  };
   const double* src = a.sys;
   const double* hm = a.himu;  // kModelImu: the IMU links' part of the system (else NULL)
   // S + lambda I with identity padding (D = 1, L = 0): 16 loads in flight per
@@ -835,13 +848,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
-      v[u] = e < N * N && r < n && cc < n ? src[(size_t)r * n + cc] + (hm ? hm[(size_t)r * n + cc] : 0.0)
-                                           : 0.0;
+      v[u] = e < N * N && r < n && cc < n && (cc >> 4) <= (r >> 4)
+                 ? src[(size_t)r * n + cc] + (hm ? hm[(size_t)r * n + cc] : 0.0)
+                 : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
-      if (e < N * N) S[(size_t)r * LD + cc] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
+      if (e < N * N && (cc >> 4) <= (r >> 4))
+        tile(r >> 4, cc >> 4)[(r & 15) * TS + (cc & 15)] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
     }
   }
   for (int r = t; r < N; r += kSolveThreads)
@@ -852,13 +867,14 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 
   for (int K = 0; K < T; ++K) {
     const int k0 = 16 * K;
+    double* const SKK = tile(K, K);
     if (wave == 0) {
       // 1. diagonal tile: lane li owns row li (full symmetric row), right-
       // looking, the pivot row broadcast by v_readlane; branch-free (rows at
       // or above the pivot take l = 0)
       double r[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) r[j] = S[(size_t)(k0 + li) * LD + k0 + j];
+      for (int j = 0; j < 16; ++j) r[j] = SKK[li * TS + j];
       double dmine = 0;
       int zero = 0;
 #pragma unroll
@@ -875,7 +891,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
       if (lane < 16) {
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-          if (j < li) S[(size_t)(k0 + li) * LD + k0 + j] = r[j];
+          if (j < li) SKK[li * TS + j] = r[j];
         Dg[k0 + li] = dmine;
       }
       __threadfence_block();  // the rows are re-read by the other lanes
@@ -888,7 +904,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
       for (int k = 0; k < 15; ++k)
 #pragma unroll
-        for (int i = k + 1; i < 16; ++i) x[i] = fma(-S[(size_t)(k0 + i) * LD + k0 + k], x[k], x[i]);
+        for (int i = k + 1; i < 16; ++i) x[i] = fma(-SKK[i * TS + k], x[k], x[i]);
       if (lane < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) Li[(size_t)K * 256 + i * 16 + li] = x[i];
@@ -910,11 +926,12 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     // substitution y_I -= L_IK y_K (DPP row sums over the tile's columns)
     for (int I = K + 1 + wave; I < T; I += kSolveWaves) {
       const int i0 = 16 * I;
+      double* const SIK = tile(I, K);
       d4 acc = {0, 0, 0, 0};
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc) {
         const int kk = 4 * kc + lk;
-        const double av = S[(size_t)(i0 + li) * LD + k0 + kk];
+        const double av = SIK[li * TS + kk];
         const double bv = Li[(size_t)K * 256 + li * 16 + kk];  // (L^-1)^T[kk][li]
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
@@ -923,7 +940,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const double l = acc[rr] * dinv;
-        S[(size_t)(i0 + lk + 4 * rr) * LD + k0 + li] = l;
+        SIK[(lk + 4 * rr) * TS + li] = l;
         double p = l * ykl;
         p += dpp_f64<0x111, 0xf>(p);
         p += dpp_f64<0x112, 0xf>(p);
@@ -942,19 +959,21 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
       int I = 0;
       while ((I + 1) * (I + 2) / 2 <= q) ++I;
       const int J = q - I * (I + 1) / 2;
-      const int i0 = 16 * (K + 1 + I), j0 = 16 * (K + 1 + J);
+      double* const SIJ = tile(K + 1 + I, K + 1 + J);
+      const double* const SIK = tile(K + 1 + I, K);
+      const double* const SJK = tile(K + 1 + J, K);
       d4 acc;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[rr] = S[(size_t)(i0 + lk + 4 * rr) * LD + j0 + li];
+      for (int rr = 0; rr < 4; ++rr) acc[rr] = SIJ[(lk + 4 * rr) * TS + li];
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc) {
         const int kk = 4 * kc + lk;
-        const double av = -S[(size_t)(i0 + li) * LD + k0 + kk];
-        const double bv = S[(size_t)(j0 + li) * LD + k0 + kk] * Dg[k0 + kk];
+        const double av = -SIK[li * TS + kk];
+        const double bv = SJK[li * TS + kk] * Dg[k0 + kk];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) S[(size_t)(i0 + lk + 4 * rr) * LD + j0 + li] = acc[rr];
+      for (int rr = 0; rr < 4; ++rr) SIJ[(lk + 4 * rr) * TS + li] = acc[rr];
     }
     __syncthreads();
     LBA_STAMP(4);
@@ -977,7 +996,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     for (int r = t; r < k0; r += kSolveThreads) {
       double s = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s = fma(S[(size_t)(k0 + k) * LD + r], y[k0 + k], s);
+      for (int k = 0; k < 16; ++k) s = fma(tile(K, r >> 4)[k * TS + (r & 15)], y[k0 + k], s);
       y[r] -= s;
     }
     __syncthreads();
@@ -1430,7 +1449,7 @@ inline unsigned blocks(long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 size_t lba_solve_lds_bytes(int n_pad) {
   const size_t T = (size_t)n_pad / 16;
-  return 8 * ((size_t)n_pad * (n_pad + 1) + T * 256 + 2 * (size_t)n_pad);
+  return 8 * (T * (T + 1) / 2 * kTileSz + T * 256 + 2 * (size_t)n_pad);
 }
 
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {

@@ -1,23 +1,25 @@
 // Dynamic-LDS opt-in above 64 KB (hipFuncAttributeMaxDynamicSharedMemorySize)
-// applies to the CURRENT device: record it per (kernel, device), thread-safe.
+// applies to the CURRENT device: record the largest size raised per (kernel,
+// device), thread-safe; a later launch needing more raises it again.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <mutex>
-#include <set>
 #include <utility>
 
 namespace orbgpu {
 
 inline hipError_t lds_optin(const void* fn, int bytes) {
   static std::mutex mu;
-  static std::set<std::pair<const void*, int>> done;
+  static std::map<std::pair<const void*, int>, int> raised;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lock(mu);
-  if (done.count({fn, dev})) return hipSuccess;
+  auto it = raised.find({fn, dev});
+  if (it != raised.end() && it->second >= bytes) return hipSuccess;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-  if (e == hipSuccess) done.insert({fn, dev});
+  if (e == hipSuccess) raised[{fn, dev}] = bytes;
   return e;
 }
 

@@ -269,3 +269,159 @@ def write_back(win: LbaWindow, result: dict):
     kf_poses = [(k, result["poses"][i]) for i, k in enumerate(win.local_kfs)]
     mp_pos = [(mp, result["pts"][p]) for p, mp in enumerate(win.local_mps)]
     return to_erase, kf_poses, mp_pos
+
+
+# ---------------------------------------------------------------------------
+# Optimizer::LocalInertialBA around the solve: the temporal window
+# (optimizer.cc:2332-2436), the flat graph (:2461-2781) and the FAIL test /
+# write-back (:2796-2901), over duck-typed objects with the reference's
+# members.  KeyFrame: id_, mPrevKF, bImu, mnBALocalForKF, mnBAFixedForKF,
+# isBad(), GetMap(), GetVectorCovisibleKeyFrames(), GetMapPointMatches(),
+# GetImuRotation(), GetImuPosition(), GetRotation(), GetTranslation() (Tcw),
+# GetVelocity(), GetGyroBias(), GetAccBias(), mvKeysUn (.x, .y, .octave),
+# mvuRight, mvInvLevelSigma2 and mpImuPreintegrated (None, or the
+# IMU_PREINT_DTYPE record the C++ drop-in forms from IMU::Preintegrated and
+# EdgeInertial's constructor); MapPoint: id_, mnBALocalForKF, isBad(),
+# GetObservations() (ordered KeyFrame -> (left, right)), GetWorldPos(),
+# mTrackDepth; Map: KeyFramesInMap().  The pinhole Uncertainty2 is 1.  (The
+# C++ drop-in, shim/optimizer_lia_gpu.cc, is the same code over the real
+# classes.)  LocalInertialBA leaves num_fixedKF / num_OptKF / num_MPs /
+# num_edges unwritten, as the reference does.
+# ---------------------------------------------------------------------------
+class LiaWindow:
+    """One gathered temporal window in orbgpu_lia_optimize's layout plus the
+    map objects behind it: opt_kfs (pKF, its mPrevKF, ... newest first),
+    fixed_kfs (the key frame before the window first), local_mps,
+    edge_refs [(KeyFrame, MapPoint)] per visual edge."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _kf_state(k):
+    s = np.zeros((), IMU_STATE_DTYPE)
+    s["Rwb"] = np.asarray(k.GetImuRotation(), np.float32).ravel()
+    s["twb"] = np.asarray(k.GetImuPosition(), np.float32)
+    s["Rcw"] = np.asarray(k.GetRotation(), np.float32).ravel()
+    s["tcw"] = np.asarray(k.GetTranslation(), np.float32)
+    s["v"] = np.asarray(k.GetVelocity(), np.float32)
+    s["bg"] = np.asarray(k.GetGyroBias(), np.float32)
+    s["ba"] = np.asarray(k.GetAccBias(), np.float32)
+    return s
+
+
+def gather_inertial_window(pKF, calib, b_large: bool = False, b_rec_init: bool = False) -> LiaWindow:
+    """optimizer.cc:2332-2436 (marks written as the reference writes them),
+    then the graph of :2461-2781."""
+    cur_map = pKF.GetMap()
+    kid = pKF.id_
+    max_opt, opt_it = (25, 4) if b_large else (10, 10)
+    Nd = min(cur_map.KeyFramesInMap() - 2, max_opt)
+    opt = [pKF]
+    pKF.mnBALocalForKF = kid
+    for _ in range(1, Nd):
+        if opt[-1].mPrevKF is None:
+            break
+        opt.append(opt[-1].mPrevKF)
+        opt[-1].mnBALocalForKF = kid
+    local_mps = []
+    for k in opt:
+        for mp in k.GetMapPointMatches():
+            if mp is not None and not mp.isBad() and mp.mnBALocalForKF != kid:
+                local_mps.append(mp)
+                mp.mnBALocalForKF = kid
+    fixed = []
+    if opt[-1].mPrevKF is not None:
+        fixed.append(opt[-1].mPrevKF)
+        opt[-1].mPrevKF.mnBAFixedForKF = kid
+    else:
+        opt[-1].mnBALocalForKF = 0
+        opt[-1].mnBAFixedForKF = kid
+        fixed.append(opt[-1])
+        opt.pop()
+    # optimizable covisible (visual) key frames: maxCovKF = 0 admits none (:2388-2412)
+    max_fix = 200
+    for mp in local_mps:
+        for k in mp.GetObservations():
+            if k.mnBALocalForKF != kid and k.mnBAFixedForKF != kid:
+                k.mnBAFixedForKF = kid
+                if not k.isBad():
+                    fixed.append(k)
+                    break
+        if len(fixed) >= max_fix:
+            break
+    N = len(opt)
+    kfs = opt + fixed
+    index = {id(k): i for i, k in enumerate(kfs)}
+    states = np.array([_kf_state(k) for k in kfs], IMU_STATE_DTYPE)
+    fixed_flags = np.array([0] * N + [1] * len(fixed), np.uint8)
+    imu = np.array([1 if k.bImu else 0 for k in kfs], np.uint8)
+    # inertial links (:2531-2604): temporal key frame i -> its mPrevKF
+    links = []
+    for i, k in enumerate(opt):
+        prev = k.mPrevKF
+        if prev is None or not (k.bImu and prev.bImu and k.mpImuPreintegrated is not None):
+            continue
+        if id(prev) not in index:
+            continue  # the reference finds no vertex and skips the edge
+        rec = np.zeros((), LIA_IMU_EDGE_DTYPE)
+        rec["kf1"], rec["kf2"] = index[id(prev)], i
+        rec["flags"] = ((1 | 2) if i == N - 1 else 0) | (1 if b_rec_init else 0)
+        rec["preint"] = k.mpImuPreintegrated
+        links.append(rec)
+    imu_edges = np.array(links, LIA_IMU_EDGE_DTYPE) if links else np.zeros(0, LIA_IMU_EDGE_DTYPE)
+    # map point vertices and visual edges (:2648-2781), left-camera observations
+    rows, refs = [], []
+    for p, mp in enumerate(local_mps):
+        for k, (left, _right) in mp.GetObservations().items():
+            if k.mnBALocalForKF != kid and k.mnBAFixedForKF != kid:
+                continue
+            if k.isBad() or k.GetMap() is not cur_map or left == -1:
+                continue
+            i = index.get(id(k))
+            if i is None:  # a stale mark: the reference would find no vertex
+                continue
+            kp = k.mvKeysUn[left]
+            ur = float(k.mvuRight[left])
+            rows.append((p, i, kp.x, kp.y, ur if ur >= 0 else -1.0,
+                         k.mvInvLevelSigma2[kp.octave] / 1.0))  # / Uncertainty2 (pinhole: 1)
+            refs.append((k, mp))
+    edges = np.array(rows, LBA_EDGE_DTYPE) if rows else np.zeros(0, LBA_EDGE_DTYPE)
+    pts = np.array([np.asarray(mp.GetWorldPos(), np.float32) for mp in local_mps],
+                   np.float32).reshape(-1, 3)
+    close = np.array([mp.mTrackDepth < np.float32(10.0) for mp in local_mps], np.uint8)
+    return LiaWindow(opt_kfs=opt, fixed_kfs=fixed, local_mps=local_mps, edge_refs=refs,
+                     calib=np.array(calib), kfs=states, fixed=fixed_flags, imu=imu,
+                     pts_init=pts, close=close, edges=edges, imu_edges=imu_edges,
+                     iterations=opt_it, lambda_init=1e-2 if b_large else 1e0, b_large=b_large)
+
+
+def write_back_inertial(win: LiaWindow, result: dict):
+    """:2796-2901 -> dict(failed, to_erase, kf_updates, mp_positions).
+    failed: the reference's "FAIL LOCAL-INERTIAL BA!!!!" return (err and
+    err_end as floats, 2 err < err_end or NaN, unless bLarge): nothing is
+    erased or written and the marks stay.  Otherwise to_erase = (KeyFrame,
+    MapPoint) pairs, mono edges first, then stereo, bad points skipped;
+    kf_updates = (KeyFrame, Rcw, tcw, v, bg, ba) per temporal key frame
+    (SetPose, SetVelocity, SetNewBias, float casts); mp_positions =
+    (MapPoint, Xw); the caller clears the fixed marks and the temporal
+    key frames' local marks as :2847-2888 do."""
+    st = result["stats"]
+    err, err_end = np.float32(st[0]), np.float32(st[1])
+    failed = bool((np.float32(2) * err < err_end or np.isnan(err) or np.isnan(err_end))
+                  and not win.b_large)
+    if failed:
+        return {"failed": True, "to_erase": [], "kf_updates": [], "mp_positions": []}
+    out = result["outlier"]
+    mono = win.edges["ur"] < 0
+    to_erase = []
+    for sel in (np.nonzero(mono)[0], np.nonzero(~mono)[0]):
+        for e in sel:
+            k, mp = win.edge_refs[e]
+            if not mp.isBad() and out[e]:
+                to_erase.append((k, mp))
+    kfo = result["kfs"]
+    upd = [(k, kfo[i]["Rcw"].reshape(3, 3), kfo[i]["tcw"], kfo[i]["v"], kfo[i]["bg"], kfo[i]["ba"])
+           for i, k in enumerate(win.opt_kfs)]
+    mp_pos = [(mp, result["pts"][p]) for p, mp in enumerate(win.local_mps)]
+    return {"failed": False, "to_erase": to_erase, "kf_updates": upd, "mp_positions": mp_pos}

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "imu/imu_types.h"
+#include "imu_marshal.h"
 #include "map/frame.h"
 #include "map/keyframe.h"
 #include "map/mappoint.h"
@@ -26,6 +27,8 @@ namespace ORB_SLAM_FUSION {
 
 namespace {
 
+using namespace orbgpu_shim;
+
 orbgpu_inertial_ctx *thread_ctx() {
   thread_local struct Holder {
     orbgpu_inertial_ctx *c = nullptr;
@@ -34,31 +37,6 @@ orbgpu_inertial_ctx *thread_ctx() {
   if (!h.c && orbgpu_inertial_ctx_create(0, 1, 8192, &h.c) != ORBGPU_OK)
     throw std::runtime_error("orbgpu_inertial_ctx_create failed");
   return h.c;
-}
-
-template <typename M>
-void put(float *dst, const M &m) {  // row-major copy of a float matrix / vector
-  for (int i = 0; i < m.rows(); ++i)
-    for (int j = 0; j < m.cols(); ++j) dst[i * m.cols() + j] = m(i, j);
-}
-template <typename M>
-void putd(double *dst, const M &m) {
-  for (int i = 0; i < m.rows(); ++i)
-    for (int j = 0; j < m.cols(); ++j) dst[i * m.cols() + j] = m(i, j);
-}
-
-orbgpu_imu_calib calib_of(Frame *pF) {
-  orbgpu_imu_calib c{};
-  c.fx = pF->fx;
-  c.fy = pF->fy;
-  c.cx = pF->cx;
-  c.cy = pF->cy;
-  c.bf = pF->bf_;
-  put(c.Rcb, pF->mImuCalib.mTcb.rotationMatrix());
-  put(c.tcb, pF->mImuCalib.mTcb.translation());
-  put(c.Rbc, pF->mImuCalib.mTbc.rotationMatrix());
-  put(c.tbc, pF->mImuCalib.mTbc.translation());
-  return c;
 }
 
 orbgpu_imu_state state_of(Frame *pF) {
@@ -85,30 +63,6 @@ orbgpu_imu_state state_of(KeyFrame *pKF) {
   put(s.bg, pKF->GetGyroBias());
   put(s.ba, pKF->GetAccBias());
   return s;
-}
-
-orbgpu_imu_preint preint_of(IMU::Preintegrated *p) {
-  orbgpu_imu_preint o{};
-  o.dT = p->dT;
-  put(o.dR, p->dR);
-  put(o.dV, p->dV);
-  put(o.dP, p->dP);
-  put(o.JRg, p->JRg);
-  put(o.JVg, p->JVg);
-  put(o.JVa, p->JVa);
-  put(o.JPg, p->JPg);
-  put(o.JPa, p->JPa);
-  o.bg[0] = p->b.bwx;
-  o.bg[1] = p->b.bwy;
-  o.bg[2] = p->b.bwz;
-  o.ba[0] = p->b.bax;
-  o.ba[1] = p->b.bay;
-  o.ba[2] = p->b.baz;
-  EdgeInertial ei(p);  // its constructor forms the information (g2o_types.cc:472-492)
-  putd(o.info, ei.information());
-  putd(o.info_g, Eigen::Matrix3d(p->C.block<3, 3>(9, 9).cast<double>().inverse()));
-  putd(o.info_a, Eigen::Matrix3d(p->C.block<3, 3>(12, 12).cast<double>().inverse()));
-  return o;
 }
 
 int run(Frame *pFrame, bool bRecInit, int mode) {

@@ -41,6 +41,42 @@ def measure(calls: int = 10, cpu_calls: int = 3) -> dict:
     return out
 
 
+def measure_lia(calls: int = 10, cpu_calls: int = 3, b_large: bool = False) -> dict:
+    """LocalInertialBA (optimizer.cc:2329-2902) on the synthetic stereo-inertial
+    window: 10 temporal key frames (15 DoF each), the key frame before them and
+    10 older observers fixed, 2000 map points, ~16k visual edges, 10 IMU
+    links, optimize(10) with user lambda 1 (bLarge: 25 key frames, 4
+    iterations, lambda 1e-2)."""
+    from orb_slam_fusion_amd import LocalBundleAdjuster, synth
+
+    p = synth.lia_problem(b_large=b_large, **({"n_opt": 25, "n_fixed_cov": 6} if b_large else {}))
+    lba = LocalBundleAdjuster()
+    for _ in range(2):
+        lba.optimize_inertial(p)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        r = lba.optimize_inertial(p)
+    gpu_ms = (time.perf_counter() - t0) / calls * 1e3
+    n_opt = int((p.fixed == 0).sum())
+    out = {"workload": f"LocalInertialBA{' bLarge' if b_large else ''}: {n_opt} temporal KF x 15 DoF, "
+                       f"{len(p.kfs) - n_opt} fixed KF, {len(p.pts_init)} MP, {len(p.edges)} visual edges "
+                       f"(50% stereo), {len(p.imu_edges)} IMU links, optimize({p.iterations})",
+           "gpu_ms_per_call": round(gpu_ms, 3), "lm_iterations": int(r["stats"][2]),
+           "lm_trials": int(r["stats"][3]), "err": r["stats"][0], "err_end": r["stats"][1]}
+    if cpu_calls > 0:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import binding as oracle  # cpu baseline leg only
+
+        t0 = time.perf_counter()
+        for _ in range(cpu_calls):
+            ref = oracle.lia(p)
+        out["cpu_oracle_ms_per_call"] = round((time.perf_counter() - t0) / cpu_calls * 1e3, 3)
+        out["cpu_cores"] = 1
+        out["err_end_oracle"] = ref["stats"][1]
+        out["max_state_diff_vs_oracle"] = float(abs(r["kfs21"] - ref["kfs21"]).max())
+    return out
+
+
 def measure_sharded(calls: int = 10) -> dict:
     """The C4 window point-sharded over 2 ranks on ONE GPU (two fresh child
     processes, gloo all-reduce of the device buffers through lba.dist_reduce):
@@ -77,4 +113,11 @@ def measure_sharded(calls: int = 10) -> dict:
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=10)
-    print(json.dumps(measure(ap.parse_args().calls)))
+    ap.add_argument("--lia", action="store_true", help="LocalInertialBA instead of LBA")
+    ap.add_argument("--large", action="store_true", help="LocalInertialBA bLarge window")
+    ap.add_argument("--cpu-calls", type=int, default=3)
+    a = ap.parse_args()
+    if a.lia:
+        print(json.dumps(measure_lia(a.calls, a.cpu_calls, a.large)))
+    else:
+        print(json.dumps(measure(a.calls, a.cpu_calls)))
