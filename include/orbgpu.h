@@ -420,6 +420,72 @@ orbgpu_status orbgpu_search_local_points(
     int far_points, float th_far_points, orbgpu_track_view* views, int32_t* match,
     int* nmatches);
 
+/* Replaces: int ORBmatcher::SearchByProjection(Frame& CurrentFrame,
+ *   KeyFrame* pKF, const set<MapPoint*>& sAlreadyFound, const float th,
+ *   const int ORBdist) (orb_matcher.cc:1730-1839, Nleft == -1), the search
+ *   Tracking::Relocalization runs before its PoseOptimization calls
+ *   (tracking.cc:2967-2997: ORBmatcher(0.9, true), th 10 / 3, ORBdist 100 /
+ *   64).  pts[i] = pKF->GetMapPointMatches()[i] (ORBGPU_MP_SKIP: NULL,
+ *   isBad() or in sAlreadyFound; normal unused), angles[i] =
+ *   pKF->mvKeysUn[i].angle (may be NULL without the orientation check);
+ *   claimed[k] = CurrentFrame.mvpMapPoints[k] != NULL (every claimed keypoint
+ *   is skipped, and so is every keypoint this call matches).  Tcw =
+ *   CurrentFrame.GetPose().  match[k] >= 0: mvpMapPoints[k] = the point of
+ *   key-frame index match[k]; -1 untouched; -2 set to NULL by the rotation
+ *   check. */
+orbgpu_status orbgpu_search_by_projection_kf(
+    orbgpu_matcher* m, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    const orbgpu_pose* Tcw, const orbgpu_keypoint* kps, const uint8_t* descs,
+    const uint8_t* claimed, int n, const orbgpu_map_point* pts, const float* angles, int n_pts,
+    float th, int orb_dist, int check_orientation, int32_t* match, int* nmatches);
+
+/* Device-resident batch of the above: frame f against its key frame's points
+ * d_pts + f * pt_stride (d_npts[f] of them; angles likewise), pose d_Tcw[f];
+ * layout and outputs as orbgpu_search_by_projection_last_batch. */
+orbgpu_status orbgpu_search_by_projection_kf_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    const orbgpu_pose* d_Tcw, const orbgpu_keypoint* d_kps, const uint8_t* d_descs,
+    const uint8_t* d_claimed, const int* d_n, int kp_stride, const orbgpu_map_point* d_pts,
+    const float* d_angles, const int* d_npts, int pt_stride, float th, int orb_dist,
+    int check_orientation, int32_t* d_match, int* d_nmatches, void* hip_stream);
+
+/* Replaces: int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F,
+ *   vector<MapPoint*>& vpMapPointMatches) (orb_matcher.cc:215-389, Nleft ==
+ *   -1), the search of Tracking::TrackReferenceKeyFrame (tracking.cc:
+ *   2043-2067, ORBmatcher(0.7, true)) and Relocalization (:2904-2926,
+ *   ORBmatcher(0.75, true)).  The FeatureVectors pKF->mFeatVec / F.mFeatVec
+ *   as orbgpu_bow_transform writes them (ascending node ids; node j's
+ *   feature indices at features[offsets[j] .. offsets[j + 1])); kf_valid[i] =
+ *   vpMapPointsKF[i] && !isBad(); kf_angles[i] = pKF->mvKeysUn[i].angle,
+ *   f_angles[k] = F.mvKeys[k].angle (both may be NULL without the
+ *   orientation check).  match[k] = i: vpMapPointMatches[k] = the point of
+ *   key-frame feature i; -1: NULL.  *nmatches = the return value. */
+orbgpu_status orbgpu_search_by_bow(orbgpu_matcher* m, const uint32_t* kf_nodes,
+                                   const int32_t* kf_offsets, const uint32_t* kf_features,
+                                   int kf_n_nodes, const uint8_t* kf_descs, const float* kf_angles,
+                                   const uint8_t* kf_valid, int kf_n, const uint32_t* f_nodes,
+                                   const int32_t* f_offsets, const uint32_t* f_features,
+                                   int f_n_nodes, const uint8_t* f_descs, const float* f_angles,
+                                   int f_n, float nn_ratio, int check_orientation, int32_t* match,
+                                   int* nmatches);
+
+/* Device-resident batch: pair f reads the key frame's FeatureVector at
+ * d_kf_* + f * kf_stride (offsets at f * (kf_stride + 1), d_kf_n_nodes[f]
+ * nodes), its descriptors / angles / valid flags at f * kf_stride, and the
+ * frame's at f * f_stride the same way -- orbgpu_bow_transform_batch's output
+ * layout; the frame's angle of keypoint k at d_f_angles[(f * f_stride + k) *
+ * f_angle_step] (1 for a float array, 7 for orbgpu_keypoint rows starting at
+ * the first row's angle), d_f_n[f] keypoints.  Writes d_match + f * f_stride
+ * and d_nmatches[f]; asynchronous on hip_stream (NULL: the context's). */
+orbgpu_status orbgpu_search_by_bow_batch(
+    orbgpu_matcher* m, int n_frames, const uint32_t* d_kf_nodes, const int32_t* d_kf_offsets,
+    const uint32_t* d_kf_features, const int* d_kf_n_nodes, const uint8_t* d_kf_descs,
+    const float* d_kf_angles, const uint8_t* d_kf_valid, int kf_stride, const uint32_t* d_f_nodes,
+    const int32_t* d_f_offsets, const uint32_t* d_f_features, const int* d_f_n_nodes,
+    const uint8_t* d_f_descs, const float* d_f_angles, int f_angle_step, const int* d_f_n,
+    int f_stride, float nn_ratio, int check_orientation, int32_t* d_match, int* d_nmatches,
+    void* hip_stream);
+
 /* ------------------------------------------------------------------------
  * DBoW2 bag-of-words conversion (3rdparty/DBoW2, ORBVocabulary =
  * TemplatedVocabulary<FORB::TDescriptor, FORB>): Frame::ComputeBoW

@@ -60,6 +60,9 @@ def lib() -> ctypes.CDLL:
                          LBA_REDUCE_FN, _P, _P, _P, _P, _P]),
         "orc_search_last": (_I, [_P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _I, _I, _P]),
         "orc_frustum": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
+        "orc_search_kf": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _I, _I, _P]),
+        "orc_search_bow": (_I, [_P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _I,
+                                _P]),
         "orc_search_local": (_I, [_P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _I, _F, _P]),
         "orc_predict_scale": (_I, [_F, _F, _F, _I]),
         "orc_predict_scale_check": (ctypes.c_long, [_F, _I, _P, ctypes.c_uint32, ctypes.c_uint32]),
@@ -326,6 +329,37 @@ def search_last(geom, cam, mb, Tcw, Tlw, kps, desc, uright, claimed, pts, th, mo
                                _p(cl), len(k), _p(p), len(p), float(th), int(mono),
                                int(check_ori), _p(match))
     return nm, match[:len(k)]
+
+
+def search_kf(geom, cam, Tcw, kps, desc, claimed, pts, angles, th, orb_dist, check_ori):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) -> (nmatches, match)."""
+    g = _geom(geom)
+    c = np.ascontiguousarray(cam, np.float32)
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    d = np.ascontiguousarray(desc, np.uint8)
+    p = np.ascontiguousarray(pts, MAP_POINT_DTYPE)
+    a = np.ascontiguousarray(angles, np.float32)
+    tc = np.ascontiguousarray(Tcw, np.float32)
+    match = np.zeros(max(len(k), 1), np.int32)
+    nm = lib().orc_search_kf(_p(g), _p(c), _p(tc), _p(k), _p(d), _p(_opt(claimed, np.uint8)),
+                             len(k), _p(p), _p(a), len(p), float(th), int(orb_dist),
+                             int(check_ori), _p(match))
+    return nm, match[:len(k)]
+
+
+def search_bow(kf_fv, kf_desc, kf_angle, kf_valid, f_fv, f_desc, f_angle, nn_ratio, check_ori):
+    """SearchByBoW(pKF, F, vpMapPointMatches); a FeatureVector is (nodes uint32
+    ascending, offsets int32 [n + 1], features uint32) -> (nmatches, match)."""
+    kn, ko, kf = (np.ascontiguousarray(x, t) for x, t in zip(kf_fv, (np.uint32, np.int32, np.uint32)))
+    fn, fo, ff = (np.ascontiguousarray(x, t) for x, t in zip(f_fv, (np.uint32, np.int32, np.uint32)))
+    kd, fd = np.ascontiguousarray(kf_desc, np.uint8), np.ascontiguousarray(f_desc, np.uint8)
+    ka, fa = np.ascontiguousarray(kf_angle, np.float32), np.ascontiguousarray(f_angle, np.float32)
+    kv = np.ascontiguousarray(kf_valid, np.uint8)
+    match = np.zeros(max(len(fd), 1), np.int32)
+    nm = lib().orc_search_bow(_p(kn), _p(ko), _p(kf), len(kn), _p(kd), _p(ka), _p(kv), _p(fn),
+                              _p(fo), _p(ff), len(fn), _p(fd), _p(fa), len(fd), float(nn_ratio),
+                              int(check_ori), _p(match))
+    return nm, match[:len(fd)]
 
 
 def frustum(geom, cam, Rcw, tcw, Ow, pts, cos_limit, views=None):

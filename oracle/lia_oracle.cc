@@ -384,7 +384,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
       std::vector<double> Sm(Hpp), bs(bp);
       bool ok = true;
       for (int p = 0; p < n_pts; ++p) {
-        double Dm[3][3], Di[3][3];
+        double Dm[3][3], Di[3][3] = {};  // a singular block leaves 0 (and fails the trial)
         for (int a = 0; a < 3; ++a)
           for (int b2 = 0; b2 < 3; ++b2) Dm[a][b2] = Hll[(size_t)9 * p + 3 * a + b2] + (a == b2 ? lambda : 0.0);
         if (!inv3(Dm, Di)) ok = false;

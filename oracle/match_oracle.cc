@@ -14,7 +14,12 @@
 //     (:208-213);
 //   * ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame&
 //     LastFrame, th, bMono) (orb_matcher.cc:1518-1728), ComputeThreeMaxima
-//     (:1841-1873), DescriptorDistance (:1877-1891).
+//     (:1841-1873), DescriptorDistance (:1877-1891);
+//   * ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
+//     const set<MapPoint*>& sAlreadyFound, th, ORBdist) (orb_matcher.cc:
+//     1730-1839), Relocalization's search;
+//   * ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&)
+//     (orb_matcher.cc:215-389), over the two DBoW2 FeatureVectors.
 //
 // Float arithmetic: the reference is g++ -O2 -march=native C++ (contraction
 // on in C++ dialects), so Eigen / Sophus sums of products are fused.  The
@@ -328,6 +333,142 @@ int orc_search_last(const Geom* g, const Cam* cam, float mb, const float* Tcw, c
     }
   }
   write_match(F, nulled, match);
+  return nmatches;
+}
+
+// ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+// ORBdist) -- orb_matcher.cc:1730-1839.  pts[i]: the key frame's point of
+// keypoint i (flags & 1: NULL, isBad() or in sAlreadyFound); angles[i]:
+// pKF->mvKeysUn[i].angle; claimed: CurrentFrame.mvpMapPoints[k] != NULL.
+int orc_search_kf(const Geom* g, const Cam* cam, const float* Tcw, const Kp* kps,
+                  const uint8_t* desc, const uint8_t* claimed, int n, const MapPt* pts,
+                  const float* angles, int n_pts, float th, int orb_dist, int check_ori,
+                  int32_t* match) {
+  Frame F(g, kps, desc, nullptr, claimed, n);
+  int nmatches = 0;
+  std::vector<int> rot_hist[kHistoLength];
+  const float factor = kHistoLength / 360.0f;
+  const V3 Ow = se3_inverse_translation(Tcw);  // Tcw.inverse().translation()
+  for (int i = 0; i < n_pts; ++i) {
+    const MapPt& M = pts[i];
+    if (M.flags & 1) continue;
+    const V3 x3Dw{M.Xw[0], M.Xw[1], M.Xw[2]};
+    const V3 x3Dc = se3_apply(Tcw, x3Dw);
+    const float u = project_u(*cam, x3Dc), v = project_v(*cam, x3Dc);
+    if (u < g->min_x || u > g->max_x) continue;
+    if (v < g->min_y || v > g->max_y) continue;
+    const V3 PO{x3Dw.x - Ow.x, x3Dw.y - Ow.y, x3Dw.z - Ow.z};
+    const float dist3D = std::sqrt(dot3(PO, PO));
+    const float maxD = 1.2f * M.max_dist, minD = 0.8f * M.min_dist;  // mappoint.cc:524-532
+    if (dist3D < minD || dist3D > maxD) continue;
+    const int level = predict_scale(M.max_dist, dist3D, g->log_scale, g->n_levels);
+    const float radius = th * g->scale[level];
+    const std::vector<int> cand = F.features_in_area(u, v, radius, level - 1, level + 1);
+    if (cand.empty()) continue;
+    int best = 256, best_idx = -1;
+    for (int i2 : cand) {
+      if (F.holder[i2] != -1) continue;  // CurrentFrame.mvpMapPoints[i2]
+      const int d = desc_dist(M.desc, desc + 32 * (size_t)i2);
+      if (d < best) best = d, best_idx = i2;
+    }
+    if (best <= orb_dist) {
+      F.holder[best_idx] = i;
+      F.holder_obs[best_idx] = 1;
+      ++nmatches;
+      if (check_ori) {
+        float rot = angles[i] - kps[best_idx].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHistoLength) bin = 0;
+        rot_hist[bin].push_back(best_idx);
+      }
+    }
+  }
+  std::vector<char> nulled(n, 0);
+  if (check_ori) {
+    int i1, i2, i3;
+    three_maxima(rot_hist, i1, i2, i3);
+    for (int b = 0; b < kHistoLength; ++b) {
+      if (b == i1 || b == i2 || b == i3) continue;
+      for (int idx : rot_hist[b]) {
+        F.holder[idx] = -1;
+        nulled[idx] = 1;
+        --nmatches;
+      }
+    }
+  }
+  write_match(F, nulled, match);
+  return nmatches;
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&
+// vpMapPointMatches) -- orb_matcher.cc:215-389, Nleft == -1.  FeatureVectors
+// as ascending node ids with CSR feature lists (node j: features
+// [off[j], off[j + 1])); kf_valid[i]: vpMapPointsKF[i] && !isBad(); angles:
+// pKF->mvKeysUn[i].angle / F.mvKeys[k].angle.  match[k] = the key-frame index
+// whose point F's keypoint k receives, -1 none (vpMapPointMatches starts all
+// NULL).  The right-camera branch never fires for Nleft == -1 (its best
+// distance stays 256).
+int orc_search_bow(const uint32_t* kf_nodes, const int32_t* kf_off, const uint32_t* kf_feat,
+                   int kf_n_nodes, const uint8_t* kf_desc, const float* kf_angle,
+                   const uint8_t* kf_valid, const uint32_t* f_nodes, const int32_t* f_off,
+                   const uint32_t* f_feat, int f_n_nodes, const uint8_t* f_desc,
+                   const float* f_angle, int f_n, float nn_ratio, int check_ori, int32_t* match) {
+  constexpr int kThLow = 50;  // orb_matcher.cc:36
+  for (int k = 0; k < f_n; ++k) match[k] = -1;
+  int nmatches = 0;
+  std::vector<int> rot_hist[kHistoLength];
+  const float factor = kHistoLength / 360.0f;
+  int a = 0, b = 0;
+  while (a < kf_n_nodes && b < f_n_nodes) {
+    if (kf_nodes[a] == f_nodes[b]) {
+      for (int ia = kf_off[a]; ia < kf_off[a + 1]; ++ia) {
+        const int realIdxKF = (int)kf_feat[ia];
+        if (!kf_valid[realIdxKF]) continue;
+        int best1 = 256, best_idx = -1, best2 = 256;
+        for (int ib = f_off[b]; ib < f_off[b + 1]; ++ib) {
+          const int realIdxF = (int)f_feat[ib];
+          if (match[realIdxF] >= 0) continue;
+          const int d = desc_dist(kf_desc + 32 * (size_t)realIdxKF, f_desc + 32 * (size_t)realIdxF);
+          if (d < best1) {
+            best2 = best1;
+            best1 = d;
+            best_idx = realIdxF;
+          } else if (d < best2) {
+            best2 = d;
+          }
+        }
+        if (best1 <= kThLow && (float)best1 < nn_ratio * (float)best2) {
+          match[best_idx] = realIdxKF;
+          if (check_ori) {
+            float rot = kf_angle[realIdxKF] - f_angle[best_idx];
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)std::round(rot * factor);
+            if (bin == kHistoLength) bin = 0;
+            rot_hist[bin].push_back(best_idx);
+          }
+          ++nmatches;
+        }
+      }
+      ++a;
+      ++b;
+    } else if (kf_nodes[a] < f_nodes[b]) {  // KFit = vFeatVecKF.lower_bound(Fit->first)
+      a = (int)(std::lower_bound(kf_nodes + a, kf_nodes + kf_n_nodes, f_nodes[b]) - kf_nodes);
+    } else {
+      b = (int)(std::lower_bound(f_nodes + b, f_nodes + f_n_nodes, kf_nodes[a]) - f_nodes);
+    }
+  }
+  if (check_ori) {
+    int i1, i2, i3;
+    three_maxima(rot_hist, i1, i2, i3);
+    for (int bn = 0; bn < kHistoLength; ++bn) {
+      if (bn == i1 || bn == i2 || bn == i3) continue;
+      for (int idx : rot_hist[bn]) {
+        match[idx] = -1;
+        --nmatches;
+      }
+    }
+  }
   return nmatches;
 }
 

@@ -219,6 +219,23 @@ SIGNATURES = {
         [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _P, _P, _P, _I, _P,
          _I, _F, _F, _F, _I, _F, _P, _P, _P],
     ),
+    "orbgpu_search_by_projection_kf": (
+        _I,
+        [_P, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _I, _P, _P, _I, _F,
+         _I, _I, _P, _P],
+    ),
+    "orbgpu_search_by_projection_kf_batch": (
+        _I,
+        [_P, _I, ctypes.POINTER(FrameGeom), ctypes.POINTER(Camera), _P, _P, _P, _P, _P, _I, _P, _P,
+         _P, _I, _F, _I, _I, _P, _P, _P],
+    ),
+    "orbgpu_search_by_bow": (
+        _I, [_P, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _F, _I, _P, _P],
+    ),
+    "orbgpu_search_by_bow_batch": (
+        _I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _I,
+             _P, _P, _P],
+    ),
     "orbgpu_level_thresholds": (_I, [_F, _I, _P]),
     "orbgpu_vocab_load_text": (_I, [_I, ctypes.c_char_p, ctypes.POINTER(_P)]),
     "orbgpu_vocab_destroy": (None, [_P]),

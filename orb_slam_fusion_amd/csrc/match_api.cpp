@@ -156,6 +156,7 @@ struct Bump {
 size_t in_bytes(int n, int n_pts, size_t pt_size) {
   return align_up(sizeof(orbgpu_keypoint) * n) + align_up(32 * (size_t)n) + align_up(4 * (size_t)n) +
          align_up(n) + align_up(pt_size * n_pts) + align_up(sizeof(orbgpu_track_view) * n_pts) +
+         align_up(4 * (size_t)n_pts) +
          align_up(2 * sizeof(orbgpu_pose)) + align_up(16 * sizeof(float)) + align_up(2 * sizeof(int)) +
          8 * 256;
 }
@@ -558,6 +559,198 @@ orbgpu_status orbgpu_search_local_points(
   return local_common(m, geom, cam, pose15, kps, descs, uright, claimed, n, pts, nullptr, n_pts,
                       view_cos_limit, th, nn_ratio, far_points, th_far_points, views, match,
                       nmatches);
+}
+
+orbgpu_status orbgpu_search_by_projection_kf(
+    orbgpu_matcher* m, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    const orbgpu_pose* Tcw, const orbgpu_keypoint* kps, const uint8_t* descs,
+    const uint8_t* claimed, int n, const orbgpu_map_point* pts, const float* angles, int n_pts,
+    float th, int orb_dist, int check_orientation, int32_t* match, int* nmatches) {
+  if (!m || !cam || !Tcw || bad_frame(kps, descs, n, match, nmatches) || n_pts < 0 ||
+      (n_pts > 0 && (!pts || (check_orientation && !angles))))
+    return ORBGPU_ERR_INVALID;
+  if (n > m->max_kp || n_pts > m->max_pts) return ORBGPU_ERR_CAPACITY;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  HostCall c(m);
+  orbgpu_status st = fill_params(m, geom, cam, 0.0f, c.L.p);
+  if (st != ORBGPU_OK) return st;
+  c.L.p.th = th;
+  c.L.p.orb_dist = orb_dist;
+  c.L.p.check_ori = check_orientation != 0;
+  c.L.mode = orbgpu::kModeKeyFrame;
+  if ((st = stage_frame(c, kps, descs, nullptr, claimed, n, n_pts)) != ORBGPU_OK) return st;
+  orbgpu_map_point* hp;
+  float* ha;
+  orbgpu_pose* hpose;
+  c.L.mpts = c.bi.take<orbgpu_map_point>(n_pts, &hp);
+  if (n_pts > 0) std::memcpy(hp, pts, sizeof(orbgpu_map_point) * n_pts);
+  c.L.q_angle = c.bi.take<float>(n_pts, &ha);
+  if (n_pts > 0 && angles) std::memcpy(ha, angles, sizeof(float) * n_pts);
+  c.L.Tcw = c.bi.take<orbgpu_pose>(1, &hpose);
+  hpose[0] = *Tcw;
+  int32_t dummy = 0;
+  return run_host(c, n, n > 0 ? match : &dummy, nmatches, nullptr, n_pts);
+}
+
+orbgpu_status orbgpu_search_by_projection_kf_batch(
+    orbgpu_matcher* m, int n_frames, const orbgpu_frame_geom* geom, const orbgpu_camera* cam,
+    const orbgpu_pose* d_Tcw, const orbgpu_keypoint* d_kps, const uint8_t* d_descs,
+    const uint8_t* d_claimed, const int* d_n, int kp_stride, const orbgpu_map_point* d_pts,
+    const float* d_angles, const int* d_npts, int pt_stride, float th, int orb_dist,
+    int check_orientation, int32_t* d_match, int* d_nmatches, void* hip_stream) {
+  if (!m || !cam || n_frames <= 0 || !d_Tcw || !d_kps || !d_descs || !d_n || kp_stride <= 0 ||
+      kp_stride > orbgpu::kMatchMaxKeypoints || !d_pts || (check_orientation && !d_angles) ||
+      !d_npts || pt_stride <= 0 || pt_stride > orbgpu::kMatchMaxPoints || !d_match || !d_nmatches)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  MatchLaunch L{};
+  orbgpu_status st = fill_params(m, geom, cam, 0.0f, L.p);
+  if (st != ORBGPU_OK) return st;
+  L.p.th = th;
+  L.p.orb_dist = orb_dist;
+  L.p.check_ori = check_orientation != 0;
+  L.mode = orbgpu::kModeKeyFrame;
+  L.n_frames = n_frames;
+  L.kps = reinterpret_cast<const float*>(d_kps);
+  L.desc = d_descs;
+  L.claimed = d_claimed;
+  L.n = d_n;
+  L.kp_stride = kp_stride;
+  L.mpts = d_pts;
+  L.q_angle = d_angles;
+  L.npts = d_npts;
+  L.pt_stride = pt_stride;
+  L.max_pts = pt_stride;
+  L.Tcw = d_Tcw;
+  if (ensure_scratch(m, n_frames, kp_stride, pt_stride) != ORBGPU_OK) return ORBGPU_ERR_NOMEM;
+  L.cell_start = m->d_cell_start;
+  L.cell_idx = m->d_cell_idx;
+  L.res = m->d_res;
+  L.acc = m->d_acc;
+  L.match = d_match;
+  L.nmatches = d_nmatches;
+  L.err = m->d_err;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+  return orbgpu::launch_match(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
+orbgpu_status orbgpu_search_by_bow_batch(
+    orbgpu_matcher* m, int n_frames, const uint32_t* d_kf_nodes, const int32_t* d_kf_offsets,
+    const uint32_t* d_kf_features, const int* d_kf_n_nodes, const uint8_t* d_kf_descs,
+    const float* d_kf_angles, const uint8_t* d_kf_valid, int kf_stride, const uint32_t* d_f_nodes,
+    const int32_t* d_f_offsets, const uint32_t* d_f_features, const int* d_f_n_nodes,
+    const uint8_t* d_f_descs, const float* d_f_angles, int f_angle_step, const int* d_f_n,
+    int f_stride, float nn_ratio, int check_orientation, int32_t* d_match, int* d_nmatches,
+    void* hip_stream) {
+  if (!m || n_frames <= 0 || !d_kf_nodes || !d_kf_offsets || !d_kf_features || !d_kf_n_nodes ||
+      !d_kf_descs || (check_orientation && !d_kf_angles) || !d_kf_valid || kf_stride <= 0 ||
+      !d_f_nodes || !d_f_offsets || !d_f_features || !d_f_n_nodes || !d_f_descs ||
+      (check_orientation && !d_f_angles) || f_angle_step <= 0 || !d_f_n || f_stride <= 0 ||
+      f_stride > orbgpu::kMatchMaxKeypoints || kf_stride > 32767 || !d_match || !d_nmatches)
+    return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  orbgpu::BowSearchLaunch L{};
+  L.n_frames = n_frames;
+  L.nn_ratio = nn_ratio;
+  L.check_ori = check_orientation != 0;
+  L.kf_nodes = d_kf_nodes, L.kf_off = d_kf_offsets, L.kf_feat = d_kf_features;
+  L.kf_n_nodes = d_kf_n_nodes, L.kf_desc = d_kf_descs, L.kf_angle = d_kf_angles;
+  L.kf_valid = d_kf_valid, L.kf_stride = kf_stride;
+  L.f_nodes = d_f_nodes, L.f_off = d_f_offsets, L.f_feat = d_f_features;
+  L.f_n_nodes = d_f_n_nodes, L.f_desc = d_f_descs, L.f_angle = d_f_angles;
+  L.angle_step = f_angle_step, L.f_n = d_f_n, L.f_stride = f_stride;
+  L.match = d_match, L.nmatches = d_nmatches, L.err = m->d_err;
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : m->stream;
+  return orbgpu::launch_bow_search(L, s) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
+orbgpu_status orbgpu_search_by_bow(orbgpu_matcher* m, const uint32_t* kf_nodes,
+                                   const int32_t* kf_offsets, const uint32_t* kf_features,
+                                   int kf_n_nodes, const uint8_t* kf_descs, const float* kf_angles,
+                                   const uint8_t* kf_valid, int kf_n, const uint32_t* f_nodes,
+                                   const int32_t* f_offsets, const uint32_t* f_features,
+                                   int f_n_nodes, const uint8_t* f_descs, const float* f_angles,
+                                   int f_n, float nn_ratio, int check_orientation, int32_t* match,
+                                   int* nmatches) {
+  if (!m || kf_n < 0 || f_n < 0 || kf_n_nodes < 0 || f_n_nodes < 0 || !nmatches ||
+      (kf_n_nodes > 0 && (!kf_nodes || !kf_offsets || !kf_features)) ||
+      (f_n_nodes > 0 && (!f_nodes || !f_offsets || !f_features)) ||
+      (kf_n > 0 && (!kf_descs || !kf_valid || (check_orientation && !kf_angles))) ||
+      (f_n > 0 && (!f_descs || !match || (check_orientation && !f_angles))) ||
+      kf_n_nodes > kf_n || f_n_nodes > f_n)
+    return ORBGPU_ERR_INVALID;
+  if (f_n > m->max_kp || kf_n > 32767) return ORBGPU_ERR_CAPACITY;
+  for (int j = 0; j < kf_n_nodes; ++j)
+    if (kf_offsets[j + 1] < kf_offsets[j] || kf_offsets[j + 1] > kf_n) return ORBGPU_ERR_INVALID;
+  for (int j = 0; j < f_n_nodes; ++j)
+    if (f_offsets[j + 1] < f_offsets[j] || f_offsets[j + 1] > f_n) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(m->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  const int KS = std::max(kf_n, 1), FS = std::max(f_n, 1);
+  // one upload: both FeatureVectors, descriptors, angles, valid flags, counts
+  const size_t need = 3 * align_up(4 * (size_t)KS) + align_up(4 * (size_t)(KS + 1)) +
+                      align_up(32 * (size_t)KS) + align_up(KS) + 3 * align_up(4 * (size_t)FS) +
+                      align_up(4 * (size_t)(FS + 1)) + align_up(32 * (size_t)FS) + align_up(12);
+  if (arena_reserve(m->in, need) != ORBGPU_OK) return ORBGPU_ERR_NOMEM;
+  Bump b2{m->in};
+  uint32_t *hkn, *hkf, *hfn, *hff;
+  int32_t *hko, *hfo;
+  uint8_t *hkd, *hkv, *hfd;
+  float *hka, *hfa;
+  int* hcnt;
+  const uint32_t* dkn = b2.take<uint32_t>(KS, &hkn);
+  const int32_t* dko = b2.take<int32_t>(KS + 1, &hko);
+  const uint32_t* dkf = b2.take<uint32_t>(KS, &hkf);
+  const uint8_t* dkd = b2.take<uint8_t>(32 * (size_t)KS, &hkd);
+  const float* dka = b2.take<float>(KS, &hka);
+  const uint8_t* dkv = b2.take<uint8_t>(KS, &hkv);
+  const uint32_t* dfn = b2.take<uint32_t>(FS, &hfn);
+  const int32_t* dfo = b2.take<int32_t>(FS + 1, &hfo);
+  const uint32_t* dff = b2.take<uint32_t>(FS, &hff);
+  const uint8_t* dfd = b2.take<uint8_t>(32 * (size_t)FS, &hfd);
+  const float* dfa = b2.take<float>(FS, &hfa);
+  int* dcnt = b2.take<int>(3, &hcnt);
+  hko[0] = 0;
+  if (kf_n_nodes > 0) {
+    std::memcpy(hkn, kf_nodes, 4 * (size_t)kf_n_nodes);
+    std::memcpy(hko, kf_offsets, 4 * (size_t)(kf_n_nodes + 1));
+    std::memcpy(hkf, kf_features, 4 * (size_t)kf_offsets[kf_n_nodes]);
+  }
+  hfo[0] = 0;
+  if (f_n_nodes > 0) {
+    std::memcpy(hfn, f_nodes, 4 * (size_t)f_n_nodes);
+    std::memcpy(hfo, f_offsets, 4 * (size_t)(f_n_nodes + 1));
+    std::memcpy(hff, f_features, 4 * (size_t)f_offsets[f_n_nodes]);
+  }
+  if (kf_n > 0) {
+    std::memcpy(hkd, kf_descs, 32 * (size_t)kf_n);
+    std::memcpy(hkv, kf_valid, kf_n);
+    if (kf_angles) std::memcpy(hka, kf_angles, 4 * (size_t)kf_n);
+  }
+  if (f_n > 0) {
+    std::memcpy(hfd, f_descs, 32 * (size_t)f_n);
+    if (f_angles) std::memcpy(hfa, f_angles, 4 * (size_t)f_n);
+  }
+  hcnt[0] = kf_n_nodes, hcnt[1] = f_n_nodes, hcnt[2] = f_n;
+  Bump bo{m->out};
+  int32_t* dmatch = bo.take<int32_t>(FS);
+  int* dnm = bo.take<int>(1);
+  hipStream_t s = m->stream;
+  if (hipMemsetAsync(m->d_err, 0, sizeof(int), s) ||
+      hipMemcpyAsync(m->in.d, m->in.h, b2.off, hipMemcpyHostToDevice, s))
+    return ORBGPU_ERR_DEVICE;
+  const orbgpu_status st = orbgpu_search_by_bow_batch(
+      m, 1, dkn, dko, dkf, dcnt, dkd, dka, dkv, KS, dfn, dfo, dff, dcnt + 1, dfd, dfa, 1, dcnt + 2, FS,
+      nn_ratio, check_orientation, dmatch, dnm, s);
+  if (st != ORBGPU_OK) return st;
+  int err = 0;
+  const size_t dl = (size_t)((uint8_t*)dnm - m->out.d) + sizeof(int);
+  if (hipMemcpyAsync(m->out.h, m->out.d, dl, hipMemcpyDeviceToHost, s) ||
+      hipMemcpyAsync(&err, m->d_err, sizeof(int), hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+    return ORBGPU_ERR_DEVICE;
+  if (err) return ORBGPU_ERR_CAPACITY;
+  if (f_n > 0) std::memcpy(match, m->out.h + ((uint8_t*)dmatch - m->out.d), 4 * (size_t)f_n);
+  std::memcpy(nmatches, m->out.h + ((uint8_t*)dnm - m->out.d), sizeof(int));
+  return ORBGPU_OK;
 }
 
 int orbgpu_level_thresholds(float log_scale_factor, int n_levels, float* thr) {

@@ -6,7 +6,8 @@
 //                 index inside a cell), counting sort in LDS
 //   k_mt_search   wave / query point: projection (SearchByProjection(Frame&,
 //                 const Frame&) orb_matcher.cc:1538-1577, or Frame::isInFrustum
-//                 frame.cc:548-603 + orb_matcher.cc:50-69), then
+//                 frame.cc:548-603 + orb_matcher.cc:50-69, or the key frame
+//                 form of Relocalization :1747-1779), then
 //                 GetFeaturesInArea (frame.cc:679-746): lanes own grid cells
 //                 of the window, filter, Hamming distance from 8 v_bcnt, and
 //                 the wave keeps the best and second candidate by the packed
@@ -178,6 +179,42 @@ __device__ bool frustum(const MatchParams& p, const float* pose15, const orbgpu_
   return true;
 }
 
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) query
+// setup (orb_matcher.cc:1747-1779): the key frame's point q (ORBGPU_MP_SKIP:
+// NULL, bad or already found) projected by Tcw without a depth test, the
+// image bounds, the scale-invariance distances, PredictScale's level, the
+// window th * scale[level] over levels [level - 1, level + 1].
+__device__ Query query_keyframe(const MatchLaunch& a, int f, int q) {
+  const MatchParams& p = a.p;
+  Query Q;
+  Q.valid = false;
+  const orbgpu_map_point* M = a.mpts + (size_t)f * a.pt_stride + q;
+  if (M->flags & ORBGPU_MP_SKIP) return Q;
+  const orbgpu_pose Tcw = a.Tcw[f];
+  const V3 X{M->Xw[0], M->Xw[1], M->Xw[2]};
+  const V3 x3Dc = se3_apply(Tcw, X);
+  const float u = p.fx * x3Dc.x / x3Dc.z + p.cx;
+  const float v = p.fy * x3Dc.y / x3Dc.z + p.cy;
+  if (u < p.min_x || u > p.max_x) return Q;
+  if (v < p.min_y || v > p.max_y) return Q;
+  const V3 Ow = se3_inverse_translation(Tcw);
+  const V3 PO{X.x - Ow.x, X.y - Ow.y, X.z - Ow.z};
+  const float dist = sqrtf(dot3(PO, PO));
+  const float maxD = 1.2f * M->max_dist, minD = 0.8f * M->min_dist;
+  if (dist < minD || dist > maxD) return Q;
+  const float ratio = M->max_dist / dist;  // MapPoint::PredictScale by the host's thresholds
+  int level = 0;
+  if (ratio != __builtin_inff())
+    for (int j = 1; j < p.n_levels; ++j) level += ratio >= p.level_thr[j - 1];
+  Q.r = p.th * p.scale[level];
+  Q.min_level = level - 1, Q.max_level = level + 1;
+  Q.x = u, Q.y = v;
+  Q.ur_ref = 0.0f;  // no right-coordinate test in this search
+  load_desc(M->desc, Q.d);
+  Q.valid = true;
+  return Q;
+}
+
 // SearchByProjection(Frame&, vector<MapPoint*>) query setup (orb_matcher.cc:50-69)
 __device__ Query query_local(const MatchParams& p, const orbgpu_map_point* M,
                              const orbgpu_track_view& V) {
@@ -300,6 +337,7 @@ __device__ void wave_topk(const MatchParams& p, const FrameRef& F, const Query& 
 
 __device__ __forceinline__ Query make_query(const MatchLaunch& a, int f, int q, bool write_view) {
   if (a.mode == kModeLast) return query_last(a, f, q);
+  if (a.mode == kModeKeyFrame) return query_keyframe(a, f, q);
   const size_t o = (size_t)f * a.pt_stride + q;
   const orbgpu_map_point* M = a.mpts + o;
   orbgpu_track_view V;
@@ -411,13 +449,18 @@ __global__ __launch_bounds__(256) void k_mt_search(MatchLaunch a) {
   }
 }
 
+// the distance a best candidate must not exceed (TH_HIGH, or ORBdist)
+__device__ __forceinline__ int accept_dist(const MatchLaunch& a) {
+  return a.mode == kModeKeyFrame ? a.p.orb_dist : kThHigh;
+}
+
 // accept decision of one query from its (best, second)
 __device__ __forceinline__ bool accept_of(const MatchLaunch& a, const float* kps, uint32_t best,
                                           uint32_t second) {
   if (best == kNone) return false;
   const int d1 = (int)(best >> 16);
-  if (d1 > kThHigh) return false;
-  if (a.mode == kModeLast) return true;
+  if (d1 > accept_dist(a)) return false;
+  if (a.mode == kModeLast || a.mode == kModeKeyFrame) return true;
   // orb_matcher.cc:117-121: reject iff same level and d1 > ratio * d2
   const int l1 = kp_octave(kps + (size_t)(best & 0xFFFF) * kKpFloats);
   const int l2 = second == kNone ? -1 : kp_octave(kps + (size_t)(second & 0xFFFF) * kKpFloats);
@@ -425,16 +468,21 @@ __device__ __forceinline__ bool accept_of(const MatchLaunch& a, const float* kps
   return !(l1 == l2 && (float)d1 > a.p.nn_ratio * (float)d2);
 }
 
+// does a match by query q hide its keypoint from later queries?  (the key
+// frame search skips every keypoint holding a point, orb_matcher.cc:1791)
 __device__ __forceinline__ bool has_obs(const MatchLaunch& a, int f, int q) {
   const size_t o = (size_t)f * a.pt_stride + q;
+  if (a.mode == kModeKeyFrame) return true;
   return a.mode == kModeLast ? a.ppts[o].has_obs != 0 : (a.mpts[o].flags & ORBGPU_MP_HAS_OBS) != 0;
 }
 
-// rotation bin of a match (orb_matcher.cc:1626-1630)
+// rotation bin of a match (orb_matcher.cc:1626-1630, 1808-1812)
 __device__ __forceinline__ int rot_bin(const MatchLaunch& a, const float* kps, int f, int q,
                                        int idx) {
   const float factor = kHistoLength / 360.0f;
-  float rot = a.ppts[(size_t)f * a.pt_stride + q].angle - kps[(size_t)idx * kKpFloats + 3];
+  const size_t o = (size_t)f * a.pt_stride + q;
+  const float ang = a.mode == kModeKeyFrame ? a.q_angle[o] : a.ppts[o].angle;
+  float rot = ang - kps[(size_t)idx * kKpFloats + 3];
   if ((double)rot < 0.0) rot += 360.0f;
   int bin = (int)roundf(rot * factor);
   if (bin == kHistoLength) bin = 0;
@@ -450,8 +498,8 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   const int n = a.n[f], nq = min(a.npts[f], a.pt_stride);
   if (n > kMatchMaxKeypoints || n > a.kp_stride) return;  // reported by k_mt_grid
   const FrameRef F = frame_ref(a, f);
-  const bool rot_check = a.mode == kModeLast && a.p.check_ori;
-  const bool local = a.mode != kModeLast;
+  const bool rot_check = (a.mode == kModeLast || a.mode == kModeKeyFrame) && a.p.check_ori;
+  const bool local = a.mode == kModeLocal || a.mode == kModeLocalFrustum;
   // mvpMapPoints of this call: the last matching query (later matches
   // overwrite, orb_matcher.cc:122, 1611), kept with atomicMax in the output
   int32_t* match = a.match + (size_t)f * a.kp_stride;
@@ -491,7 +539,7 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
         }
       }
       // a best beyond TH_HIGH can only get worse as claims accumulate
-      const bool hopeless = b != kNone && (int)(b >> 16) > kThHigh;
+      const bool hopeless = b != kNone && (int)(b >> 16) > accept_dist(a);
       const int need = local ? 2 : 1;
       const bool exhausted = !done && !hopeless && found < need && count > kMatchTopK;
       const bool ok = !done && !exhausted && accept_of(a, F.kps, b, s2);
@@ -712,6 +760,152 @@ hipError_t launch_unproject(const UnprojLaunch& a, hipStream_t st) {
 hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st) {
   if (a.n_frames <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_mt_pose_obs, dim3(a.n_frames), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---- SearchByBoW(KeyFrame* pKF, Frame& F) (orb_matcher.cc:215-389) ------
+// Block / (key frame, frame) pair, a wave per key-frame node (strided): the
+// node's partner in the frame by binary search (the reference's merge join
+// with lower_bound visits exactly the common nodes, in ascending order), then
+// the node's key-frame features in order, each against the frame features of
+// the node not yet matched: lanes over the features (64 per pass), the key
+// (dist << 32 | position) -- the first strict minimum is the smallest key,
+// the running second best the smallest of the rest.  A feature belongs to one
+// node in each FeatureVector, so nodes are independent and only the claims
+// inside a node are sequential.  Then the rotation histogram over every
+// match (ComputeThreeMaxima) and the output.
+constexpr int kBowSearchThreads = 256;
+constexpr int kThLow = 50;  // ORBmatcher::TH_LOW (orb_matcher.cc:36)
+
+__global__ __launch_bounds__(kBowSearchThreads) void k_bow_search(BowSearchLaunch a) {
+  __shared__ int16_t mk[kMatchMaxKeypoints];  // matched key-frame feature per frame keypoint, -1
+  __shared__ uint8_t bins[kMatchMaxKeypoints];
+  __shared__ uint32_t claims[kMatchMaxKeypoints / 32];
+  __shared__ int hist[kHistoLength];
+  __shared__ int red[kBowSearchThreads / 64];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nf = a.f_n[f];
+  if (nf > kMatchMaxKeypoints || nf > a.f_stride || a.kf_n_nodes[f] > a.kf_stride ||
+      a.f_n_nodes[f] > a.f_stride) {
+    if (t == 0) atomicOr(a.err, 1);
+    return;
+  }
+  for (int k = t; k < kMatchMaxKeypoints; k += kBowSearchThreads) mk[k] = -1;
+  for (int k = t; k < kMatchMaxKeypoints / 32; k += kBowSearchThreads) claims[k] = 0;
+  if (t < kHistoLength) hist[t] = 0;
+  __syncthreads();
+  const size_t ko = (size_t)f * a.kf_stride, fo = (size_t)f * a.f_stride;
+  const uint32_t* kn = a.kf_nodes + ko;
+  const int32_t* koff = a.kf_off + (size_t)f * (a.kf_stride + 1);
+  const uint32_t* kfe = a.kf_feat + ko;
+  const uint32_t* fn = a.f_nodes + fo;
+  const int32_t* foff = a.f_off + (size_t)f * (a.f_stride + 1);
+  const uint32_t* ffe = a.f_feat + fo;
+  const int nkn = a.kf_n_nodes[f], nfn = a.f_n_nodes[f];
+  const float factor = kHistoLength / 360.0f;
+  for (int na = wave; na < nkn; na += kBowSearchThreads / 64) {
+    const uint32_t node = kn[na];
+    int lo = 0, hi = nfn;  // lower_bound over the frame's nodes (wave-uniform)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (fn[mid] < node) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= nfn || fn[lo] != node) continue;
+    const int fb = foff[lo], fe = min(foff[lo + 1], a.f_stride);
+    const int kb = koff[na], ke = min(koff[na + 1], a.kf_stride);
+    for (int ia = kb; ia < ke; ++ia) {
+      const int ik = (int)kfe[ia];
+      if (ik >= a.kf_stride || !a.kf_valid[ko + ik]) continue;
+      const uint32_t* qd = (const uint32_t*)(a.kf_desc + (ko + ik) * 32);
+      uint32_t d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = qd[i];
+      uint64_t k1 = kNoKey, k2 = kNoKey;  // this lane's two smallest keys
+      for (int base = fb; base < fe; base += 64) {
+        const int j = base + lane;
+        if (j >= fe) continue;
+        const int idx = (int)ffe[j];
+        if (idx >= nf || ((claims[idx >> 5] >> (idx & 31)) & 1u)) continue;
+        const uint4* fd = (const uint4*)(a.f_desc + (fo + idx) * 32);
+        const uint4 d0 = fd[0], d1 = fd[1];
+        const int dist = __popc(d0.x ^ d[0]) + __popc(d0.y ^ d[1]) + __popc(d0.z ^ d[2]) +
+                         __popc(d0.w ^ d[3]) + __popc(d1.x ^ d[4]) + __popc(d1.y ^ d[5]) +
+                         __popc(d1.z ^ d[6]) + __popc(d1.w ^ d[7]);
+        const uint64_t key = ((uint64_t)dist << 32) | (uint64_t)(j - fb);
+        if (key < k1) k2 = k1, k1 = key;
+        else if (key < k2) k2 = key;
+      }
+      const uint64_t m1 = wave_min_u64(k1);
+      const uint64_t m2 = wave_min_u64(k1 == m1 ? k2 : k1);
+      const int best1 = m1 == kNoKey ? 256 : (int)(m1 >> 32);
+      const int best2 = m2 == kNoKey ? 256 : (int)(m2 >> 32);
+      if (best1 <= kThLow && (float)best1 < a.nn_ratio * (float)best2) {
+        const int idx = (int)ffe[fb + (int)(m1 & 0xFFFFFFFFu)];
+        if (lane == 0) {
+          mk[idx] = (int16_t)ik;
+          atomicOr(&claims[idx >> 5], 1u << (idx & 31));
+          int bin = 0;
+          if (a.check_ori) {
+            float rot = a.kf_angle[ko + ik] - a.f_angle[(fo + idx) * a.angle_step];
+            if ((double)rot < 0.0) rot += 360.0f;
+            bin = (int)roundf(rot * factor);
+            if (bin == kHistoLength) bin = 0;
+            atomicAdd(&hist[bin], 1);
+          }
+          bins[idx] = (uint8_t)bin;
+        }
+        // the claim is read by this wave's next feature: drain the LDS write
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __syncthreads();
+  int ind1 = -1, ind2 = -1, ind3 = -1;
+  if (a.check_ori) {  // ComputeThreeMaxima (orb_matcher.cc:1841-1873), every thread
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < kHistoLength; ++i) {
+      const int sz = hist[i];
+      if (sz > max1) {
+        max3 = max2, max2 = max1, max1 = sz;
+        ind3 = ind2, ind2 = ind1, ind1 = i;
+      } else if (sz > max2) {
+        max3 = max2, max2 = sz;
+        ind3 = ind2, ind2 = i;
+      } else if (sz > max3) {
+        max3 = sz, ind3 = i;
+      }
+    }
+    if ((float)max2 < 0.1f * (float)max1) ind2 = ind3 = -1;
+    else if ((float)max3 < 0.1f * (float)max1) ind3 = -1;
+  }
+  int kept = 0;
+  int32_t* out = a.match + fo;
+  for (int k = t; k < nf; k += kBowSearchThreads) {
+    int v = mk[k];
+    if (v >= 0 && a.check_ori) {
+      const int b = bins[k];
+      if (b != ind1 && b != ind2 && b != ind3) v = -1;
+    }
+    kept += v >= 0;
+    out[k] = v;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) kept += __shfl_xor(kept, off, 64);
+  __syncthreads();
+  if (lane == 0) red[wave] = kept;
+  __syncthreads();
+  if (t == 0) {
+    int tot = 0;
+    for (int w = 0; w < kBowSearchThreads / 64; ++w) tot += red[w];
+    a.nmatches[f] = tot;
+  }
+}
+
+hipError_t launch_bow_search(const BowSearchLaunch& a, hipStream_t st) {
+  if (a.n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bow_search, dim3(a.n_frames), dim3(kBowSearchThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 // Launch descriptor of the ORBmatcher projection searches
-// (orb_matcher.cc:42-206, 1518-1728) over a batch of frames.
+// (orb_matcher.cc:42-206, 1518-1728, 1730-1839) over a batch of frames.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -19,7 +19,11 @@ constexpr int kMatchMaxPoints = 1 << 20;  // per frame
 constexpr int kMatchTopK = 4;
 constexpr int kMatchResWords = kMatchTopK + 1;
 
-enum MatchMode : int { kModeLast = 0, kModeLocal = 1, kModeLocalFrustum = 2 };
+// kModeLast: SearchByProjection(CurrentFrame, LastFrame); kModeLocal /
+// kModeLocalFrustum: SearchByProjection(F, vpMapPoints) (with isInFrustum);
+// kModeKeyFrame: SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+// ORBdist) of Relocalization.
+enum MatchMode : int { kModeLast = 0, kModeLocal = 1, kModeLocalFrustum = 2, kModeKeyFrame = 3 };
 
 // Everything scalar the searches read (passed by value).
 struct MatchParams {
@@ -33,6 +37,7 @@ struct MatchParams {
   float fx, fy, cx, cy, bf, mb;
   float th, nn_ratio, th_far, cos_limit;
   int mono, check_ori, far_points;
+  int orb_dist;  // kModeKeyFrame: accept bestDist <= ORBdist
 };
 
 struct MatchLaunch {
@@ -48,7 +53,8 @@ struct MatchLaunch {
   int kp_stride;
   // queries: frame f's points start at f * pt_stride
   const orbgpu_proj_point* ppts;  // kModeLast
-  const orbgpu_map_point* mpts;   // kModeLocal*
+  const orbgpu_map_point* mpts;   // kModeLocal*, kModeKeyFrame (the key frame's points)
+  const float* q_angle;           // kModeKeyFrame: pKF->mvKeysUn[i].angle per point
   orbgpu_track_view* views;       // kModeLocal*: read (kModeLocal) / written (kModeLocalFrustum)
   // kModeLocalFrustum: prior field values for the ones isInFrustum does not
   // write (null: views itself, updated in place)
@@ -56,7 +62,7 @@ struct MatchLaunch {
   const int* npts;                // points per frame (device)
   int pt_stride;
   int max_pts;                    // max over frames of npts (grid sizing)
-  const orbgpu_pose* Tcw;         // kModeLast: [n_frames]
+  const orbgpu_pose* Tcw;         // kModeLast, kModeKeyFrame: [n_frames]
   const orbgpu_pose* Tlw;
   // Rcw (row-major), tcw, Ow per frame, 15 floats: kModeLocalFrustum
   const float* frustum_pose;
@@ -94,6 +100,37 @@ struct ObsLaunch {
 };
 
 hipError_t launch_pose_obs(const ObsLaunch& a, hipStream_t st);
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) over a batch
+// of (key frame, frame) pairs; FeatureVectors as orbgpu_bow_transform_batch
+// writes them (ascending node ids, CSR feature lists).
+struct BowSearchLaunch {
+  int n_frames;
+  float nn_ratio;
+  int check_ori;
+  const uint32_t* kf_nodes;    // [n_frames][kf_stride]
+  const int32_t* kf_off;       // [n_frames][kf_stride + 1]
+  const uint32_t* kf_feat;     // [n_frames][kf_stride]
+  const int* kf_n_nodes;       // [n_frames]
+  const uint8_t* kf_desc;      // [n_frames][kf_stride][32]
+  const float* kf_angle;       // [n_frames][kf_stride]
+  const uint8_t* kf_valid;     // [n_frames][kf_stride]
+  int kf_stride;
+  const uint32_t* f_nodes;     // [n_frames][f_stride]
+  const int32_t* f_off;
+  const uint32_t* f_feat;
+  const int* f_n_nodes;
+  const uint8_t* f_desc;       // [n_frames][f_stride][32]
+  const float* f_angle;        // frame f keypoint k at f_angle[(f * f_stride + k) * angle_step]
+  int angle_step;              // 1 (float array) or 7 (orbgpu_keypoint rows, &kps->angle)
+  const int* f_n;              // keypoints per frame
+  int f_stride;
+  int32_t* match;              // [n_frames][f_stride]
+  int* nmatches;
+  int* err;
+};
+
+hipError_t launch_bow_search(const BowSearchLaunch& a, hipStream_t st);
 
 // Frame::UnprojectStereo over the frames' stereo keypoints -> LastFrame points
 struct UnprojLaunch {

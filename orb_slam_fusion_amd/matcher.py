@@ -12,7 +12,15 @@ for the pinhole rig (Frame::Nleft == -1):
   thFarPoints) (orb_matcher.cc:42-206);
 * ``is_in_frustum(F, points, viewingCosLimit)`` -- Frame::isInFrustum
   (frame.cc:548-603) over Tracking::SearchLocalPoints' loop;
-* ``search_local_points(...)`` -- both in one call (tracking.cc:2626-2690).
+* ``search_local_points(...)`` -- both in one call (tracking.cc:2626-2690);
+* ``SearchByProjection_kf(F, kf_points, kf_angles, th, ORBdist)`` --
+  SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const
+  set<MapPoint*>& sAlreadyFound, th, ORBdist) (orb_matcher.cc:1730-1839), the
+  search of Tracking::Relocalization (tracking.cc:2967-2997);
+* ``SearchByBoW(kf, F)`` -- SearchByBoW(KeyFrame* pKF, Frame& F,
+  vector<MapPoint*>&) (orb_matcher.cc:215-389), the search of
+  Tracking::TrackReferenceKeyFrame and Relocalization (tracking.cc:2043-2067,
+  2904-2926).
 
 ``MatchFrame`` carries the Frame fields the searches read.  Results: match[i]
 per current keypoint (>= 0: mvpMapPoints[i] = that query point; -1:
@@ -171,6 +179,79 @@ class ORBmatcher:
             check(lib().orbgpu_matcher_status(self._h, s, int(reset), ctypes.byref(err)),
                   "orbgpu_matcher_status")
         return err.value
+
+    # -- SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) ---
+    def SearchByProjection_kf(self, F: MatchFrame, kf_points: np.ndarray, kf_angles: np.ndarray,
+                              th: float, ORBdist: int) -> Tuple[int, np.ndarray]:
+        """kf_points: MAP_POINT_DTYPE per key-frame keypoint (MP_SKIP for NULL,
+        bad or already-found points); kf_angles: pKF->mvKeysUn[i].angle;
+        F.claimed: CurrentFrame.mvpMapPoints[i] != NULL; F.pose = Tcw."""
+        kps, desc = _c(F.kps, KEYPOINT_DTYPE), _c(F.desc, np.uint8)
+        pts, ang = _c(kf_points, MAP_POINT_DTYPE), _c(kf_angles, np.float32)
+        cl, Tcw = _c(F.claimed, np.uint8), _c(F.pose, np.float32)
+        n = len(kps)
+        match = np.zeros(max(n, 1), np.int32)
+        nm = ctypes.c_int()
+        cam = Camera(*[float(v) for v in F.cam])
+        check(lib().orbgpu_search_by_projection_kf(
+            self._h, ctypes.byref(F.geom), ctypes.byref(cam), ptr(Tcw), ptr(kps), ptr(desc),
+            ptr(cl), n, ptr(pts), ptr(ang), len(pts), float(th), int(ORBdist),
+            int(self.mbCheckOrientation), ptr(match), ctypes.byref(nm)),
+            "orbgpu_search_by_projection_kf")
+        return nm.value, match[:n]
+
+    def search_kf_batch(self, geom: FrameGeom, cam, Tcw, kps, desc, claimed, n, pts, angles, npts,
+                        th: float, ORBdist: int, match, nmatches, stream=None) -> None:
+        """Device tensors: Tcw float32 [B, 7]; kps [B, K, 7]; desc uint8 [B, K, 32];
+        claimed uint8 [B, K] or None; n int32 [B]; pts uint8 [B, P, 68] (MAP_POINT
+        layout); angles float32 [B, P]; npts int32 [B]; match int32 [B, K];
+        nmatches int32 [B]."""
+        B, K = kps.shape[0], kps.shape[1]
+        c = Camera(*[float(v) for v in cam])
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_search_by_projection_kf_batch(
+                self._h, B, ctypes.byref(geom), ctypes.byref(c), ptr(Tcw), ptr(kps), ptr(desc),
+                ptr(claimed), ptr(n), K, ptr(pts), ptr(angles), ptr(npts), pts.shape[1],
+                float(th), int(ORBdist), int(self.mbCheckOrientation), ptr(match),
+                ptr(nmatches), s), "orbgpu_search_by_projection_kf_batch")
+
+    # -- SearchByBoW(pKF, F, vpMapPointMatches) ----------------------------------
+    def SearchByBoW(self, kf_featvec, kf_desc, kf_angles, kf_valid, f_featvec, f_desc,
+                    f_angles) -> Tuple[int, np.ndarray]:
+        """FeatureVectors as (nodes uint32 ascending, offsets int32 [n + 1],
+        features uint32) -- BowVocabulary.transform's fv output; kf_valid uint8
+        (point present and not bad).  -> (nmatches, match int32 [N_F]: key-frame
+        feature index whose point F's keypoint receives, -1 none)."""
+        kn, ko, kf = (_c(x, t) for x, t in zip(kf_featvec, (np.uint32, np.int32, np.uint32)))
+        fn, fo, ff = (_c(x, t) for x, t in zip(f_featvec, (np.uint32, np.int32, np.uint32)))
+        kd, fd = _c(kf_desc, np.uint8), _c(f_desc, np.uint8)
+        ka, fa = _c(kf_angles, np.float32), _c(f_angles, np.float32)
+        kv = _c(kf_valid, np.uint8)
+        n = len(fd)
+        match = np.zeros(max(n, 1), np.int32)
+        nm = ctypes.c_int()
+        check(lib().orbgpu_search_by_bow(
+            self._h, ptr(kn), ptr(ko), ptr(kf), len(kn), ptr(kd), ptr(ka), ptr(kv), len(kd),
+            ptr(fn), ptr(fo), ptr(ff), len(fn), ptr(fd), ptr(fa), n, self.mfNNratio,
+            int(self.mbCheckOrientation), ptr(match), ctypes.byref(nm)), "orbgpu_search_by_bow")
+        return nm.value, match[:n]
+
+    def search_bow_batch(self, kf_fv, kf_desc, kf_angles, kf_valid, f_fv, f_desc, f_angles, f_n,
+                         match, nmatches, f_angle_step: int = 1, stream=None) -> None:
+        """Device tensors; kf_fv / f_fv = (nodes uint32 [B, S], offsets int32
+        [B, S + 1], features uint32 [B, S], n_nodes int32 [B]) as
+        BowVocabulary.transform_batch fills them; descriptors uint8 [B, S, 32];
+        kf_angles float32 [B, S]; kf_valid uint8 [B, S]; f_angles: float32 [B, S]
+        (step 1) or the frame keypoints' angle column (step 7); f_n int32 [B];
+        match int32 [B, S]; nmatches int32 [B]."""
+        B, KS, FS = kf_desc.shape[0], kf_desc.shape[1], f_desc.shape[1]
+        with launch_stream(stream) as s:
+            check(lib().orbgpu_search_by_bow_batch(
+                self._h, B, ptr(kf_fv[0]), ptr(kf_fv[1]), ptr(kf_fv[2]), ptr(kf_fv[3]),
+                ptr(kf_desc), ptr(kf_angles), ptr(kf_valid), KS, ptr(f_fv[0]), ptr(f_fv[1]),
+                ptr(f_fv[2]), ptr(f_fv[3]), ptr(f_desc), ptr(f_angles), int(f_angle_step),
+                ptr(f_n), FS, self.mfNNratio, int(self.mbCheckOrientation), ptr(match),
+                ptr(nmatches), s), "orbgpu_search_by_bow_batch")
 
     # -- Frame::isInFrustum ---------------------------------------------------
     def is_in_frustum(self, F: MatchFrame, points: np.ndarray, viewingCosLimit: float,

@@ -59,6 +59,7 @@ class MatchCase:
     Rcw: np.ndarray = None
     tcw: np.ndarray = None
     Ow: np.ndarray = None
+    angles: np.ndarray = None  # key-frame keypoint angles (local_case points as a key frame's)
 
 
 def _frame(rng, n_kp, n_levels, stereo, claimed_frac):
@@ -182,9 +183,11 @@ def local_case(seed: int, n_kp: int = 600, n_pts: int = 500, stereo: bool = True
     sf = scale_factors(n_levels)
     pts = np.zeros(n_pts, MAP_POINT_DTYPE)
     targets = rng.integers(0, n_kp, n_pts)
+    aimed = np.zeros(n_pts, np.int64)
     for j in range(n_pts):
         r = rng.uniform()
         i = int(targets[rng.integers(0, j)]) if (r < 0.12 and j > 0) else int(targets[j])
+        aimed[j] = i
         depth = rng.uniform(0.8, 10.0)
         if r > 0.93:
             X = rng.normal(0, 4, 3) + np.array([0, 0, rng.choice([-3.0, 5.0])])
@@ -213,5 +216,68 @@ def local_case(seed: int, n_kp: int = 600, n_pts: int = 500, stereo: bool = True
         pts["desc"][j] = d
     geom = frame_geom(W, H, sf)
     Rcw, tcw, Owf = pose_matrices(Tcw)
+    # the same points read as a key frame's (SearchByProjection(CurrentFrame, pKF, ...)):
+    # its keypoint angles near the aimed keypoint's, 15 % unrelated
+    ra = np.random.default_rng(seed + 1000)
+    ang = (kps["angle"][aimed].astype(np.float64) + ra.normal(0, 4.0, n_pts)) % 360.0
+    wild = ra.uniform(0, 1, n_pts) < 0.15
+    ang[wild] = ra.uniform(0, 360, wild.sum())
     return MatchCase(geom, cam, mb, kps, desc, uright, claimed, Tcw, Tcw.copy(), pts, Rcw, tcw,
-                     Owf)
+                     Owf, ang.astype(np.float32))
+
+
+@dataclass
+class BowCase:
+    kf_fv: dict       # node -> ascending key-frame feature indices (pKF->mFeatVec)
+    f_fv: dict        # node -> ascending frame feature indices (F.mFeatVec)
+    kf_desc: np.ndarray
+    f_desc: np.ndarray
+    kf_angle: np.ndarray
+    f_angle: np.ndarray
+    kf_valid: np.ndarray  # vpMapPointsKF[i] && !isBad()
+
+
+def fv_arrays(fv: dict):
+    """FeatureVector dict -> (nodes ascending, CSR offsets, features)."""
+    nodes = np.array(sorted(fv), np.uint32)
+    off = np.zeros(len(nodes) + 1, np.int32)
+    feats = []
+    for j, nd in enumerate(nodes):
+        feats += list(fv[int(nd)])
+        off[j + 1] = len(feats)
+    return nodes, off, np.array(feats, np.uint32)
+
+
+def bow_case(seed: int, n_kf: int = 600, n_f: int = 650, n_nodes: int = 70, shared: float = 0.8,
+             pair_frac: float = 0.7) -> BowCase:
+    """Two frames' FeatureVectors over a common node space: most nodes shared,
+    key-frame descriptors copied from a frame feature of the same node with
+    0-60 flipped bits (near ties and ratio-test rejections), duplicates
+    aimed at one frame feature (later key-frame features find it taken),
+    orientation outliers, key-frame features without a valid point."""
+    rng = np.random.default_rng(seed)
+    node_ids = np.sort(rng.choice(5000, int(n_nodes * 1.4), replace=False))
+    f_nodes = node_ids[rng.uniform(0, 1, len(node_ids)) < 0.85]
+    kf_nodes = np.array([nd for nd in node_ids if (nd in f_nodes and rng.uniform() < shared)
+                         or (nd not in f_nodes and rng.uniform() < 0.5)])
+    f_of = rng.choice(f_nodes, n_f)
+    f_fv = {}
+    for i in range(n_f):
+        f_fv.setdefault(int(f_of[i]), []).append(i)
+    f_desc = rng.integers(0, 256, (n_f, 32), dtype=np.uint8)
+    f_angle = rng.uniform(0, 360, n_f).astype(np.float32)
+    kf_desc = rng.integers(0, 256, (n_kf, 32), dtype=np.uint8)
+    kf_angle = rng.uniform(0, 360, n_kf).astype(np.float32)
+    kf_of = rng.choice(kf_nodes, n_kf)
+    for i in range(n_kf):
+        nd = int(kf_of[i])
+        if nd in f_fv and rng.uniform() < pair_frac:
+            k = int(rng.choice(f_fv[nd]))
+            kf_desc[i] = _flip(rng, f_desc[k], int(rng.choice([0, 3, 10, 25, 40, 60])))
+            if rng.uniform() < 0.85:
+                kf_angle[i] = np.float32((float(f_angle[k]) + rng.normal(0, 5)) % 360.0)
+    kf_fv = {}
+    for i in range(n_kf):
+        kf_fv.setdefault(int(kf_of[i]), []).append(i)
+    kf_valid = (rng.uniform(0, 1, n_kf) < 0.85).astype(np.uint8)
+    return BowCase(kf_fv, f_fv, kf_desc, f_desc, kf_angle, f_angle, kf_valid)

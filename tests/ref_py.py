@@ -490,6 +490,114 @@ def search_local_py(geom, kps, desc, uright, claimed, pts, views, th, nn):
     return nm, np.array([h if h >= 0 else -1 for h in F.holder], np.int32)
 
 
+def _three_maxima_keep(hist):
+    sizes = [len(h) for h in hist]
+    order = sorted(range(30), key=lambda b: (-sizes[b], b))
+    m1 = sizes[order[0]]
+    keep = {order[0]} if m1 > 0 else set()
+    if m1 > 0 and sizes[order[1]] > 0 and not (_f(sizes[order[1]]) < _f(0.1) * _f(m1)):
+        keep.add(order[1])
+        if sizes[order[2]] > 0 and not (_f(sizes[order[2]]) < _f(0.1) * _f(m1)):
+            keep.add(order[2])
+    return keep
+
+
+def _rot_bin(a_ref, a_cur):
+    rot = _f(_f(a_ref) - _f(a_cur))
+    if rot < 0:
+        rot = _f(rot + _f(360))
+    b = _round(_f(rot * _f(_f(30) / _f(360))))
+    return 0 if b == 30 else b
+
+
+def search_kf_py(geom, cam, Tcw, kps, desc, claimed, pts, angles, th, orb_dist, check_ori):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+    (orb_matcher.cc:1730-1839): every keypoint holding a point is skipped."""
+    import binding as orc  # the restated PredictScale of the oracle (pinned separately)
+
+    F = _PyFrame(geom, kps, desc, None, claimed)
+    fx, fy, cx, cy = (_f(v) for v in cam[:4])
+    q = [-_f(Tcw[0]), -_f(Tcw[1]), -_f(Tcw[2]), _f(Tcw[3])]
+    s = _f(_f(_f(q[0] * q[0]) + _f(q[2] * q[2])) + _f(_f(q[1] * q[1]) + _f(q[3] * q[3])))
+    ln = np.sqrt(s, dtype=np.float32)
+    q = [_f(c / ln) for c in q]
+    Ow = _qrot(q, [-_f(Tcw[4]), -_f(Tcw[5]), -_f(Tcw[6])])
+    hist = [[] for _ in range(30)]
+    nm = 0
+    th = _f(th)
+    for j, P in enumerate(pts):
+        if P["flags"] & 1:
+            continue
+        X = [_f(v) for v in P["Xw"]]
+        Xc = _se3(Tcw, X)
+        u = _f(_f(fx * Xc[0]) / Xc[2] + cx)
+        v = _f(_f(fy * Xc[1]) / Xc[2] + cy)
+        if u < _f(geom.min_x) or u > _f(geom.max_x) or v < _f(geom.min_y) or v > _f(geom.max_y):
+            continue
+        PO = [_f(X[i] - Ow[i]) for i in range(3)]
+        d3 = np.sqrt(_fmaf(PO[2], PO[2], _fmaf(PO[0], PO[0], _f(PO[1] * PO[1]))), dtype=np.float32)
+        if d3 < _f(_f(0.8) * _f(P["min_dist"])) or d3 > _f(_f(1.2) * _f(P["max_dist"])):
+            continue
+        lv = orc.predict_scale(P["max_dist"], d3, geom.log_scale_factor, geom.n_levels)
+        rad = _f(th * _f(geom.scale_factors[lv]))
+        cand = F.area(u, v, rad, lv - 1, lv + 1)
+        best, bi = 256, -1
+        for i in cand:
+            if F.holder[i] != -1:
+                continue
+            d = _popcount_dist(P["desc"], desc[i])
+            if d < best:
+                best, bi = d, i
+        if best <= orb_dist:
+            F.holder[bi], F.hobs[bi] = j, True
+            nm += 1
+            if check_ori:
+                hist[_rot_bin(angles[j], kps["angle"][bi])].append(bi)
+    nulled = set()
+    if check_ori:
+        keep = _three_maxima_keep(hist)
+        for b in range(30):
+            if b not in keep:
+                for i in hist[b]:
+                    F.holder[i] = -1
+                    nulled.add(i)
+                    nm -= 1
+    return nm, np.array([-2 if i in nulled else (h if h >= 0 else -1)
+                         for i, h in enumerate(F.holder)], np.int32)
+
+
+def search_bow_py(kf_fv, kf_desc, kf_angle, kf_valid, f_fv, f_desc, f_angle, nn, check_ori):
+    """SearchByBoW(pKF, F) (orb_matcher.cc:215-389) over two FeatureVectors given
+    as dicts node -> [feature indices]: the common nodes in ascending order."""
+    match = [-1] * len(f_desc)
+    hist = [[] for _ in range(30)]
+    nm = 0
+    for node in sorted(set(kf_fv) & set(f_fv)):
+        for ik in kf_fv[node]:
+            if not kf_valid[ik]:
+                continue
+            ranked = [(_popcount_dist(kf_desc[ik], f_desc[i]), pos, i)
+                      for pos, i in enumerate(f_fv[node]) if match[i] < 0]
+            if not ranked:
+                continue
+            ranked.sort()
+            d1, _, i1 = ranked[0]
+            d2 = ranked[1][0] if len(ranked) > 1 else 256
+            if d1 <= 50 and _f(d1) < _f(_f(nn) * _f(d2)):
+                match[i1] = ik
+                nm += 1
+                if check_ori:
+                    hist[_rot_bin(kf_angle[ik], f_angle[i1])].append(i1)
+    if check_ori:
+        keep = _three_maxima_keep(hist)
+        for b in range(30):
+            if b not in keep:
+                for i in hist[b]:
+                    match[i] = -1
+                    nm -= 1
+    return nm, np.array(match, np.int32)
+
+
 # --- DBoW2 transform (TemplatedVocabulary.h:1057-1179) -----------------------
 def load_vocab_py(path):
     """loadFromTextFile restated in Python: nodes as dicts."""

@@ -142,3 +142,55 @@ def test_gcc_contraction_pattern(tmp_path):
     assert fn["_Z2abffff"] == ["vmulss", "vfmsub132ss"]             # fma(a, b, -(c*d))
     assert fn["_Z2rcffff"] == ["vfmadd132ss", "vaddss"]             # fma(w, u, p) + c
     assert fn["_Z2urfff"] == ["vfnmadd231ss"]                       # fma(-bf, iz, u)
+
+
+@pytest.mark.parametrize("seed,th,orb_dist,ori", [(31, 10, 100, True), (32, 3, 64, True),
+                                                  (33, 10, 100, False), (34, 15, 50, True)])
+def test_search_kf_matches_python(seed, th, orb_dist, ori):
+    """Relocalization's SearchByProjection(CurrentFrame, pKF, sAlreadyFound,
+    th, ORBdist) (orb_matcher.cc:1730-1839) vs the independent restatement."""
+    from ref_py import search_kf_py
+    from match_cases import local_case
+
+    c = local_case(seed, n_kp=250, n_pts=220)
+    nm, m = orc.search_kf(c.geom, c.cam, c.Tcw, c.kps, c.desc, c.claimed, c.pts, c.angles, th,
+                          orb_dist, ori)
+    nm_py, m_py = search_kf_py(c.geom, c.cam, c.Tcw, c.kps, c.desc, c.claimed, c.pts, c.angles,
+                               th, orb_dist, ori)
+    assert nm == nm_py
+    np.testing.assert_array_equal(m, m_py)
+    assert nm > 20
+    if ori:
+        assert (m == -2).any()  # the rotation check removed some
+
+
+@pytest.mark.parametrize("seed,nn,ori", [(41, 0.75, True), (42, 0.7, True), (43, 0.9, False),
+                                         (44, 0.6, True)])
+def test_search_bow_matches_python(seed, nn, ori):
+    """SearchByBoW(pKF, F) (orb_matcher.cc:215-389) vs the independent restatement."""
+    from ref_py import search_bow_py
+    from match_cases import bow_case, fv_arrays
+
+    c = bow_case(seed)
+    nm, m = orc.search_bow(fv_arrays(c.kf_fv), c.kf_desc, c.kf_angle, c.kf_valid,
+                           fv_arrays(c.f_fv), c.f_desc, c.f_angle, nn, ori)
+    nm_py, m_py = search_bow_py(c.kf_fv, c.kf_desc, c.kf_angle, c.kf_valid, c.f_fv, c.f_desc,
+                                c.f_angle, nn, ori)
+    assert nm == nm_py
+    np.testing.assert_array_equal(m, m_py)
+    assert nm > 50
+    assert (m >= 0).sum() == nm
+
+
+def test_search_bow_disjoint_and_empty():
+    from match_cases import bow_case, fv_arrays
+
+    c = bow_case(45)
+    empty = (np.zeros(0, np.uint32), np.zeros(1, np.int32), np.zeros(0, np.uint32))
+    nm, m = orc.search_bow(empty, c.kf_desc, c.kf_angle, c.kf_valid, fv_arrays(c.f_fv), c.f_desc,
+                           c.f_angle, 0.75, True)
+    assert nm == 0 and (m == -1).all()
+    shifted = {k + 100000: v for k, v in c.f_fv.items()}  # no common node
+    nm, m = orc.search_bow(fv_arrays(c.kf_fv), c.kf_desc, c.kf_angle, c.kf_valid,
+                           fv_arrays(shifted), c.f_desc, c.f_angle, 0.75, True)
+    assert nm == 0 and (m == -1).all()
