@@ -1,7 +1,8 @@
-// ORBmatcher projection searches over the gfx950 C ABI.
-// Compiled inside the reference build (its include paths: frame.h, mappoint.h,
-// orb_matcher.h, Sophus, Eigen); the original definitions in orb_matcher.cc
-// (:42-206 and :1518-1728) are guarded with ORBGPU_MATCH.
+// ORBmatcher searches over the gfx950 C ABI.
+// Compiled inside the reference build (its include paths: frame.h, keyframe.h,
+// mappoint.h, orb_matcher.h, DBoW2, Sophus, Eigen); the original definitions
+// in orb_matcher.cc (:42-206, :215-389, :1518-1728 and :1730-1839) are guarded
+// with ORBGPU_MATCH.
 // Same reads and writes as the reference for the pinhole rig (Nleft == -1):
 //   SearchByProjection(CurrentFrame, LastFrame, th, bMono): LastFrame's
 //     non-outlier map points (GetWorldPos, GetDescriptor, Observations),
@@ -12,13 +13,22 @@
 //     points' tracking fields written by Frame::isInFrustum (mbTrackInView,
 //     mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mTrackDepth), isBad,
 //     Observations, GetDescriptor; F as above.
+//   SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist): the key
+//     frame's points (isBad, GetWorldPos, min/max distance, GetDescriptor),
+//     pKF->mvKeysUn angles; CurrentFrame's pose, keypoints, descriptors,
+//     mvpMapPoints (read: every held keypoint is skipped; written).
+//   SearchByBoW(pKF, F, vpMapPointMatches): both mFeatVec, descriptors, the
+//     key frame's points (isBad) and mvKeysUn angles, F.mvKeys angles.
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <vector>
 
+#include <set>
+
 #include "cam/orb_feature/orb_matcher.h"
 #include "map/frame.h"
+#include "map/keyframe.h"
 #include "map/mappoint.h"
 #include "orbgpu.h"
 
@@ -65,6 +75,34 @@ std::vector<uint8_t> claimed_mask(const Frame &F) {
 }
 
 void copy_desc(const cv::Mat &d, uint8_t out[32]) { std::memcpy(out, d.ptr<uint8_t>(0), 32); }
+
+// mfMinDistance / mfMaxDistance under mMutexPos, as MapPoint::PredictScale and
+// GetMin/MaxDistanceInvariance read them (mappoint.cc:524-563).  They are
+// protected members without getters; a member pointer taken through a
+// derived class names them without touching the reference's header.
+struct MapPointDistances : MapPoint {
+  static void read(MapPoint *p, float &min_d, float &max_d) {
+    static constexpr float MapPoint::*kMin = &MapPointDistances::mfMinDistance;
+    static constexpr float MapPoint::*kMax = &MapPointDistances::mfMaxDistance;
+    static constexpr std::mutex MapPoint::*kMutex = &MapPointDistances::mMutexPos;
+    std::unique_lock<std::mutex> lock(p->*kMutex);
+    min_d = p->*kMin;
+    max_d = p->*kMax;
+  }
+};
+
+// DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>) as CSR arrays
+struct FeatVecArrays {
+  std::vector<uint32_t> nodes, features;
+  std::vector<int32_t> offsets{0};
+  explicit FeatVecArrays(const DBoW2::FeatureVector &fv) {
+    for (const auto &kv : fv) {
+      nodes.push_back(kv.first);
+      features.insert(features.end(), kv.second.begin(), kv.second.end());
+      offsets.push_back((int32_t)features.size());
+    }
+  }
+};
 
 }  // namespace
 
@@ -149,6 +187,78 @@ int ORBmatcher::SearchByProjection(Frame &F, const std::vector<MapPoint *> &vpMa
     throw std::runtime_error("orbgpu_search_by_projection_local failed");
   for (int i = 0; i < F.N; ++i)
     if (match[i] >= 0) F.mvpMapPoints[i] = who[match[i]];
+  return nmatches;
+}
+
+int ORBmatcher::SearchByProjection(Frame &CurrentFrame, KeyFrame *pKF,
+                                   const std::set<MapPoint *> &sAlreadyFound, const float th,
+                                   const int ORBdist) {
+  if (CurrentFrame.Nleft != -1)
+    throw std::logic_error("orbgpu SearchByProjection: fisheye rig not supported");
+  const std::vector<MapPoint *> vpMPs = pKF->GetMapPointMatches();
+  std::vector<orbgpu_map_point> pts(vpMPs.size());
+  std::vector<float> angles(vpMPs.size());
+  for (size_t i = 0; i < vpMPs.size(); ++i) {
+    MapPoint *pMP = vpMPs[i];
+    orbgpu_map_point &p = pts[i];
+    p = orbgpu_map_point{};
+    angles[i] = pKF->mvKeysUn[i].angle;
+    if (!pMP || pMP->isBad() || sAlreadyFound.count(pMP)) {
+      p.flags = ORBGPU_MP_SKIP;
+      continue;
+    }
+    const Eigen::Vector3f X = pMP->GetWorldPos();
+    p.Xw[0] = X[0], p.Xw[1] = X[1], p.Xw[2] = X[2];
+    MapPointDistances::read(pMP, p.min_dist, p.max_dist);
+    copy_desc(pMP->GetDescriptor(), p.desc);
+  }
+  const orbgpu_frame_geom g = frame_geom(CurrentFrame);
+  const orbgpu_camera cam{CurrentFrame.fx, CurrentFrame.fy, CurrentFrame.cx, CurrentFrame.cy,
+                          CurrentFrame.bf_};
+  const orbgpu_pose Tcw = to_pose(CurrentFrame.GetPose());
+  std::vector<uint8_t> claimed(CurrentFrame.N);  // every held keypoint is skipped (:1791)
+  for (int i = 0; i < CurrentFrame.N; ++i) claimed[i] = CurrentFrame.mvpMapPoints[i] != NULL;
+  std::vector<int32_t> match(CurrentFrame.N);
+  int nmatches = 0;
+  if (orbgpu_search_by_projection_kf(
+          thread_matcher(), &g, &cam, &Tcw,
+          reinterpret_cast<const orbgpu_keypoint *>(CurrentFrame.mvKeysUn.data()),
+          CurrentFrame.mDescriptors.ptr<uint8_t>(0), claimed.data(), CurrentFrame.N, pts.data(),
+          angles.data(), (int)pts.size(), th, ORBdist, mbCheckOrientation, match.data(),
+          &nmatches) != ORBGPU_OK)
+    throw std::runtime_error("orbgpu_search_by_projection_kf failed");
+  for (int i = 0; i < CurrentFrame.N; ++i) {
+    if (match[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[match[i]];
+    else if (match[i] == -2) CurrentFrame.mvpMapPoints[i] = static_cast<MapPoint *>(NULL);
+  }
+  return nmatches;
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame *pKF, Frame &F, std::vector<MapPoint *> &vpMapPointMatches) {
+  if (F.Nleft != -1 || pKF->cam2_)
+    throw std::logic_error("orbgpu SearchByBoW: fisheye rig not supported");
+  const std::vector<MapPoint *> vpMapPointsKF = pKF->GetMapPointMatches();
+  vpMapPointMatches = std::vector<MapPoint *>(F.N, static_cast<MapPoint *>(NULL));
+  const FeatVecArrays kfv(pKF->mFeatVec), ffv(F.mFeatVec);
+  const int nk = (int)vpMapPointsKF.size();
+  std::vector<uint8_t> valid(nk);
+  std::vector<float> ka(nk), fa(F.N);
+  for (int i = 0; i < nk; ++i) {
+    valid[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad();
+    ka[i] = pKF->mvKeysUn[i].angle;
+  }
+  for (int i = 0; i < F.N; ++i) fa[i] = F.mvKeys[i].angle;
+  std::vector<int32_t> match(F.N);
+  int nmatches = 0;
+  if (orbgpu_search_by_bow(thread_matcher(), kfv.nodes.data(), kfv.offsets.data(),
+                           kfv.features.data(), (int)kfv.nodes.size(),
+                           pKF->mDescriptors.ptr<uint8_t>(0), ka.data(), valid.data(), nk,
+                           ffv.nodes.data(), ffv.offsets.data(), ffv.features.data(),
+                           (int)ffv.nodes.size(), F.mDescriptors.ptr<uint8_t>(0), fa.data(), F.N,
+                           mfNNratio, mbCheckOrientation, match.data(), &nmatches) != ORBGPU_OK)
+    throw std::runtime_error("orbgpu_search_by_bow failed");
+  for (int i = 0; i < F.N; ++i)
+    if (match[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[match[i]];
   return nmatches;
 }
 
