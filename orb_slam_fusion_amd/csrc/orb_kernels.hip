@@ -451,27 +451,40 @@ __device__ __forceinline__ ushort2_t max2(ushort2_t a, ushort2_t b) {
 }
 
 // S(p) for the pixel at p (ROI bytes, row stride ls), clamped below at 0.
-// Dark and bright arcs run together: x_k = (sat(v - p_k), sat(p_k - v)), and the
-// saturation is exact wherever S >= 0 (min/max commute with it).
+// Dark and bright arcs run together as a packed f16 pair: a byte b becomes the
+// f16 1024 + b (bit pattern 0x6400 | b, ulp 1 on [1024, 2048)), so
+// x_k = (v - p_k, p_k - v) is exact, and the 9-arc minima and their maximum
+// are v_pk_minimum3_f16 / v_pk_maximum3_f16 on exact integers:
+// m3_k = min(x_k..x_k+2), arc_k = min(m3_k, m3_k+3, m3_k+6), 40 packed ops.
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2_t hmin3(half2_t a, half2_t b, half2_t c) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+__device__ __forceinline__ half2_t hmax3(half2_t a, half2_t b, half2_t c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
 __device__ __forceinline__ int fast_score(const uint8_t* p, int ls) {
   constexpr int cx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
   constexpr int cy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-  const uint32_t v = p[0];
-  ushort2_t x[16];
+  const uint32_t vb = (uint32_t)p[0] | 0x64006400u;
+  half2_t x[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const ushort2_t r = as_us2(v | ((uint32_t)p[cx[k] + cy[k] * ls] << 16));
-    x[k] = sub_sat2(r, r.yx);
+    // (vb.b0, 0x64, p_k, 0x64): one v_perm_b32
+    const half2_t r = __builtin_bit_cast(
+        half2_t, __builtin_amdgcn_perm((uint32_t)p[cx[k] + cy[k] * ls], vb, 0x03040100u));
+    x[k] = r - r.yx;
   }
-  ushort2_t m2[16], m4[16];
+  half2_t m3[16], a[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) m2[k] = min2(x[k], x[(k + 1) & 15]);
+  for (int k = 0; k < 16; ++k) m3[k] = hmin3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) m4[k] = min2(m2[k], m2[(k + 2) & 15]);
-  ushort2_t best = as_us2(0u);
+  for (int k = 0; k < 16; ++k) a[k] = hmin3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+  half2_t b = hmax3(a[0], a[1], a[2]);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) best = max2(best, min2(min2(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]));
-  return max((int)max(best.x, best.y) - 1, 0);
+  for (int k = 3; k < 15; k += 2) b = hmax3(b, a[k], a[k + 1]);
+  b = __builtin_elementwise_maximum(b, a[15]);
+  return max((int)__builtin_fmaxf((float)b.x, (float)b.y) - 1, 0);
 }
 
 // compass value of 4 pixels (two u16 pairs): corner at th => value > th
@@ -540,11 +553,12 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         uint32_t v[kFastPf];
 #pragma unroll
         for (int u = 0; u < kFastPf; ++u)
-          v[u] = *reinterpret_cast<const uint32_t*>(Sa + (uint32_t)(min(r0 + 4 * (k0 + u), c.rows - 1) * sp + 4 * qa));
+          v[u] = *reinterpret_cast<const uint32_t*>(
+              Sa + __umul24((uint32_t)min(r0 + 4 * (k0 + u), c.rows - 1), (uint32_t)sp) + 4 * qa);
 #pragma unroll
         for (int u = 0; u < kFastPf; ++u) {
           const int r = r0 + 4 * (k0 + u);
-          if (qv && r < c.rows) *reinterpret_cast<uint32_t*>(roi + r * ls + 4 * q) = v[u];
+          if (qv && r < c.rows) *reinterpret_cast<uint32_t*>(roi + __umul24((uint32_t)r, (uint32_t)ls) + 4 * q) = v[u];
         }
       }
     } else {
@@ -574,7 +588,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     const ushort2_t th2 = as_us2((uint32_t)th * 0x10001u);
     int ns = 0;
     for (int r = g_r0, g = g_q0; __builtin_amdgcn_ballot_w64(r < dh) != 0;) {
-      const uint8_t* C = roi + (min(r, dh - 1) + 3) * ls + 4 * g;
+      const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 4 * g;
       auto win = [&](const uint8_t* row, int o) {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (o & ~3));
         return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
@@ -606,7 +620,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     STAMP(0);
     for (int j = lane; j < ns; j += 64) {
       const int i = sv[j];
-      const int s = fast_score(base + (i >> 7) * ls + (i & 127), ls);
+      const int s = fast_score(base + __umul24((uint32_t)i >> 7, (uint32_t)ls) + (i & 127), ls);
       sc[sci(i)] = (uint8_t)(s >= th ? s : 0);
     }
     __syncthreads();
