@@ -191,6 +191,15 @@ orbgpu_status orbgpu_pose_opt_batch(orbgpu_pose_ctx* c, const orbgpu_camera* cam
                                     orbgpu_pose* d_Tcw_out, uint8_t* d_outlier, int* d_inliers,
                                     double* d_pose_out_d, void* hip_stream);
 
+/* Speculative LM trials: g2o retries a rejected step with lambda *= ni,
+ * ni *= 2 on the same system, so `groups` (1 or 2) trial sweeps of an
+ * iteration can run side by side, the outcomes scanned in trial order (same
+ * path).  Defaults 1 / 1; the sweeps are issue-bound inside one CU, so two
+ * groups cut the serial trial rounds (42.6 -> 28.9 per problem) but not the
+ * time -- kept as an option. */
+orbgpu_status orbgpu_pose_ctx_set_trial_groups(orbgpu_pose_ctx* c, int groups_single,
+                                               int groups_batch);
+
 /* ------------------------------------------------------------------------
  * LocalBundleAdjustment -- replaces the solve of
  * Optimizer::LocalBundleAdjustment(KeyFrame*, bool* pbStopFlag, Map*, int&,

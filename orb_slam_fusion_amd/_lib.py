@@ -179,6 +179,7 @@ SIGNATURES = {
     "orbgpu_extractor_profile": (_I, [_P, _I]),
     "orbgpu_extractor_profile_read": (_I, [_P, _P]),
     "orbgpu_pose_ctx_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
+    "orbgpu_pose_ctx_set_trial_groups": (_I, [_P, _I, _I]),
     "orbgpu_pose_ctx_destroy": (None, [_P]),
     "orbgpu_pose_opt": (_I, [_P, ctypes.POINTER(Camera), _P, _P, _I, _P, _P, _P]),
     "orbgpu_pose_opt_batch": (

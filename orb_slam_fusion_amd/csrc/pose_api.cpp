@@ -1,6 +1,7 @@
 // C-ABI implementation of the pose-only optimisation half of include/orbgpu.h.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <new>
 
 #include "../../include/orbgpu.h"
@@ -9,7 +10,7 @@ namespace orbgpu {
 hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const void* d_obs,
                            const int* d_nobs, int obs_stride, int n_problems, float* d_pose_out,
                            uint8_t* d_outlier, int* d_inliers, double* d_pose_out_d,
-                           hipStream_t st);
+                           hipStream_t st, int groups);
 }
 
 static_assert(sizeof(orbgpu_pose) == 7 * sizeof(float), "orbgpu_pose layout");
@@ -23,6 +24,10 @@ struct orbgpu_pose_ctx {
   float* d_pose = nullptr;  // in[7], out[7]
   uint8_t* d_outlier = nullptr;
   int* d_ints = nullptr;  // n, inliers
+  // speculative LM trial groups per problem (k_pose_opt), see
+  // orbgpu_pose_ctx_set_trial_groups
+  int groups_single = 1;
+  int groups_batch = 1;
 };
 
 extern "C" {
@@ -36,6 +41,10 @@ orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
   if (!c) return ORBGPU_ERR_NOMEM;
   c->device = device;
   c->max_obs = max_obs;
+  if (const char* e = getenv("ORBGPU_POSE_GROUPS")) {  // A/B runs (tools/pose_ab.sh)
+    const int g = atoi(e);
+    if (g == 1 || g == 2) c->groups_single = c->groups_batch = g;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_obs, sizeof(orbgpu_pose_obs) * max_obs) != hipSuccess ||
       hipMalloc(&c->d_pose, sizeof(float) * 14) != hipSuccess ||
@@ -45,6 +54,15 @@ orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
     return ORBGPU_ERR_DEVICE;
   }
   *out = c;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_pose_ctx_set_trial_groups(orbgpu_pose_ctx* c, int groups_single,
+                                               int groups_batch) {
+  auto valid = [](int g) { return g == 1 || g == 2; };
+  if (!c || !valid(groups_single) || !valid(groups_batch)) return ORBGPU_ERR_INVALID;
+  c->groups_single = groups_single;
+  c->groups_batch = groups_batch;
   return ORBGPU_OK;
 }
 
@@ -76,7 +94,8 @@ orbgpu_status orbgpu_pose_opt(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
       hipMemcpyAsync(c->d_ints, ints, sizeof(int), hipMemcpyHostToDevice, c->stream))
     return ORBGPU_ERR_DEVICE;
   if (orbgpu::launch_pose_opt(cd, c->d_pose, c->d_obs, c->d_ints, c->max_obs, 1, c->d_pose + 7,
-                              c->d_outlier, c->d_ints + 1, nullptr, c->stream) != hipSuccess)
+                              c->d_outlier, c->d_ints + 1, nullptr, c->stream,
+                              c->groups_single) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
   if (hipMemcpyAsync(Tcw_out, c->d_pose + 7, sizeof(orbgpu_pose), hipMemcpyDeviceToHost,
                      c->stream) ||
@@ -102,7 +121,7 @@ orbgpu_status orbgpu_pose_opt_batch(orbgpu_pose_ctx* c, const orbgpu_camera* cam
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   if (orbgpu::launch_pose_opt(cd, reinterpret_cast<const float*>(d_Tcw_in), d_obs, d_nobs,
                               obs_stride, n_problems, reinterpret_cast<float*>(d_Tcw_out),
-                              d_outlier, d_inliers, d_pose_out_d, s) != hipSuccess)
+                              d_outlier, d_inliers, d_pose_out_d, s, c->groups_batch) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
   return ORBGPU_OK;
 }

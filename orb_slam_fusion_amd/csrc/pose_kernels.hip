@@ -1,11 +1,13 @@
-// gfx950 PoseOptimization: one 256-thread workgroup runs a whole problem --
-// Optimizer::PoseOptimization (optimizer.cc:762-1051): 4 outlier-rejection
-// rounds x g2o Levenberg-Marquardt (optimization_algorithm_levenberg.cpp:59-168)
-// over unary SE3 edges, dense 6x6 LDLT.  The working set (< 40 KB) stays on
-// chip; edges are swept by all lanes, per-sweep sums use a fixed reduction
-// tree (deterministic), the 6x6 solve and the se3 exp run on lane 0.  The
-// pass is latency-bound (40+ dependent sweeps), so problems are batched one
-// workgroup each.
+// gfx950 PoseOptimization: one workgroup (G x 256 threads) runs a whole
+// problem -- Optimizer::PoseOptimization (optimizer.cc:762-1051): 4
+// outlier-rejection rounds x g2o Levenberg-Marquardt
+// (optimization_algorithm_levenberg.cpp:59-168) over unary SE3 edges, dense
+// 6x6 LDLT.  The working set (< 40 KB) stays on chip; edges are swept by all
+// lanes (stereo observations first, so waves take one projection branch),
+// per-sweep sums use a fixed reduction tree (deterministic), the 6x6 solve is
+// lane-parallel per wave.  The pass is a chain of 60+ dependent sweeps that
+// keep one CU's SIMDs issuing (4 waves), so problems are batched one
+// workgroup each; G = 2 evaluates consecutive LM trials side by side.
 //
 // Per-edge errors are not stored: g2o's classification reads the error of the
 // last computeActiveErrors() (possibly at a rejected trial pose), so the
@@ -61,7 +63,7 @@ struct CamDev {
   double fx, fy, cx, cy, bf;
 };
 
-constexpr int kPoseThreads = 256;
+constexpr int kPoseThreads = 256;  // threads per trial group
 constexpr int kPoseWaves = kPoseThreads / 64;
 
 __device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3& T, const CamDev& c,
@@ -155,33 +157,14 @@ __device__ __forceinline__ double uniform_f64(double v) {  // wave-uniform value
                           __builtin_amdgcn_readfirstlane(__double2loint(v)));
 }
 
-// Block-wide sum of NV doubles per thread (fixed tree: DPP wave sums, then the
-// wave partials in wave order).  Result broadcast to every thread.
-template <int NV>
-__device__ __forceinline__ void block_sum_d(double (&v)[NV], double* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = wave_sum_to_lane63(v[k]);
-  if (lane == 63)
-#pragma unroll
-    for (int k = 0; k < NV; ++k) red[wave * NV + k] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double a = red[k];
-#pragma unroll
-    for (int w = 1; w < kPoseWaves; ++w) a += red[w * NV + k];
-    v[k] = uniform_f64(a);
-  }
-  __syncthreads();
-}
-
 // Block-wide sums of NV doubles per thread into LDS (out[0..NV)), fixed tree:
-// DPP row sums (lane 15 of each 16-lane row), the 16 row partials of the
-// block in LDS, then thread k adds value k's partials in row order.  Only
-// LDS consumers need the result (the build sweep's system): no broadcast.
-template <int NV>
-__device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, double* out) {
+// DPP row sums (lane 15 of each 16-lane row), the 4 NW row partials of the
+// block in LDS, then (NW == 4) thread k adds value k's 16 partials in row
+// order, or (NW > 4) 16-row slices first, the slices next.  Only LDS
+// consumers need the result (the build sweep's system): no broadcast.
+template <int NV, int NW>
+__device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, double* red2,
+                                                 double* out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -196,30 +179,62 @@ __device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, d
 #pragma unroll
     for (int k = 0; k < NV; ++k) red[(wave * 4 + (lane >> 4)) * NV + k] = v[k];
   __syncthreads();
-  if (threadIdx.x < NV) {
-    double a = 0;
+  if constexpr (NW == 4) {
+    if (threadIdx.x < NV) {
+      double a = 0;
 #pragma unroll
-    for (int r = 0; r < kPoseWaves * 4; ++r) a += red[r * NV + threadIdx.x];
-    out[threadIdx.x] = a;
+      for (int r = 0; r < 16; ++r) a += red[r * NV + threadIdx.x];
+      out[threadIdx.x] = a;
+    }
+  } else {
+    constexpr int S = NW / 4;  // 16-row slices
+    if (threadIdx.x < NV * S) {
+      const int k = threadIdx.x % NV, sl = threadIdx.x / NV;
+      double a = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a += red[(16 * sl + r) * NV + k];
+      red2[sl * NV + k] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+      double a = red2[threadIdx.x];
+#pragma unroll
+      for (int sl = 1; sl < S; ++sl) a += red2[sl * NV + threadIdx.x];
+      out[threadIdx.x] = a;
+    }
   }
   __syncthreads();
 }
 
+__device__ __forceinline__ unsigned mbcnt64(uint64_t m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <int NW>
 __device__ __forceinline__ int block_sum_i(int v, int* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   int r = 0;
 #pragma unroll
-  for (int w = 0; w < kPoseWaves; ++w) r += red[w];
+  for (int w = 0; w < NW; ++w) r += red[w];
   __syncthreads();
   return r;
 }
 
+// G trial groups of kPoseThreads threads each.  The build sweep and the
+// classification use the whole block; the LM trials of an iteration are
+// evaluated G at a time (see k_pose_opt).
+template <int G>
 struct PoseShared {
-  double red[kPoseWaves * 4 * 28];
-  double hb[28];  // chi2, H (lower, 21), b (6) at the current pose
-  int ired[kPoseWaves];
+  double red[G * kPoseWaves * 4 * 28];
+  double red2[G * 28];
+  double hb[28];                        // chi2, H (lower, 21), b (6) at the current pose
+  double chi[2][G][kPoseWaves];         // trial chi2 wave partials, double-buffered by round
+  double trial[2][G][14];               // x (6), Tn (qx qy qz qw t0 t1 t2), ok
+  double init[7];                       // the input pose (qx qy qz qw t0 t1 t2)
+  int ired[G * kPoseWaves];
+  int pcnt[2][G * kPoseWaves];          // observation partition: stereo / mono per wave
 };
 
 constexpr int kPoseLdsObs = 4096;  // observations staged in LDS (the rest re-read from HBM)
@@ -263,13 +278,28 @@ __device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3& 
   }
 }
 
-__global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
+// One workgroup of G x 256 threads per problem.  g2o's inner LM loop
+// (optimization_algorithm_levenberg.cpp:83-150) retries a rejected step with
+// lambda *= ni, ni *= 2 and the same system, so the trial sequence of an
+// iteration is known up front: group g evaluates trial q + g (its own LDLT,
+// exp and chi2 sweep -- the same thread-to-edge map and reduction tree as a
+// single group, so every trial's chi2 is the value the sequential loop would
+// compute), then every thread scans the G outcomes in trial order and stops
+// where the sequential loop would have.  Same path, G-fold fewer serial
+// trial sweeps on rejection runs.  The build sweep spreads over all G x 256
+// threads.
+template <int G>
+__global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     CamDev cam, const float* __restrict__ pose_in, const PoseObsDev* __restrict__ obs_all,
     const int* __restrict__ nobs, int obs_stride, float* __restrict__ pose_out,
     uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d,
     int lds_obs) {
-  __shared__ PoseShared sh;
+  constexpr int NT = kPoseThreads * G, NW = NT / 64;
+  constexpr int kB = G == 1 ? 3 : 1;  // build-sweep edges in flight per thread
+  __shared__ PoseShared<G> sh;
   const int p = blockIdx.x, t = threadIdx.x;
+  const int grp = __builtin_amdgcn_readfirstlane(t >> 8), tg = t & (kPoseThreads - 1);
+  const int lane = t & 63, gw = (t >> 6) & (kPoseWaves - 1);
   const int n = nobs[p];
   const PoseObsDev* obs = obs_all + (size_t)p * obs_stride;
   uint8_t* level = outlier_all + (size_t)p * obs_stride;
@@ -280,40 +310,77 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     return;
   }
   // observations (and their levels) live in LDS for the whole call: one
-  // HBM read; only n > cap falls back to re-reading per sweep
+  // HBM read; only n > cap falls back to re-reading per sweep.  They are
+  // stored as a stable partition, stereo first (pm[slot] = observation
+  // index): a wave's 64 consecutive slots then take one projection branch
+  // (EdgeStereo / EdgeMono) instead of both.  Only the order of the
+  // per-thread partial sums changes.
   extern __shared__ __attribute__((aligned(16))) uint8_t pose_lds[];
   const int cap = min(n, lds_obs);
   PoseObsDev* ob = reinterpret_cast<PoseObsDev*>(pose_lds);
   uint8_t* lv = pose_lds + (size_t)lds_obs * sizeof(PoseObsDev);
-  for (int i = t; i < cap; i += kPoseThreads) {
-    ob[i] = obs[i];
-    lv[i] = 0;
+  uint16_t* pm = reinterpret_cast<uint16_t*>(lv + ((lds_obs + 1) & ~1));
+  {
+    int c = 0;
+    for (int i = t; i < cap; i += NT) c += obs[i].ur >= 0.f ? 1 : 0;
+    const int n_st = block_sum_i<NW>(c, sh.ired);
+    const int w = t >> 6;
+    int base_s = 0, base_m = n_st;
+    for (int i0 = 0; i0 < cap; i0 += NT) {
+      const int i = i0 + t;
+      const bool in = i < cap;
+      float o[7];  // PoseObsDev as 7 floats (no aggregate copy through scratch)
+#pragma unroll
+      for (int k = 0; k < 7; ++k) o[k] = reinterpret_cast<const float*>(obs + min(i, cap - 1))[k];
+      const bool st = in && o[5] >= 0.f;  // ur
+      const uint64_t bs = __ballot(st), bm = __ballot(in && !st);
+      if (lane == 0) {
+        sh.pcnt[0][w] = __popcll(bs);
+        sh.pcnt[1][w] = __popcll(bm);
+      }
+      __syncthreads();
+      int ps = 0, pmn = 0, ts = 0, tm = 0;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) {
+        const int a = sh.pcnt[0][v], b = sh.pcnt[1][v];
+        ps += v < w ? a : 0;
+        pmn += v < w ? b : 0;
+        ts += a;
+        tm += b;
+      }
+      if (in) {
+        const int pos = st ? base_s + ps + (int)mbcnt64(bs) : base_m + pmn + (int)mbcnt64(bm);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) reinterpret_cast<float*>(ob + pos)[k] = o[k];
+        lv[pos] = 0;
+        pm[pos] = (uint16_t)i;
+      }
+      base_s += ts;
+      base_m += tm;
+      __syncthreads();
+    }
   }
-  for (int i = cap + t; i < n; i += kPoseThreads) level[i] = 0;
-  Se3 init{0, 0, 0, 1, {0, 0, 0}};
-  init.qx = pin[0];
-  init.qy = pin[1];
-  init.qz = pin[2];
-  init.qw = pin[3];
-  init.t[0] = pin[4];
-  init.t[1] = pin[5];
-  init.t[2] = pin[6];
+  for (int i = cap + t; i < n; i += NT) level[i] = 0;
+  if (t < 7) sh.init[t] = pin[t];
+  // poses kept in LDS and re-read where needed (register pressure)
+  auto pose_at = [&](const double* a) { return Se3{a[0], a[1], a[2], a[3], {a[4], a[5], a[6]}}; };
   const double dmono = (double)(float)sqrt(5.991);  // `const float deltaMono = sqrt(5.991)`
   const double dstereo = (double)(float)sqrt(7.815);
   bool robust = true;
   int nbad_round = 0;
-  Se3 T = init;
+  Se3 T;
   __syncthreads();
   PSTAMP_INIT;
 
-  // computeActiveErrors at pose X (robust chi2, block-reduced).  A thread's
-  // edges i = t + 256 j are taken three at a time: their chains are
-  // independent (ILP), the accumulation stays in edge order.
-  constexpr int kU = 3;
-  auto chi_sweep = [&](const Se3& X) -> double {
+  // computeActiveErrors at pose X (robust chi2) by this thread's group: a
+  // thread's edges i = tg + 256 j are taken three at a time (independent
+  // chains, ILP), the accumulation stays in edge order; the wave sums land in
+  // dst[wave of the group] (added in wave order by the readers).
+  constexpr int kU = 3;  // (ILP only: the sums are the same for any kU)
+  auto chi_sweep = [&](const Se3& X, double* dst) {
     double acc[28];
     acc[0] = 0;
-    for (int i0 = t; i0 < cap; i0 += kU * kPoseThreads) {
+    for (int i0 = tg; i0 < cap; i0 += kU * kPoseThreads) {
       PoseObsDev o[kU];
       bool live[kU];
 #pragma unroll
@@ -332,35 +399,38 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       for (int u = 0; u < kU; ++u)
         if (live[u]) acc[0] += part[u][0];
     }
-    for (int i = cap + t; i < n; i += kPoseThreads)
+    for (int i = cap + tg; i < n; i += kPoseThreads)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, false, acc);
-    double r[1] = {acc[0]};
-    block_sum_d<1>(r, sh.red);
-    return r[0];
+    const double s = wave_sum_to_lane63(acc[0]);
+    if (lane == 63) dst[gw] = s;
   };
   // computeActiveErrors + buildSystem at pose X -> sh.hb (chi2, H, b)
   auto build_sweep = [&](const Se3& X) {
     double acc[28];
 #pragma unroll
     for (int k = 0; k < 28; ++k) acc[k] = 0;
-    for (int i0 = t; i0 < cap; i0 += kU * kPoseThreads) {
-      PoseObsDev o[kU];
-      bool live[kU];
+    if constexpr (kB == 1) {  // wide block: one edge per thread at a time, straight into acc
+      for (int i = t; i < cap; i += NT)
+        if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
+    } else
+    for (int i0 = t; i0 < cap; i0 += kB * NT) {
+      PoseObsDev o[kB];
+      bool live[kB];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int i = i0 + u * kPoseThreads;
+      for (int u = 0; u < kB; ++u) {
+        const int i = i0 + u * NT;
         live[u] = i < cap && !lv[min(i, cap - 1)];
         o[u] = ob[min(i, cap - 1)];
       }
-      double part[kU][28];
+      double part[kB][28];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
+      for (int u = 0; u < kB; ++u) {
 #pragma unroll
         for (int k = 0; k < 28; ++k) part[u][k] = 0;
         edge_accumulate(o[u], X, cam, robust, dmono, dstereo, true, part[u]);
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u)
+      for (int u = 0; u < kB; ++u)
         if (live[u]) {
           // g2o adds each edge's block into H/b in edge order; the chi2 term
           // first as in computeActiveErrors
@@ -369,20 +439,21 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
           for (int k = 1; k < 28; ++k) acc[k] += part[u][k];
         }
     }
-    for (int i = cap + t; i < n; i += kPoseThreads)
+    for (int i = cap + t; i < n; i += NT)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
-    block_sum_to_lds<28>(acc, sh.red, sh.hb);
+    block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb);
   };
 
   const double* hb = sh.hb;
+  int buf = 0;
   for (int it = 0; it < 4; ++it) {
-    T = init;
+    T = pose_at(sh.init);
     PSTAMP(0);
     build_sweep(T);  // computeActiveErrors + buildSystem at the round's start
     PSTAMP(1);
     PSTAMP_ADD(8, 1);
     double cur = hb[0];
-    Se3 Teval = T;
+    const double* teval = sh.init;  // the pose of the last computeActiveErrors (a trial's)
     double lambda = 0, ni = 2;
     int nbad = 0;
     for (int iter = 0; iter < 10; ++iter) {
@@ -401,41 +472,78 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       }
       double rho = 0;
       int q = 0;
-      bool accepted = false;
+      bool accepted = false, done = false;
       do {
+        // this group's trial (q + grp): the lambda the sequential loop would
+        // reach after grp more rejections
+        double lg = lambda, ng = ni;
+        for (int k = 0; k < grp; ++k) {
+          lg *= ng;
+          ng *= 2;
+        }
         // each wave solves the (identical) 6x6 system lane-parallel: no
         // broadcast barrier
         double x[6];
         PSTAMP(0);
-        const bool ok = ldlt6_wave(hb, lambda, x);
+        const bool ok = ldlt6_wave(hb, lg, x);
         PSTAMP(2);
         const Se3 Tn = se3_compose(se3_exp(x), T);
         PSTAMP(3);
-        double tmp = chi_sweep(Tn);
-        PSTAMP(4);
-        PSTAMP_ADD(9, 1);
-        Teval = Tn;
-        if (!ok) tmp = 1.79769313486231570815e+308;
-        rho = cur - tmp;
-        double scale = 0;
+        chi_sweep(Tn, sh.chi[buf][grp]);
+        if (tg == 0) {
+          double* tr = sh.trial[buf][grp];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) scale += x[j] * (lambda * x[j] + hb[22 + j]);
-        scale += 1e-3;
-        rho /= scale;
-        if (rho > 0 && isfinite(tmp)) {
-          double alpha = 1. - cube(2 * rho - 1);
-          alpha = fmin(alpha, 2. / 3.);
-          lambda *= fmax(1. / 3., alpha);
-          ni = 2;
-          cur = tmp;
-          T = Tn;
-          accepted = true;
-        } else {
+          for (int j = 0; j < 6; ++j) tr[j] = x[j];
+          tr[6] = Tn.qx;
+          tr[7] = Tn.qy;
+          tr[8] = Tn.qz;
+          tr[9] = Tn.qw;
+          tr[10] = Tn.t[0];
+          tr[11] = Tn.t[1];
+          tr[12] = Tn.t[2];
+          tr[13] = ok ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        PSTAMP(4);
+        PSTAMP_ADD(10, 1);
+        // the outcomes in trial order, exactly as the sequential do-while
+        const int gn = min(G, 10 - q);
+        for (int g = 0; g < gn; ++g) {
+          const double* tr = sh.trial[buf][g];
+          const double* cg = sh.chi[buf][g];
+          double tmp = cg[0];
+#pragma unroll
+          for (int w = 1; w < kPoseWaves; ++w) tmp += cg[w];
+          PSTAMP_ADD(9, 1);
+          teval = tr + 6;
+          if (tr[13] == 0.0) tmp = 1.79769313486231570815e+308;
+          rho = cur - tmp;
+          double scale = 0;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) scale += tr[j] * (lambda * tr[j] + hb[22 + j]);
+          scale += 1e-3;
+          rho /= scale;
+          ++q;
+          if (rho > 0 && isfinite(tmp)) {
+            double alpha = 1. - cube(2 * rho - 1);
+            alpha = fmin(alpha, 2. / 3.);
+            lambda *= fmax(1. / 3., alpha);
+            ni = 2;
+            cur = tmp;
+            T = pose_at(teval);
+            accepted = true;
+            done = true;
+            break;
+          }
           lambda *= ni;
           ni *= 2;
+          if (!(rho < 0) || q == 10) {
+            done = true;
+            break;
+          }
         }
-        ++q;
-      } while (rho < 0 && q < 10);
+        buf ^= 1;
+      } while (!done);
       if (q == 10 || rho == 0) break;
       if ((ini - cur) * 1e3 < ini)
         nbad++;
@@ -457,6 +565,7 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
     // classify (optimizer.cc:966-1037): level-1 edges recompute at T, level-0
     // edges keep the error of the last sweep (at Teval)
     int bad = 0;
+    const Se3 Teval = pose_at(teval);
     auto classify = [&](const PoseObsDev& o, uint8_t& l) {
       double e[3];
       bool st;
@@ -466,19 +575,19 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
       l = out ? 1 : 0;
       bad += out;
     };
-    for (int i = t; i < cap; i += kPoseThreads) classify(ob[i], lv[i]);
-    for (int i = cap + t; i < n; i += kPoseThreads) {
+    for (int i = t; i < cap; i += NT) classify(ob[i], lv[i]);
+    for (int i = cap + t; i < n; i += NT) {
       uint8_t l = level[i];
       classify(obs[i], l);
       level[i] = l;
     }
-    nbad_round = block_sum_i(bad, sh.ired);
+    nbad_round = block_sum_i<NW>(bad, sh.ired);
     PSTAMP(5);
     if (it == 2) robust = false;
     if (n < 10) break;
   }
 
-  for (int i = t; i < cap; i += kPoseThreads) level[i] = lv[i];
+  for (int i = t; i < cap; i += NT) level[pm[i]] = lv[i];
   if (t == 0) {
     const double o[7] = {T.qx, T.qy, T.qz, T.qw, T.t[0], T.t[1], T.t[2]};
     float f[7];
@@ -495,21 +604,43 @@ __global__ __launch_bounds__(kPoseThreads) void k_pose_opt(
   PSTAMP_END;
 }
 
+template <int G>
+static hipError_t launch_pose_opt_g(const CamDev& c, const float* d_pose_in, const void* d_obs,
+                                    const int* d_nobs, int obs_stride, int n_problems,
+                                    float* d_pose_out, uint8_t* d_outlier, int* d_inliers,
+                                    double* d_pose_out_d, hipStream_t st) {
+  const int lds_obs = obs_stride < kPoseLdsObs ? obs_stride : kPoseLdsObs;
+  // observations, levels, slot -> observation index (k_pose_opt)
+  const size_t lds = ((size_t)lds_obs * sizeof(PoseObsDev) + (((size_t)lds_obs + 1) & ~(size_t)1) +
+                      2 * (size_t)lds_obs + 15) & ~(size_t)15;
+  if (lds + sizeof(PoseShared<G>) > 64 * 1024) {
+    if (lds_optin(reinterpret_cast<const void*>(&k_pose_opt<G>), 150 * 1024) != hipSuccess)
+      return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_pose_opt<G>, dim3(n_problems), dim3(kPoseThreads * G), lds, st, c,
+                     d_pose_in, reinterpret_cast<const PoseObsDev*>(d_obs), d_nobs, obs_stride,
+                     d_pose_out, d_outlier, d_inliers, d_pose_out_d, lds_obs);
+  return hipGetLastError();
+}
+
+// groups: trial groups per problem (1 or 2); see k_pose_opt.  Four groups
+// (1024 threads) cap a thread at 128 VGPRs and spill the build sweep
+// (measured 0.61 ms per 64 problems vs 0.32 for two).
 hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const void* d_obs,
                            const int* d_nobs, int obs_stride, int n_problems, float* d_pose_out,
                            uint8_t* d_outlier, int* d_inliers, double* d_pose_out_d,
-                           hipStream_t st) {
+                           hipStream_t st, int groups) {
   CamDev c{cam[0], cam[1], cam[2], cam[3], cam[4]};
-  const int lds_obs = obs_stride < kPoseLdsObs ? obs_stride : kPoseLdsObs;
-  const size_t lds = ((size_t)lds_obs * (sizeof(PoseObsDev) + 1) + 15) & ~(size_t)15;
-  if (lds > 64 * 1024) {
-    if (lds_optin(reinterpret_cast<const void*>(&k_pose_opt), 150 * 1024) != hipSuccess)
+  switch (groups) {
+    case 1:
+      return launch_pose_opt_g<1>(c, d_pose_in, d_obs, d_nobs, obs_stride, n_problems, d_pose_out,
+                                  d_outlier, d_inliers, d_pose_out_d, st);
+    case 2:
+      return launch_pose_opt_g<2>(c, d_pose_in, d_obs, d_nobs, obs_stride, n_problems, d_pose_out,
+                                  d_outlier, d_inliers, d_pose_out_d, st);
+    default:
       return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(k_pose_opt, dim3(n_problems), dim3(kPoseThreads), lds, st, c, d_pose_in,
-                     reinterpret_cast<const PoseObsDev*>(d_obs), d_nobs, obs_stride, d_pose_out,
-                     d_outlier, d_inliers, d_pose_out_d, lds_obs);
-  return hipGetLastError();
 }
 
 }  // namespace orbgpu

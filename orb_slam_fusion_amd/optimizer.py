@@ -30,13 +30,17 @@ class PoseFrame:
 
 
 class PoseOptimizer:
-    def __init__(self, device: int = 0, max_problems: int = 1, max_obs: int = 4096):
+    def __init__(self, device: int = 0, max_problems: int = 1, max_obs: int = 4096,
+                 trial_groups: int | None = None):
         self._h = ctypes.c_void_p()
         self.max_obs = max_obs
         check(
             lib().orbgpu_pose_ctx_create(device, max_problems, max_obs, ctypes.byref(self._h)),
             "orbgpu_pose_ctx_create",
         )
+        if trial_groups is not None:  # speculative LM trial groups (1 or 2), see orbgpu.h
+            check(lib().orbgpu_pose_ctx_set_trial_groups(self._h, trial_groups, trial_groups),
+                  "orbgpu_pose_ctx_set_trial_groups")
 
     def PoseOptimization(self, frame: PoseFrame) -> int:
         obs = np.ascontiguousarray(frame.obs, dtype=POSE_OBS_DTYPE)

@@ -66,6 +66,7 @@ def test_invalid_params_rejected_before_device():
     assert so.orbgpu_extract(None, None, 0, 0, 0, None, None, None, 0, None, None) == \
         _lib.ORBGPU_ERR_INVALID
     assert so.orbgpu_pose_opt(None, None, None, None, 0, None, None, None) == _lib.ORBGPU_ERR_INVALID
+    assert so.orbgpu_pose_ctx_set_trial_groups(None, 1, 1) == _lib.ORBGPU_ERR_INVALID
     # inertial entry points: null handle / bad mode / missing prior rejected before any device work
     assert so.orbgpu_pose_inertial(None, 0, None, None, None, None, None, None, 0, 0, None,
                                    None) == _lib.ORBGPU_ERR_INVALID

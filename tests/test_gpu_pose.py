@@ -77,3 +77,37 @@ def test_pose_batch_matches_oracle(gpu_available):
         assert inl[i] == inl_ref and np.array_equal(out[i], out_ref)
         assert np.max(np.abs(pout[i] - p_ref)) <= TOL_F
         assert np.max(np.abs(pd[i] - pd_ref) / np.maximum(np.abs(pd_ref), 1.0)) <= TOL_D
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_pose_speculative_trial_groups(gpu_available, groups):
+    """Two trial groups evaluate consecutive LM trials side by side and scan the
+    outcomes in trial order: same path (flags, inliers) as the oracle, single
+    problem and batch."""
+    import torch
+
+    P, N = 8, 600
+    probs = [synth.pose_problem(300 + i, N, 15) for i in range(P)]
+    cam = probs[0][0]
+    opt = PoseOptimizer(max_problems=P, max_obs=N, trial_groups=groups)
+    for c, pi, pt, ob in probs[:3]:
+        inl_ref, p_ref, out_ref, _ = oracle.pose_opt(c, pi, ob)
+        fr = PoseFrame(cam=c, pose=pi, obs=ob)
+        assert opt.PoseOptimization(fr) == inl_ref
+        assert np.array_equal(fr.outlier, out_ref)
+        assert np.max(np.abs(fr.pose - p_ref)) <= TOL_F
+    obs = np.stack([p[3] for p in probs])
+    d_obs = torch.from_numpy(obs.view(np.float32).reshape(P, N, 7).copy()).cuda()
+    d_pin = torch.from_numpy(np.stack([p[1] for p in probs])).cuda()
+    d_n = torch.full((P,), N, dtype=torch.int32, device="cuda")
+    d_pout = torch.zeros((P, 7), dtype=torch.float32, device="cuda")
+    d_pd = torch.zeros((P, 7), dtype=torch.float64, device="cuda")
+    d_out = torch.zeros((P, N), dtype=torch.uint8, device="cuda")
+    d_inl = torch.zeros(P, dtype=torch.int32, device="cuda")
+    opt.batch(cam, d_pin, d_obs, d_n, d_pout, d_out, d_inl, d_pd)
+    torch.cuda.synchronize()
+    pd, out, inl = d_pd.cpu().numpy(), d_out.cpu().numpy(), d_inl.cpu().numpy()
+    for i, (c, pi, pt, ob) in enumerate(probs):
+        inl_ref, p_ref, out_ref, pd_ref = oracle.pose_opt(c, pi, ob)
+        assert inl[i] == inl_ref and np.array_equal(out[i], out_ref)
+        assert np.max(np.abs(pd[i] - pd_ref) / np.maximum(np.abs(pd_ref), 1.0)) <= TOL_D

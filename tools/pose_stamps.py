@@ -43,6 +43,7 @@ def main():
     names = {0: "control", 1: "build_sweep", 2: "ldlt", 3: "se3_exp", 4: "chi_sweep", 5: "classify"}
     print(json.dumps({"ticks_per_problem": tot / (B * iters), "builds_per_problem": v[8] / (B * iters),
                       "trials_per_problem": v[9] / (B * iters),
+                      "trial_rounds_per_problem": v[10] / (B * iters),
                       "share": {names[i]: round(v[i] / max(tot, 1), 3) for i in names}}))
 
 
