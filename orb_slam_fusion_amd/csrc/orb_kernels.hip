@@ -208,8 +208,11 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   for (int k = 0; k < 4; ++k) xa[k] = xt[min(x + k, g.w - 1)];
   const int2 tl = yt[min(ys + (lane & (RW - 1)), yl)];
 
-  if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && c1 < sp) {
-    const int nq = ncol >> 4, total = nrow * nq;
+  // 16-byte chunks when rows are 16-aligned and no chunk straddles the end of a
+  // source row: chunks wholly past it are skipped (their LDS bytes only meet
+  // the zero weight of the single-tap columns, sx + 1 = sw)
+  if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && (c1 < sp || (sw & 15) == 0)) {
+    const int nq = (c1 < sp ? ncol : min(ncol, sw - c0)) >> 4, total = nrow * nq;
     const uint32_t mg = ((1u << 19) + nq - 1) / nq;
     for (int i0 = 0; i0 < total; i0 += 1024) {
       uint4 v[4];
@@ -217,9 +220,10 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = min(i0 + 256 * u + (int)threadIdx.x, total - 1);
-        const int r = (int)(((uint32_t)i * mg) >> 19), q = i - r * nq;
-        v[u] = *reinterpret_cast<const uint4*>(S + (size_t)(rr0 + r) * sp + c0 + 16 * q);
-        at[u] = 16 * i;
+        // i < 2^13, mg < 2^19: the 24-bit multiply's low word is the product
+        const int r = (int)(__umul24((uint32_t)i, mg) >> 19), q = i - __mul24(r, nq);
+        v[u] = *reinterpret_cast<const uint4*>(S + __umul24((uint32_t)(rr0 + r), (uint32_t)sp) + c0 + 16 * q);
+        at[u] = __mul24(r, ncol) + 16 * q;  // LDS rows keep the window pitch ncol
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(lds + at[u]) = v[u];
