@@ -30,7 +30,7 @@ timeout -k 10 120 rocprofv3 --pmc $SQ --kernel-trace -d $O/calib -o calib --outp
 echo "sq passes ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/bench_prof -o bench \
   -- python3 bench.py --no-cpu-baseline --no-lba --no-lia --no-stereo --no-match --no-bow --no-inertial \
-     --no-track --no-latency > $O/bench_under_rocprof.json 2> $O/bench_prof.err \
+     --no-track --no-latency --no-c5 --no-lba-sharded > $O/bench_under_rocprof.json 2> $O/bench_prof.err \
   || { echo "rocprof bench failed"; tail -5 $O/bench_prof.err; exit 1; }
 f=$(find $O/bench_prof -name '*kernel_stats.csv' | head -n1)
 cp "$f" $O/bench_kernel_stats.csv
