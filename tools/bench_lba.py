@@ -97,7 +97,8 @@ def measure_sharded(calls: int = 10) -> dict:
     worker = REPO / "tools" / "lba_shard_worker.py"
     with tempfile.TemporaryDirectory() as tmp:
         procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), tmp,
-                                   str(calls)], env=env) for r in range(2)]
+                                   str(calls)], env=env, stdout=sys.stderr) for r in range(2)]
+        # (gloo's connection messages go to stderr: bench.py's stdout is its one JSON line)
         if any(p.wait(timeout=300) != 0 for p in procs):
             return {"error": "worker failed"}
         r = [np.load(Path(tmp) / f"r{k}.npz") for k in range(2)]
