@@ -29,7 +29,7 @@ STAGES = {"resize": ("k_resize", 7), "blur": ("k_blur", 1), "fast_cells": ("k_fa
 
 
 def short(name: str) -> str:
-    return name.split("(")[0].replace("void ", "").split("::")[-1].strip('"')
+    return name.split("(")[0].replace("void ", "").split("::")[-1].split("<")[0].strip('"')
 
 
 def counters(d: str):
