@@ -295,7 +295,10 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d,
     int lds_obs) {
   constexpr int NT = kPoseThreads * G, NW = NT / 64;
-  constexpr int kB = G == 1 ? 3 : 1;  // build-sweep edges in flight per thread
+  // build sweep: one edge at a time straight into the accumulators (three in
+  // flight held 84 partials: 306 VGPRs, 0.312 ms per 64 problems; one: 185
+  // VGPRs, 0.296 ms -- fewer registers beat the ILP)
+  constexpr int kB = 1;
   __shared__ PoseShared<G> sh;
   const int p = blockIdx.x, t = threadIdx.x;
   const int grp = __builtin_amdgcn_readfirstlane(t >> 8), tg = t & (kPoseThreads - 1);
