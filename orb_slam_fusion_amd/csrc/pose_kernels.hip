@@ -295,10 +295,6 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d,
     int lds_obs) {
   constexpr int NT = kPoseThreads * G, NW = NT / 64;
-  // build sweep: one edge at a time straight into the accumulators (three in
-  // flight held 84 partials: 306 VGPRs, 0.312 ms per 64 problems; one: 185
-  // VGPRs, 0.296 ms -- fewer registers beat the ILP)
-  constexpr int kB = 1;
   __shared__ PoseShared<G> sh;
   const int p = blockIdx.x, t = threadIdx.x;
   const int grp = __builtin_amdgcn_readfirstlane(t >> 8), tg = t & (kPoseThreads - 1);
@@ -407,41 +403,17 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     const double s = wave_sum_to_lane63(acc[0]);
     if (lane == 63) dst[gw] = s;
   };
-  // computeActiveErrors + buildSystem at pose X -> sh.hb (chi2, H, b)
+  // computeActiveErrors + buildSystem at pose X -> sh.hb (chi2, H, b); one
+  // edge at a time straight into the accumulators (three in flight held 84
+  // partials: 306 VGPRs and 0.312 ms per 64 problems; one: 185 VGPRs, 0.296)
   auto build_sweep = [&](const Se3& X) {
     double acc[28];
 #pragma unroll
     for (int k = 0; k < 28; ++k) acc[k] = 0;
-    if constexpr (kB == 1) {  // wide block: one edge per thread at a time, straight into acc
-      for (int i = t; i < cap; i += NT)
-        if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
-    } else
-    for (int i0 = t; i0 < cap; i0 += kB * NT) {
-      PoseObsDev o[kB];
-      bool live[kB];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        const int i = i0 + u * NT;
-        live[u] = i < cap && !lv[min(i, cap - 1)];
-        o[u] = ob[min(i, cap - 1)];
-      }
-      double part[kB][28];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-#pragma unroll
-        for (int k = 0; k < 28; ++k) part[u][k] = 0;
-        edge_accumulate(o[u], X, cam, robust, dmono, dstereo, true, part[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < kB; ++u)
-        if (live[u]) {
-          // g2o adds each edge's block into H/b in edge order; the chi2 term
-          // first as in computeActiveErrors
-          acc[0] += part[u][0];
-#pragma unroll
-          for (int k = 1; k < 28; ++k) acc[k] += part[u][k];
-        }
-    }
+    // g2o adds each edge's block into H/b in edge order, the chi2 term first
+    // as in computeActiveErrors
+    for (int i = t; i < cap; i += NT)
+      if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
     for (int i = cap + t; i < n; i += NT)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
     block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb);
