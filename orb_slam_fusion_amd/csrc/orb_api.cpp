@@ -72,6 +72,7 @@ struct orbgpu_extractor {
   hipGraphExec_t graph_exec = nullptr;
   ExtractLaunch graph_launch{};  // what graph_exec was captured for
   ExtractLaunch eager_launch{};  // the last launch run eagerly (captured when repeated)
+  int graph_wh[2] = {0, 0}, eager_wh[2] = {0, 0};  // plan size of each (grids are baked in)
   bool graph_valid = false, eager_valid = false;
   std::vector<uint8_t> host_pyr;
   bool host_pyr_valid = false;
@@ -279,8 +280,11 @@ static hipError_t enqueue_chain(orbgpu_extractor* h, const ExtractLaunch& a) {
 }
 
 static hipError_t run_single_chain(orbgpu_extractor* h, const ExtractLaunch& a) {
-  if (h->graph_valid && same_launch(h->graph_launch, a)) return hipGraphLaunch(h->graph_exec, h->stream);
-  if (h->eager_valid && same_launch(h->eager_launch, a)) {
+  const bool g_same = h->graph_wh[0] == h->plan_w && h->graph_wh[1] == h->plan_h;
+  const bool e_same = h->eager_wh[0] == h->plan_w && h->eager_wh[1] == h->plan_h;
+  if (h->graph_valid && g_same && same_launch(h->graph_launch, a))
+    return hipGraphLaunch(h->graph_exec, h->stream);
+  if (h->eager_valid && e_same && same_launch(h->eager_launch, a)) {
     if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
     if (h->graph) (void)hipGraphDestroy(h->graph);
     h->graph_exec = nullptr;
@@ -295,12 +299,16 @@ static hipError_t run_single_chain(orbgpu_extractor* h, const ExtractLaunch& a) 
     if (e == hipSuccess) e = hipGraphInstantiate(&h->graph_exec, h->graph, nullptr, nullptr, 0);
     if (e == hipSuccess) {
       h->graph_launch = a;
+      h->graph_wh[0] = h->plan_w;
+      h->graph_wh[1] = h->plan_h;
       h->graph_valid = true;
       return hipGraphLaunch(h->graph_exec, h->stream);
     }
     (void)hipGetLastError();  // capture unsupported here: stay eager
   }
   h->eager_launch = a;
+  h->eager_wh[0] = h->plan_w;
+  h->eager_wh[1] = h->plan_h;
   h->eager_valid = true;
   return enqueue_chain(h, a);
 }

@@ -173,3 +173,23 @@ def test_repeat_calls_deterministic(gpu_available):
     r1 = ex(left)
     r2 = ex(left)
     assert r1[0] == r2[0] and r1[1].tobytes() == r2[1].tobytes() and r1[2].tobytes() == r2[2].tobytes()
+
+
+def test_graph_replay_across_sizes(gpu_available):
+    """The host path replays a captured hipGraph once a launch repeats; a
+    handle alternating between sizes (752x480 and its transpose 480x752 have
+    the same byte count) must give each size's own result every time --
+    compared with fresh handles, whose first call runs eagerly."""
+    rng = np.random.default_rng(3)
+    imgs = {(480, 752): synth.stereo_frame(3)[0],
+            (752, 480): np.ascontiguousarray(synth.stereo_frame(4)[0].T),
+            (400, 640): rng.integers(0, 255, (400, 640), dtype=np.uint8)}
+    ref = {}
+    for hw, im in imgs.items():
+        r = OrbExtractor(*C2, max_width=800, max_height=800)(im)
+        ref[hw] = (r[0], r[1].tobytes(), r[2].tobytes())
+    ex = OrbExtractor(*C2, max_width=800, max_height=800)
+    for hw in [(480, 752), (480, 752), (480, 752), (752, 480), (752, 480), (752, 480), (480, 752),
+               (400, 640), (400, 640), (480, 752), (752, 480)]:
+        r = ex(imgs[hw])
+        assert (r[0], r[1].tobytes(), r[2].tobytes()) == ref[hw], hw
