@@ -111,3 +111,25 @@ def test_pose_speculative_trial_groups(gpu_available, groups):
         inl_ref, p_ref, out_ref, pd_ref = oracle.pose_opt(c, pi, ob)
         assert inl[i] == inl_ref and np.array_equal(out[i], out_ref)
         assert np.max(np.abs(pd[i] - pd_ref) / np.maximum(np.abs(pd_ref), 1.0)) <= TOL_D
+
+
+def test_pose_context_reuse_graph_replay(gpu_available):
+    """One context, many problems: from the second call the copy + kernel +
+    copy chain is a replayed hipGraph (fixed-size copies, n on the device);
+    varying sizes (incl. the n < 3 early return) and a camera change (a
+    kernel argument: the graph is re-captured) must each match the oracle."""
+    opt = PoseOptimizer(max_obs=1200)
+    cases = [(7, 600, 10), (8, 50, 30), (9, 1200, 10), (5, 2, 0), (10, 600, 10), (11, 9, 0)]
+    for k, (seed, n, pct) in enumerate(cases * 2):
+        cam, pi, pt, obs = synth.pose_problem(seed, n, pct)
+        if k >= len(cases):
+            cam = (cam * np.array([1.01, 1.01, 1, 1, 1], np.float32)).astype(np.float32)
+        fr = PoseFrame(cam=cam, pose=pi, obs=obs)
+        inl = opt.PoseOptimization(fr)
+        if n < 3:
+            assert inl == 0 and np.array_equal(fr.pose, pi)
+            continue
+        inl_ref, p_ref, out_ref, _ = oracle.pose_opt(cam, pi, obs)
+        assert inl == inl_ref, (seed, n)
+        assert np.array_equal(fr.outlier, out_ref)
+        assert np.max(np.abs(fr.pose - p_ref)) <= TOL_F
