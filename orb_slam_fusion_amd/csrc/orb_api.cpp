@@ -68,6 +68,13 @@ struct orbgpu_extractor {
   // the single-image chain (13 kernels + the count / error copies into the
   // pinned h_small) replayed as one hipGraph while its launch is unchanged
   int* h_small = nullptr;  // n, mono, err (pinned)
+  // pinned staging of the image and of the outputs: the copies are part of
+  // the graph (fixed addresses and sizes), the host only memcpys
+  uint8_t* h_img = nullptr;
+  size_t h_img_bytes = 0;
+  orbgpu_keypoint* h_kps = nullptr;
+  uint8_t* h_descs = nullptr;
+  size_t h_out_cap = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   ExtractLaunch graph_launch{};  // what graph_exec was captured for
@@ -264,18 +271,26 @@ static bool same_launch(const ExtractLaunch& x, const ExtractLaunch& y) {
          x.mono_out == y.mono_out && x.err == y.err && x.n_cu == y.n_cu && x.events == y.events;
 }
 
-// Enqueue the single-image chain and the copies of (n, mono, err) into the
-// pinned h_small.  A launch seen twice in a row (same plan, buffers, lapping)
+// Enqueue the single-image chain between its copies: the image from pinned
+// h_img, then (n, mono, err) and the full-capacity keypoint / descriptor
+// blocks into pinned memory.  A launch seen twice in a row (same plan, buffers, lapping)
 // is captured into a hipGraph and replayed from then on: the per-frame
-// host path submits one graph instead of 13 kernels and 2 copies.  The
+// host path submits one graph instead of 13 kernels and 5 copies.  The
 // first run of a launch stays eager (it also performs the one-time LDS
 // opt-ins, which are not stream work).
 static hipError_t enqueue_chain(orbgpu_extractor* h, const ExtractLaunch& a) {
-  hipError_t e = launch_extract(a, h->stream);
+  hipError_t e = hipMemcpyAsync(const_cast<uint8_t*>(a.imgs), h->h_img, a.image_pitch,
+                                hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = launch_extract(a, h->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(h->h_small, h->d_nm, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(h->h_small + 2, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h->h_kps, a.kps_out, (size_t)a.cap * sizeof(orbgpu_keypoint),
+                       hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h->h_descs, a.desc_out, (size_t)a.cap * 32, hipMemcpyDeviceToHost, h->stream);
   return e;
 }
 
@@ -376,6 +391,9 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
   if (h->h_small) (void)hipHostFree(h->h_small);
+  if (h->h_img) (void)hipHostFree(h->h_img);
+  if (h->h_kps) (void)hipHostFree(h->h_kps);
+  if (h->h_descs) (void)hipHostFree(h->h_descs);
   dfree(h->d_st_lists);
   dfree(h->d_st_rowend);
   dfree(h->d_st_sad);
@@ -428,6 +446,13 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
     if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
     h->d_img_bytes = bytes;
   }
+  if (bytes > h->h_img_bytes) {
+    if (h->h_img) (void)hipHostFree(h->h_img);
+    h->h_img = nullptr;
+    h->h_img_bytes = 0;
+    if (hipHostMalloc(&h->h_img, bytes) != hipSuccess) return ORBGPU_ERR_NOMEM;
+    h->h_img_bytes = bytes;
+  }
   if ((size_t)P.kp_slots > h->out_cap) {
     dfree(h->d_kps);
     dfree(h->d_descs);
@@ -435,9 +460,24 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
       return ORBGPU_ERR_NOMEM;
     h->out_cap = P.kp_slots;
   }
-  if (hipMemcpy2DAsync(h->d_img, pitch0, img, stride, width, height, hipMemcpyHostToDevice,
-                       h->stream) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
+  if ((size_t)P.kp_slots > h->h_out_cap) {
+    if (h->h_kps) (void)hipHostFree(h->h_kps);
+    if (h->h_descs) (void)hipHostFree(h->h_descs);
+    h->h_kps = nullptr;
+    h->h_descs = nullptr;
+    h->h_out_cap = 0;
+    if (hipHostMalloc(&h->h_kps, (size_t)P.kp_slots * sizeof(orbgpu_keypoint)) != hipSuccess ||
+        hipHostMalloc(&h->h_descs, (size_t)P.kp_slots * 32) != hipSuccess)
+      return ORBGPU_ERR_NOMEM;
+    h->h_out_cap = P.kp_slots;
+  }
+  // the image into pinned staging (rows at the level-0 pitch); the graph copies it
+  if (stride == pitch0) {
+    std::memcpy(h->h_img, img, bytes);
+  } else {
+    for (int r = 0; r < height; ++r)
+      std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
+  }
   const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
   ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
                                 P.kp_slots, h->d_nm, h->d_nm + 1);
@@ -454,12 +494,10 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   *n_out = nm[0];
   if (mono_out) *mono_out = nm[1];
   if (nm[0] > cap) return ORBGPU_ERR_CAPACITY;
-  if (nm[0] > 0 &&
-      (hipMemcpyAsync(kps, h->d_kps, (size_t)nm[0] * sizeof(orbgpu_keypoint), hipMemcpyDeviceToHost,
-                      h->stream) ||
-       hipMemcpyAsync(descs, h->d_descs, (size_t)nm[0] * 32, hipMemcpyDeviceToHost, h->stream) ||
-       hipStreamSynchronize(h->stream)))
-    return ORBGPU_ERR_DEVICE;
+  if (nm[0] > 0) {
+    std::memcpy(kps, h->h_kps, (size_t)nm[0] * sizeof(orbgpu_keypoint));
+    std::memcpy(descs, h->h_descs, (size_t)nm[0] * 32);
+  }
   return ORBGPU_OK;
 }
 
