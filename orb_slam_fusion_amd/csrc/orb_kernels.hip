@@ -261,39 +261,28 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   __syncthreads();
   if (ys > yl) return;  // after the barrier: every wave staged its share
 
-  // stream the source rows: hA/qA = row p, hB/qB = row p+1, row p+2 in flight
+  // stream the source rows: two register slots hold rows p and p+1 (slot sa
+  // = row p; a wave-uniform flag, so advancing one row recomputes into the
+  // freed slot and flips sa -- no register moves), row p+2 in flight
   const int last = nrow - 1;
   auto rowp = [&](int r) { return lds + min(r, last) * ncol; };
-  uint32_t hA[4], hB[4], qA[4], qB[4];
+  uint32_t h0[4], h1[4], q0[4], q1[4];
+  int sa = 0;
   RsRow nd;
   int p = -1000;
   uint8_t* D = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + x;
   const int ye = min(ys + RW - 1, yl);
-  for (int y = ys; y <= ye; ++y) {
-    const int tx = __builtin_amdgcn_readlane(tl.x, y - ys), ty = __builtin_amdgcn_readlane(tl.y, y - ys);
-    const int r0 = (tx & 0xffff) - rr0, r1 = (int)((uint32_t)tx >> 16) - rr0;
-    if (r0 < p || r0 > p + 2) {
-      p = r0;
-      rs_horiz(rs_load(rowp(p), base4, bi, bytewise), off, sel, aw, bytewise, hA, qA);
-      rs_horiz(rs_load(rowp(p + 1), base4, bi, bytewise), off, sel, aw, bytewise, hB, qB);
-      nd = rs_load(rowp(p + 2), base4, bi, bytewise);
-    } else {
-      while (p < r0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) hA[k] = hB[k], qA[k] = qB[k];
-        rs_horiz(nd, off, sel, aw, bytewise, hB, qB);
-        ++p;
-        nd = rs_load(rowp(p + 2), base4, bi, bytewise);
-      }
-    }
-    // r1 is r0 + 1, or r0 at the clamped first / last source row
-    const bool same = r1 == r0;
-    const uint32_t b0 = (uint32_t)ty & 0xffffu, b1 = (uint32_t)ty >> 16;
+  // one output row from source rows A (= r0) and B (= r1); `same` (r1 == r0,
+  // the clamped first / last source row) and the tail are wave-uniform
+  auto out_row = [&](int y, const uint32_t (&hA)[4], const uint32_t (&qA)[4], const uint32_t (&hB)[4],
+                     const uint32_t (&qB)[4], bool same, uint32_t b0, uint32_t b1) {
     uint32_t v[4];
+    if (!same) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t q1 = same ? qA[k] : qB[k];
-      v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(q1, b1) >> 16) + 2) >> 2;
+      for (int k = 0; k < 4; ++k) v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(qB[k], b1) >> 16) + 2) >> 2;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(qA[k], b1) >> 16) + 2) >> 2;
     }
     if (any_tail) {
 #pragma unroll
@@ -302,7 +291,35 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
     }
     // columns past w land in the pitch padding (pitch is a multiple of 16)
     if (active)
-      *reinterpret_cast<uint32_t*>(D + (size_t)y * g.pitch) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+      *reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)y, (uint32_t)g.pitch)) =
+          v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+  };
+  for (int y = ys; y <= ye; ++y) {
+    const int tx = __builtin_amdgcn_readlane(tl.x, y - ys), ty = __builtin_amdgcn_readlane(tl.y, y - ys);
+    const int r0 = (tx & 0xffff) - rr0, r1 = (int)((uint32_t)tx >> 16) - rr0;
+    if (r0 < p || r0 > p + 2) {
+      p = r0;
+      sa = 0;
+      rs_horiz(rs_load(rowp(p), base4, bi, bytewise), off, sel, aw, bytewise, h0, q0);
+      rs_horiz(rs_load(rowp(p + 1), base4, bi, bytewise), off, sel, aw, bytewise, h1, q1);
+      nd = rs_load(rowp(p + 2), base4, bi, bytewise);
+    } else {
+      while (p < r0) {  // row p + 2 into the slot of row p, which becomes row p + 1's partner
+        if (sa == 0)
+          rs_horiz(nd, off, sel, aw, bytewise, h0, q0);
+        else
+          rs_horiz(nd, off, sel, aw, bytewise, h1, q1);
+        sa ^= 1;
+        ++p;
+        nd = rs_load(rowp(p + 2), base4, bi, bytewise);
+      }
+    }
+    const bool same = r1 == r0;
+    const uint32_t b0 = (uint32_t)ty & 0xffffu, b1 = (uint32_t)ty >> 16;
+    if (sa == 0)
+      out_row(y, h0, q0, h1, q1, same, b0, b1);
+    else
+      out_row(y, h1, q1, h0, q0, same, b0, b1);
   }
 }
 
