@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--groups", type=int, default=40)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--pipes", type=int, default=2)
+    ap.add_argument("--pose-priority", type=int, default=-1, help="torch stream priority of the pose stream")
     a = ap.parse_args()
     import torch
 
@@ -49,7 +50,7 @@ def main():
     desc = torch.zeros((2 * Bg, cap, 32), dtype=torch.uint8, device="cuda")
     n = torch.zeros(2 * Bg, dtype=torch.int32, device="cuda")
     mono = torch.zeros(2 * Bg, dtype=torch.int32, device="cuda")
-    s_pose = torch.cuda.Stream(priority=-1)
+    s_pose = torch.cuda.Stream(priority=a.pose_priority)
 
     def run(ext, pose):
         for _ in range(a.groups):
