@@ -909,6 +909,18 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
   }
   __syncthreads();
   for (int k = t; k < K; k += kOctThreads) set_kn(k, s.tmp2[KN(k)]);
+  // per-node round state, prepared where the node list is (re)written so a
+  // round starts without its own barriers for it: not yet chosen (rank -1),
+  // the phase-1 flag cnt >= 2 (in ncnt, the scan input), the division
+  // midlines, zeroed child counts
+  auto prep = [&](int i) {
+    s.rank[i] = -1;
+    s.ncnt[i] = s.cnt[i] >= 2 ? 1 : 0;
+    s.mx[i] = s.x0[i] + (int)ceilf((float)(s.x1[i] - s.x0[i]) / 2);
+    s.my[i] = s.y0[i] + (int)ceilf((float)(s.y1[i] - s.y0[i]) / 2);
+    s.ccnt[4 * i] = s.ccnt[4 * i + 1] = s.ccnt[4 * i + 2] = s.ccnt[4 * i + 3] = 0;
+  };
+  for (int i = t; i < S; i += kOctThreads) prep(i);
   __syncthreads();
 
   OSTAMP(1);
@@ -919,14 +931,10 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     // ---- choose D and its processing order (rank), uniform across the block
     int m;  // |D|
     OSTAMP_ADD(12 + (phase == 2), 1);
-    for (int i = t; i < S; i += kOctThreads) s.rank[i] = -1;
-    __syncthreads();
     if (phase == 1) {
-      for (int i = t; i < S; i += kOctThreads) s.tmp2[i] = s.cnt[i] >= 2 ? 1 : 0;
-      __syncthreads();
-      m = block_scan(s.tmp2, S, s.scan_tmp);
+      m = block_scan(s.ncnt, S, s.scan_tmp);  // ranks of the nodes with cnt >= 2
       for (int i = t; i < S; i += kOctThreads)
-        if (s.cnt[i] >= 2) s.rank[i] = s.tmp2[i];
+        if (s.cnt[i] >= 2) s.rank[i] = s.ncnt[i];
     } else {
       // stable sort of exp_list[0..n_exp) by (cnt, x0); processed from the back.
       // Keys (cnt, x0, list index) are unique, so a node's rank is the number
@@ -950,15 +958,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
     __syncthreads();
 
     OSTAMP(4);
-    // ---- midlines of D and child point counts
-    for (int i = t; i < S; i += kOctThreads) {
-      if (s.rank[i] >= 0) {
-        s.mx[i] = s.x0[i] + (int)ceilf((float)(s.x1[i] - s.x0[i]) / 2);
-        s.my[i] = s.y0[i] + (int)ceilf((float)(s.y1[i] - s.y0[i]) / 2);
-      }
-      s.ccnt[4 * i] = s.ccnt[4 * i + 1] = s.ccnt[4 * i + 2] = s.ccnt[4 * i + 3] = 0;
-    }
-    __syncthreads();
+    // ---- child point counts of D (midlines prepared with the list)
     for (int k = t; k < K; k += kOctThreads) {
       const int n = KN(k);
       if (s.rank[n] >= 0) {
@@ -1076,6 +1076,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
       s.x1[i] = s.nx1[i];
       s.y1[i] = s.ny1[i];
       s.cnt[i] = s.ncnt[i];
+      prep(i);  // reads the entries this thread just wrote
     }
     __syncthreads();
 
