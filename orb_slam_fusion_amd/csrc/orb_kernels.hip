@@ -767,6 +767,23 @@ __device__ __forceinline__ int block_sum(int v, int* tmp) {
 // which is computed with two block scans.  The node kept per leaf is the
 // highest response, first in to_dist order on ties (64-bit LDS atomic max).
 // --------------------------------------------------------------------------
+// cnt[key] += 1 for every lane with key >= 0, one LDS atomic per run of equal
+// keys over consecutive lanes: the candidates of a wave are consecutive in
+// to_dist order (cell-major raster), so most of them fall into the same node
+// and quadrant, and per-candidate atomics on a few counters serialise.  The
+// whole wave must be active.
+__device__ __forceinline__ void run_add(int* cnt, int key) {
+  const int lane = threadIdx.x & 63;
+  const int prev = __shfl_up(key, 1, 64);
+  const bool head = lane == 0 || key != prev;
+  const uint64_t heads = __ballot(head);
+  if (head && key >= 0) {
+    const uint64_t after = lane == 63 ? 0ull : (heads >> (lane + 1));
+    const int len = after ? __builtin_ctzll(after) + 1 : 64 - lane;
+    atomicAdd(&cnt[key], len);
+  }
+}
+
 struct OctLds {
   int *x0, *y0, *x1, *y1, *cnt;      // current list, position-indexed
   int *nx0, *ny0, *nx1, *ny1, *ncnt; // next list
@@ -887,11 +904,15 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
   const float hx = g.root_w;
   for (int i = t; i < R; i += kOctThreads) s.ccnt[i] = 0;
   __syncthreads();
-  for (int k = t; k < K; k += kOctThreads) {
-    const float x = (float)(KD(k) & 0xfff);
-    const int r = (int)(x / hx);
-    set_kn(k, r);
-    atomicAdd(&s.ccnt[r], 1);
+  for (int k0 = 0; k0 < K; k0 += kOctThreads) {  // whole waves active (run_add)
+    const int k = k0 + t;
+    int r = -1;
+    if (k < K) {
+      const float x = (float)(KD(k) & 0xfff);
+      r = (int)(x / hx);
+      set_kn(k, r);
+    }
+    run_add(s.ccnt, r);
   }
   __syncthreads();
   for (int i = t; i < R; i += kOctThreads) s.tmp2[i] = s.ccnt[i] > 0 ? 1 : 0;
@@ -959,14 +980,18 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
 
     OSTAMP(4);
     // ---- child point counts of D (midlines prepared with the list)
-    for (int k = t; k < K; k += kOctThreads) {
-      const int n = KN(k);
-      if (s.rank[n] >= 0) {
-        const uint32_t e = KD(k);
-        const int x = e & 0xfff, y = (e >> 12) & 0xfff;
-        const int q = (x < s.mx[n] ? 0 : 1) + (y < s.my[n] ? 0 : 2);
-        atomicAdd(&s.ccnt[4 * n + q], 1);
+    for (int k0 = 0; k0 < K; k0 += kOctThreads) {  // whole waves active (run_add)
+      const int k = k0 + t;
+      int key = -1;
+      if (k < K) {
+        const int n = KN(k);
+        if (s.rank[n] >= 0) {
+          const uint32_t e = KD(k);
+          const int x = e & 0xfff, y = (e >> 12) & 0xfff;
+          key = 4 * n + (x < s.mx[n] ? 0 : 1) + (y < s.my[n] ? 0 : 2);
+        }
       }
+      run_add(s.ccnt, key);
     }
     __syncthreads();
     for (int i = t; i < S; i += kOctThreads) {
