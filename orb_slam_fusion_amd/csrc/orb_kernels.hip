@@ -597,42 +597,58 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
 
   const uint8_t* base = roi + 3 * ls + lead + 3;  // detection pixel (0, 0)
   const uint64_t lt = (1ull << lane) - 1ull;
-  const int gpr = (dw + 3) >> 2;  // 4-pixel groups per detection row
+  const int gpr = (dw + 7) >> 3;  // 8-pixel groups per detection row
   const int g_r0 = lane / gpr, g_q0 = lane - (lane / gpr) * gpr;
   const int g_dr = 64 / gpr, g_dq = 64 - g_dr * gpr;
 
   // One threshold pass; returns the number of keypoints, leaves the survivor
   // list (raster order, kp flag in bit 15) in sv[0..*n_sv).
   auto pass = [&](int th, int* n_sv) -> int {
-    // compass pre-test on 4 pixels per lane in packed u16 pairs; the window
-    // of centres q..q+3 starts at row byte lead + q + 3 (wave-uniform shifts)
+    // compass pre-test on 8 pixels per lane in packed u16 pairs; the window
+    // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
     const ushort2_t th2 = as_us2((uint32_t)th * 0x10001u);
     int ns = 0;
     for (int r = g_r0, g = g_q0; __builtin_amdgcn_ballot_w64(r < dh) != 0;) {
-      const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 4 * g;
-      auto win = [&](const uint8_t* row, int o) {
+      const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 8 * g;
+      // 8 window bytes at row byte o: (lo, hi) dwords
+      auto win = [&](const uint8_t* row, int o, uint32_t& lo, uint32_t& hi) {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (o & ~3));
-        return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
+        lo = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
+        hi = __builtin_amdgcn_alignbyte(w[2], w[1], o & 3);
       };
-      const uint32_t wv = win(C, lead + 3), wl = win(C, lead), wr = win(C, lead + 6);
-      const uint32_t wu = win(C - 3 * ls, lead + 3), wd = win(C + 3 * ls, lead + 3);
-      const uint32_t te = __builtin_bit_cast(
-          uint32_t, sub_sat2(compass2(even_bytes(wv), even_bytes(wu), even_bytes(wd), even_bytes(wl),
-                                      even_bytes(wr)), th2));  // pixels 0, 2
-      const uint32_t to = __builtin_bit_cast(
-          uint32_t, sub_sat2(compass2(odd_bytes(wv), odd_bytes(wu), odd_bytes(wd), odd_bytes(wl),
-                                      odd_bytes(wr)), th2));   // pixels 1, 3
-      const int nv = r < dh ? min(dw - 4 * g, 4) : 0;  // valid pixels of the group
-      const bool f0 = nv > 0 && (te & 0xffffu), f1 = nv > 1 && (to & 0xffffu);
-      const bool f2 = nv > 2 && (te >> 16), f3 = nv > 3 && (to >> 16);
+      uint32_t v0, v1, l0, l1, r0, r1, u0, u1, d0, d1;
+      win(C, lead + 3, v0, v1);
+      win(C, lead, l0, l1);
+      win(C, lead + 6, r0, r1);
+      win(C - 3 * ls, lead + 3, u0, u1);
+      win(C + 3 * ls, lead + 3, d0, d1);
+      auto test = [&](ushort2_t (*pick)(uint32_t), uint32_t v, uint32_t u, uint32_t d, uint32_t l, uint32_t rr) {
+        return __builtin_bit_cast(uint32_t, sub_sat2(compass2(pick(v), pick(u), pick(d), pick(l), pick(rr)), th2));
+      };
+      const uint32_t te0 = test(even_bytes, v0, u0, d0, l0, r0);  // pixels 0, 2
+      const uint32_t to0 = test(odd_bytes, v0, u0, d0, l0, r0);   // pixels 1, 3
+      const uint32_t te1 = test(even_bytes, v1, u1, d1, l1, r1);  // pixels 4, 6
+      const uint32_t to1 = test(odd_bytes, v1, u1, d1, l1, r1);   // pixels 5, 7
+      const int nv = r < dh ? min(dw - 8 * g, 8) : 0;  // valid pixels of the group
+      const bool f0 = nv > 0 && (te0 & 0xffffu), f1 = nv > 1 && (to0 & 0xffffu);
+      const bool f2 = nv > 2 && (te0 >> 16), f3 = nv > 3 && (to0 >> 16);
+      const bool f4 = nv > 4 && (te1 & 0xffffu), f5 = nv > 5 && (to1 & 0xffffu);
+      const bool f6 = nv > 6 && (te1 >> 16), f7 = nv > 7 && (to1 >> 16);
       const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
-      int pos = ns + (int)mbcnt64(m3, mbcnt64(m2, mbcnt64(m1, mbcnt64(m0, 0u))));
-      const int i0 = (r << 7) | (4 * g);
+      const uint64_t m4 = __ballot(f4), m5 = __ballot(f5), m6 = __ballot(f6), m7 = __ballot(f7);
+      int pos = ns + (int)mbcnt64(m7, mbcnt64(m6, mbcnt64(m5, mbcnt64(m4, mbcnt64(m3, mbcnt64(m2,
+                         mbcnt64(m1, mbcnt64(m0, 0u))))))));
+      const int i0 = (r << 7) | (8 * g);
       if (f0) sv[pos++] = (uint16_t)i0;
       if (f1) sv[pos++] = (uint16_t)(i0 + 1);
       if (f2) sv[pos++] = (uint16_t)(i0 + 2);
-      if (f3) sv[pos] = (uint16_t)(i0 + 3);
-      ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+      if (f3) sv[pos++] = (uint16_t)(i0 + 3);
+      if (f4) sv[pos++] = (uint16_t)(i0 + 4);
+      if (f5) sv[pos++] = (uint16_t)(i0 + 5);
+      if (f6) sv[pos++] = (uint16_t)(i0 + 6);
+      if (f7) sv[pos] = (uint16_t)(i0 + 7);
+      ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3) + __popcll(m4) + __popcll(m5) +
+            __popcll(m6) + __popcll(m7);
       g += g_dq;
       r += g_dr;
       if (g >= gpr) g -= gpr, ++r;
