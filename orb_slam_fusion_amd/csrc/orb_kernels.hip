@@ -378,36 +378,45 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
   const uint32_t base = (uint32_t)min(max(x - 4, 0), g.w - 12);
-  // 3 dword loads per source row (unaligned only when the level-0 stride is),
-  // all issued before any use
+  // Streamed down the strip: the 3 dword loads of source row r + kPf are
+  // issued while row r is filtered horizontally, and output row r - 6 leaves
+  // as soon as its 7 rows exist, so only a 7-row window of sums is live.
+  constexpr int kPf = 8;  // rows of loads in flight
+  const bool edge = __builtin_amdgcn_ballot_w64((int)base != x - 4) != 0;
+  uint32_t lo_sel[3] = {0, 0, 0}, hi_sel[3] = {0, 0, 0};
+  if (edge) blur_window_sel(x, g.w, (int)base, lo_sel, hi_sel);
   uint32_t d[R + 6][3];
-#pragma unroll
-  for (int r = 0; r < R + 6; ++r) {
+  auto load_row = [&](int r) {
     const uint8_t* row = S + (uint32_t)(reflect101(ys - 3 + r, g.h) * sp);
 #pragma unroll
     for (int k = 0; k < 3; ++k) d[r][k] = *reinterpret_cast<const uint32_t*>(row + base + 4 * k);
-  }
-  if (__builtin_amdgcn_ballot_w64((int)base != x - 4)) {
-    uint32_t lo[3], hi[3];
-    blur_window_sel(x, g.w, (int)base, lo, hi);
+  };
 #pragma unroll
-    for (int r = 0; r < R + 6; ++r) {
-      uint32_t v[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        v[k] = __builtin_amdgcn_perm(d[r][1], d[r][0], lo[k]) |
-               __builtin_amdgcn_perm(d[r][2], d[r][2], hi[k]);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) d[r][k] = v[k];
-    }
-  }
+  for (int r = 0; r < kPf && r < R + 6; ++r) load_row(r);
   // horizontal taps: two v_dot4_u32_u8 per output on windows cut by alignbyte;
   // sums are <= 65280, so row pairs pack into one dword for the vertical dot2s
   const uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24);
   const uint32_t K1 = 48u | (34u << 8) | (18u << 16);
+  // vertical taps (18,34)(48,56)(48,34)(18,0) as four v_dot2_u32_u16, the
+  // +2^15 rounding in the first accumulator; results < 2^24, so each output
+  // byte is byte 2 of its sum and two v_perm_b32 pack four of them.
+  const ushort2_t k01 = as_us2(18u | (34u << 16)), k23 = as_us2(48u | (56u << 16));
+  const ushort2_t k45 = as_us2(48u | (34u << 16)), k6 = as_us2(18u);
+  // columns past w land in the row's pitch padding (pitch is a multiple of 16)
+  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + (uint32_t)x;
   uint32_t hw[R + 6][4];
+  uint32_t pr[R + 5][4];  // pr[r] = hw[r] | hw[r+1] << 16
 #pragma unroll
   for (int r = 0; r < R + 6; ++r) {
+    if (r + kPf < R + 6) load_row(r + kPf);
+    if (edge) {  // edge lanes rebuild their reflect-101 window (wave-uniform branch)
+      uint32_t v[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        v[k] = __builtin_amdgcn_perm(d[r][1], d[r][0], lo_sel[k]) | __builtin_amdgcn_perm(d[r][2], d[r][2], hi_sel[k]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d[r][k] = v[k];
+    }
     const uint32_t lo[4] = {__builtin_amdgcn_alignbyte(d[r][1], d[r][0], 1),
                             __builtin_amdgcn_alignbyte(d[r][1], d[r][0], 2),
                             __builtin_amdgcn_alignbyte(d[r][1], d[r][0], 3), d[r][1]};
@@ -417,32 +426,23 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       hw[r][j] = __builtin_amdgcn_udot4(lo[j], K0, __builtin_amdgcn_udot4(hi[j], K1, 0u, false), false);
-  }
-  uint32_t pr[R + 5][4];  // pr[r] = hw[r] | hw[r+1] << 16
+    if (r >= 1)
 #pragma unroll
-  for (int r = 0; r < R + 5; ++r)
+      for (int j = 0; j < 4; ++j) pr[r - 1][j] = hw[r - 1][j] | (hw[r][j] << 16);
+    if (r >= 6) {
+      const int o = r - 6;
+      if (ys + o < g.h) {
+        uint32_t v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pr[r][j] = hw[r][j] | (hw[r + 1][j] << 16);
-  // vertical taps (18,34)(48,56)(48,34)(18,0) as four v_dot2_u32_u16, the
-  // +2^15 rounding in the first accumulator; results < 2^24, so each output
-  // byte is byte 2 of its sum and two v_perm_b32 pack four of them.
-  const ushort2_t k01 = as_us2(18u | (34u << 16)), k23 = as_us2(48u | (56u << 16));
-  const ushort2_t k45 = as_us2(48u | (34u << 16)), k6 = as_us2(18u);
-  // columns past w land in the row's pitch padding (pitch is a multiple of 16)
-  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + (uint32_t)x;
-#pragma unroll
-  for (int o = 0; o < R; ++o) {
-    if (ys + o < g.h) {
-      uint32_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t a = __builtin_amdgcn_udot2(as_us2(pr[o][j]), k01, 1u << 15, false);
-        a = __builtin_amdgcn_udot2(as_us2(pr[o + 2][j]), k23, a, false);
-        a = __builtin_amdgcn_udot2(as_us2(pr[o + 4][j]), k45, a, false);
-        v[j] = __builtin_amdgcn_udot2(as_us2(hw[o + 6][j]), k6, a, false);
+        for (int j = 0; j < 4; ++j) {
+          uint32_t a = __builtin_amdgcn_udot2(as_us2(pr[o][j]), k01, 1u << 15, false);
+          a = __builtin_amdgcn_udot2(as_us2(pr[o + 2][j]), k23, a, false);
+          a = __builtin_amdgcn_udot2(as_us2(pr[o + 4][j]), k45, a, false);
+          v[j] = __builtin_amdgcn_udot2(as_us2(hw[o + 6][j]), k6, a, false);
+        }
+        *reinterpret_cast<uint32_t*>(D + (uint32_t)((ys + o) * g.pitch)) =
+            __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
       }
-      *reinterpret_cast<uint32_t*>(D + (uint32_t)((ys + o) * g.pitch)) =
-          __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
     }
   }
 }
