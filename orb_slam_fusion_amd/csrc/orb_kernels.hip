@@ -1466,9 +1466,12 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t set_octree_lds_limit(size_t bytes) {
-  return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)bytes);
+hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes) {
+  hipError_t e = hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)octree_bytes);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)k_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)resize_bytes);
 }
 
 }  // namespace orbgpu

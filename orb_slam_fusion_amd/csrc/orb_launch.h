@@ -43,6 +43,6 @@ struct ExtractLaunch {
 enum Stage : int { kStResize, kStBlur, kStFast, kStOctree, kStDescribe, kStAssemble, kStages };
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
-hipError_t set_octree_lds_limit(size_t bytes);
+hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes);
 
 }  // namespace orbgpu

@@ -214,7 +214,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   P.max_roi = (max_roi + 15) & ~15;
   P.max_roi_lds = (max_roi_lds + 15) & ~15;
   P.rs_lds = (rs_lds + 15) & ~15;
-  if (P.rs_lds > 64 * 1024) return why = "scale factor too large for the resize tile", false;
+  if (P.rs_lds > 160 * 1024) return why = "scale factor too large for the resize tile", false;
   if (P.max_roi_lds > 64 * 1024) return why = "FAST cell too large", false;
   if (P.kp_slots > 4096) return why = "too many keypoints per image for the assembly kernel", false;
   if (octree_lds_bytes(P) > 160 * 1024) return why = "num_features too large for the octree LDS", false;

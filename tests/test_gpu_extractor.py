@@ -214,3 +214,17 @@ def test_saturated_patterns_bit_exact(gpu_available, kind):
     else:
         img = np.where((x + 2 * y) % 11 < 3, 255, 0).astype(np.uint8)
     _compare(C2, img)
+
+
+def test_handles_with_different_plans_coexist(gpu_available):
+    """The dynamic-LDS opt-in is a per-kernel attribute: creating a handle with
+    a small octree (few features) after one with a large octree must not
+    shrink the limit the first handle's launches need."""
+    left, _ = synth.stereo_frame(8)
+    big = OrbExtractor(4000, 1.2, 8, 20, 7)
+    ref = big(left)
+    small = OrbExtractor(300, 1.2, 8, 20, 7)
+    small(left)
+    again = big(left)
+    assert ref[0] == again[0] and ref[1].tobytes() == again[1].tobytes()
+    _compare((4000, 1.2, 8, 20, 7), left)
