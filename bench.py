@@ -3,9 +3,9 @@
 PoseOptimization (600 observations) per frame on MI355X.
 
 A step = B distinct synthetic stereo frames per GPU (default 5120, all
-resident in HBM before the timed region), in launch groups of 64 frames: 128
+resident in HBM before the timed region), in launch groups of 256 frames: 512
 images through the gfx950 extractor (orbgpu_extract_batch, two pipelines of
-64 images, each its own HIP stream) and 64 pose-only problems through the
+256 images, each its own HIP stream) and 256 pose-only problems through the
 gfx950 PoseOptimization (orbgpu_pose_opt_batch) on a concurrent
 high-priority stream.  Frames shard across ranks (contiguous
 blocks of B frame ids per rank, orb_slam_fusion_amd/dist.py): no
@@ -126,7 +126,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=5120,
                     help="stereo frames per GPU per step (all distinct, resident in HBM)")
-    ap.add_argument("--batch", type=int, default=64, help="stereo frames per launch group")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="stereo frames per launch group (tools/sweep_batch.sh: 256 fills the "
+                         "device's tail-latency gaps best, DESIGN §5)")
     ap.add_argument("--pipes", type=int, default=2,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
                          "each launch group split evenly between them)")
