@@ -129,8 +129,9 @@ __device__ __forceinline__ const uint8_t* level_plane(const PlanHeader* P, const
 // two v_alignbyte_b32, then per column a v_perm_b32 with a per-lane selector
 // and one v_dot2_u32_u16: h = s0*a0 + s1*a1) is kept in registers for the
 // output rows that share it, with the next row's dwords already in flight.
-// Tap weights lie in [0, 2048] and sum to <= 2049, so (h>>4)*b < 2^24 (full-
-// rate v_mul_u32_u24) and every result is <= 255.
+// Tap weights lie in [0, 2048] and sum to <= 2049, so h < 2^19 and
+// ((h>>4)*b) >> 16 is one full-rate v_mul_hi_u32_u24 of (h & ~15, b << 12);
+// every result is <= 255.
 // --------------------------------------------------------------------------
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
@@ -157,7 +158,13 @@ __device__ __forceinline__ RsRow rs_load(const uint8_t* __restrict__ row, int ba
   }
   return r;
 }
-// h[k] = s0*a0 + s1*a1 of column k; hq[k] = h[k] >> 4 (the SIMD path's input)
+// (a * b) >> 32 of 24-bit operands: one full-rate v_mul_hi_u32_u24
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
+}
+// h[k] = s0*a0 + s1*a1 of column k; hq[k] = (h[k] >> 4) << 4 (the SIMD path's
+// input, kept 16x scaled so the vertical step's ((h >> 4) * b) >> 16 is one
+// mulhi24(hq, b << 12): h < 2^19, b << 12 <= 2^23)
 __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t (&sel)[4],
                                          const uint32_t (&aw)[4], bool bytewise, uint32_t (&h)[4],
                                          uint32_t (&hq)[4]) {
@@ -174,7 +181,7 @@ __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t
                                     as_us2(aw[k]), 0u, false);
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) hq[k] = h[k] >> 4;
+  for (int k = 0; k < 4; ++k) hq[k] = h[k] & ~15u;
 }
 
 __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
@@ -277,12 +284,13 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   auto out_row = [&](int y, const uint32_t (&hA)[4], const uint32_t (&qA)[4], const uint32_t (&hB)[4],
                      const uint32_t (&qB)[4], bool same, uint32_t b0, uint32_t b1) {
     uint32_t v[4];
+    const uint32_t s0 = b0 << 12, s1 = b1 << 12;
     if (!same) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(qB[k], b1) >> 16) + 2) >> 2;
+      for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2) >> 2;
     } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = ((__umul24(qA[k], b0) >> 16) + (__umul24(qA[k], b1) >> 16) + 2) >> 2;
+      for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qA[k], s1) + 2) >> 2;
     }
     if (any_tail) {
 #pragma unroll
