@@ -279,23 +279,18 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   int p = -1000;
   uint8_t* D = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + x;
   const int ye = min(ys + RW - 1, yl);
-  // one output row from source rows A (= r0) and B (= r1); `same` (r1 == r0,
-  // the clamped first / last source row) and the tail are wave-uniform
+  // one output row from source rows A (= r0) and B (= r1; the call sites pass
+  // A twice when r1 == r0, the clamped first / last source row)
   auto out_row = [&](int y, const uint32_t (&hA)[4], const uint32_t (&qA)[4], const uint32_t (&hB)[4],
-                     const uint32_t (&qB)[4], bool same, uint32_t b0, uint32_t b1) {
+                     const uint32_t (&qB)[4], uint32_t b0, uint32_t b1) {
     uint32_t v[4];
     const uint32_t s0 = b0 << 12, s1 = b1 << 12;
-    if (!same) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2) >> 2;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qA[k], s1) + 2) >> 2;
-    }
+    for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2) >> 2;
     if (any_tail) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (tail_k & (1u << k)) v[k] = (hA[k] * b0 + (same ? hA[k] : hB[k]) * b1 + (1u << 21)) >> 22;
+        if (tail_k & (1u << k)) v[k] = (hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22;
     }
     // columns past w land in the pitch padding (pitch is a multiple of 16)
     if (active)
@@ -322,12 +317,17 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
         nd = rs_load(rowp(p + 2), base4, bi, bytewise);
       }
     }
-    const bool same = r1 == r0;
     const uint32_t b0 = (uint32_t)ty & 0xffffu, b1 = (uint32_t)ty >> 16;
-    if (sa == 0)
-      out_row(y, h0, q0, h1, q1, same, b0, b1);
-    else
-      out_row(y, h1, q1, h0, q0, same, b0, b1);
+    if (r1 == r0) {  // wave-uniform (SGPR) branch, rare
+      if (sa == 0)
+        out_row(y, h0, q0, h0, q0, b0, b1);
+      else
+        out_row(y, h1, q1, h1, q1, b0, b1);
+    } else if (sa == 0) {
+      out_row(y, h0, q0, h1, q1, b0, b1);
+    } else {
+      out_row(y, h1, q1, h0, q0, b0, b1);
+    }
   }
 }
 
