@@ -283,19 +283,23 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   // A twice when r1 == r0, the clamped first / last source row)
   auto out_row = [&](int y, const uint32_t (&hA)[4], const uint32_t (&qA)[4], const uint32_t (&hB)[4],
                      const uint32_t (&qB)[4], uint32_t b0, uint32_t b1) {
-    uint32_t v[4];
+    uint32_t v[4];  // 4x the output byte (< 2^12); the >> 2 is done packed below
     const uint32_t s0 = b0 << 12, s1 = b1 << 12;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = (mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2) >> 2;
+    for (int k = 0; k < 4; ++k) v[k] = mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2;
     if (any_tail) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (tail_k & (1u << k)) v[k] = (hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22;
+        if (tail_k & (1u << k)) v[k] = ((hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22) << 2;
     }
+    // two columns per 16-bit half: one packed shift per pair, one byte perm
+    const ushort2_t p01 = as_us2(v[0] | (v[1] << 16)) >> (ushort2_t){2, 2};
+    const ushort2_t p23 = as_us2(v[2] | (v[3] << 16)) >> (ushort2_t){2, 2};
     // columns past w land in the pitch padding (pitch is a multiple of 16)
     if (active)
       *reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)y, (uint32_t)g.pitch)) =
-          v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+          __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01),
+                                0x06040200u);
   };
   for (int y = ys; y <= ye; ++y) {
     const int tx = __builtin_amdgcn_readlane(tl.x, y - ys), ty = __builtin_amdgcn_readlane(tl.y, y - ys);
