@@ -24,14 +24,15 @@ namespace orbgpu {
 constexpr int8_t kPattern[1024] = {
 #include "pattern31.inc"
 };
-// bit_pattern_31_ as floats (x0, y0, x1, y1) per test: one dwordx4 per lane
+// bit_pattern_31_ as floats (x0, x1, y0, y1) per test: one dwordx4 per lane,
+// the x pair and the y pair each a packed-FP32 operand
 struct PatternF {
   float4 p[256];
 };
 constexpr PatternF make_pattern_f() {
   PatternF t{};
   for (int i = 0; i < 256; ++i)
-    t.p[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 1], (float)kPattern[4 * i + 2],
+    t.p[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 2], (float)kPattern[4 * i + 1],
                     (float)kPattern[4 * i + 3]};
   return t;
 }
@@ -1176,6 +1177,7 @@ __global__ __launch_bounds__(kOctThreads) void k_octree(
 // i/64, so the 4 ballots are the 32 descriptor bytes, LSB-first as
 // ComputeOrbDescriptor packs them.
 // --------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kRawW = 36, kRawH = 31;   // 31x31 patch + dword alignment slack
 constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slack
 constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
@@ -1315,17 +1317,25 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   const float ang = angle * (float)(3.14159265358979323846 / 180.0);
   const float a = dev_cosf(ang), b = dev_sinf(ang);
   const uint8_t* ctr = blp + 18 * kBlurW + (cx - bx0);
+  const uint8_t* ctr_m = ctr - (uint32_t)(0x400000u * kBlurW + 0x4B400000u);
   uint64_t words[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     const float4 pt = c_pattern_f[64 * w + lane];
-    const float x0 = pt.x, y0 = pt.y, x1 = pt.z, y1 = pt.w;
-    const int r0 = dev_round(__builtin_fmaf(x0, b, y0 * a));
-    const int q0 = dev_round(__builtin_fmaf(x0, a, -(y0 * b)));
-    const int r1 = dev_round(__builtin_fmaf(x1, b, y1 * a));
-    const int q1 = dev_round(__builtin_fmaf(x1, a, -(y1 * b)));
-    // |r|, |q| <= 18: 24-bit multiplies (full rate)
-    const int t0 = ctr[__mul24(r0, kBlurW) + q0], t1 = ctr[__mul24(r1, kBlurW) + q1];
+    const f32x2 X = {pt.x, pt.y}, Y = {pt.z, pt.w};
+    // the reference's fma(x, b, y * a) and fma(x, a, -(y * b)) for both points
+    // as packed FP32 (v_pk_mul_f32 / v_pk_fma_f32, each lane IEEE-exact);
+    // cvRound of |v| <= 18 by the 1.5 * 2^23 magic add (round-half-even, the
+    // same as rintf): bits = 0x4B400000 + round(v).  The row bits' low 24 go
+    // through one v_mad_u32_u24, so the offset carries the constant
+    // 0x400000 * kBlurW + 0x4B400000, taken off the uniform base (mod 2^32).
+    constexpr float kMagic = 12582912.0f;
+    const f32x2 R = __builtin_elementwise_fma(X, (f32x2){b, b}, Y * (f32x2){a, a}) + (f32x2){kMagic, kMagic};
+    const f32x2 Q = __builtin_elementwise_fma(X, (f32x2){a, a}, Y * (f32x2){-b, -b}) + (f32x2){kMagic, kMagic};
+    const uint32_t r0 = __float_as_uint(R.x), r1 = __float_as_uint(R.y);
+    const uint32_t q0 = __float_as_uint(Q.x), q1 = __float_as_uint(Q.y);
+    const int t0 = ctr_m[__umul24(r0, (uint32_t)kBlurW) + q0];
+    const int t1 = ctr_m[__umul24(r1, (uint32_t)kBlurW) + q1];
     words[w] = __ballot(t0 < t1);
   }
   const size_t o = (size_t)img * P->kp_slots + slot;
