@@ -578,22 +578,24 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     const uint8_t* Sa = S - lead;  // rows stay dword-aligned iff sp is; else unaligned loads
     const int ndw = (lead + c.cols + 3) >> 2;
     if (ndw <= 16) {
-      // 16 lanes per ROI row, 4 rows per step: lane (q, r0) loads dword q of
-      // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight
-      const int q = lane & 15, r0 = lane >> 4;
-      const bool qv = q < ndw;
-      const int qa = min(q, ndw - 1);  // idle lanes re-read an in-ROI dword
+      // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
+      // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight.
+      // Lanes past the ROI width or height are clamped onto its last dword /
+      // row: they copy the same dword to the same LDS address as the lane
+      // that owns it, so the stores need no predicate; 32-bit offsets from
+      // the wave-uniform row base keep the loads on the scalar base.
+      const uint32_t q4 = 4u * (uint32_t)min(lane & 15, ndw - 1), r0 = (uint32_t)lane >> 4;
+      const uint32_t rlast = (uint32_t)c.rows - 1u;
       for (int k0 = 0; 4 * k0 < c.rows; k0 += kFastPf) {
-        uint32_t v[kFastPf];
+        uint32_t v[kFastPf], rr[kFastPf];
+#pragma unroll
+        for (int u = 0; u < kFastPf; ++u) rr[u] = min(r0 + 4u * (uint32_t)(k0 + u), rlast);
 #pragma unroll
         for (int u = 0; u < kFastPf; ++u)
-          v[u] = *reinterpret_cast<const uint32_t*>(
-              Sa + __umul24((uint32_t)min(r0 + 4 * (k0 + u), c.rows - 1), (uint32_t)sp) + 4 * qa);
+          v[u] = *reinterpret_cast<const uint32_t*>(Sa + (__umul24(rr[u], (uint32_t)sp) + q4));
 #pragma unroll
-        for (int u = 0; u < kFastPf; ++u) {
-          const int r = r0 + 4 * (k0 + u);
-          if (qv && r < c.rows) *reinterpret_cast<uint32_t*>(roi + __umul24((uint32_t)r, (uint32_t)ls) + 4 * q) = v[u];
-        }
+        for (int u = 0; u < kFastPf; ++u)
+          *reinterpret_cast<uint32_t*>(roi + (__umul24(rr[u], (uint32_t)ls) + q4)) = v[u];
       }
     } else {
       for (int i = lane; i < c.rows * ndw; i += 64) {
