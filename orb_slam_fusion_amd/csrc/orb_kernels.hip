@@ -649,8 +649,14 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const bool f2 = nv > 2 && (te0 >> 16), f3 = nv > 3 && (to0 >> 16);
       const bool f4 = nv > 4 && (te1 & 0xffffu), f5 = nv > 5 && (to1 & 0xffffu);
       const bool f6 = nv > 6 && (te1 >> 16), f7 = nv > 7 && (to1 >> 16);
-      const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2), m3 = __ballot(f3);
-      const uint64_t m4 = __ballot(f4), m5 = __ballot(f5), m6 = __ballot(f6), m7 = __ballot(f7);
+      // the masks as ANDs of single-compare ballots (scalar ANDs of the
+      // compares' lane masks): a ballot of an && rematerialises the bool with
+      // a v_cndmask + v_cmp pair per pixel
+      auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
+      const uint64_t m0 = bal(nv > 0) & bal(te0 & 0xffffu), m1 = bal(nv > 1) & bal(to0 & 0xffffu);
+      const uint64_t m2 = bal(nv > 2) & bal(te0 >> 16), m3 = bal(nv > 3) & bal(to0 >> 16);
+      const uint64_t m4 = bal(nv > 4) & bal(te1 & 0xffffu), m5 = bal(nv > 5) & bal(to1 & 0xffffu);
+      const uint64_t m6 = bal(nv > 6) & bal(te1 >> 16), m7 = bal(nv > 7) & bal(to1 >> 16);
       int pos = ns + (int)mbcnt64(m7, mbcnt64(m6, mbcnt64(m5, mbcnt64(m4, mbcnt64(m3, mbcnt64(m2,
                          mbcnt64(m1, mbcnt64(m0, 0u))))))));
       const int i0 = (r << 7) | (8 * g);
