@@ -615,6 +615,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   const int gpr = (dw + 7) >> 3;  // 8-pixel groups per detection row
   const int g_r0 = lane / gpr, g_q0 = lane - (lane / gpr) * gpr;
   const int g_dr = 64 / gpr, g_dq = 64 - g_dr * gpr;
+  const int tail = dw - 8 * (gpr - 1);  // valid pixels of a row's last group (1..8)
 
   // One threshold pass; returns the number of keypoints, leaves the survivor
   // list (raster order, kp flag in bit 15) in sv[0..*n_sv).
@@ -644,19 +645,26 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint32_t to0 = test(odd_bytes, v0, u0, d0, l0, r0);   // pixels 1, 3
       const uint32_t te1 = test(even_bytes, v1, u1, d1, l1, r1);  // pixels 4, 6
       const uint32_t to1 = test(odd_bytes, v1, u1, d1, l1, r1);   // pixels 5, 7
-      const int nv = r < dh ? min(dw - 8 * g, 8) : 0;  // valid pixels of the group
-      const bool f0 = nv > 0 && (te0 & 0xffffu), f1 = nv > 1 && (to0 & 0xffffu);
-      const bool f2 = nv > 2 && (te0 >> 16), f3 = nv > 3 && (to0 >> 16);
-      const bool f4 = nv > 4 && (te1 & 0xffffu), f5 = nv > 5 && (to1 & 0xffffu);
-      const bool f6 = nv > 6 && (te1 >> 16), f7 = nv > 7 && (to1 >> 16);
+      // pixel k of the group is valid iff its row is (rv) and, for the row's
+      // tail group (tl), k < tail; g < gpr - 1 groups are whole.  Both masks
+      // come from one compare each, the per-pixel masks from scalar ANDs
+      // (per-pixel nv > k compares cost 8 VALU a group)
+      const bool rv = r < dh, tl = g == gpr - 1;
+      auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
+      const uint64_t mrv = bal(rv), mwhole = mrv & ~bal(tl);
+      auto ok = [&](int k) { return rv && (k < tail || !tl); };
+      auto okm = [&](int k) { return k < tail ? mrv : mwhole; };
+      const bool f0 = ok(0) && (te0 & 0xffffu), f1 = ok(1) && (to0 & 0xffffu);
+      const bool f2 = ok(2) && (te0 >> 16), f3 = ok(3) && (to0 >> 16);
+      const bool f4 = ok(4) && (te1 & 0xffffu), f5 = ok(5) && (to1 & 0xffffu);
+      const bool f6 = ok(6) && (te1 >> 16), f7 = ok(7) && (to1 >> 16);
       // the masks as ANDs of single-compare ballots (scalar ANDs of the
       // compares' lane masks): a ballot of an && rematerialises the bool with
       // a v_cndmask + v_cmp pair per pixel
-      auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
-      const uint64_t m0 = bal(nv > 0) & bal(te0 & 0xffffu), m1 = bal(nv > 1) & bal(to0 & 0xffffu);
-      const uint64_t m2 = bal(nv > 2) & bal(te0 >> 16), m3 = bal(nv > 3) & bal(to0 >> 16);
-      const uint64_t m4 = bal(nv > 4) & bal(te1 & 0xffffu), m5 = bal(nv > 5) & bal(to1 & 0xffffu);
-      const uint64_t m6 = bal(nv > 6) & bal(te1 >> 16), m7 = bal(nv > 7) & bal(to1 >> 16);
+      const uint64_t m0 = okm(0) & bal(te0 & 0xffffu), m1 = okm(1) & bal(to0 & 0xffffu);
+      const uint64_t m2 = okm(2) & bal(te0 >> 16), m3 = okm(3) & bal(to0 >> 16);
+      const uint64_t m4 = okm(4) & bal(te1 & 0xffffu), m5 = okm(5) & bal(to1 & 0xffffu);
+      const uint64_t m6 = okm(6) & bal(te1 >> 16), m7 = okm(7) & bal(to1 >> 16);
       int pos = ns + (int)mbcnt64(m7, mbcnt64(m6, mbcnt64(m5, mbcnt64(m4, mbcnt64(m3, mbcnt64(m2,
                          mbcnt64(m1, mbcnt64(m0, 0u))))))));
       const int i0 = (r << 7) | (8 * g);
