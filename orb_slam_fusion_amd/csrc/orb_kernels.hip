@@ -372,6 +372,9 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
   }
 }
 
+// buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
+constexpr int kBufRsrcWord3 = 0x00020000;
+
 __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
@@ -399,10 +402,17 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
   uint32_t lo_sel[3] = {0, 0, 0}, hi_sel[3] = {0, 0, 0};
   if (edge) blur_window_sel(x, g.w, (int)base, lo_sel, hi_sel);
   uint32_t d[R + 6][3];
+  // the level's height and pitch held in registers: the buffer stores are
+  // opaque to alias analysis and would make them reloaded every row
+  const int gh = g.h, pitch = g.pitch;
+  // raw buffer accesses: the lane's column is the VGPR offset, the row the
+  // SGPR offset, so no per-row 64-bit address arithmetic on the VALU
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(S), (short)0, (int)0xffffffff, kBufRsrcWord3);
   auto load_row = [&](int r) {
-    const uint8_t* row = S + (uint32_t)(reflect101(ys - 3 + r, g.h) * sp);
+    const auto w = __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base, reflect101(ys - 3 + r, gh) * sp, 0);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) d[r][k] = *reinterpret_cast<const uint32_t*>(row + base + 4 * k);
+    for (int k = 0; k < 3; ++k) d[r][k] = w[k];
   };
 #pragma unroll
   for (int r = 0; r < kPf && r < R + 6; ++r) load_row(r);
@@ -416,7 +426,8 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
   const ushort2_t k01 = as_us2(18u | (34u << 16)), k23 = as_us2(48u | (56u << 16));
   const ushort2_t k45 = as_us2(48u | (34u << 16)), k6 = as_us2(18u);
   // columns past w land in the row's pitch padding (pitch is a multiple of 16)
-  uint8_t* D = blur + (size_t)img * P->blur_bytes + g.blur_off + (uint32_t)x;
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      blur + (size_t)img * P->blur_bytes + g.blur_off, (short)0, (int)0xffffffff, kBufRsrcWord3);
   uint32_t hw[R + 6][4];
   uint32_t pr[R + 5][4];  // pr[r] = hw[r] | hw[r+1] << 16
 #pragma unroll
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
       for (int j = 0; j < 4; ++j) pr[r - 1][j] = hw[r - 1][j] | (hw[r][j] << 16);
     if (r >= 6) {
       const int o = r - 6;
-      if (ys + o < g.h) {
+      if (ys + o < gh) {
         uint32_t v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -453,8 +464,9 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
           a = __builtin_amdgcn_udot2(as_us2(pr[o + 4][j]), k45, a, false);
           v[j] = __builtin_amdgcn_udot2(as_us2(hw[o + 6][j]), k6, a, false);
         }
-        *reinterpret_cast<uint32_t*>(D + (uint32_t)((ys + o) * g.pitch)) =
-            __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu),
+            drs, x, (ys + o) * pitch, 0);
       }
     }
   }
