@@ -185,6 +185,9 @@ __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t
   for (int k = 0; k < 4; ++k) hq[k] = h[k] & ~15u;
 }
 
+// buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
+constexpr int kBufRsrcWord3 = 0x00020000;
+
 __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
                                                 const int* __restrict__ rs_tab, ImgSrc src,
                                                 uint8_t* __restrict__ pyr, int l) {
@@ -222,6 +225,10 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && (c1 < sp || (sw & 15) == 0)) {
     const int nq = (c1 < sp ? ncol : min(ncol, sw - c0)) >> 4, total = nrow * nq;
     const uint32_t mg = ((1u << 19) + nq - 1) / nq;
+    // raw buffer loads on the window's first column: one 32-bit VGPR offset
+    // per chunk, no 64-bit address arithmetic
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(S + c0), (short)0, (int)0xffffffff, kBufRsrcWord3);
     for (int i0 = 0; i0 < total; i0 += 1024) {
       uint4 v[4];
       int at[4];
@@ -230,7 +237,9 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
         const int i = min(i0 + 256 * u + (int)threadIdx.x, total - 1);
         // i < 2^13, mg < 2^19: the 24-bit multiply's low word is the product
         const int r = (int)(__umul24((uint32_t)i, mg) >> 19), q = i - __mul24(r, nq);
-        v[u] = *reinterpret_cast<const uint4*>(S + __umul24((uint32_t)(rr0 + r), (uint32_t)sp) + c0 + 16 * q);
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(
+            srs, (int)(__umul24((uint32_t)(rr0 + r), (uint32_t)sp) + 16u * (uint32_t)q), 0, 0);
+        v[u] = make_uint4(w[0], w[1], w[2], w[3]);
         at[u] = __mul24(r, ncol) + 16 * q;  // LDS rows keep the window pitch ncol
       }
 #pragma unroll
@@ -371,9 +380,6 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
     }
   }
 }
-
-// buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
-constexpr int kBufRsrcWord3 = 0x00020000;
 
 __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
