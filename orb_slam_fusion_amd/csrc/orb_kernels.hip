@@ -642,7 +642,10 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
     const ushort2_t th2 = as_us2((uint32_t)th * 0x10001u);
     int ns = 0;
-    for (int r = g_r0, g = g_q0; __builtin_amdgcn_ballot_w64(r < dh) != 0;) {
+    auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
+    for (int r = g_r0, g = g_q0;;) {
+      const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
+      if (mrv == 0) break;
       const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 8 * g;
       // 8 window bytes at row byte o: (lo, hi) dwords
       auto win = [&](const uint8_t* row, int o, uint32_t& lo, uint32_t& hi) {
@@ -668,8 +671,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       // come from one compare each, the per-pixel masks from scalar ANDs
       // (per-pixel nv > k compares cost 8 VALU a group)
       const bool rv = r < dh, tl = g == gpr - 1;
-      auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
-      const uint64_t mrv = bal(rv), mwhole = mrv & ~bal(tl);
+      const uint64_t mwhole = mrv & ~bal(tl);
       auto ok = [&](int k) { return rv && (k < tail || !tl); };
       auto okm = [&](int k) { return k < tail ? mrv : mwhole; };
       const bool f0 = ok(0) && (te0 & 0xffffu), f1 = ok(1) && (to0 & 0xffffu);
