@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "lba_launch.h"
 #include "lds_optin.h"
 #include "pose_math_dev.h"
@@ -787,6 +789,59 @@ __device__ __forceinline__ double rcp_f64(double d) {
   return fma(x, fma(-d, x, 1.0), x);
 }
 
+constexpr int kSolveStageTiles = 7;  // LDS path: n_pad <= 160 -> <= 55 tiles, <= 7 per wave
+
+// ---- DPP64 row broadcasts for the diagonal tile (lane li of every 16-lane
+// row owns row li): v_mov_b64_dpp / v_fmac_f64_dpp with row_newbcast:N read
+// lane N of the lane's row, so an updated entry costs one instruction instead
+// of a v_readlane pair + an FMA.  Inline asm: the compiler forms neither DPP64
+// form itself.  Each block starts with s_nop 1: a VALU write of a VGPR
+// followed by a DPP read of it needs 2 wait states, and a block's inputs may
+// come straight from compiler-scheduled VALU code.
+template <int N>
+__device__ __forceinline__ double row_bcast_f64(double v) {
+  double o;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "=v"(o)
+               : "v"(v), "i"(N));
+  return o;
+}
+
+#define LBA_FMAC_BC(k) "v_fmac_f64_dpp %" #k ", %" #k ", %17 row_newbcast:%18 row_mask:0xf bank_mask:0xf\n\t"
+// Pivot N of the augmented elimination: the 16 entries after the pivot column
+// (aug[N+1 .. N+16] = the rest of the A_KK row, then the first N+1 entries of
+// the inverse row, the only non-zero entries of pivot row N's inverse part)
+// and y take nl = -l_i times lane N's value; aug[N+1] first (the next pivot).
+template <int N>
+__device__ __forceinline__ void pivot_update(double (&aug)[32], double& y, double nl) {
+  asm volatile("s_nop 1\n\t" LBA_FMAC_BC(0) LBA_FMAC_BC(1) LBA_FMAC_BC(2) LBA_FMAC_BC(3) LBA_FMAC_BC(4)
+                   LBA_FMAC_BC(5) LBA_FMAC_BC(6) LBA_FMAC_BC(7) LBA_FMAC_BC(8) LBA_FMAC_BC(9) LBA_FMAC_BC(10)
+                       LBA_FMAC_BC(11) LBA_FMAC_BC(12) LBA_FMAC_BC(13) LBA_FMAC_BC(14) LBA_FMAC_BC(15)
+                           LBA_FMAC_BC(16)
+               : "+v"(aug[N + 1]), "+v"(aug[N + 2]), "+v"(aug[N + 3]), "+v"(aug[N + 4]), "+v"(aug[N + 5]),
+                 "+v"(aug[N + 6]), "+v"(aug[N + 7]), "+v"(aug[N + 8]), "+v"(aug[N + 9]), "+v"(aug[N + 10]),
+                 "+v"(aug[N + 11]), "+v"(aug[N + 12]), "+v"(aug[N + 13]), "+v"(aug[N + 14]),
+                 "+v"(aug[N + 15]), "+v"(aug[N + 16]), "+v"(y)
+               : "v"(nl), "i"(N));
+}
+#undef LBA_FMAC_BC
+
+// Pivots N..15 of the diagonal tile: d_N broadcast from lane N (zero pivot =
+// Eigen's NumericalIssue: flagged, the pivot's multipliers 0), l_i = a_iN / d_N
+// below the pivot, 0 at and above it (those rows are unchanged).
+template <int N>
+__device__ __forceinline__ void diag_pivots(double (&aug)[32], double& y, double& dmine, int& zero, int li) {
+  if constexpr (N < 16) {
+    const double dc = row_bcast_f64<N>(aug[N]);
+    dmine = li == N ? dc : dmine;
+    zero |= dc == 0.0;
+    const double inv = dc != 0.0 ? rcp_f64(dc) : 0.0;
+    const double l = li > N ? aug[N] * inv : 0.0;
+    pivot_update<N>(aug, y, -l);
+    diag_pivots<N + 1>(aug, y, dmine, zero, li);
+  }
+}
+
 #ifdef LBA_SOLVE_STAMPS
 __device__ unsigned long long g_lba_stamps[16];
 #define LBA_STAMP(k)                                                  \
@@ -841,22 +896,72 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   };
   const double* src = a.sys;
   const double* hm = a.himu;  // kModelImu: the IMU links' part of the system (else NULL)
-  // S + lambda I with identity padding (D = 1, L = 0): 16 loads in flight per
-  // thread before the LDS writes
-  for (int e0 = t; e0 < N * N; e0 += 16 * kSolveThreads) {
-    double v[16];
+  if constexpr (kLds) {
+    // S + lambda I (lower tiles) with identity padding (D = 1, L = 0): wave w
+    // stages tiles w, w + 8, ... (tile (I, J) of the row-major enumeration),
+    // a lane 4 consecutive entries of one tile row; every load of the wave in
+    // flight before the LDS writes, no index divisions
+    const int ntile = T * (T + 1) / 2;
+    const int lr = lane >> 2, lc = 4 * (lane & 3);
+    double v[kSolveStageTiles][4];
+    auto tile_of = [&](int q, int& I, int& J) {
+      I = 0;
+      while ((I + 1) * (I + 2) / 2 <= q) ++I;
+      J = q - I * (I + 1) / 2;
+    };
+    auto stage = [&](auto with_imu) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
-      v[u] = e < N * N && r < n && cc < n && (cc >> 4) <= (r >> 4)
-                 ? src[(size_t)r * n + cc] + (hm ? hm[(size_t)r * n + cc] : 0.0)
-                 : 0.0;
+      for (int u = 0; u < kSolveStageTiles; ++u) {
+        const int q = wave + kSolveWaves * u;
+        if (q < ntile) {
+          int I, J;
+          tile_of(q, I, J);
+          const int r = 16 * I + lr, c0 = 16 * J + lc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const size_t o = (size_t)r * n + c0 + e;
+            const bool in = r < n && c0 + e < n;
+            double x = in ? src[o] : 0.0;
+            if constexpr (decltype(with_imu)::value) x += in ? hm[o] : 0.0;
+            v[u][e] = x;
+          }
+        }
+      }
+    };
+    if (hm)
+      stage(std::true_type{});
+    else
+      stage(std::false_type{});
+#pragma unroll
+    for (int u = 0; u < kSolveStageTiles; ++u) {
+      const int q = wave + kSolveWaves * u;
+      if (q < ntile) {
+        int I, J;
+        tile_of(q, I, J);
+        const int r = 16 * I + lr, c0 = 16 * J + lc;
+        double* dst = tile(I, J) + lr * TS + lc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[e] = v[u][e] + (r == c0 + e ? (r < n ? lambda : 1.0) : 0.0);
+      }
     }
+  } else {
+    // S row-major in a.work (n_pad beyond the LDS budget): 16 loads in flight
+    // per thread before the writes
+    for (int e0 = t; e0 < N * N; e0 += 16 * kSolveThreads) {
+      double v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
-      if (e < N * N && (cc >> 4) <= (r >> 4))
-        tile(r >> 4, cc >> 4)[(r & 15) * TS + (cc & 15)] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
+        v[u] = e < N * N && r < n && cc < n && (cc >> 4) <= (r >> 4)
+                   ? src[(size_t)r * n + cc] + (hm ? hm[(size_t)r * n + cc] : 0.0)
+                   : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * kSolveThreads, r = e / N, cc = e - r * N;
+        if (e < N * N && (cc >> 4) <= (r >> 4))
+          tile(r >> 4, cc >> 4)[(r & 15) * TS + (cc & 15)] = v[u] + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
+      }
     }
   }
   for (int r = t; r < N; r += kSolveThreads)
@@ -869,55 +974,28 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     const int k0 = 16 * K;
     double* const SKK = tile(K, K);
     if (wave == 0) {
-      // 1. diagonal tile: lane li owns row li (full symmetric row), right-
-      // looking, the pivot row broadcast by v_readlane; branch-free (rows at
-      // or above the pivot take l = 0)
-      double r[16];
+      // 1-3. the diagonal tile by elimination of the augmented rows
+      // [A_KK | I | y_K] (lane li of every 16-lane row owns row li): pivot c
+      // subtracts l_i = a_ic / d_c times row c from the rows below it, which
+      // leaves D_K on the diagonal, L_KK^-1 in the identity's place and
+      // L_KK^-1 y_K in y -- the factorisation, the inverse and the tile's
+      // forward substitution in one pass of 16 row-broadcast FMAs per pivot
+      double aug[32];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) r[j] = SKK[li * TS + j];
+      for (int j = 0; j < 16; ++j) aug[j] = SKK[li * TS + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
+      double yv = y[k0 + li];
       double dmine = 0;
       int zero = 0;
-#pragma unroll
-      for (int cI = 0; cI < 16; ++cI) {
-        const double dc = readlane_f64(r[cI], cI);
-        dmine = li == cI ? dc : dmine;
-        zero |= dc == 0.0;
-        const double inv = dc != 0.0 ? rcp_f64(dc) : 0.0;
-        const double l = li > cI ? r[cI] * inv : 0.0;
-#pragma unroll
-        for (int j = cI + 1; j < 16; ++j) r[j] = fma(-l, readlane_f64(r[j], cI), r[j]);
-        r[cI] = li > cI ? l : r[cI];
-      }
+      diag_pivots<0>(aug, yv, dmine, zero, li);
       if (lane < 16) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (j < li) SKK[li * TS + j] = r[j];
+        for (int j = 0; j < 16; ++j) Li[(size_t)K * 256 + li * 16 + j] = aug[16 + j];
         Dg[k0 + li] = dmine;
+        y[k0 + li] = yv;
       }
-      __threadfence_block();  // the rows are re-read by the other lanes
       LBA_STAMP(1);
-      // 2. L_KK^-1, column li, column-oriented (one FMA latency per step),
-      // the rows of L read back with one address per step (LDS broadcast)
-      double x[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) x[i] = i == li ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < 15; ++k)
-#pragma unroll
-        for (int i = k + 1; i < 16; ++i) x[i] = fma(-SKK[i * TS + k], x[k], x[i]);
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) Li[(size_t)K * 256 + i * 16 + li] = x[i];
-      }
-      // 3. this tile's forward substitution y_K = L_KK^-1 y_K: lane li holds
-      // y_li, the solved entries broadcast
-      double yv = y[k0 + li];
-#pragma unroll
-      for (int j = 0; j < 15; ++j) {
-        const double yj = readlane_f64(yv, j);
-        yv = li > j ? fma(-r[j], yj, yv) : yv;
-      }
-      if (lane < 16) y[k0 + li] = yv;
       if (lane == 0 && zero) bad = 1;
     }
     __syncthreads();

@@ -121,9 +121,9 @@ orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
                      hipMemcpyHostToDevice, h->stream) ||
       hipStreamSynchronize(h->stream))
     return ORBGPU_ERR_DEVICE;
-  // the opt-in is per kernel, not per handle: grant the CU's whole LDS so that
-  // handles with different plans never shrink each other's limit
-  if (set_lds_limits(160 * 1024, 160 * 1024) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  // the plan's own LDS needs (the plan checked both against 160 KB; a device
+  // with less LDS per workgroup refuses only the plans that need more)
+  if (set_lds_limits(octree_lds_bytes(p.hdr), (size_t)p.hdr.rs_lds) != hipSuccess) return ORBGPU_ERR_DEVICE;
   h->plan = std::move(p);
   h->plan_w = w;
   h->plan_h = ht;

@@ -1482,6 +1482,7 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
 // ==========================================================================
 // Host launchers (same translation unit as the kernels).
 // ==========================================================================
+#include "lds_optin.h"
 #include "orb_launch.h"
 
 namespace orbgpu {
@@ -1524,12 +1525,16 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// The plan's own LDS needs, raised per (kernel, device) only as far as a plan
+// asks (lds_optin never lowers a grant, so handles with different plans never
+// shrink each other's limit); sizes up to 64 KB need no opt-in.
 hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)octree_bytes);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_resize, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)resize_bytes);
+  if (octree_bytes > 64 * 1024) {
+    const hipError_t e = lds_optin((const void*)k_octree, (int)octree_bytes);
+    if (e != hipSuccess) return e;
+  }
+  if (resize_bytes > 64 * 1024) return lds_optin((const void*)k_resize, (int)resize_bytes);
+  return hipSuccess;
 }
 
 }  // namespace orbgpu

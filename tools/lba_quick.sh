@@ -1,4 +1,3 @@
-# LBA / LocalInertialBA parity + timing (one gpurun call)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 5 60 ./build/lba_solve_bench 18 200 || exit 1

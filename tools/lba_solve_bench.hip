@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
     err = std::fmax(err, std::fabs(xg[i] - x[i]));
     nrm = std::fmax(nrm, std::fabs(x[i]));
   }
-  const char* names[8] = {"load", "factor", "linv+fwd", "panel", "trailing", "dinv", "backward", "scale"};
+  const char* names[8] = {"load", "diag", "diag_sync", "panel", "trailing", "dinv", "backward", "scale"};
   std::printf("{\"n\": %d, \"lds\": %d, \"us_per_solve\": %.2f, \"max_rel_err\": %.3e, \"clocks_per_solve\": {",
               n, in_lds ? 1 : 0, ms * 1e3 / reps, err / nrm);
   for (int k = 0; k < 8; ++k)
