@@ -23,6 +23,8 @@ typedef int orbgpu_status;
 #define ORBGPU_ERR_CAPACITY (-3) /* caller buffer or internal bound too small  */
 #define ORBGPU_ERR_DEVICE (-4)   /* HIP runtime error                          */
 #define ORBGPU_ERR_NOMEM (-5)
+#define ORBGPU_ERR_UNSUPPORTED (-6) /* valid for the reference, outside what the GPU path
+                                       implements: the caller runs the CPU code instead */
 
 /* OrbExtractor(int num_feats, float scale_factor, int num_levs,
  *              int ini_th_fast, int min_th_fast)
@@ -58,6 +60,17 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h);
 orbgpu_status orbgpu_extractor_scales(const orbgpu_extractor* h, float* scale, float* inv_scale,
                                       float* sigma2, float* inv_sigma2);
 int orbgpu_extractor_levels(const orbgpu_extractor* h);
+/* The resize vertical pass's rounding (the least certain OpenCV
+ * rule: which columns take VResizeLinearVec_32s8u's SIMD rounding depends on
+ * the OpenCV build).  ORBGPU_RESIZE_SSE (default): OpenCV 4.5.4 with 128-bit
+ * universal intrinsics -- 16-lane blocks while x <= w-16, 8-lane blocks while
+ * x < w-8, FixedPtCast<int, uchar, 22> after; ORBGPU_RESIZE_SCALAR: every
+ * column FixedPtCast (a build without the vectorised pass).  Re-plans the
+ * handle; pinning parity against a real OpenCV is this one switch. */
+#define ORBGPU_RESIZE_SSE 0
+#define ORBGPU_RESIZE_SCALAR 1
+orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode);
+
 /* Upper bound on keypoints one image can produce at the given geometry. */
 int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height);
 
@@ -230,6 +243,14 @@ typedef int (*orbgpu_lba_reduce_fn)(void* user, double* d_buf, int n, int op, vo
 
 orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out);
 void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
+
+/* Bounds of the device solver: the reduced camera system of 6 rows per free
+ * key frame is factorised by one workgroup, packed in LDS up to 160 rows and
+ * in HBM beyond, with D and the right-hand side in LDS (16 bytes per row of
+ * the 16-padded system, at most 160 KB).  A window with more free key frames
+ * returns ORBGPU_ERR_CAPACITY before any device work (the C++ drop-in then
+ * runs the reference's CPU LocalBundleAdjustment). */
+#define ORBGPU_LBA_MAX_FREE_KF 1706 /* 6 * 1706 <= 10240 reduced rows */
 
 /* One window from host buffers.  Keyframe k is fixed iff fixed[k] (the map's
  * initial keyframe, :1161, and every fixed camera, :1169-1183).  Points
@@ -698,6 +719,14 @@ typedef struct orbgpu_lia_imu_edge {
  * stats (optional, 7 doubles): err = the robust chi2 before optimize()
  * (:2790-2791), err_end = the robust chi2 of the last computed errors
  * (:2793), LM iterations, trials, final lambda, outliers, accepted chi2. */
+/* Bounds of orbgpu_lia_optimize: 15 reduced rows per free key frame
+ * (ORBGPU_LIA_MAX_FREE_KF, the solver bound above) and at most
+ * ORBGPU_LIA_MAX_IMU_LINKS inertial links -> ORBGPU_ERR_CAPACITY; a free key
+ * frame without IMU vertices (imu[k] == 0: the reference's VertexPose-only
+ * key frame, optimizer.cc:2466-2484) -> ORBGPU_ERR_UNSUPPORTED.  Both are
+ * reported before any device work; the drop-in runs the CPU optimiser. */
+#define ORBGPU_LIA_MAX_FREE_KF 682
+#define ORBGPU_LIA_MAX_IMU_LINKS 64
 orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* c, const orbgpu_imu_calib* calib, int n_kf,
                                   const orbgpu_imu_state* kfs, const uint8_t* fixed,
                                   const uint8_t* imu, int n_pts, const float* pts_in,

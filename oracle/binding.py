@@ -45,6 +45,8 @@ def lib() -> ctypes.CDLL:
         "orc_level_copy": (None, [_P, _I, _I, _P]),
         "orc_stage": (_I, [_P, _I, _I, _P, _I]),
         "orc_resize": (None, [_P, _I, _I, _P, _I, _I]),
+        "orc_set_resize_rounding": (None, [_I]),
+        "orc_get_resize_rounding": (_I, []),
         "orc_gauss": (None, [_P, _I, _I, _P]),
         "orc_gauss_kernel": (None, [_P]),
         "orc_fast": (_I, [_P, _I, _I, _I, _I, _P, _I]),
@@ -57,7 +59,7 @@ def lib() -> ctypes.CDLL:
         "orc_stereo_match": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
                                   _P, _P]),
         "orc_lba": (_I, [_P, _I, _P, _P, _I, _P, _I, _P, _I, _I, _I, ctypes.c_double, _I,
-                         LBA_REDUCE_FN, _P, _P, _P, _P, _P]),
+                         LBA_REDUCE_FN, _P, _P, _P, _P, _P, _P]),
         "orc_search_last": (_I, [_P, _P, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I, _F, _I, _I, _P]),
         "orc_frustum": (None, [_P, _P, _P, _P, _P, _P, _I, _F, _P]),
         "orc_search_kf": (_I, [_P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _I, _I, _P]),
@@ -76,7 +78,7 @@ def lib() -> ctypes.CDLL:
         "orc_pose_inertial_ex": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
         "orc_sym_pinv": (None, [_P, _I, _P]),
         "orc_lia": (_I, [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _P, _I, ctypes.c_double, _P,
-                         _P, _P, _P]),
+                         _P, _P, _P, _P]),
         "orc_lia_system": (_I, [_P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _P, _P]),
         "orc_lia_vis_linearize": (None, [_P, _P, _P, _P, _P, _P, _P]),
     }
@@ -149,6 +151,27 @@ class OracleExtractor:
         return buf[:n].copy()
 
 
+RESIZE_SSE, RESIZE_SCALAR = 0, 1
+
+
+class resize_rounding:
+    """Context manager: the oracle's resize vertical-pass rounding
+    for the duration of a block -- RESIZE_SSE (OpenCV 4.5.4, 128-bit SIMD
+    body + scalar tail; the default) or RESIZE_SCALAR (every column scalar)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = lib().orc_get_resize_rounding()
+        lib().orc_set_resize_rounding(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_resize_rounding(self.prev)
+        return False
+
+
 def resize(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
     src = np.ascontiguousarray(src, np.uint8)
     out = np.zeros((dh, dw), np.uint8)
@@ -215,7 +238,8 @@ def lba(problem, iters: int = 10, pt_range=None, reduce=None, lambda_init: float
     setUserLambdaInit; stop_after_trials >= 0: terminate() turns true once
     that many LM trials have run.  Returns dict with
     poses [n_kf, 7] f64, pts [n_pts, 3] f64 (shard rows only), outlier [E] u8
-    (shard edges only), stats [6]."""
+    (shard edges only), chi2 [E] f64 (each edge's chi2 at the classification:
+    the last computeActiveErrors), stats [6]."""
     cam = np.ascontiguousarray(problem.cam, np.float32)
     poses = np.ascontiguousarray(problem.poses_init, np.float32)
     fixed = np.ascontiguousarray(problem.fixed, np.uint8)
@@ -226,6 +250,7 @@ def lba(problem, iters: int = 10, pt_range=None, reduce=None, lambda_init: float
     po = np.zeros((n_kf, 7), np.float64)
     xo = np.zeros((n_pts, 3), np.float64)
     out = np.zeros(max(ne, 1), np.uint8)
+    chi = np.zeros(max(ne, 1), np.float64)
     st = np.zeros(6, np.float64)
     if reduce is None:
         cb = LBA_REDUCE_FN(0)
@@ -240,10 +265,10 @@ def lba(problem, iters: int = 10, pt_range=None, reduce=None, lambda_init: float
         cb = LBA_REDUCE_FN(_cb)
     rc = lib().orc_lba(_p(cam), n_kf, _p(poses), _p(fixed), n_pts, _p(pts), ne, _p(edges), b, e,
                        iters, float(lambda_init), int(stop_after_trials), cb, None, _p(po), _p(xo),
-                       _p(out), _p(st))
+                       _p(out), _p(st), _p(chi))
     if rc != 0:
         raise RuntimeError(f"orc_lba failed ({rc})")
-    return {"poses": po, "pts": xo, "outlier": out[:ne].copy(), "stats": st}
+    return {"poses": po, "pts": xo, "outlier": out[:ne].copy(), "chi2": chi[:ne].copy(), "stats": st}
 
 
 def lba_edge_linearize(cam, pose7, X, edge):
@@ -484,19 +509,21 @@ def sym_pinv(A: np.ndarray) -> np.ndarray:
 def lia(pb, iterations=None, lambda_init=None):
     """LocalInertialBA's solve (oracle/lia_oracle.cc) on a synth.LiaProblem:
     -> dict(kfs21 float64 [n_kf, 21] (Rwb, twb, v, bg, ba), pts float64
-    [n_pts, 3], outlier uint8 [E], stats float64 [7])."""
+    [n_pts, 3], outlier uint8 [E], chi2 float64 [E] (each edge's chi2 at the
+    classification), stats float64 [7])."""
     n_kf, n_p, ne, ni = len(pb.kfs), len(pb.pts_init), len(pb.edges), len(pb.imu_edges)
     ko = np.zeros((n_kf, 21))
     po = np.zeros((n_p, 3))
     out = np.zeros(max(ne, 1), np.uint8)
+    chi = np.zeros(max(ne, 1))
     st = np.zeros(7)
     it = pb.iterations if iterations is None else iterations
     lam = pb.lambda_init if lambda_init is None else lambda_init
     r = lib().orc_lia(_p(pb.calib), n_kf, _p(pb.kfs), _p(pb.fixed), _p(pb.imu), n_p,
                       _p(pb.pts_init), _p(pb.close), ne, _p(pb.edges), ni, _p(pb.imu_edges), it,
-                      float(lam), _p(ko), _p(po), _p(out), _p(st))
+                      float(lam), _p(ko), _p(po), _p(out), _p(st), _p(chi))
     assert r == 0, "orc_lia rejected the problem"
-    return dict(kfs21=ko, pts=po, outlier=out[:ne].copy(), stats=st)
+    return dict(kfs21=ko, pts=po, outlier=out[:ne].copy(), chi2=chi[:ne].copy(), stats=st)
 
 
 def lia_system(pb):

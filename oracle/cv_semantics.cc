@@ -20,6 +20,8 @@ inline uint8_t sat_u8(int v) { return (uint8_t)std::min(std::max(v, 0), 255); }
 inline int16_t sat_s16(int v) { return (int16_t)std::min(std::max(v, -32768), 32767); }
 }  // namespace
 
+int g_resize_rounding = kResizeSse;
+
 void resize_linear_u8(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst,
                       int dw, int dh, int dstride) {
   // Scale factors exactly as cv::resize derives them from the sizes.
@@ -73,10 +75,12 @@ void resize_linear_u8(const uint8_t* src, int sw, int sh, int sstride, uint8_t* 
       return sat_u8((s + 2) >> 2);
     };
     int x = 0;
-    for (; x <= dw - 16; x += 16)
-      for (int k = 0; k < 16; ++k) D[x + k] = vec_px(x + k);
-    for (; x < dw - 8; x += 8)
-      for (int k = 0; k < 8; ++k) D[x + k] = vec_px(x + k);
+    if (g_resize_rounding == kResizeSse) {
+      for (; x <= dw - 16; x += 16)
+        for (int k = 0; k < 16; ++k) D[x + k] = vec_px(x + k);
+      for (; x < dw - 8; x += 8)
+        for (int k = 0; k < 8; ++k) D[x + k] = vec_px(x + k);
+    }
     // Scalar tail: FixedPtCast<int, uchar, 22>.
     for (; x < dw; ++x) D[x] = sat_u8((row0[x] * b0 + row1[x] * b1 + (1 << 21)) >> 22);
   }

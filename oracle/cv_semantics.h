@@ -35,6 +35,15 @@ struct FastCorner {
 // OPENCV-4.5.4 SEMANTICS: resize(src, dst, dsize, 0, 0, INTER_LINEAR), 8UC1,
 // non-integer downscale (hal::resize -> resizeGeneric_ with HResizeLinear and
 // VResizeLinear + VResizeLinearVec_32s8u at 128-bit universal intrinsics).
+// The vertical pass's rounding is the least certain rule: which
+// columns take the SIMD body's rounding depends on how OpenCV was built.
+// g_resize_rounding selects it: kResizeSse (default: 16-lane blocks while
+// x <= w-16, 8-lane blocks while x < w-8, the scalar FixedPtCast tail after)
+// or kResizeScalar (a build without the vectorised VResizeLinear: every
+// column FixedPtCast<int, uchar, 22>).  Test infrastructure: set it only
+// between extractions.
+enum { kResizeSse = 0, kResizeScalar = 1 };
+extern int g_resize_rounding;
 void resize_linear_u8(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst,
                       int dw, int dh, int dstride);
 

@@ -209,7 +209,7 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
                  int n_pts, const float* pts, int n_edges, const LbaEdge* edges, int pt_begin,
                  int pt_end, int iters, double lambda_init, int stop_after_trials,
                  LbaReduceFn reduce, void* user, double* poses_out, double* pts_out,
-                 uint8_t* outlier, double* stats) {
+                 uint8_t* outlier, double* stats, double* chi2_out = nullptr) {
   const Cam c{cam5[0], cam5[1], cam5[2], cam5[3], cam5[4]};
   if (n_kf <= 0 || n_pts < 0 || pt_begin < 0 || pt_end > n_pts || pt_begin > pt_end) return -1;
   auto red = [&](double* buf, int n, int op) { return reduce ? reduce(user, buf, n, op) : 0; };
@@ -440,6 +440,7 @@ int lba_optimize(const float cam5[5], int n_kf, const float* poses, const uint8_
       const double chi = edge_chi2(e, &err[(size_t)3 * i]);
       const bool out = chi > (e.ur < 0 ? 5.991 : 7.815) || !depth_ok;
       outlier[i] = out ? 1 : 0;
+      if (chi2_out) chi2_out[i] = chi;
       n_out += out;
     }
   for (int k = 0; k < n_kf; ++k) {
@@ -465,11 +466,11 @@ extern "C" int orc_lba(const float* cam5, int n_kf, const float* poses, const ui
                        int n_pts, const float* pts, int n_edges, const void* edges, int pt_begin,
                        int pt_end, int iters, double lambda_init, int stop_after_trials,
                        oracle::LbaReduceFn reduce, void* user, double* poses_out, double* pts_out,
-                       uint8_t* outlier, double* stats) {
+                       uint8_t* outlier, double* stats, double* chi2_out) {
   return oracle::lba_optimize(cam5, n_kf, poses, fixed, n_pts, pts, n_edges,
                               static_cast<const oracle::LbaEdge*>(edges), pt_begin, pt_end, iters,
                               lambda_init, stop_after_trials, reduce, user, poses_out, pts_out,
-                              outlier, stats);
+                              outlier, stats, chi2_out);
 }
 
 // Edge linearisation probe for the finite-difference tests: error (3),

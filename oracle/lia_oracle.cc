@@ -202,7 +202,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
                  const uint8_t* close, int n_edges, const VisEdge* edges, int n_imu,
                  const orbgpu_lia_imu_edge* imu_edges, int iters, double lambda_init,
                  double* kfs_out, double* pts_out, uint8_t* outlier, double* stats,
-                 double* sys_H = nullptr, double* sys_b = nullptr) {
+                 double* sys_H = nullptr, double* sys_b = nullptr, double* chi2_out = nullptr) {
   if (n_kf <= 0 || n_pts < 0 || n_edges < 0 || n_imu < 0 || !(lambda_init > 0)) return -1;
   const Calib c = load_calib(cb);
   const V3 g = gravity();
@@ -484,6 +484,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
         out = chi > th_stereo;
       }
       outlier[i] = out ? 1 : 0;
+      if (chi2_out) chi2_out[i] = chi;
       n_out += out;
     }
   for (int k = 0; k < n_kf; ++k) {
@@ -514,11 +515,12 @@ extern "C" int orc_lia(const orbgpu_imu_calib* cb, int n_kf, const orbgpu_imu_st
                        const uint8_t* fixed, const uint8_t* imu, int n_pts, const float* pts,
                        const uint8_t* close, int n_edges, const void* edges, int n_imu,
                        const orbgpu_lia_imu_edge* imu_edges, int iters, double lambda_init,
-                       double* kfs_out, double* pts_out, uint8_t* outlier, double* stats) {
+                       double* kfs_out, double* pts_out, uint8_t* outlier, double* stats,
+                       double* chi2_out) {
   return oracle::lia::lia_optimize(*cb, n_kf, kfs, fixed, imu, n_pts, pts, close, n_edges,
                                    static_cast<const oracle::lia::VisEdge*>(edges), n_imu,
                                    imu_edges, iters, lambda_init, kfs_out, pts_out, outlier,
-                                   stats);
+                                   stats, nullptr, nullptr, chi2_out);
 }
 
 extern "C" int orc_lia_system(const orbgpu_imu_calib* cb, int n_kf, const orbgpu_imu_state* kfs,

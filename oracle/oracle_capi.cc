@@ -106,6 +106,9 @@ int orc_stage(void* h, int lev, int which, float* xyr, int cap) {
 void orc_resize(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh) {
   oracle::resize_linear_u8(src, sw, sh, sw, dst, dw, dh, dw);
 }
+// 0 = SSE body + scalar tail (default), 1 = scalar everywhere.
+void orc_set_resize_rounding(int mode) { oracle::g_resize_rounding = mode; }
+int orc_get_resize_rounding() { return oracle::g_resize_rounding; }
 void orc_gauss(const uint8_t* src, int w, int h, uint8_t* dst) {
   oracle::gaussian7_sigma2_u8(src, w, h, w, dst, w);
 }

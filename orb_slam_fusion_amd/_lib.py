@@ -22,6 +22,12 @@ ORBGPU_ERR_EMPTY = -2
 ORBGPU_ERR_CAPACITY = -3
 ORBGPU_ERR_DEVICE = -4
 ORBGPU_ERR_NOMEM = -5
+ORBGPU_ERR_UNSUPPORTED = -6
+ORBGPU_RESIZE_SSE = 0
+ORBGPU_RESIZE_SCALAR = 1
+ORBGPU_LBA_MAX_FREE_KF = 1706
+ORBGPU_LIA_MAX_FREE_KF = 682
+ORBGPU_LIA_MAX_IMU_LINKS = 64
 
 STATUS_NAMES = {
     ORBGPU_OK: "OK",
@@ -30,6 +36,7 @@ STATUS_NAMES = {
     ORBGPU_ERR_CAPACITY: "CAPACITY",
     ORBGPU_ERR_DEVICE: "DEVICE",
     ORBGPU_ERR_NOMEM: "NOMEM",
+    ORBGPU_ERR_UNSUPPORTED: "UNSUPPORTED",
 }
 
 
@@ -163,6 +170,7 @@ SIGNATURES = {
     "orbgpu_extractor_scales": (_I, [_P, _P, _P, _P, _P]),
     "orbgpu_extractor_levels": (_I, [_P]),
     "orbgpu_extractor_max_keypoints": (_I, [_P, _I, _I]),
+    "orbgpu_extractor_set_resize_rounding": (_I, [_P, _I]),
     "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "orbgpu_extractor_pyramid_level": (_I, [_P, _I, ctypes.POINTER(_P), _P, _P, _P]),
     "orbgpu_extract_batch": (

@@ -102,8 +102,10 @@ __device__ __forceinline__ void wave_sync() {
 
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp_d(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  // full row mask: bound_ctrl reads 0 for out-of-range sources, so the
+  // destination needs no zeroed old value (one v_mov_b32_dpp per half)
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double wave_sum63(double v) {  // lane 63 holds the sum
@@ -475,6 +477,53 @@ __device__ bool ldlt_wave(InShared& sh, int lane) {
   return true;
 }
 
+#include "inertial_gj.inc"
+
+// The same system by Gauss-Jordan elimination (tools/gen_inertial_gj.py):
+// wave 0, lane li of each 16-lane row owns permuted rows li and li + 16 with
+// b appended, pivot k's row read by DPP64 row broadcast (one v_fmac_f64_dpp
+// per entry, no v_readlane chains, no substitution passes).  Same pivot order
+// and pivots as ldlt_wave (the rows below a pivot are eliminated alike; the
+// rows above cost nothing extra in this layout), x_i = b'_i / D_i with Eigen's
+// tolerance.  A negative pivot: not positive; a zero pivot: ldlt_wave, which
+// keeps Eigen's semantics for it.
+template <int n>
+__device__ bool gj_wave(InShared& sh, int lane) {
+  const double dl = lane < n ? fabs(sh.H[lane * kLd + lane]) : -1.0;
+  if (lane < n) sh.temp[lane] = dl;
+  wave_sync();
+  int rank = 0;
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    const double dj = sh.temp[j];
+    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
+  }
+  if (lane < n) sh.perm[rank] = lane;
+  wave_sync();
+  const int pl = lane < n ? sh.perm[lane] : 0;
+  const int li = lane & 15, ia = li, ib = li + 16;
+  const int pa = ia < n ? sh.perm[ia] : 0, pb = ib < n ? sh.perm[ib] : 0;
+  double rA[n + 1], rB[n + 1];
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    const int pj = __builtin_amdgcn_readlane(pl, j);
+    rA[j] = ia < n ? sh.H[max(pa, pj) * kLd + min(pa, pj)] : 0.0;
+    rB[j] = ib < n ? sh.H[max(pb, pj) * kLd + min(pb, pj)] : 0.0;
+  }
+  rA[n] = ia < n ? sh.b[pa] : 0.0;
+  rB[n] = ib < n ? sh.b[pb] : 0.0;
+  double dA = 1.0, dB = 1.0;
+  const int f = gj_pivots<n>(rA, rB, li, dA, dB);
+  if (f & 1) return false;
+  if (f & 2) return ldlt_wave<n>(sh, lane);
+  constexpr double kTiny = 1.0 / 1.79769313486231570815e+308;
+  if (lane < 16) {
+    if (ia < n) sh.x[pa] = fabs(dA) > kTiny ? rA[n] / dA : 0.0;
+    if (ib < n) sh.x[pb] = fabs(dB) > kTiny ? rB[n] / dB : 0.0;
+  }
+  return true;
+}
+
 __device__ __forceinline__ void load_state(StateD& s, const orbgpu_imu_state& g) {
   for (int i = 0; i < 9; ++i) {
     s.Rwb[i] = g.Rwb[i];
@@ -620,7 +669,7 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       __syncthreads();
       ISTAMP(1);
       if (wave == 0) {
-        const bool ok = ldlt_wave<n>(sh, lane);
+        const bool ok = gj_wave<n>(sh, lane);
         if (lane == 0) {
 #pragma unroll
           for (int i = 0; i < 9; ++i) sh.ev_Rcw[i] = sh.cur.Rcw[i];

@@ -151,7 +151,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     }
   const int n = m.pdim * nf;
   const int npad = (n + 15) / 16 * 16;
-  if (npad > 2048) return ORBGPU_ERR_INVALID;  // reduced system beyond the solver's LDS vectors
+  // the solver keeps D and the right-hand side in LDS (16 B per padded row)
+  if (16 * (size_t)npad > kLdsBudget) return ORBGPU_ERR_CAPACITY;
   const int np = pt_end - pt_begin;
   std::vector<int> cnt(np + 1, 0);
   for (int i = 0; i < n_edges; ++i) {
@@ -219,7 +220,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const size_t c_err = take(3 * E), c_hpl = take(18 * E), c_hppe = take(27 * E), c_hlle = take(12 * E),
                c_hll = take(9 * P), c_bl = take(3 * P), c_hpp = take(36 * F), c_bp = take(6 * F),
                c_diag = take(n + 2), c_sys = take((size_t)n * n + 2 * n + 2),
-               c_work = take(solve_lds ? 2 : (size_t)npad * (npad + 1) + (size_t)(npad / 16) * 256),
+               c_work = take(solve_lds ? 2 : (size_t)npad * (npad + 1) + (size_t)(npad / 16) * 272),  // S + the L_KK^-1 tiles (16 x 17)
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
                c_itot = take(2);
@@ -458,6 +459,11 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   ModelIn m;
   m.state0 = s0.data();
   WindowOut wo;
+  static_assert(6 * ORBGPU_LBA_MAX_FREE_KF <= kLdsBudget / 16 && 6 * (ORBGPU_LBA_MAX_FREE_KF + 1) > kLdsBudget / 16,
+                "ORBGPU_LBA_MAX_FREE_KF is the solver's bound");
+  static_assert(15 * ORBGPU_LIA_MAX_FREE_KF <= kLdsBudget / 16 && 15 * (ORBGPU_LIA_MAX_FREE_KF + 1) > kLdsBudget / 16,
+                "ORBGPU_LIA_MAX_FREE_KF is the solver's bound");
+  static_assert(ORBGPU_LIA_MAX_IMU_LINKS == kMaxImuLinks, "link bound");
   const orbgpu_status r = run_window(h, cam, n_kf, fixed, n_pts, pts_in, n_edges, edges, pt_begin, pt_end,
                                      iterations, lambda_init, stop_flag, reduce, user, m, pts_out, outlier, wo);
   if (r != ORBGPU_OK) return r;
@@ -492,11 +498,17 @@ orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* h, const orbgpu_imu_calib* cal
                                   float* pts_out, uint8_t* outlier, double* stats) {
   if (!h || !calib || n_kf <= 0 || !kfs || !fixed || !imu || n_pts < 0 || n_edges < 0 ||
       (n_edges > 0 && !edges) || (n_pts > 0 && (!pts_in || !pts_out || !close)) || n_imu < 0 ||
-      n_imu > kMaxImuLinks || (n_imu > 0 && !imu_edges) || iterations < 0 || !(lambda_init > 0) ||
-      !kfs_out || (n_edges > 0 && !outlier))
+      (n_imu > 0 && !imu_edges) || iterations < 0 || !(lambda_init > 0) || !kfs_out ||
+      (n_edges > 0 && !outlier))
     return ORBGPU_ERR_INVALID;
-  for (int k = 0; k < n_kf; ++k)
-    if (!fixed[k] && !imu[k]) return ORBGPU_ERR_INVALID;  // a free key frame carries its IMU vertices
+  if (n_imu > kMaxImuLinks) return ORBGPU_ERR_CAPACITY;
+  int n_free = 0;
+  for (int k = 0; k < n_kf; ++k) {
+    n_free += !fixed[k];
+    // a free key frame without IMU vertices (VertexPose only, optimizer.cc:2466-2484)
+    if (!fixed[k] && !imu[k]) return ORBGPU_ERR_UNSUPPORTED;
+  }
+  if (n_free > ORBGPU_LIA_MAX_FREE_KF) return ORBGPU_ERR_CAPACITY;
   for (int l = 0; l < n_imu; ++l) {
     const orbgpu_lia_imu_edge& e = imu_edges[l];
     if (e.kf1 < 0 || e.kf1 >= n_kf || e.kf2 < 0 || e.kf2 >= n_kf || e.kf1 == e.kf2 || !imu[e.kf1] ||

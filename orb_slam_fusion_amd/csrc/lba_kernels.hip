@@ -292,9 +292,17 @@ __device__ __forceinline__ double inv3_lambda(const double* __restrict__ h, doub
 // range or whose row is masked off read 0.
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  // full row mask: bound_ctrl reads 0 for out-of-range sources, so the
+  // destination needs no zeroed old value (one v_mov_b32_dpp per half)
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
   return __hiloint2double(hi, lo);
+}
+
+// The wave's own LDS writes visible to its other lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
 }
 
 // Fixed-tree sum of K doubles over a 256-thread block; valid in every thread.
@@ -842,6 +850,47 @@ __device__ __forceinline__ void diag_pivots(double (&aug)[32], double& y, double
   }
 }
 
+// The same elimination with each pivot's reciprocal chain interleaved into
+// the previous pivot's FMAs: block N applies pivot N (l = l_N, subtracted)
+// and, between its 17 row-broadcast FMAs, forms pivot N+1 -- the broadcast
+// d_{N+1} (read two FMAs after its column entry is final), v_rcp_f64 + one
+// Newton step, and l_{N+1} = [i > N+1] a_{i,N+1} / d_{N+1}.  No zero-pivot
+// guard: a zero pivot gives infinities, and the caller then redoes the tile
+// with diag_pivots (which keeps Eigen's NumericalIssue semantics).
+#define LBA_FMC(k) "v_fmac_f64_dpp %" #k ", %" #k ", -%[l] row_newbcast:%[n] row_mask:0xf bank_mask:0xf\n\t"
+template <int N>  // N <= 14
+__device__ __forceinline__ void pivot_step(double (&aug)[32], double& y, double l, double m01, double& d,
+                                           double& lnext) {
+  double inv, e, tt;
+  asm volatile("s_nop 1\n\t" LBA_FMC(0)                        // a_{i,N+1}: the next pivot column
+               "v_mul_f64 %[t], %0, %[m]\n\t" LBA_FMC(1) LBA_FMC(2)  //
+               "v_mov_b64_dpp %[d], %0 row_newbcast:%[n1] row_mask:0xf bank_mask:0xf\n\t" LBA_FMC(3)
+               "v_rcp_f64 %[inv], %[d]\n\t" LBA_FMC(4) LBA_FMC(5)  //
+               "v_fma_f64 %[e], -%[d], %[inv], 1.0\n\t" LBA_FMC(6)   //
+               "v_fma_f64 %[inv], %[inv], %[e], %[inv]\n\t" LBA_FMC(7)
+               "v_mul_f64 %[ln], %[t], %[inv]\n\t" LBA_FMC(8) LBA_FMC(9) LBA_FMC(10) LBA_FMC(11) LBA_FMC(12)
+                   LBA_FMC(13) LBA_FMC(14) LBA_FMC(15) LBA_FMC(16)
+               : "+v"(aug[N + 1]), "+v"(aug[N + 2]), "+v"(aug[N + 3]), "+v"(aug[N + 4]), "+v"(aug[N + 5]),
+                 "+v"(aug[N + 6]), "+v"(aug[N + 7]), "+v"(aug[N + 8]), "+v"(aug[N + 9]), "+v"(aug[N + 10]),
+                 "+v"(aug[N + 11]), "+v"(aug[N + 12]), "+v"(aug[N + 13]), "+v"(aug[N + 14]),
+                 "+v"(aug[N + 15]), "+v"(aug[N + 16]), "+v"(y), [d] "=&v"(d), [inv] "=&v"(inv), [e] "=&v"(e),
+                 [t] "=&v"(tt), [ln] "=&v"(lnext)
+               : [l] "v"(l), [m] "v"(m01), [n] "i"(N), [n1] "i"(N + 1));
+}
+#undef LBA_FMC
+
+template <int N>
+__device__ __forceinline__ void diag_chain(double (&aug)[32], double& y, double l, double& dmine, int li) {
+  if constexpr (N < 15) {
+    double d, ln;
+    pivot_step<N>(aug, y, l, li > N + 1 ? 1.0 : 0.0, d, ln);
+    dmine = li == N + 1 ? d : dmine;
+    diag_chain<N + 1>(aug, y, ln, dmine, li);
+  } else {
+    pivot_update<15>(aug, y, -l);
+  }
+}
+
 #ifdef LBA_SOLVE_STAMPS
 __device__ unsigned long long g_lba_stamps[16];
 #define LBA_STAMP(k)                                                  \
@@ -866,7 +915,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   const double lambda = c.lambda;
   const int n = a.n_sys, N = a.n_pad, LD = N + 1, T = N >> 4;
   const int TS = kLds ? kTileLd : LD;  // row stride inside a tile
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = lane & 15, lk = lane >> 4;
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15, lk = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar loops
 #ifdef LBA_SOLVE_STAMPS
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -874,13 +924,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   double* Li;
   double* Dg;
   double* y;
+  double* Wscr = nullptr;  // kLds: a transposition tile per wave
   __shared__ double red[kSolveWaves];
   __shared__ int bad;
   if constexpr (kLds) {
     S = smem;
     Li = smem + (size_t)(T * (T + 1) / 2) * kTileSz;
-    Dg = Li + (size_t)T * 256;
+    Dg = Li + (size_t)T * kTileSz;
     y = Dg + N;
+    Wscr = y + N;
   } else {
     S = a.work;
     Li = a.work + (size_t)N * LD;
@@ -970,91 +1022,240 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   __syncthreads();
   LBA_STAMP(0);
 
-  for (int K = 0; K < T; ++K) {
+  // 1-3. the diagonal tile K by elimination of the augmented rows
+  // [A_KK | I | y_K] (lane li of every 16-lane row owns row li): pivot c
+  // subtracts l_i = a_ic / d_c times row c from the rows below it, which
+  // leaves D_K on the diagonal, L_KK^-1 in the identity's place and
+  // L_KK^-1 y_K in y -- the factorisation, the inverse and the tile's
+  // forward substitution in one pass of 16 row-broadcast FMAs per pivot.
+  // One wave.
+  auto diag_tile = [&](int K) {
     const int k0 = 16 * K;
-    double* const SKK = tile(K, K);
-    if (wave == 0) {
-      // 1-3. the diagonal tile by elimination of the augmented rows
-      // [A_KK | I | y_K] (lane li of every 16-lane row owns row li): pivot c
-      // subtracts l_i = a_ic / d_c times row c from the rows below it, which
-      // leaves D_K on the diagonal, L_KK^-1 in the identity's place and
-      // L_KK^-1 y_K in y -- the factorisation, the inverse and the tile's
-      // forward substitution in one pass of 16 row-broadcast FMAs per pivot
-      double aug[32];
+    const double* const SKK = tile(K, K);
+    double aug[32];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aug[j] = SKK[li * TS + j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
+    double yv = y[k0 + li];
+    double dmine = 0;
+    int zero = 0;
+    {
+      const double d0 = row_bcast_f64<0>(aug[0]);
+      dmine = li == 0 ? d0 : 0.0;
+      diag_chain<0>(aug, yv, (li > 0 ? aug[0] : 0.0) * rcp_f64(d0), dmine, li);
+    }
+    if (__builtin_amdgcn_ballot_w64(lane < 16 && dmine == 0.0) != 0) {
+      // a zero pivot (Eigen: NumericalIssue): the guarded elimination of the
+      // tile from its original rows (SKK and y_K are not written above)
 #pragma unroll
       for (int j = 0; j < 16; ++j) aug[j] = SKK[li * TS + j];
 #pragma unroll
       for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
-      double yv = y[k0 + li];
-      double dmine = 0;
-      int zero = 0;
+      yv = y[k0 + li];
       diag_pivots<0>(aug, yv, dmine, zero, li);
-      if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) Li[(size_t)K * 256 + li * 16 + j] = aug[16 + j];
-        Dg[k0 + li] = dmine;
-        y[k0 + li] = yv;
-      }
-      LBA_STAMP(1);
-      if (lane == 0 && zero) bad = 1;
     }
-    __syncthreads();
-    LBA_STAMP(2);
-    // 4. panel: L_IK = (A_IK L_KK^-T) D_K^-1 (MFMA), and the rows' forward
-    // substitution y_I -= L_IK y_K (DPP row sums over the tile's columns)
-    for (int I = K + 1 + wave; I < T; I += kSolveWaves) {
-      const int i0 = 16 * I;
-      double* const SIK = tile(I, K);
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Li[(size_t)K * kTileSz + li * kTileLd + j] = aug[16 + j];
+      Dg[k0 + li] = dmine;
+      y[k0 + li] = yv;
+    }
+    if (lane == 0 && zero) bad = 1;
+  };
+
+  if constexpr (kLds) {
+    // 4. one phase per step K, a wave per block row I > K:
+    //   L_IK = (A_IK L_KK^-T) D_K^-1 and y_I -= L_IK y_K (DPP row sums);
+    //   R_I = L_IK L_KK^-1, formed transposed (R_I^T = L_KK^-T L_IK^T) so
+    //   that its MFMA result already sits in the A-operand layout;
+    //   A_IJ -= R_I A_JK^T for K < J <= I (= L_IK D_K L_JK^T).
+    // Look-ahead: wave 0 takes row K+1 (one tile) and then factors diagonal
+    // tile K+1 in the same phase, while waves 1-7 take rows K+2.. (heaviest
+    // first, on SIMDs 1, 2, 3 before sharing one): one barrier per step.
+    // Every wave reads the raw A_JK of column K, so L_IK is written back into
+    // tile (I, K) only after the step's barrier (held in registers).
+    d4 L_held[2];
+    int I_held[2] = {0, 0}, n_held = 0;
+    double* const scr = Wscr + wave * kTileSz;
+    auto row = [&](int K, int I) {
+      const int k0 = 16 * K, i0 = 16 * I;
+      const double* const SIK = tile(I, K);
       d4 acc = {0, 0, 0, 0};
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc) {
         const int kk = 4 * kc + lk;
         const double av = SIK[li * TS + kk];
-        const double bv = Li[(size_t)K * 256 + li * 16 + kk];  // (L^-1)^T[kk][li]
+        const double bv = Li[(size_t)K * kTileSz + li * kTileLd + kk];  // (L^-1)^T[kk][li]
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
       const double dinv = rcp_f64(Dg[k0 + li]);
       const double ykl = y[k0 + li];
+      double p[4];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const double l = acc[rr] * dinv;
-        SIK[(lk + 4 * rr) * TS + li] = l;
-        double p = l * ykl;
-        p += dpp_f64<0x111, 0xf>(p);
-        p += dpp_f64<0x112, 0xf>(p);
-        p += dpp_f64<0x114, 0xf>(p);
-        p += dpp_f64<0x118, 0xf>(p);
-        if (li == 15) y[i0 + lk + 4 * rr] -= p;
+        acc[rr] = l;
+        scr[(lk + 4 * rr) * kTileLd + li] = l;
+        p[rr] = l * ykl;
       }
-    }
-    __syncthreads();
-    LBA_STAMP(3);
-    // 5. trailing: A_IJ -= L_IK (D_K L_JK^T), tiles K < J <= I enumerated
-    // row-major, v_mfma_f64_16x16x4 over the tile's 16 columns
-    const int m = T - K - 1;
-    const int ntile = m * (m + 1) / 2;
-    for (int q = wave; q < ntile; q += kSolveWaves) {
-      int I = 0;
-      while ((I + 1) * (I + 2) / 2 <= q) ++I;
-      const int J = q - I * (I + 1) / 2;
-      double* const SIJ = tile(K + 1 + I, K + 1 + J);
-      const double* const SIK = tile(K + 1 + I, K);
-      const double* const SJK = tile(K + 1 + J, K);
-      d4 acc;
+      // the four row sums' DPP steps interleaved (same order per sum)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) acc[rr] = SIJ[(lk + 4 * rr) * TS + li];
+      for (int rr = 0; rr < 4; ++rr) p[rr] += dpp_f64<0x111, 0xf>(p[rr]);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) p[rr] += dpp_f64<0x112, 0xf>(p[rr]);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) p[rr] += dpp_f64<0x114, 0xf>(p[rr]);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) p[rr] += dpp_f64<0x118, 0xf>(p[rr]);
+      if (li == 15) {
+        double yo[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) yo[rr] = y[i0 + lk + 4 * rr];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) y[i0 + lk + 4 * rr] = yo[rr] - p[rr];
+      }
+      LBA_STAMP(8);
+      wave_lds_sync();  // the scratch tile back in the transposed order
+      d4 rt = {0, 0, 0, 0};
 #pragma unroll
       for (int kc = 0; kc < 4; ++kc) {
         const int kk = 4 * kc + lk;
-        const double av = -SIK[li * TS + kk];
-        const double bv = SJK[li * TS + kk] * Dg[k0 + kk];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        const double av = Li[(size_t)K * kTileSz + kk * kTileLd + li];  // (L^-T)[li][kk]
+        const double bv = scr[li * kTileLd + kk];                       // (L_IK^T)[kk][li]
+        rt = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, rt, 0, 0, 0);
       }
+      // rt[kc] = R_I[li][lk + 4 kc]: the A operand of k-step kc
+      LBA_STAMP(9);
+      // the row's tiles, the next tile's operands loaded before this one's
+      // MFMAs (neg:[1,0,0] on A: A_IJ - R_I A_JK^T)
+      auto ld = [&](int J, d4& c, d4& b) {
+        const double* const SIJ = tile(I, J);
+        const double* const SJK = tile(J, K);
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) SIJ[(lk + 4 * rr) * TS + li] = acc[rr];
-    }
+        for (int rr = 0; rr < 4; ++rr) c[rr] = SIJ[(lk + 4 * rr) * TS + li];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) b[kc] = SJK[li * TS + 4 * kc + lk];
+      };
+      d4 cn, bn;
+      ld(K + 1, cn, bn);
+      for (int J = K + 1; J <= I; ++J) {
+        d4 c = cn;
+        const d4 b = bn;
+        if (J < I) ld(J + 1, cn, bn);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) c = __builtin_amdgcn_mfma_f64_16x16x4f64(rt[kc], b[kc], c, 0, 0, 1);
+        double* const SIJ = tile(I, J);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) SIJ[(lk + 4 * rr) * TS + li] = c[rr];
+      }
+      LBA_STAMP(10);
+      // T <= 10: at most 8 rows for waves 1-7, so a wave holds two at most
+      if (n_held == 0) {
+        L_held[0] = acc;
+        I_held[0] = I;
+      } else {
+        L_held[1] = acc;
+        I_held[1] = I;
+      }
+      ++n_held;
+      wave_lds_sync();  // the scratch tile is rewritten by the wave's next row
+    };
+    auto write_back = [&](int K) {  // the L tiles this wave computed in step K
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (h < n_held) {
+          double* const SH = tile(I_held[h], K);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) SH[(lk + 4 * rr) * TS + li] = L_held[h][rr];
+        }
+      n_held = 0;
+    };
+    // rows K+2.. to waves 1..7: the heaviest on SIMDs 1, 2, 3, then 5, 6, 7, 4
+    constexpr int kRowWave[7] = {1, 2, 3, 5, 6, 7, 4};
+    int slot = -1;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+      if (kRowWave[q] == wave) slot = q;
+    if (wave == 0) diag_tile(0);
     __syncthreads();
-    LBA_STAMP(4);
+    LBA_STAMP(1);
+    for (int K = 0; K < T - 1; ++K) {
+      if (K > 0) write_back(K - 1);
+      if (wave == 0) {
+        row(K, K + 1);
+        diag_tile(K + 1);
+        LBA_STAMP(2);
+      } else {
+        for (int q = slot; q < T - K - 2; q += 7) row(K, T - 1 - q);
+      }
+      __syncthreads();
+      LBA_STAMP(3);
+    }
+    write_back(T - 2);
+    __syncthreads();
+  } else {
+    for (int K = 0; K < T; ++K) {
+      const int k0 = 16 * K;
+      if (wave == 0) diag_tile(K);
+      __syncthreads();
+      LBA_STAMP(1);
+      // 4. panel: L_IK = (A_IK L_KK^-T) D_K^-1 (MFMA), and the rows' forward
+      // substitution y_I -= L_IK y_K (DPP row sums over the tile's columns)
+      for (int I = K + 1 + wave; I < T; I += kSolveWaves) {
+        const int i0 = 16 * I;
+        double* const SIK = tile(I, K);
+        d4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+          const int kk = 4 * kc + lk;
+          const double av = SIK[li * TS + kk];
+          const double bv = Li[(size_t)K * kTileSz + li * kTileLd + kk];  // (L^-1)^T[kk][li]
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        const double dinv = rcp_f64(Dg[k0 + li]);
+        const double ykl = y[k0 + li];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double l = acc[rr] * dinv;
+          SIK[(lk + 4 * rr) * TS + li] = l;
+          double p = l * ykl;
+          p += dpp_f64<0x111, 0xf>(p);
+          p += dpp_f64<0x112, 0xf>(p);
+          p += dpp_f64<0x114, 0xf>(p);
+          p += dpp_f64<0x118, 0xf>(p);
+          if (li == 15) y[i0 + lk + 4 * rr] -= p;
+        }
+      }
+      __syncthreads();
+      LBA_STAMP(3);
+      // 5. trailing: A_IJ -= L_IK (D_K L_JK^T), tiles K < J <= I enumerated
+      // row-major, v_mfma_f64_16x16x4 over the tile's 16 columns
+      const int m = T - K - 1;
+      const int ntile = m * (m + 1) / 2;
+      for (int q = wave; q < ntile; q += kSolveWaves) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= q) ++I;
+        const int J = q - I * (I + 1) / 2;
+        double* const SIJ = tile(K + 1 + I, K + 1 + J);
+        const double* const SIK = tile(K + 1 + I, K);
+        const double* const SJK = tile(K + 1 + J, K);
+        d4 acc;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[rr] = SIJ[(lk + 4 * rr) * TS + li];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+          const int kk = 4 * kc + lk;
+          const double av = -SIK[li * TS + kk];
+          const double bv = SJK[li * TS + kk] * Dg[k0 + kk];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) SIJ[(lk + 4 * rr) * TS + li] = acc[rr];
+      }
+      __syncthreads();
+      LBA_STAMP(4);
+    }
   }
   for (int r = t; r < N; r += kSolveThreads) y[r] = y[r] * rcp_f64(Dg[r]);
   __syncthreads();
@@ -1066,7 +1267,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     if (t < 16) {
       double s = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * 256 + k * 16 + t], y[k0 + k], s);
+      for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * kTileSz + k * kTileLd + t], y[k0 + k], s);
       __builtin_amdgcn_wave_barrier();
       y[k0 + t] = s;
     }
@@ -1295,10 +1496,6 @@ __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* _
 constexpr int kImuThreads = 256;
 constexpr int kImuWaves = kImuThreads / 64;
 
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
 
 __device__ __forceinline__ void load_state(StateD& s, const double* p) {
 #pragma unroll
@@ -1527,7 +1724,7 @@ inline unsigned blocks(long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 size_t lba_solve_lds_bytes(int n_pad) {
   const size_t T = (size_t)n_pad / 16;
-  return 8 * (T * (T + 1) / 2 * kTileSz + T * 256 + 2 * (size_t)n_pad);
+  return 8 * (T * (T + 1) / 2 * kTileSz + T * kTileSz + 2 * (size_t)n_pad + (size_t)kSolveWaves * kTileSz);
 }
 
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
@@ -1572,7 +1769,11 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_lba_solve<true>, dim3(1), dim3(kSolveThreads), lds, st, a);
   } else {
-    hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kSolveThreads), 16 * (size_t)a.n_pad, st, a);
+    const size_t lds = 16 * (size_t)a.n_pad;  // D and y (the API bounds it by 160 KB)
+    if (lds > 64 * 1024 &&
+        lds_optin(reinterpret_cast<const void*>(&k_lba_solve<false>), (int)lds) != hipSuccess)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kSolveThreads), lds, st, a);
   }
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {

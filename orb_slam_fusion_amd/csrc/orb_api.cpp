@@ -44,6 +44,7 @@ struct orbgpu_extractor {
 
   HostPlan plan;
   int plan_w = -1, plan_h = -1;
+  int resize_rounding = ORBGPU_RESIZE_SSE;
   PlanHeader* d_plan = nullptr;
   Cell* d_cells = nullptr;
   int* d_rs = nullptr;
@@ -99,11 +100,25 @@ struct orbgpu_extractor {
 
 namespace {
 
+// Any (re)allocation a captured launch refers to -- device workspace or the
+// pinned staging the graph's copies read and write -- retires the captured
+// graph and the eager record it was keyed on: a new allocation can come back
+// at a freed address, so pointer equality alone cannot prove the graph valid.
+void drop_graphs(orbgpu_extractor* h) {
+  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+  if (h->graph) (void)hipGraphDestroy(h->graph);
+  h->graph_exec = nullptr;
+  h->graph = nullptr;
+  h->graph_valid = false;
+  h->eager_valid = false;
+}
+
 orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
   if (h->plan_w == w && h->plan_h == ht) return ORBGPU_OK;
+  drop_graphs(h);
   std::string why;
   HostPlan p;
-  if (!make_plan(h->params, w, ht, p, why)) return ORBGPU_ERR_INVALID;
+  if (!make_plan(h->params, w, ht, p, why, h->resize_rounding)) return ORBGPU_ERR_INVALID;
   if (p.cells.size() > h->cells_cap) {
     dfree(h->d_cells);
     if (dalloc(&h->d_cells, p.cells.size()) != hipSuccess) return ORBGPU_ERR_NOMEM;
@@ -134,6 +149,7 @@ orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
 orbgpu_status ensure_workspace(orbgpu_extractor* h, int n) {
   const PlanHeader& P = h->plan.hdr;
   if (h->ws_images >= n) return ORBGPU_OK;
+  drop_graphs(h);
   const size_t pyr = (size_t)n * P.pyr_bytes, blur = (size_t)n * P.blur_bytes;
   const size_t slots = (size_t)n * P.slots, cells = (size_t)n * P.n_cells;
   const size_t kp = (size_t)n * P.kp_slots;
@@ -420,6 +436,17 @@ orbgpu_status orbgpu_extractor_scales(const orbgpu_extractor* h, float* scale, f
 
 int orbgpu_extractor_levels(const orbgpu_extractor* h) { return h ? h->params.num_levels : 0; }
 
+orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode) {
+  if (!h || (mode != ORBGPU_RESIZE_SSE && mode != ORBGPU_RESIZE_SCALAR)) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (h->stream && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (mode == h->resize_rounding) return ORBGPU_OK;
+  h->resize_rounding = mode;
+  const int w = h->plan_w, ht = h->plan_h;
+  h->plan_w = h->plan_h = -1;  // re-plan (and retire captured graphs) with the new column split
+  return ensure_plan(h, w, ht);
+}
+
 int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height) {
   if (!h) return -1;
   HostPlan p;
@@ -443,6 +470,9 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   const PlanHeader& P = h->plan.hdr;
   const int pitch0 = P.lev[0].pitch;  // 16-byte aligned rows for the vector loads
   const size_t bytes = (size_t)pitch0 * height;
+  if (bytes > h->d_img_bytes || bytes > h->h_img_bytes || (size_t)P.kp_slots > h->out_cap ||
+      (size_t)P.kp_slots > h->h_out_cap)
+    drop_graphs(h);  // staging or output buffers about to be reallocated
   if (bytes > h->d_img_bytes) {
     dfree(h->d_img);
     if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;

@@ -1219,12 +1219,13 @@ constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slac
 constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
 
 // In-wave integer sum by DPP (row_shr 1,2,4,8 + row_bcast 15/31): lane 63
-// holds the total.
+// holds the total.  Full-mask steps read 0 out of range (bound_ctrl), so they
+// need no zeroed destination.
 __device__ __forceinline__ int wave_isum_to_lane63(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
   v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
   return v;

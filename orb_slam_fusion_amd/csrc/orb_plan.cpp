@@ -46,7 +46,8 @@ void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::ve
   feats_per_level[L - 1] = std::max(p.num_features - sum, 0);
 }
 
-bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::string& why) {
+bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::string& why,
+               int resize_rounding) {
   const int L = p.num_levels;
   if (L < 1 || L > kMaxLevels) return why = "num_levels out of range", false;
   if (!(p.scale_factor > 1.0f)) return why = "scale_factor must be > 1", false;
@@ -152,6 +153,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
       for (; x < g.w - 8; x += 8) {
       }
       g.vec8_end = x;
+      if (resize_rounding == ORBGPU_RESIZE_SCALAR) g.vec16_end = g.vec8_end = 0;
     }
 
     // FAST cell grid (:748-825)

@@ -19,7 +19,9 @@ struct HostPlan {
 void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::vector<float>& inv,
                   std::vector<float>& s2, std::vector<float>& inv_s2,
                   std::vector<int>& feats_per_level);
-bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out, std::string& why);
+// resize_rounding: ORBGPU_RESIZE_SSE / ORBGPU_RESIZE_SCALAR (include/orbgpu.h)
+bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out, std::string& why,
+               int resize_rounding = 0);
 size_t octree_lds_bytes(const PlanHeader& P);
 int fast_cell_lds_bytes(int cols, int rows);
 

@@ -135,8 +135,11 @@ __device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3& T,
 // range or whose row is masked off read 0.
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  // full row mask: bound_ctrl reads 0 for out-of-range sources, so the
+  // destination needs no zeroed old value (one v_mov_b32_dpp per half; the
+  // build sweep's 28-value reduction was 224 of its VALU instructions)
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, ROW_MASK == 0xf);
   return __hiloint2double(hi, lo);
 }
 

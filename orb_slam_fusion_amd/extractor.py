@@ -86,6 +86,13 @@ class OrbExtractor:
     def GetInverseScaleSigmaSquares(self) -> np.ndarray:
         return self._inv_sigma2.copy()
 
+    def set_resize_rounding(self, mode: int) -> None:
+        """The resize vertical pass's column split:
+        ORBGPU_RESIZE_SSE (OpenCV 4.5.4 128-bit SIMD body + scalar tail,
+        default) or ORBGPU_RESIZE_SCALAR (every column the scalar rounding)."""
+        check(lib().orbgpu_extractor_set_resize_rounding(self._h, int(mode)),
+              "orbgpu_extractor_set_resize_rounding")
+
     def max_keypoints(self, width: int, height: int) -> int:
         return int(lib().orbgpu_extractor_max_keypoints(self._h, width, height))
 

@@ -23,6 +23,14 @@
 
 namespace ORB_SLAM_FUSION {
 
+// The reference's own LocalBundleAdjustment, compiled from optimizer.cc under
+// this name when ORBGPU_LBA is defined: the fallback for a
+// window beyond the device solver (ORBGPU_LBA_MAX_FREE_KF free key frames).
+namespace orbgpu_cpu {
+void LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int &num_fixedKF, int &num_OptKF,
+                           int &num_MPs, int &num_edges);
+}  // namespace orbgpu_cpu
+
 namespace {
 // LocalMapping calls this; keep one context per calling thread.
 orbgpu_lba_ctx *lba_thread_ctx() {
@@ -55,6 +63,17 @@ void Optimizer::LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap
   for (KeyFrame *k : pKF->GetVectorCovisibleKeyFrames()) {
     k->mnBALocalForKF = pKF->id_;
     if (!k->isBad() && k->GetMap() == pCurrentMap) local_kfs.push_back(k);
+  }
+  {
+    // beyond the device solver: the reference's CPU path, decided before the
+    // map-point marks below are set (its own gather repeats the key-frame
+    // marks above, which are idempotent)
+    int n_free = 0;
+    for (KeyFrame *k : local_kfs) n_free += k->id_ != pMap->GetInitKFid();
+    if (n_free > ORBGPU_LBA_MAX_FREE_KF) {
+      orbgpu_cpu::LocalBundleAdjustment(pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_MPs, num_edges);
+      return;
+    }
   }
   num_fixedKF = 0;
   std::list<MapPoint *> local_mps;

@@ -25,6 +25,15 @@
 
 namespace ORB_SLAM_FUSION {
 
+// The reference's own LocalInertialBA, compiled from optimizer.cc under this
+// name when ORBGPU_INERTIAL_LBA is defined: the fallback for
+// windows the device path does not take (a free key frame without IMU
+// vertices, more than ORBGPU_LIA_MAX_FREE_KF free key frames).
+namespace orbgpu_cpu {
+void LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int &num_fixedKF, int &num_OptKF,
+                     int &num_MPs, int &num_edges, bool bLarge, bool bRecInit);
+}  // namespace orbgpu_cpu
+
 namespace {
 
 using namespace orbgpu_shim;
@@ -57,8 +66,8 @@ orbgpu_imu_state kf_state(KeyFrame *k) {
 void Optimizer::LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int &num_fixedKF,
                                 int &num_OptKF, int &num_MPs, int &num_edges, bool bLarge,
                                 bool bRecInit) {
-  (void)pbStopFlag;  // attached after optimize() in the reference (:2794): never stops it
-  (void)num_fixedKF, (void)num_OptKF, (void)num_MPs, (void)num_edges;
+  // pbStopFlag: attached after optimize() in the reference (:2794), never stops it;
+  // the counters are the reference's out-params (set only on its CPU path here)
   if (pKF->cam2_) throw std::logic_error("orbgpu LocalInertialBA: fisheye rig not supported");
   Map *pCurrentMap = pKF->GetMap();
   const int maxOpt = bLarge ? 25 : 10, opt_it = bLarge ? 4 : 10;
@@ -71,6 +80,18 @@ void Optimizer::LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int 
     if (!opt.back()->mPrevKF) break;
     opt.push_back(opt.back()->mPrevKF);
     opt.back()->mnBALocalForKF = pKF->id_;
+  }
+  {
+    // windows the device path does not take go to the reference's CPU code,
+    // decided before the map-point marks below are set (the key-frame marks
+    // above are repeated identically by its own gather)
+    bool cpu = (int)opt.size() > ORBGPU_LIA_MAX_FREE_KF;
+    for (KeyFrame *k : opt) cpu = cpu || !k->bImu;  // VertexPose-only key frame (:2466-2484)
+    if (cpu) {
+      orbgpu_cpu::LocalInertialBA(pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_MPs, num_edges, bLarge,
+                                  bRecInit);
+      return;
+    }
   }
   std::list<MapPoint *> local_mps;
   for (KeyFrame *k : opt)

@@ -44,8 +44,10 @@ def fast_nms_def(roi: np.ndarray, th: int):
     return out
 
 
-def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
-    """cv::resize INTER_LINEAR for 8UC1 (SURVEY Appendix A.2), vectorised."""
+def resize_linear(src: np.ndarray, dw: int, dh: int, rounding: str = "sse") -> np.ndarray:
+    """cv::resize INTER_LINEAR for 8UC1 (SURVEY Appendix A.2), vectorised.
+    rounding "sse": the 128-bit SIMD body's rounding on x < the block end,
+    the scalar tail after; "scalar": every column the scalar rounding."""
     sh, sw = src.shape
     sx_scale = 1.0 / (dw / sw)
     sy_scale = 1.0 / (dh / sh)
@@ -87,7 +89,7 @@ def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
         x += 16
     while x < dw - 8:
         x += 8
-    vec_end = x
+    vec_end = x if rounding == "sse" else 0
 
     def s16(a):
         return np.clip(a, -32768, 32767)

@@ -52,13 +52,19 @@ def _diagnose(ex, orc, L):
     return "; ".join(lines) or "stages equal"
 
 
-def _compare(params, img, lapping=(0, 0)):
+def _compare(params, img, lapping=(0, 0), rounding=None):
     h, w = img.shape
     ex = OrbExtractor(*params, max_width=w, max_height=h)
+    if rounding is not None:
+        ex.set_resize_rounding(rounding)
     orc = oracle.OracleExtractor(*params)
-    m_ref, k_ref, d_ref = orc.extract(img, lapping)
+    if rounding is None:
+        m_ref, k_ref, d_ref = orc.extract(img, lapping)
+    else:
+        with oracle.resize_rounding(rounding):  # the oracle's levels follow the same split
+            m_ref, k_ref, d_ref = orc.extract(img, lapping)
     m, k, d = ex(img, None, lapping)
-    ctx = f"{w}x{h} params={params} lapping={lapping}"
+    ctx = f"{w}x{h} params={params} lapping={lapping} rounding={rounding}"
     # the reference blurs only levels that kept keypoints (orb_extractor.cc
     # operator(): `if (nkeypointsLevel == 0) continue;`), the GPU every level
     ref_levels = set(k_ref["octave"].tolist())
@@ -90,6 +96,22 @@ def test_stereo_frame_c2_bit_exact(gpu_available, frame):
 def test_euroc_params_bit_exact(gpu_available):
     left, _ = synth.stereo_frame(10)
     assert _compare(EUROC, left) > 1100
+
+
+@pytest.mark.parametrize("rounding", [0, 1])  # ORBGPU_RESIZE_SSE, ORBGPU_RESIZE_SCALAR
+def test_resize_rounding_switch(gpu_available, rounding):
+    """the resize vertical pass's column split is one switch; both
+    settings bit-exact against the oracle under the same setting, and the two
+    pyramids differ (the switch reaches the kernel)."""
+    left, _ = synth.stereo_frame(4)
+    assert _compare(C2, left, rounding=rounding) > 900
+    ex = OrbExtractor(*C2)
+    ex.set_resize_rounding(rounding)
+    ex(left, None, (0, 0))
+    a = [l.copy() for l in ex.img_pyramid_]
+    ex.set_resize_rounding(1 - rounding)
+    ex(left, None, (0, 0))
+    assert any(not np.array_equal(x, y) for x, y in zip(a, ex.img_pyramid_))
 
 
 def test_lapping_partition(gpu_available):

@@ -2,8 +2,8 @@
 windows.  Floating point, so parity is by tolerance: the GPU sums in a
 different (fixed) order and factors the reduced camera system by 16 x 16
 MFMA tiles; poses and points agree to ~1e-6 relative, the LM path
-(iterations, trials) and the outlier flags away from the thresholds agree
-exactly.  The LM loop runs on the device (lba_kernels.hip): the stop flag,
+(iterations, trials) agrees exactly, and so do the outlier flags of every
+edge whose oracle chi2 is not within 1e-6 relative of its threshold.  The LM loop runs on the device (lba_kernels.hip): the stop flag,
 the user lambda, the LDS / global solver paths and the point-sharded
 two-rank run are each checked against the oracle or the one-rank result."""
 import sys
@@ -26,6 +26,24 @@ def _quat_sign(q, ref):
     return q if np.dot(q[:4], ref[:4]) >= 0 else np.concatenate([-q[:4], q[4:]])
 
 
+# Outlier flags: identical on every edge except those whose oracle chi2 lies
+# within CHI2_BAND (relative) of its threshold -- there the states' last-digit
+# differences (poses agree to ~1e-12 relative) may decide the comparison.  The
+# exempt set is listed and must stay tiny.
+CHI2_BAND = 1e-6
+MAX_EXEMPT = 3
+
+
+def check_flags(got_out, ref, thr):
+    near = np.abs(ref["chi2"] - thr) <= CHI2_BAND * thr
+    diff = got_out != ref["outlier"]
+    bad = np.nonzero(diff & ~near)[0]
+    assert bad.size == 0, [(int(i), float(ref["chi2"][i]), float(thr[i])) for i in bad[:10]]
+    exempt = np.nonzero(near)[0]
+    print(f"exempt edges (chi2 within {CHI2_BAND:g} of the threshold): {exempt.tolist()}")
+    assert exempt.size <= MAX_EXEMPT, exempt.tolist()
+
+
 def _compare(p, iters=10, tol=1e-6, lambda_init=0.0):
     ref = oracle.lba(p, iters=iters, lambda_init=lambda_init)
     got = LocalBundleAdjuster().optimize(p, iterations=iters, lambda_init=lambda_init)
@@ -36,8 +54,8 @@ def _compare(p, iters=10, tol=1e-6, lambda_init=0.0):
         g = _quat_sign(got["poses_d"][k], ref["poses"][k])
         assert np.allclose(g, ref["poses"][k], rtol=tol, atol=tol), k
     assert np.allclose(got["pts"], ref["pts"], rtol=1e-5, atol=1e-5)
-    diff = (got["outlier"] != ref["outlier"]).sum()
-    assert diff <= max(1, len(p.edges) // 2000), diff
+    # optimizer.cc:1366-1401: chi2 > 5.991 (mono) / 7.815 (stereo), double literals
+    check_flags(got["outlier"], ref, np.where(p.edges["ur"] < 0, 5.991, 7.815))
     return got, ref
 
 
@@ -52,6 +70,24 @@ def test_lba_with_outliers(gpu_available):
 def test_lba_c4_window(gpu_available):
     got, ref = _compare(synth.lba_problem())  # 20 KF, 3000 MP, 18000 edges
     assert got["stats"][1] < got["stats"][0]
+
+
+def test_lba_window_past_2048_rows(gpu_available):
+    """344 free key frames: a 2064-row reduced system (the HBM solve path; the
+    round-2 API refused it) -- one LM iteration against the oracle."""
+    _compare(synth.lba_problem(seed=21, n_kf=346, n_pts=3460, obs_per_pt=6, n_fixed=2), iters=1)
+
+
+def test_lba_capacity_bound(gpu_available):
+    """One free key frame past ORBGPU_LBA_MAX_FREE_KF: ORBGPU_ERR_CAPACITY before
+    any device work (the C++ drop-in then runs the reference's CPU code)."""
+    from orb_slam_fusion_amd import _lib
+
+    nf = _lib.ORBGPU_LBA_MAX_FREE_KF + 1
+    p = synth.lba_problem(seed=22, n_kf=nf + 1, n_pts=nf, obs_per_pt=2, n_fixed=1)
+    with pytest.raises(_lib.OrbGpuError) as e:
+        LocalBundleAdjuster().optimize(p, iterations=1)
+    assert e.value.status == _lib.ORBGPU_ERR_CAPACITY
 
 
 def test_lba_all_fixed_and_empty(gpu_available):

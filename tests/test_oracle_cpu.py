@@ -79,6 +79,20 @@ def test_resize_matches_numpy_restatement(sw, sh, dw, dh):
     assert np.array_equal(oracle.resize(src, dw, dh), ref_py.resize_linear(src, dw, dh))
 
 
+@pytest.mark.parametrize("sw,sh,dw,dh", [(752, 480, 627, 400), (101, 77, 84, 64)])
+def test_resize_scalar_rounding_switch(sw, sh, dw, dh):
+    """SURVEY A.2's switch: every column the scalar FixedPtCast rounding; it
+    matches the numpy restatement and differs from the SSE split somewhere."""
+    rng = np.random.default_rng(sw + dw)
+    src = rng.integers(0, 256, (sh, sw), dtype=np.uint8)
+    with oracle.resize_rounding(oracle.RESIZE_SCALAR):
+        sca = oracle.resize(src, dw, dh)
+    assert np.array_equal(sca, ref_py.resize_linear(src, dw, dh, rounding="scalar"))
+    sse = oracle.resize(src, dw, dh)  # the default is restored on exit
+    assert np.array_equal(sse, ref_py.resize_linear(src, dw, dh))
+    assert (sca != sse).any()
+
+
 @pytest.mark.parametrize("w,h", [(64, 48), (33, 17), (210, 134)])
 def test_gauss_matches_numpy_restatement(w, h):
     rng = np.random.default_rng(w * h)

@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_sys, sizeof(double) * sys.size()));
   CK(hipMalloc(&d_xp, sizeof(double) * (n + 2)));
   CK(hipMalloc(&d_scal, sizeof(double) * 4));
-  CK(hipMalloc(&d_work, sizeof(double) * ((size_t)npad * (npad + 1) + (npad / 16) * 256 + 2)));
+  CK(hipMalloc(&d_work, sizeof(double) * ((size_t)npad * (npad + 1) + (npad / 16) * 272 + 2)));
   CK(hipMalloc(&d_ctrl, sizeof(LbaCtrl)));
   CK(hipMemcpy(d_sys, sys.data(), sizeof(double) * sys.size(), hipMemcpyHostToDevice));
   LbaCtrl c0{};
@@ -115,10 +115,10 @@ int main(int argc, char** argv) {
     err = std::fmax(err, std::fabs(xg[i] - x[i]));
     nrm = std::fmax(nrm, std::fabs(x[i]));
   }
-  const char* names[8] = {"load", "diag", "diag_sync", "panel", "trailing", "dinv", "backward", "scale"};
+  const char* names[11] = {"load", "diag0", "w0_row+diag", "step_sync", "trailing(hbm path)", "dinv", "backward", "scale", "w0_row_L", "w0_row_R", "w0_row_tiles"};
   std::printf("{\"n\": %d, \"lds\": %d, \"us_per_solve\": %.2f, \"max_rel_err\": %.3e, \"clocks_per_solve\": {",
               n, in_lds ? 1 : 0, ms * 1e3 / reps, err / nrm);
-  for (int k = 0; k < 8; ++k)
+  for (int k = 0; k < 11; ++k)
     std::printf("%s\"%s\": %.0f", k ? ", " : "", names[k], (double)st[k] / reps);
   std::printf("}}\n");
   return err / nrm < 1e-9 ? 0 : 2;
