@@ -35,7 +35,7 @@ W, H = 752, 480
 PARAMS = (1000, 1.2, 8, 20, 7)
 POSE_OBS = 600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PROFILE_ROUND = "r02"  # profiles/<round>/kernels.json (tools/profile_round.sh)
+PROFILE_ROUND = "r03"  # profiles/<round>/kernels.json (tools/profile_round.sh)
 
 
 def level_sizes(inv_scale):
@@ -54,6 +54,14 @@ def stage_bytes(sizes, n_kp):
         "describe": n_kp * (749 + 512),                                # IC_Angle circle + BRIEF samples
         "assemble": n_kp * (28 + 32),                                  # keypoint record + descriptor
     }
+
+
+def describe_plane_floor(sizes, n_kp):
+    """k_describe's fetch floor per image: 1000 keypoints' 31x31 (raw) and 37x37
+    (blurred) patches cover every level, so the raw and blurred planes are each
+    fetched about once whatever the staging: both planes + the
+    angle / descriptor writes."""
+    return 2 * sum(w * h for w, h in sizes) + n_kp * (4 + 32)
 
 
 STAGE_KERNELS = {"resize": "k_resize", "blur": "k_blur", "fast_cells": "k_fast_cells",
@@ -102,6 +110,9 @@ def cpu_baseline(frames, probs, budget_s: float):
         "kind": "port",
         "sample": f"{done} synthetic 752x480 stereo frames: oracle extract (2 threads, one per "
         f"image) + oracle PoseOptimization ({POSE_OBS} obs, 1 thread), {el:.1f} s",
+        "build": "oracle/Makefile: g++ -O2 -march=x86-64-v3 -ffp-contract=off; a scalar "
+                 "restatement -- no OpenCV SIMD in FAST / resize / GaussianBlur, so slower than "
+                 "the reference's OpenCV build (the GPU/CPU ratio overstates the gap)",
         **host_cpu(),
     }
 
@@ -122,7 +133,8 @@ def load_profile():
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=25,
+                    help="timed steps (25 x ~42 ms: a timed region over 1 s)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=5120,
                     help="stereo frames per GPU per step (all distinct, resident in HBM)")
@@ -146,6 +158,8 @@ def main() -> int:
                     help="skip the device-resident tracking-chain side line")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the per-frame host-path latency side line")
+    ap.add_argument("--no-latency-inertial", action="store_true",
+                    help="skip the stereo-inertial per-frame host-path latency side line")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the synthetic-sequence (C5 layout) side line")
     ap.add_argument("--no-lba-sharded", action="store_true",
@@ -284,10 +298,17 @@ def main() -> int:
         if b:
             row["achieved_GBs"] = round(b / (ms * 1e-3) / 1e9, 2)
             row["frac"] = round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if st == "describe":
+            pf = describe_plane_floor(sizes, kp_mean) * imgs_per_launch
+            row["plane_floor_bytes_per_launch"] = int(pf)
+            row["plane_floor_frac"] = round(pf / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         p = pk.get(st)
         if p:
             if p.get("hbm_bytes_per_image") is not None and st != "pose_opt":
                 row["traffic_per_launch"] = round(p["hbm_bytes_per_image"] * imgs_per_launch)
+                if st == "describe":
+                    row["traffic_over_plane_floor"] = round(row["traffic_per_launch"] /
+                                                            row["plane_floor_bytes_per_launch"], 3)
             for key in ("valu_busy", "rocprof_avg_ms_per_launch", "bound"):
                 if p.get(key) is not None:
                     row[key] = p[key]
@@ -395,6 +416,14 @@ def main() -> int:
         from bench_latency import measure as measure_latency  # noqa: E402
 
         result["latency"] = measure_latency(frames=40, cpu_frames=0 if args.no_cpu_baseline else 8)
+    if rank == 0 and world == 1 and not args.no_latency_inertial:
+        # the same target in the mode EuRoC MH01 runs (stereo-inertial after IMU
+        # initialisation): extract + stereo + SearchLocalPoints +
+        # PoseInertialOptimizationLastFrame, one frame at a time through the ABI
+        sys.path.insert(0, str(REPO / "tools"))
+        from bench_latency_inertial import measure as measure_lat_in  # noqa: E402
+
+        result["latency_inertial"] = measure_lat_in(frames=16, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_c5:
         # config C5's per-GPU unit on synthetic data: 8 sequences tracked frame to
         # frame (tools/c5_runner.py), frames/s of the GPU and the drift vs truth

@@ -244,6 +244,17 @@ typedef int (*orbgpu_lba_reduce_fn)(void* user, double* d_buf, int n, int op, vo
 orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out);
 void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
 
+/* Stream-ordered reductions for the point-sharded call (ordered != 0): the
+ * reduce callback then only ENQUEUES its all-reduce on the hip_stream it is
+ * given (e.g. ncclAllReduce / an RCCL all-reduce on that stream) and returns
+ * without waiting, and the whole LM loop stays on the device as in the
+ * one-rank call: no host synchronisation inside orbgpu_lba_optimize but the
+ * final copy.  Every rank enqueues the same kernel + collective sequence
+ * (4 all-reduces per LM trial: the pose diagonal (sum) and the point maximum
+ * (max) for lambda init, [S | b_s | b_p] (sum), [chi2, scale, failures, stop]
+ * (sum)), and the same number of trials, so the collectives stay matched. */
+orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered);
+
 /* Bounds of the device solver: the reduced camera system of 6 rows per free
  * key frame is factorised by one workgroup, packed in LDS up to 160 rows and
  * in HBM beyond, with D and the right-hand side in LDS (16 bytes per row of

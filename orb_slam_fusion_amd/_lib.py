@@ -260,6 +260,7 @@ SIGNATURES = {
         _I, [_P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P],
     ),
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
+    "orbgpu_lba_ctx_set_reduce_ordered": (_I, [_P, _I]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (
         _I,

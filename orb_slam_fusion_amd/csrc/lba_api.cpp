@@ -39,6 +39,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct orbgpu_lba_ctx {
   int device = 0;
+  int reduce_ordered = 0;  // orbgpu_lba_ctx_set_reduce_ordered
   hipStream_t stream = nullptr;
   char* arena = nullptr;  // device
   size_t arena_cap = 0;
@@ -94,6 +95,12 @@ orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out) {
   }
   c->host_dev = static_cast<LbaHostWords*>(dp);
   *out = c;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered) {
+  if (!c) return ORBGPU_ERR_INVALID;
+  c->reduce_ordered = ordered ? 1 : 0;
   return ORBGPU_OK;
 }
 
@@ -166,7 +173,32 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     cnt[p + 1] += cnt[p];
   }
   const int ne = cnt[np];
-  const int n_pairs = nf * (nf + 1) / 2;
+  // the structurally non-zero pose pairs of S: every diagonal block, and (i, j)
+  // when some point of the shard is seen by both (the other blocks stay the
+  // zeros the per-call clear leaves; a sharded rank's zeros add nothing)
+  std::vector<int> pair_list;
+  {
+    std::vector<int> pf(std::max(ne, 1)), fill(cnt.begin(), cnt.end() - 1);
+    for (int i = 0; i < n_edges; ++i) {
+      const orbgpu_lba_edge& e = edges[i];
+      if (e.point >= pt_begin && e.point < pt_end) pf[fill[e.point - pt_begin]++] = hidx[e.kf];
+    }
+    std::vector<uint8_t> nz((size_t)nf * nf, 0);
+    for (int f = 0; f < nf; ++f) nz[(size_t)f * nf + f] = 1;
+    for (int p = 0; p < np; ++p)
+      for (int u = cnt[p]; u < cnt[p + 1]; ++u)
+        for (int v = u + 1; v < cnt[p + 1]; ++v) {
+          const int fa = pf[u], fb = pf[v];
+          if (fa >= 0 && fb >= 0) nz[(size_t)std::min(fa, fb) * nf + std::max(fa, fb)] = 1;
+        }
+    for (int i = 0; i < nf; ++i)
+      for (int j = i; j < nf; ++j)
+        if (nz[(size_t)i * nf + j]) {
+          pair_list.push_back(i);
+          pair_list.push_back(j);
+        }
+  }
+  const int n_pairs = (int)pair_list.size() / 2;
   std::vector<int> gidx(ne);  // shard edge -> caller's edge index
   std::vector<int> pose_cnt(nf + 1, 0);
   // IMU links incident to each free key frame (link order)
@@ -275,11 +307,10 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       r[3] = cnt[p + 1];
     }
   }
-  for (int i = 0, k = 0; i < nf; ++i)
-    for (int j = i; j < nf; ++j, ++k) {
-      I_pi[k] = i;
-      I_pj[k] = j;
-    }
+  for (int k = 0; k < n_pairs; ++k) {
+    I_pi[k] = pair_list[2 * k];
+    I_pj[k] = pair_list[2 * k + 1];
+  }
   std::copy(free_kf.begin(), free_kf.end(), I_fk);
   std::copy(inc.begin(), inc.end(), I_inc);
   std::copy(inc_list.begin(), inc_list.end(), I_incl);
@@ -357,10 +388,11 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     a.imu_q = dp(c_imuq);
     a.himu = dp(c_himu);
     a.imu_tot = dp(c_itot);
-    // the reduced system's IMU rows get no Schur terms: zero once per call
-    if (hipMemsetAsync(a.sys, 0, sizeof(double) * ((size_t)n * n + 2 * n), st) != hipSuccess)
-      return ORBGPU_ERR_DEVICE;
   }
+  // blocks no launched pose pair writes (and, kModelImu, the IMU rows, which
+  // get no Schur terms) stay zero: clear the system once per call
+  if (hipMemsetAsync(a.sys, 0, sizeof(double) * ((size_t)n * n + 2 * n), st) != hipSuccess)
+    return ORBGPU_ERR_DEVICE;
 
   volatile LbaHostWords* hw = h->host;
   hw->progress = 0;
@@ -377,6 +409,46 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
         if (lba_step(a, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
+        ++issued;
+      } else {
+        std::this_thread::yield();
+      }
+    }
+  } else if (h->reduce_ordered) {
+    // ---- point-sharded, LM on the device: every reduction is enqueued on
+    // the stream between the stage kernels (no host synchronisation); the
+    // kernels and k_lba_ctl skip what is not due (need_build, lambda_due,
+    // done), so a step is the same kernel + collective sequence on every
+    // rank.  The host keeps kAhead steps queued like the one-rank path and,
+    // once the device reports done at trial j, tops the queue up to exactly
+    // j + kAhead - 1 steps: it can have issued at most that many (it issues
+    // step s only after seeing s - kAhead complete), and every rank issuing
+    // the same number keeps the collectives matched.
+    auto red = [&](double* buf, int cnt_, int op) {
+      return reduce(user, buf, cnt_, op, reinterpret_cast<void*>(st)) == 0;
+    };
+    auto issue = [&]() {
+      return lba_build(a, st) == hipSuccess && red(a.diag, n, 0) && red(a.diag + n, 1, 1) &&
+             lba_ctl(a, kCtlLambda, st) == hipSuccess && lba_schur(a, st) == hipSuccess &&
+             red(a.sys, n * n + 2 * n, 0) && lba_solve_trial(a, st) == hipSuccess && red(a.red, 4, 0) &&
+             lba_ctl(a, kCtlDecide, st) == hipSuccess;
+    };
+    if (!red(a.red, 2, 0) || lba_ctl(a, kCtlInit, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    const int max_steps = iterations * 10;
+    int issued = 0;
+    while (issued < max_steps) {
+      const unsigned long long p = hw->progress;
+      if (p >> 32) {
+        const int target = std::min(max_steps, (int)(p & 0xffffffffu) + kAhead - 1);
+        while (issued < target) {
+          if (!issue()) return ORBGPU_ERR_DEVICE;
+          ++issued;
+        }
+        break;
+      }
+      if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
+      if (issued - (int)(p & 0xffffffffu) < kAhead) {
+        if (!issue()) return ORBGPU_ERR_DEVICE;
         ++issued;
       } else {
         std::this_thread::yield();

@@ -656,6 +656,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
       double hm = 0;
       for (int b = a.n_free; b < (int)gridDim.x; ++b) hm = fmax(hm, a.partials[b]);
       a.diag[a.n_sys] = hm;
+      cw.lambda_due = cw.it == 0 ? 1 : 0;
     } else if (cw.it == 0) {
       ctl_lambda(a, mx);
     }
@@ -702,6 +703,14 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
     int fs[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) fs[u] = sl.z + u < sl.w ? a.ef[sl.z + u] : -2;
+    // a point not seen by pose fj adds nothing off the diagonal: skip its
+    // inverse and W (points seen by more than 8 key frames take the full path)
+    if (!diag && sl.w - sl.z <= 8) {
+      bool hit = false;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hit |= fs[u] == fj;
+      if (!hit) continue;
+    }
     double Di[9];
     inv3_lambda(hll, lambda, Di);
     double W[6][3];
@@ -1441,9 +1450,13 @@ __global__ void k_lba_ctl(LbaArgs a, int mode) {
   }
   if (c.done) return;
   if (mode == kCtlLambda) {
+    // due once, after the first build (k_lba_sums sets the flag when it == 0);
+    // a stream-ordered run enqueues this every step
+    if (!c.lambda_due) return;
+    c.lambda_due = 0;
     double m = a.diag[a.n_sys];
     for (int k = 0; k < a.n_sys; ++k) m = fmax(m, fabs(a.diag[k]));
-    if (c.it == 0) ctl_lambda(a, m);
+    ctl_lambda(a, m);
     return;
   }
   ctl_decide(a, a.red[0], a.red[1], a.red[2] > 0 || a.scal[1] != 0, a.red[3] > 0);

@@ -55,6 +55,7 @@ struct LbaCtrl {
   double lambda, ni, cur, ini, chi_init, user_lambda;
   double last;  // robust chi2 of the last computeActiveErrors (LocalInertialBA's err_end)
   int it, q, nbad, need_build, done, state, iters_done, trials, max_iters, stopped;
+  int lambda_due;  // sharded: the first build's lambda init waits for the all-reduce (k_lba_ctl)
 };
 
 // LM decision points whose inputs a point-sharded run all-reduces first

@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
         // broadcast barrier
         double x[6];
         PSTAMP(0);
-        const bool ok = ldlt6_wave(hb, lg, x);
+        const bool ok = ldlt6_gj(hb, lg, x);
         PSTAMP(2);
         const Se3 Tn = se3_compose(se3_exp(x), T);
         PSTAMP(3);

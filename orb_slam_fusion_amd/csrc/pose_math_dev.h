@@ -95,8 +95,32 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) R[i][j] = V[i][j] = (i == j ? 1.0 : 0.0) + O[i][j] + O2[i][j];
   } else {
-    const double s = sin(theta), c = cos(theta);
-    const double a = s / theta, b = (1 - c) / (theta * theta), d = (theta - s) / cube(theta);
+    // a = sin t / t, b = (1 - cos t) / t^2, d = (t - sin t) / t^3 (se3quat.h:210-217).
+    // Below t = 0.25 (every LM step but the first few) as their Taylor series
+    // in t^2 to the last term above 1e-19 (Horner, no sin / cos / divisions;
+    // the series are at least as accurate as the closed forms, which lose
+    // digits to cancellation there), else the closed forms.
+    const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
+    const int series = t2 < 0.0625 ? 1 : 0;
+    double a, b, d;
+    if (kUniform ? __builtin_amdgcn_readfirstlane(series) : series) {
+      // 1/(2k+1)!, 1/(2k+2)!, 1/(2k+3)! with alternating signs, k = 0..7
+      a = fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, -7.6471637318198164759e-13,
+          1.6059043836821614599e-10), -2.5052108385441718775e-08), 2.7557319223985890653e-06),
+          -1.9841269841269841270e-04), 8.3333333333333333333e-03), -1.6666666666666666667e-01), 1.0);
+      b = fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, -4.7794773323873852974e-14,
+          1.1470745597729724714e-11), -2.0876756987868098979e-09), 2.7557319223985890653e-07),
+          -2.4801587301587301587e-05), 1.3888888888888888889e-03), -4.1666666666666666667e-02), 0.5);
+      d = fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, -2.8114572543455207632e-15,
+          7.6471637318198164759e-13), -1.6059043836821614599e-10), 2.5052108385441718775e-08),
+          -2.7557319223985890653e-06), 1.9841269841269841270e-04), -8.3333333333333333333e-03),
+          1.6666666666666666667e-01);
+    } else {
+      const double s = sin(theta), c = cos(theta);
+      a = s / theta;
+      b = (1 - c) / (theta * theta);
+      d = (theta - s) / cube(theta);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -340,6 +364,78 @@ __device__ __forceinline__ bool ldlt6_wave(const double* hb, double lambda, doub
 #pragma unroll
   for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, __builtin_amdgcn_readlane(rank, k));
   return !neg;
+}
+
+// The same system by Gauss-Jordan elimination with DPP64 row broadcasts: lane
+// li of every 16-lane row owns permuted row li (li < 6; the others zero) with
+// b appended; pivot K's row is read from lane K of the lane's own row by
+// v_fmac_f64_dpp row_newbcast, one instruction per entry (a fixed window of 6
+// entries after the pivot column: the row's rest, b, zero padding), every row
+// but the pivot's subtracting l_i times it.  Same pivot order and pivots as
+// ldlt6_wave, so the same isPositive(); x_i = b'_i / D_i with Eigen's
+// tolerance, solved even when a pivot is negative (as ldlt6_wave).  A zero
+// pivot takes ldlt6_wave, which keeps Eigen's semantics for it.
+template <int N>
+__device__ __forceinline__ double row16_bcast_f64(double v) {
+  double o;
+  asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "=v"(o)
+               : "v"(v), "i"(N));
+  return o;
+}
+#define POSE_FMC(k) "v_fmac_f64_dpp %" #k ", %" #k ", -%6 row_newbcast:%7 row_mask:0xf bank_mask:0xf\n\t"
+template <int K>
+__device__ __forceinline__ void gj6_pivot(double (&w)[12], double l) {
+  asm volatile("s_nop 1\n\t" POSE_FMC(0) POSE_FMC(1) POSE_FMC(2) POSE_FMC(3) POSE_FMC(4) POSE_FMC(5)
+               : "+v"(w[K + 1]), "+v"(w[K + 2]), "+v"(w[K + 3]), "+v"(w[K + 4]), "+v"(w[K + 5]),
+                 "+v"(w[K + 6])
+               : "v"(l), "i"(K));
+}
+#undef POSE_FMC
+template <int K>
+__device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmine, int& flags) {
+  if constexpr (K < 6) {
+    const double d = row16_bcast_f64<K>(w[K]);
+    flags |= (d < 0.0 ? 1 : 0) | (d == 0.0 ? 2 : 0);
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    dmine = li == K ? d : dmine;
+    gj6_pivot<K>(w, li != K ? w[K] * r : 0.0);
+    gj6_pivots<K + 1>(w, li, dmine, flags);
+  }
+}
+
+__device__ __forceinline__ bool ldlt6_gj(const double* hb, double lambda, double (&x)[6]) {
+  const int lane = threadIdx.x & 63, li = lane & 15;
+  const int l6 = lane < 6 ? lane : 0;
+  const double dl = lane < 6 ? fabs(hb[1 + l6 * (l6 + 1) / 2 + l6] + lambda) : -1.0;
+  int rank = 0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double dj = readlane_f64(dl, j);
+    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
+  }
+  int pi = 0;  // the original index at permuted position li
+#pragma unroll
+  for (int j = 0; j < 6; ++j) pi = __builtin_amdgcn_readlane(rank, j) == li ? j : pi;
+  double w[12];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int pj = __builtin_amdgcn_readlane(pi, j);
+    const int r = max(pi, pj), c = min(pi, pj);
+    w[j] = li < 6 ? hb[1 + r * (r + 1) / 2 + c] + (r == c ? lambda : 0.0) : 0.0;
+  }
+  w[6] = li < 6 ? hb[22 + pi] : 0.0;
+#pragma unroll
+  for (int j = 7; j < 12; ++j) w[j] = 0.0;
+  double dmine = 1.0;
+  int flags = 0;
+  gj6_pivots<0>(w, li, dmine, flags);
+  if (flags & 2) return ldlt6_wave(hb, lambda, x);
+  const double z = li < 6 && fabs(dmine) > 1.0 / 1.79769313486231570815e+308 ? w[6] / dmine : 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, __builtin_amdgcn_readlane(rank, k));
+  return !(flags & 1);
 }
 
 __device__ __forceinline__ void huber_rho(double e2, double delta, double& rho0, double& rho1) {

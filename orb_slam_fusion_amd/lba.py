@@ -54,6 +54,35 @@ def dist_reduce(group=None):
     return reduce
 
 
+def dist_enqueue(group=None, device: int = 0):
+    """-> enqueue(ptr, n, op, stream) for the stream-ordered sharded call
+    (orbgpu_lba_ctx_set_reduce_ordered): the all-reduce of the library's
+    device buffer goes onto the library's HIP stream.  RCCL (backend "nccl")
+    runs it in stream order without a host wait (torch makes its collective
+    stream wait on the current stream and the current stream on the result);
+    gloo has no device path, so it stages through the host (a host wait per
+    reduction: the two-ranks-on-one-GPU test path)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", device)
+    gloo = dist.get_backend(group) == "gloo"
+
+    def enqueue(d_buf: int, n: int, op: int, stream: int) -> None:
+        rop = dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM
+        ext = torch.cuda.ExternalStream(stream, device=dev)
+        with torch.cuda.stream(ext):
+            t = torch.as_tensor(_DeviceDoubles(d_buf, n), device=dev)
+            if gloo:
+                h = t.cpu()  # synchronises with the stream's pending work
+                dist.all_reduce(h, op=rop, group=group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=rop, group=group)
+
+    return enqueue
+
+
 class LocalBundleAdjuster:
     def __init__(self, device: int = 0):
         self.device = device
@@ -72,11 +101,14 @@ class LocalBundleAdjuster:
             pass
 
     def optimize(self, problem, iterations: int = 10, pt_range=None, group=None,
-                 stop_flag: Optional[ctypes.c_uint8] = None, lambda_init: float = 0.0) -> dict:
+                 stop_flag: Optional[ctypes.c_uint8] = None, lambda_init: float = 0.0,
+                 ordered: bool = False) -> dict:
         """Returns {"poses": float32 [n_kf, 7], "poses_d": float64 [n_kf, 7],
         "pts": float32 [n_pts, 3] (this shard's rows), "outlier": uint8 [E]
         (this shard's edges), "stats": float64 [6]}.  ``group``: a
         torch.distributed group whose ranks hold the other point shards.
+        ``ordered``: with a group, the reductions are enqueued on the library's
+        stream and the LM loop stays on the device (dist_enqueue).
         ``lambda_init`` > 0: g2o's setUserLambdaInit (100 for an inertial map,
         optimizer.cc:1137).  ``stop_flag``: the reference's pbStopFlag, read
         by the device where g2o polls terminate()."""
@@ -92,8 +124,21 @@ class LocalBundleAdjuster:
         xo = np.array(pts, copy=True)
         out = np.zeros(max(ne, 1), np.uint8)
         st = np.zeros(6, np.float64)
+        check(lib().orbgpu_lba_ctx_set_reduce_ordered(self._h, 1 if (ordered and group is not None) else 0),
+              "orbgpu_lba_ctx_set_reduce_ordered")
         if group is None:
             cb = LBA_REDUCE_FN(0)
+        elif ordered:
+            enq = dist_enqueue(group, self.device)
+
+            def _cb(_user, d_buf, n, op, stream):
+                try:
+                    enq(d_buf, n, op, stream)
+                    return 0
+                except Exception:  # noqa: BLE001 -- reported as a failed reduce
+                    return -1
+
+            cb = LBA_REDUCE_FN(_cb)
         else:
             import torch
 

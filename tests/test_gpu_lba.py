@@ -127,6 +127,32 @@ def test_lba_shard_with_identity_reduce_matches(gpu_available):
     assert np.array_equal(got["pts"], ref["pts"])
 
 
+def test_lba_ordered_reduce_world1_matches(gpu_available):
+    """The stream-ordered sharded form (reductions enqueued on the library's
+    stream over RCCL, the LM loop on the device) at world size 1: bit-identical
+    to the plain call, LM path included."""
+    import torch.distributed as dist
+
+    from orb_slam_fusion_amd import dist as odist
+
+    p = synth.lba_problem()
+    ref = LocalBundleAdjuster().optimize(p)
+    if not dist.is_initialized():
+        import os
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29613")
+        dist.init_process_group("nccl", rank=0, world_size=1)
+    adj = LocalBundleAdjuster()
+    got = adj.optimize(p, group=dist.group.WORLD, ordered=True)
+    again = adj.optimize(p, group=dist.group.WORLD, ordered=True)  # the context reused
+    odist.finalize()
+    for g in (got, again):
+        assert np.array_equal(g["stats"], ref["stats"])
+        assert np.array_equal(g["poses_d"], ref["poses_d"])
+        assert np.array_equal(g["pts"], ref["pts"])
+        assert np.array_equal(g["outlier"], ref["outlier"])
+
+
 def test_lba_inertial_map_user_lambda(gpu_available):
     """setUserLambdaInit(100.0) when the map is inertial (optimizer.cc:1137)."""
     got, ref = _compare(synth.lba_problem(seed=6, n_kf=10, n_pts=600, obs_per_pt=4, n_fixed=2),
@@ -186,11 +212,14 @@ def test_lba_stop_flag_mid_run(gpu_available):
     assert any(0 < t < full["stats"][3] for t in seen), (seen, full["stats"][3])
 
 
-def test_lba_two_ranks_one_gpu(gpu_available, tmp_path):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_lba_two_ranks_one_gpu(gpu_available, tmp_path, ordered):
     """The point-sharded C4 window on two ranks (fresh child processes, both on
     cuda:0), partial reduced camera systems / chi2 / LM scale summed through
     lba.dist_reduce over gloo (optimizer.cc:1359-1360, block_solver.hpp:383-460
-    split by points): the same LM path and state as the one-rank GPU run."""
+    split by points): the same LM path and state as the one-rank GPU run.
+    ordered: the stream-ordered form (lba.dist_enqueue; gloo stages through
+    the host), which must issue the same collective sequence on both ranks."""
     import os
     import socket
     import subprocess
@@ -201,8 +230,8 @@ def test_lba_two_ranks_one_gpu(gpu_available, tmp_path):
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     worker = REPO / "tools" / "lba_shard_worker.py"
-    procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), str(tmp_path)],
-                              env=env) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), str(tmp_path), "0",
+                               "1" if ordered else "0"], env=env) for r in range(2)]
     for pr in procs:
         assert pr.wait(timeout=100) == 0
     r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]

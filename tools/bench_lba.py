@@ -13,6 +13,44 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 
+PROFILE = REPO / "profiles" / "r03" / "ba" / "ba_kernels.json"
+
+
+def roofline(window: str, n_sys: int) -> dict:
+    """The back-end's roofline block from the committed rocprofv3 evidence
+    (tools/ba_prof.sh -> tools/ba_roofline.py -> profiles/r03/ba/): fp64
+    FLOP/s and MFMA busy of k_lba_solve against the gfx950 fp64 matrix peak
+    (the chip's, and the one CU a single-workgroup solve can use), HBM GB/s
+    of the per-edge / per-pair stages against 8 TB/s.  Recomputable from the
+    CSVs next to the JSON."""
+    import json
+
+    if not PROFILE.exists():
+        return {"source": None}
+    d = json.loads(PROFILE.read_text())
+    rows = d.get(window, {})
+    out = {"source": str(PROFILE.relative_to(REPO)), "peaks": d.get("peaks"),
+           "bound": "latency: the solve is one workgroup (one CU) working down a 16-pivot-tile "
+                    "chain; the edge / pair stages move a few MB per launch"}
+    solve = next((k for k in rows if k.startswith("k_lba_solve")), None)
+    if solve:
+        r = rows[solve]
+        alg = n_sys ** 3 / 3 + 2 * n_sys ** 2  # LDL^T + the two substitutions
+        out["solve"] = {"kernel": solve, "n": n_sys, "avg_us": round(r["avg_ns"] / 1e3, 2),
+                        "mfma_f64_flop": r.get("mfma_f64_flop"),
+                        "fp64_GFLOPs_mfma": r.get("fp64_GFLOPs"),
+                        "frac_chip_fp64_peak": r.get("fp64_frac_chip"),
+                        "frac_one_cu_fp64_peak": r.get("fp64_frac_cus_used"),
+                        "mfma_busy_frac_one_cu": r.get("mfma_busy_frac_cus_used"),
+                        "algorithmic_flop": int(alg),
+                        "algorithmic_GFLOPs": round(alg / r["avg_ns"], 3)}
+    out["hbm"] = {k: {"avg_us": round(r["avg_ns"] / 1e3, 2), "hbm_bytes": r.get("hbm_bytes"),
+                      "GBs": r.get("hbm_GBs"), "frac": r.get("hbm_frac"),
+                      "share_of_kernel_time": r.get("share_of_kernel_time")}
+                  for k, r in rows.items() if not k.startswith("__") and "solve" not in k}
+    return out
+
+
 def measure(calls: int = 10, cpu_calls: int = 3) -> dict:
     from orb_slam_fusion_amd import LocalBundleAdjuster, synth
 
@@ -27,7 +65,8 @@ def measure(calls: int = 10, cpu_calls: int = 3) -> dict:
     out = {"workload": "C4 LocalBundleAdjustment: 20 KF (2 fixed), 3000 MP, 18000 edges "
                        "(50% stereo), optimize(10)",
            "gpu_ms_per_call": round(gpu_ms, 3), "lm_iterations": int(r["stats"][2]),
-           "lm_trials": int(r["stats"][3]), "chi2_gpu": r["stats"][1]}
+           "lm_trials": int(r["stats"][3]), "chi2_gpu": r["stats"][1],
+           "roofline": roofline("lba", 6 * int((p.fixed == 0).sum()))}
     if cpu_calls > 0:
         sys.path.insert(0, str(REPO / "oracle"))
         import binding as oracle  # cpu baseline leg only
@@ -63,6 +102,8 @@ def measure_lia(calls: int = 10, cpu_calls: int = 3, b_large: bool = False) -> d
                        f"(50% stereo), {len(p.imu_edges)} IMU links, optimize({p.iterations})",
            "gpu_ms_per_call": round(gpu_ms, 3), "lm_iterations": int(r["stats"][2]),
            "lm_trials": int(r["stats"][3]), "err": r["stats"][0], "err_end": r["stats"][1]}
+    if not b_large:
+        out["roofline"] = roofline("lia", 15 * n_opt)
     if cpu_calls > 0:
         sys.path.insert(0, str(REPO / "oracle"))
         import binding as oracle  # cpu baseline leg only

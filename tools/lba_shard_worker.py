@@ -4,7 +4,11 @@ a gloo group; started as a fresh interpreter before it touches the GPU by
 tests/test_gpu_lba.py::test_lba_two_ranks_one_gpu and by bench_lba's
 sharded side line.  CALLS > 0: also time that many calls (barrier first).
 
-    python tools/lba_shard_worker.py RANK WORLD PORT OUT_DIR [CALLS]
+    python tools/lba_shard_worker.py RANK WORLD PORT OUT_DIR [CALLS] [ORDERED]
+
+ORDERED = 1: the stream-ordered form (orbgpu_lba_ctx_set_reduce_ordered,
+lba.dist_enqueue): the LM loop stays on the device and the reductions are
+enqueued on the library's stream.
 """
 import os
 import sys
@@ -19,6 +23,7 @@ sys.path.insert(0, str(REPO))
 def main() -> None:
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], Path(sys.argv[4])
     calls = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    ordered = len(sys.argv) > 6 and sys.argv[6] == "1"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch.distributed as dist
 
@@ -29,7 +34,7 @@ def main() -> None:
     n = len(p.pts_init)
     cut = [0, n // 2 + 13, n]  # uneven shards on purpose
     lba = LocalBundleAdjuster(0)
-    r = lba.optimize(p, pt_range=(cut[rank], cut[rank + 1]), group=dist.group.WORLD)
+    r = lba.optimize(p, pt_range=(cut[rank], cut[rank + 1]), group=dist.group.WORLD, ordered=ordered)
     ms = 0.0
     if calls > 0:
         import time
@@ -37,7 +42,7 @@ def main() -> None:
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(calls):
-            lba.optimize(p, pt_range=(cut[rank], cut[rank + 1]), group=dist.group.WORLD)
+            lba.optimize(p, pt_range=(cut[rank], cut[rank + 1]), group=dist.group.WORLD, ordered=ordered)
         ms = (time.perf_counter() - t0) / calls * 1e3
     np.savez(out / f"r{rank}.npz", poses_d=r["poses_d"], pts=r["pts"], outlier=r["outlier"],
              stats=r["stats"], cut=np.array(cut), ms_per_call=np.array(ms))
