@@ -2,8 +2,10 @@
 // (orbgpu_pose_inertial*, include/orbgpu.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "../../include/orbgpu.h"
 
@@ -26,11 +28,23 @@ struct orbgpu_inertial_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_problems = 0, max_obs = 0;
-  // single-problem staging: [cur | prev | preint | prior | nobs] then obs, result, outliers
+  // single-problem path: the input and the output as one block each, pinned
+  // on the host and mirrored on the device -- in: [cur | prev | preint |
+  // prior | n_obs | obs], out: [result | outlier flags] -- so a call is one
+  // H2D copy, the kernel and one D2H copy, sized by the observation count's
+  // bucket, replayed as a hipGraph per (mode, bucket, rec_init, calibration)
+  // from the second call of that key on
+  uint8_t* h_in = nullptr;
+  uint8_t* h_out = nullptr;
   uint8_t* d_in = nullptr;
-  orbgpu_inertial_obs* d_obs = nullptr;
-  orbgpu_inertial_result* d_res = nullptr;
   uint8_t* d_out = nullptr;
+  struct Graph {
+    int mode = 0, bucket = 0, rec_init = 0;
+    orbgpu_imu_calib calib{};
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<Graph> graphs;  // a few keys, oldest replaced first
 };
 
 namespace {
@@ -38,11 +52,40 @@ constexpr size_t kOffPrev = 136, kOffPreint = 272, kOffPrior = 1336, kOffN = 330
 static_assert(kOffPrev >= sizeof(orbgpu_imu_state) && kOffPreint - kOffPrev >= sizeof(orbgpu_imu_state) &&
                   kOffPrior - kOffPreint >= sizeof(orbgpu_imu_preint) &&
                   kOffN - kOffPrior >= sizeof(orbgpu_imu_prior) && kOffPreint % 8 == 0 &&
-                  kOffPrior % 8 == 0,
+                  kOffPrior % 8 == 0 && kInBytes % 16 == 0,
               "staging layout");
+constexpr size_t kOutFlags = 2064;  // the result record, then the flags
+static_assert(sizeof(orbgpu_inertial_result) <= kOutFlags && kOutFlags % 16 == 0, "output layout");
+constexpr int kObsBucket = 128;
+constexpr size_t kMaxGraphs = 6;
 
 bool valid_calib(const orbgpu_imu_calib* c) {
   return c && c->fx > 0 && c->fy > 0;
+}
+
+hipError_t enqueue_single(orbgpu_inertial_ctx* c, int mode, const orbgpu_imu_calib& calib, int bucket,
+                          int rec_init) {
+  hipStream_t st = c->stream;
+  hipError_t e = hipMemcpyAsync(c->d_in, c->h_in, kInBytes + sizeof(orbgpu_inertial_obs) * bucket,
+                                hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = orbgpu::launch_pose_inertial(
+        mode, calib, 1, reinterpret_cast<const orbgpu_imu_state*>(c->d_in),
+        reinterpret_cast<const orbgpu_imu_state*>(c->d_in + kOffPrev),
+        reinterpret_cast<const orbgpu_imu_preint*>(c->d_in + kOffPreint),
+        reinterpret_cast<const orbgpu_imu_prior*>(c->d_in + kOffPrior),
+        reinterpret_cast<const orbgpu_inertial_obs*>(c->d_in + kInBytes),
+        reinterpret_cast<const int*>(c->d_in + kOffN), bucket, rec_init,
+        reinterpret_cast<orbgpu_inertial_result*>(c->d_out), c->d_out + kOutFlags, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out, c->d_out, kOutFlags + bucket, hipMemcpyDeviceToHost, st);
+  return e;
+}
+
+void destroy_graph(orbgpu_inertial_ctx::Graph& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
 }
 }  // namespace
 
@@ -58,11 +101,11 @@ orbgpu_status orbgpu_inertial_ctx_create(int device, int max_problems, int max_o
   c->device = device;
   c->max_problems = max_problems;
   c->max_obs = max_obs;
+  const size_t nb = (size_t)(max_obs + kObsBucket - 1) / kObsBucket * kObsBucket;
+  const size_t in_bytes = kInBytes + sizeof(orbgpu_inertial_obs) * nb, out_bytes = kOutFlags + nb;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_in, kInBytes) != hipSuccess ||
-      hipMalloc(&c->d_obs, sizeof(orbgpu_inertial_obs) * max_obs) != hipSuccess ||
-      hipMalloc(&c->d_res, sizeof(orbgpu_inertial_result)) != hipSuccess ||
-      hipMalloc(&c->d_out, max_obs) != hipSuccess) {
+      hipMalloc(&c->d_in, in_bytes) != hipSuccess || hipMalloc(&c->d_out, out_bytes) != hipSuccess ||
+      hipHostMalloc(&c->h_in, in_bytes) != hipSuccess || hipHostMalloc(&c->h_out, out_bytes) != hipSuccess) {
     orbgpu_inertial_ctx_destroy(c);
     return ORBGPU_ERR_DEVICE;
   }
@@ -74,10 +117,11 @@ void orbgpu_inertial_ctx_destroy(orbgpu_inertial_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& g : c->graphs) destroy_graph(g);
   if (c->d_in) (void)hipFree(c->d_in);
-  if (c->d_obs) (void)hipFree(c->d_obs);
-  if (c->d_res) (void)hipFree(c->d_res);
   if (c->d_out) (void)hipFree(c->d_out);
+  if (c->h_in) (void)hipHostFree(c->h_in);
+  if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -94,31 +138,56 @@ orbgpu_status orbgpu_pose_inertial(orbgpu_inertial_ctx* c, int mode, const orbgp
     return ORBGPU_ERR_INVALID;
   if (n_obs > c->max_obs) return ORBGPU_ERR_CAPACITY;
   if (hipSetDevice(c->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
-  uint8_t host[kInBytes];
-  std::memset(host, 0, sizeof(host));
+  uint8_t* host = c->h_in;
   std::memcpy(host, cur, sizeof(*cur));
   std::memcpy(host + kOffPrev, prev, sizeof(*prev));
   std::memcpy(host + kOffPreint, preint, sizeof(*preint));
-  if (prior) std::memcpy(host + kOffPrior, prior, sizeof(*prior));
+  if (prior)
+    std::memcpy(host + kOffPrior, prior, sizeof(*prior));
+  else
+    std::memset(host + kOffPrior, 0, sizeof(orbgpu_imu_prior));
   std::memcpy(host + kOffN, &n_obs, sizeof(int));
-  hipStream_t st = c->stream;
-  if (hipMemcpyAsync(c->d_in, host, kInBytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-      (n_obs > 0 && hipMemcpyAsync(c->d_obs, obs, sizeof(*obs) * n_obs, hipMemcpyHostToDevice,
-                                   st) != hipSuccess))
-    return ORBGPU_ERR_DEVICE;
-  const auto* d_cur = reinterpret_cast<const orbgpu_imu_state*>(c->d_in);
-  const auto* d_prev = reinterpret_cast<const orbgpu_imu_state*>(c->d_in + kOffPrev);
-  const auto* d_pre = reinterpret_cast<const orbgpu_imu_preint*>(c->d_in + kOffPreint);
-  const auto* d_pri = reinterpret_cast<const orbgpu_imu_prior*>(c->d_in + kOffPrior);
-  const auto* d_n = reinterpret_cast<const int*>(c->d_in + kOffN);
-  if (orbgpu::launch_pose_inertial(mode, *calib, 1, d_cur, d_prev, d_pre, d_pri, c->d_obs, d_n,
-                                   c->max_obs, rec_init, c->d_res, c->d_out, st) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
-  if (hipMemcpyAsync(res, c->d_res, sizeof(*res), hipMemcpyDeviceToHost, st) != hipSuccess ||
-      (n_obs > 0 &&
-       hipMemcpyAsync(outlier, c->d_out, n_obs, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
+  if (n_obs > 0) std::memcpy(host + kInBytes, obs, sizeof(*obs) * n_obs);
+  const int bucket = std::min(c->max_obs, std::max(1, (n_obs + kObsBucket - 1) / kObsBucket) * kObsBucket);
+  const int ri = rec_init ? 1 : 0;
+  orbgpu_inertial_ctx::Graph* g = nullptr;
+  for (auto& x : c->graphs)
+    if (x.mode == mode && x.bucket == bucket && x.rec_init == ri && memcmp(&x.calib, calib, sizeof(*calib)) == 0)
+      g = &x;
+  hipError_t e = hipSuccess;
+  if (g && g->exec) {
+    e = hipGraphLaunch(g->exec, c->stream);
+  } else if (g) {  // second call of this key: capture (the LDS opt-in is done)
+    e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed);
+    if (e == hipSuccess) {
+      const hipError_t le = enqueue_single(c, mode, *calib, bucket, ri);
+      e = hipStreamEndCapture(c->stream, &g->graph);
+      if (e == hipSuccess) e = le;
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    if (e == hipSuccess) {
+      e = hipGraphLaunch(g->exec, c->stream);
+    } else {
+      (void)hipGetLastError();
+      destroy_graph(*g);
+      e = enqueue_single(c, mode, *calib, bucket, ri);
+    }
+  } else {
+    e = enqueue_single(c, mode, *calib, bucket, ri);
+    if (c->graphs.size() >= kMaxGraphs) {
+      destroy_graph(c->graphs.front());
+      c->graphs.erase(c->graphs.begin());
+    }
+    orbgpu_inertial_ctx::Graph ng;
+    ng.mode = mode;
+    ng.bucket = bucket;
+    ng.rec_init = ri;
+    ng.calib = *calib;
+    c->graphs.push_back(ng);
+  }
+  if (e != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  std::memcpy(res, c->h_out, sizeof(*res));
+  if (n_obs > 0) std::memcpy(outlier, c->h_out + kOutFlags, n_obs);
   return ORBGPU_OK;
 }
 

@@ -59,23 +59,26 @@ struct orbgpu_extractor {
   uint64_t* d_desc = nullptr;
   int* d_err = nullptr;
 
-  // single-image (host-buffer) path
+  // single-image (host-buffer) path: the outputs as ONE device block
+  // [n, mono, err, pad | keypoints (kp_slots x 28, 16-B aligned) | descriptors]
+  // mirrored by one pinned block, so the chain ends in a single D2H copy; the
+  // pointers below are views into the blocks (d_sout / h_sout own them)
   uint8_t* d_img = nullptr;
   size_t d_img_bytes = 0;
+  char* d_sout = nullptr;
+  char* h_sout = nullptr;
+  size_t sout_bytes = 0;
   orbgpu_keypoint* d_kps = nullptr;
   uint8_t* d_descs = nullptr;
   size_t out_cap = 0;
-  int* d_nm = nullptr;  // n, mono
-  // the single-image chain (13 kernels + the count / error copies into the
-  // pinned h_small) replayed as one hipGraph while its launch is unchanged
+  int* d_nm = nullptr;     // n, mono, err (the single-image launch's error word)
   int* h_small = nullptr;  // n, mono, err (pinned)
-  // pinned staging of the image and of the outputs: the copies are part of
-  // the graph (fixed addresses and sizes), the host only memcpys
-  uint8_t* h_img = nullptr;
-  size_t h_img_bytes = 0;
   orbgpu_keypoint* h_kps = nullptr;
   uint8_t* h_descs = nullptr;
-  size_t h_out_cap = 0;
+  // pinned staging of the image: the copies are part of the graph (fixed
+  // addresses and sizes), the host only memcpys
+  uint8_t* h_img = nullptr;
+  size_t h_img_bytes = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   ExtractLaunch graph_launch{};  // what graph_exec was captured for
@@ -111,6 +114,30 @@ void drop_graphs(orbgpu_extractor* h) {
   h->graph = nullptr;
   h->graph_valid = false;
   h->eager_valid = false;
+}
+
+// The single-image output blocks for `slots` keypoints (see orbgpu_extractor).
+orbgpu_status ensure_single_out(orbgpu_extractor* h, size_t slots) {
+  if (slots <= h->out_cap && h->d_sout) return ORBGPU_OK;
+  drop_graphs(h);
+  const size_t kp_bytes = (slots * sizeof(orbgpu_keypoint) + 15) & ~(size_t)15;
+  const size_t bytes = 16 + kp_bytes + slots * 32;
+  if (h->d_sout) (void)hipFree(h->d_sout);
+  if (h->h_sout) (void)hipHostFree(h->h_sout);
+  h->d_sout = h->h_sout = nullptr;
+  h->out_cap = 0;
+  if (hipMalloc(&h->d_sout, bytes) != hipSuccess || hipHostMalloc(&h->h_sout, bytes) != hipSuccess)
+    return ORBGPU_ERR_NOMEM;
+  if (hipMemset(h->d_sout, 0, 16) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  h->sout_bytes = bytes;
+  h->out_cap = slots;
+  h->d_nm = reinterpret_cast<int*>(h->d_sout);
+  h->d_kps = reinterpret_cast<orbgpu_keypoint*>(h->d_sout + 16);
+  h->d_descs = reinterpret_cast<uint8_t*>(h->d_sout + 16 + kp_bytes);
+  h->h_small = reinterpret_cast<int*>(h->h_sout);
+  h->h_kps = reinterpret_cast<orbgpu_keypoint*>(h->h_sout + 16);
+  h->h_descs = reinterpret_cast<uint8_t*>(h->h_sout + 16 + kp_bytes);
+  return ORBGPU_OK;
 }
 
 orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
@@ -290,8 +317,8 @@ static bool same_launch(const ExtractLaunch& x, const ExtractLaunch& y) {
 }
 
 // Enqueue the single-image chain between its copies: the image from pinned
-// h_img, then (n, mono, err) and the full-capacity keypoint / descriptor
-// blocks into pinned memory.  A launch seen twice in a row (same plan, buffers, lapping)
+// h_img, then the output block (n, mono, err, the full-capacity keypoints and
+// descriptors) into pinned memory in one copy.  A launch seen twice in a row (same plan, buffers, lapping)
 // is captured into a hipGraph and replayed from then on: the per-frame
 // host path submits one graph instead of 13 kernels and 5 copies.  The
 // first run of a launch stays eager (it also performs the one-time LDS
@@ -300,15 +327,9 @@ static hipError_t enqueue_chain(orbgpu_extractor* h, const ExtractLaunch& a) {
   hipError_t e = hipMemcpyAsync(const_cast<uint8_t*>(a.imgs), h->h_img, a.image_pitch,
                                 hipMemcpyHostToDevice, h->stream);
   if (e == hipSuccess) e = launch_extract(a, h->stream);
+  // n, mono, err, keypoints and descriptors: one copy of the output block
   if (e == hipSuccess)
-    e = hipMemcpyAsync(h->h_small, h->d_nm, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(h->h_small + 2, h->d_err, sizeof(int), hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(h->h_kps, a.kps_out, (size_t)a.cap * sizeof(orbgpu_keypoint),
-                       hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(h->h_descs, a.desc_out, (size_t)a.cap * 32, hipMemcpyDeviceToHost, h->stream);
+    e = hipMemcpyAsync(h->h_sout, h->d_sout, h->sout_bytes, hipMemcpyDeviceToHost, h->stream);
   return e;
 }
 
@@ -368,14 +389,14 @@ orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int devic
       h->n_cu < 1)
     h->n_cu = 256;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1) || dalloc(&h->d_nm, 2) ||
-      hipHostMalloc(&h->h_small, 4 * sizeof(int)) != hipSuccess) {
+      dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1)) {
     orbgpu_extractor_destroy(h);
     return ORBGPU_ERR_DEVICE;
   }
   (void)hipMemset(h->d_err, 0, sizeof(int));
   orbgpu_status st = ensure_plan(h, max_width, max_height);
   if (st == ORBGPU_OK) st = ensure_workspace(h, max_images);
+  if (st == ORBGPU_OK) st = ensure_single_out(h, (size_t)h->plan.hdr.kp_slots);
   if (st != ORBGPU_OK) {
     orbgpu_extractor_destroy(h);
     return st;
@@ -403,15 +424,11 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_desc);
   dfree(h->d_err);
   dfree(h->d_img);
-  dfree(h->d_kps);
-  dfree(h->d_descs);
-  dfree(h->d_nm);
+  if (h->d_sout) (void)hipFree(h->d_sout);
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
-  if (h->h_small) (void)hipHostFree(h->h_small);
+  if (h->h_sout) (void)hipHostFree(h->h_sout);
   if (h->h_img) (void)hipHostFree(h->h_img);
-  if (h->h_kps) (void)hipHostFree(h->h_kps);
-  if (h->h_descs) (void)hipHostFree(h->h_descs);
   dfree(h->d_st_lists);
   dfree(h->d_st_rowend);
   dfree(h->d_st_sad);
@@ -470,9 +487,8 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   const PlanHeader& P = h->plan.hdr;
   const int pitch0 = P.lev[0].pitch;  // 16-byte aligned rows for the vector loads
   const size_t bytes = (size_t)pitch0 * height;
-  if (bytes > h->d_img_bytes || bytes > h->h_img_bytes || (size_t)P.kp_slots > h->out_cap ||
-      (size_t)P.kp_slots > h->h_out_cap)
-    drop_graphs(h);  // staging or output buffers about to be reallocated
+  if (bytes > h->d_img_bytes || bytes > h->h_img_bytes)
+    drop_graphs(h);  // image staging about to be reallocated
   if (bytes > h->d_img_bytes) {
     dfree(h->d_img);
     if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
@@ -485,24 +501,7 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
     if (hipHostMalloc(&h->h_img, bytes) != hipSuccess) return ORBGPU_ERR_NOMEM;
     h->h_img_bytes = bytes;
   }
-  if ((size_t)P.kp_slots > h->out_cap) {
-    dfree(h->d_kps);
-    dfree(h->d_descs);
-    if (dalloc(&h->d_kps, P.kp_slots) || dalloc(&h->d_descs, (size_t)P.kp_slots * 32))
-      return ORBGPU_ERR_NOMEM;
-    h->out_cap = P.kp_slots;
-  }
-  if ((size_t)P.kp_slots > h->h_out_cap) {
-    if (h->h_kps) (void)hipHostFree(h->h_kps);
-    if (h->h_descs) (void)hipHostFree(h->h_descs);
-    h->h_kps = nullptr;
-    h->h_descs = nullptr;
-    h->h_out_cap = 0;
-    if (hipHostMalloc(&h->h_kps, (size_t)P.kp_slots * sizeof(orbgpu_keypoint)) != hipSuccess ||
-        hipHostMalloc(&h->h_descs, (size_t)P.kp_slots * 32) != hipSuccess)
-      return ORBGPU_ERR_NOMEM;
-    h->h_out_cap = P.kp_slots;
-  }
+  if ((st = ensure_single_out(h, (size_t)P.kp_slots)) != ORBGPU_OK) return st;
   // the image into pinned staging (rows at the level-0 pitch); the graph copies it
   if (stride == pitch0) {
     std::memcpy(h->h_img, img, bytes);
@@ -513,6 +512,7 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
   ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
                                 P.kp_slots, h->d_nm, h->d_nm + 1);
+  a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs
   if (run_single_chain(h, a) != hipSuccess || hipStreamSynchronize(h->stream))
     return ORBGPU_ERR_DEVICE;
   const int nm[2] = {h->h_small[0], h->h_small[1]}, err = h->h_small[2];
@@ -520,7 +520,7 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
   h->last_w = width;
   h->last_h = height;
   if (err) {
-    (void)hipMemset(h->d_err, 0, sizeof(int));
+    (void)hipMemset(h->d_nm + 2, 0, sizeof(int));
     return ORBGPU_ERR_CAPACITY;
   }
   *n_out = nm[0];
@@ -741,7 +741,7 @@ orbgpu_status orbgpu_extractor_check(orbgpu_extractor* h) {
       hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
   if (err) {
-    (void)hipMemset(h->d_err, 0, sizeof(int));
+    (void)hipMemset(h->d_nm + 2, 0, sizeof(int));
     return ORBGPU_ERR_CAPACITY;
   }
   return ORBGPU_OK;

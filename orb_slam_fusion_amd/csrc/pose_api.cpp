@@ -1,6 +1,9 @@
 // C-ABI implementation of the pose-only optimisation half of include/orbgpu.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <vector>
+
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -21,51 +24,58 @@ struct orbgpu_pose_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_obs = 0;
-  orbgpu_pose_obs* d_obs = nullptr;
-  float* d_pose = nullptr;  // in[7], out[7]
-  uint8_t* d_outlier = nullptr;
-  int* d_ints = nullptr;  // n, inliers
   // speculative LM trial groups per problem (k_pose_opt), see
   // orbgpu_pose_ctx_set_trial_groups
   int groups_single = 1;
   int groups_batch = 1;
-  // single-problem path: pinned staging (obs[max_obs], pose in, n | pose out,
-  // inliers, outlier[max_obs]) and the fixed-size copy + kernel + copy chain,
-  // replayed as a hipGraph from the second call on
+  // single-problem path: the input and output as one block each, pinned on
+  // the host and mirrored on the device -- in: pose (28 B), n (4 B), obs;
+  // out: pose (28 B), inliers (4 B), outlier flags -- so a call is one H2D
+  // copy, the kernel and one D2H copy, sized by the observation count's
+  // bucket (kObsBucket), replayed as a hipGraph per (bucket, groups, camera)
+  // from the second call of that key on
   uint8_t* h_in = nullptr;
   uint8_t* h_out = nullptr;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t graph_exec = nullptr;
-  int graph_groups = 0;
-  double graph_cam[5] = {};
-  bool warm = false;
+  uint8_t* d_in = nullptr;
+  uint8_t* d_out = nullptr;
+  struct Graph {
+    int bucket = 0, groups = 0;
+    double cam[5] = {};
+    bool warm = false;  // seen once: captured on the next call
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<Graph> graphs;  // a few keys, oldest replaced first
 };
 
 namespace {
-constexpr size_t kInPose = 0;  // h_in layout: pose (28 B), n (4 B), pad, obs
+constexpr size_t kInPose = 0;  // h_in / d_in layout: pose (28 B), n (4 B), obs
 constexpr size_t kInN = 28;
 constexpr size_t kInObs = 32;
-constexpr size_t kOutPose = 0;  // h_out layout: pose (28 B), inliers (4 B), outlier flags
+constexpr size_t kOutPose = 0;  // h_out / d_out layout: pose (28 B), inliers (4 B), outlier flags
 constexpr size_t kOutInl = 28;
 constexpr size_t kOutFlags = 32;
+constexpr int kObsBucket = 128;  // copy sizes rounded up to this many observations
+constexpr size_t kMaxGraphs = 6;
 
-hipError_t enqueue_single(orbgpu_pose_ctx* c, const double cd[5]) {
-  const size_t obs_bytes = sizeof(orbgpu_pose_obs) * c->max_obs;
-  hipError_t e = hipMemcpyAsync(c->d_obs, c->h_in + kInObs, obs_bytes, hipMemcpyHostToDevice, c->stream);
+hipError_t enqueue_single(orbgpu_pose_ctx* c, const double cd[5], int bucket, int groups) {
+  hipError_t e = hipMemcpyAsync(c->d_in, c->h_in, kInObs + sizeof(orbgpu_pose_obs) * bucket,
+                                hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(c->d_pose, c->h_in + kInPose, sizeof(orbgpu_pose), hipMemcpyHostToDevice, c->stream);
+    e = orbgpu::launch_pose_opt(cd, reinterpret_cast<const float*>(c->d_in + kInPose), c->d_in + kInObs,
+                                reinterpret_cast<const int*>(c->d_in + kInN), bucket, 1,
+                                reinterpret_cast<float*>(c->d_out + kOutPose), c->d_out + kOutFlags,
+                                reinterpret_cast<int*>(c->d_out + kOutInl), nullptr, c->stream, groups);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(c->d_ints, c->h_in + kInN, sizeof(int), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess)
-    e = orbgpu::launch_pose_opt(cd, c->d_pose, c->d_obs, c->d_ints, c->max_obs, 1, c->d_pose + 7,
-                                c->d_outlier, c->d_ints + 1, nullptr, c->stream, c->groups_single);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(c->h_out + kOutPose, c->d_pose + 7, sizeof(orbgpu_pose), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(c->h_out + kOutInl, c->d_ints + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(c->h_out + kOutFlags, c->d_outlier, c->max_obs, hipMemcpyDeviceToHost, c->stream);
+    e = hipMemcpyAsync(c->h_out, c->d_out, kOutFlags + bucket, hipMemcpyDeviceToHost, c->stream);
   return e;
+}
+
+void destroy_graph(orbgpu_pose_ctx::Graph& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
 }
 }  // namespace
 
@@ -84,13 +94,11 @@ orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
     const int g = atoi(e);
     if (g == 1 || g == 2) c->groups_single = c->groups_batch = g;
   }
+  const size_t in_bytes = kInObs + sizeof(orbgpu_pose_obs) * ((max_obs + kObsBucket - 1) / kObsBucket * kObsBucket);
+  const size_t out_bytes = kOutFlags + (max_obs + kObsBucket - 1) / kObsBucket * kObsBucket;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_obs, sizeof(orbgpu_pose_obs) * max_obs) != hipSuccess ||
-      hipMalloc(&c->d_pose, sizeof(float) * 14) != hipSuccess ||
-      hipMalloc(&c->d_outlier, max_obs) != hipSuccess ||
-      hipMalloc(&c->d_ints, sizeof(int) * 2) != hipSuccess ||
-      hipHostMalloc(&c->h_in, kInObs + sizeof(orbgpu_pose_obs) * max_obs) != hipSuccess ||
-      hipHostMalloc(&c->h_out, kOutFlags + max_obs) != hipSuccess) {
+      hipMalloc(&c->d_in, in_bytes) != hipSuccess || hipMalloc(&c->d_out, out_bytes) != hipSuccess ||
+      hipHostMalloc(&c->h_in, in_bytes) != hipSuccess || hipHostMalloc(&c->h_out, out_bytes) != hipSuccess) {
     orbgpu_pose_ctx_destroy(c);
     return ORBGPU_ERR_DEVICE;
   }
@@ -111,12 +119,9 @@ void orbgpu_pose_ctx_destroy(orbgpu_pose_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->d_obs) (void)hipFree(c->d_obs);
-  if (c->d_pose) (void)hipFree(c->d_pose);
-  if (c->d_outlier) (void)hipFree(c->d_outlier);
-  if (c->d_ints) (void)hipFree(c->d_ints);
-  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-  if (c->graph) (void)hipGraphDestroy(c->graph);
+  if (c->d_in) (void)hipFree(c->d_in);
+  if (c->d_out) (void)hipFree(c->d_out);
+  for (auto& g : c->graphs) destroy_graph(g);
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -137,34 +142,40 @@ orbgpu_status orbgpu_pose_opt(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
   memcpy(c->h_in + kInPose, Tcw_in, sizeof(orbgpu_pose));
   memcpy(c->h_in + kInN, &n_obs, sizeof(int));
   if (n_obs > 0) memcpy(c->h_in + kInObs, obs, sizeof(orbgpu_pose_obs) * n_obs);
-  const bool same_graph = c->graph_exec && c->graph_groups == c->groups_single &&
-                          memcmp(c->graph_cam, cd, sizeof(cd)) == 0;
+  const int bucket = std::min(c->max_obs, std::max(1, (n_obs + kObsBucket - 1) / kObsBucket) * kObsBucket);
+  const int groups = c->groups_single;
+  orbgpu_pose_ctx::Graph* g = nullptr;
+  for (auto& x : c->graphs)
+    if (x.bucket == bucket && x.groups == groups && memcmp(x.cam, cd, sizeof(cd)) == 0) g = &x;
   hipError_t e = hipSuccess;
-  if (same_graph) {
-    e = hipGraphLaunch(c->graph_exec, c->stream);
-  } else if (c->warm) {  // second call: capture the chain (LDS opt-ins already done)
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->graph_exec = nullptr;
-    c->graph = nullptr;
+  if (g && g->exec) {
+    e = hipGraphLaunch(g->exec, c->stream);
+  } else if (g) {  // second call of this key: capture the chain (LDS opt-ins already done)
     e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed);
     if (e == hipSuccess) {
-      const hipError_t le = enqueue_single(c, cd);
-      e = hipStreamEndCapture(c->stream, &c->graph);
+      const hipError_t le = enqueue_single(c, cd, bucket, groups);
+      e = hipStreamEndCapture(c->stream, &g->graph);
       if (e == hipSuccess) e = le;
     }
-    if (e == hipSuccess) e = hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
     if (e == hipSuccess) {
-      c->graph_groups = c->groups_single;
-      memcpy(c->graph_cam, cd, sizeof(cd));
-      e = hipGraphLaunch(c->graph_exec, c->stream);
+      e = hipGraphLaunch(g->exec, c->stream);
     } else {
       (void)hipGetLastError();
-      e = enqueue_single(c, cd);
+      destroy_graph(*g);
+      e = enqueue_single(c, cd, bucket, groups);
     }
   } else {
-    e = enqueue_single(c, cd);
-    c->warm = true;
+    e = enqueue_single(c, cd, bucket, groups);
+    if (c->graphs.size() >= kMaxGraphs) {
+      destroy_graph(c->graphs.front());
+      c->graphs.erase(c->graphs.begin());
+    }
+    orbgpu_pose_ctx::Graph ng;
+    ng.bucket = bucket;
+    ng.groups = groups;
+    memcpy(ng.cam, cd, sizeof(cd));
+    c->graphs.push_back(ng);
   }
   if (e != hipSuccess || hipStreamSynchronize(c->stream)) return ORBGPU_ERR_DEVICE;
   memcpy(Tcw_out, c->h_out + kOutPose, sizeof(orbgpu_pose));
