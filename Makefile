@@ -15,7 +15,7 @@ GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
 GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
 
-all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so build/valu_calib oracle
+all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial oracle
 
 OBJDIR   := build/obj
 GPU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(GPU_SRCS))
@@ -37,6 +37,12 @@ $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 build/valu_calib: tools/valu_calib.hip
 	@mkdir -p build
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fno-slp-vectorize -o $@ $<
+
+# C++ caller of the C ABI for the per-frame stereo-inertial latency
+# (tools/bench_latency_inertial.py runs it beside its Python leg)
+build/latency_inertial: tools/latency_inertial.cc include/orbgpu.h $(LIB)/liborbgpu.so
+	@mkdir -p build
+	$(CXX) -std=c++17 -O2 -pthread -o $@ $< -L$(LIB) -lorbgpu -Wl,-rpath,'$$ORIGIN/../$(LIB)'
 
 oracle:
 	$(MAKE) -C oracle

@@ -15,7 +15,11 @@ The local map is the previous frame's stereo points (tools/bench_track.Chain,
 built once); the IMU inputs follow the chain's camera (tools/inertial_chain).
 Timed end to end per frame (host copies included), median over frames, beside
 the CPU oracle running the same sequence on the same host (2 threads for the
-extractions, 1 for the rest).
+extractions, 1 for the rest).  Two GPU legs on the same frames: this Python
+process through ctypes, and tools/latency_inertial.cc (build/latency_inertial)
+calling the C ABI from C++ as the drop-ins do, which also checks that every
+frame's observation count and n_good equal the Python leg's; the C++ leg is
+the headline (`host` names it), the Python one stays under `python_host`.
 
     python tools/bench_latency_inertial.py [--frames 16]
 """
@@ -67,7 +71,65 @@ def _obs(kps, ur, match, mp, views, inv_sigma2):
     return o
 
 
-def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4) -> dict:
+def _dump(path, c, maps, imus, inv_sigma2, n_obs, good):
+    """The C++ leg's inputs (tools/latency_inertial.cc reads them in this order)."""
+    import ctypes
+
+    from orb_slam_fusion_amd._lib import (IMU_CALIB_DTYPE, IMU_PREINT_DTYPE, IMU_PRIOR_DTYPE,
+                                          IMU_STATE_DTYPE, INERTIAL_OBS_DTYPE, MAP_POINT_DTYPE,
+                                          Camera, OrbParams)
+    from orb_slam_fusion_amd.matcher import pose_matrices
+
+    frames = len(n_obs)
+    H, W = c.quads[0][2].shape
+    cam = Camera(*[float(v) for v in c.cam])
+    sizes = [ctypes.sizeof(c.geom), ctypes.sizeof(cam), MAP_POINT_DTYPE.itemsize,
+             IMU_CALIB_DTYPE.itemsize, IMU_STATE_DTYPE.itemsize, IMU_PREINT_DTYPE.itemsize,
+             IMU_PRIOR_DTYPE.itemsize, INERTIAL_OBS_DTYPE.itemsize]
+    with open(path, "wb") as fp:
+        fp.write(b"OSLATIN1")
+        fp.write(np.array([frames, W, H, len(inv_sigma2), c.cap], np.int32).tobytes())
+        fp.write(np.array(sizes, np.int32).tobytes())
+        fp.write(bytes(OrbParams(*PARAMS)))
+        fp.write(np.array([c.bf, c.mb, TH_LOCAL, NN_LOCAL, 0.5], np.float32).tobytes())
+        fp.write(bytes(c.geom) + bytes(cam))
+        fp.write(np.ascontiguousarray(imus[0][0], IMU_CALIB_DTYPE).tobytes())
+        fp.write(np.asarray(inv_sigma2, np.float32).tobytes())
+        for f in range(frames):
+            _, _, cl, cr = c.quads[f]
+            R, t, Ow = pose_matrices(c.Tcw[f])
+            fp.write(np.ascontiguousarray(cl, np.uint8).tobytes() + np.ascontiguousarray(cr, np.uint8).tobytes())
+            fp.write(R.tobytes() + t.tobytes() + Ow.tobytes())
+            fp.write(np.array([len(maps[f])], np.int32).tobytes())
+            fp.write(np.ascontiguousarray(maps[f], MAP_POINT_DTYPE).tobytes())
+            _, cur, prev, pre, prior = imus[f]
+            for a, dt in ((cur, IMU_STATE_DTYPE), (prev, IMU_STATE_DTYPE), (pre, IMU_PREINT_DTYPE),
+                          (prior, IMU_PRIOR_DTYPE)):
+                fp.write(np.ascontiguousarray(a, dt).tobytes())
+            fp.write(np.array([n_obs[f], good[f]], np.int32).tobytes())
+
+
+def _cpp_leg(c, maps, imus, inv_sigma2, n_obs, good, warmup):
+    """tools/latency_inertial.cc (build/latency_inertial, built by `make`) on the
+    same frames: the per-frame cost a C++ tracking thread sees through the C ABI."""
+    import subprocess
+    import tempfile
+
+    exe = REPO / "build" / "latency_inertial"
+    if not exe.exists():
+        raise RuntimeError(f"{exe} missing: run make")
+    with tempfile.TemporaryDirectory() as tmp:
+        path = Path(tmp) / "latin.bin"
+        _dump(path, c, maps, imus, inv_sigma2, n_obs, good)
+        r = subprocess.run([str(exe), str(path), str(warmup)], capture_output=True, text=True,
+                           timeout=120)
+    if r.returncode != 0:
+        raise RuntimeError(f"latency_inertial exited {r.returncode}: {r.stderr.strip()[-400:]} "
+                           f"{r.stdout.strip()[-600:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4, cpp_host: bool = True) -> dict:
     from bench_track import Chain
     from inertial_chain import imu_inputs
 
@@ -112,22 +174,34 @@ def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4) -> dict:
         p, n, g = one(i % frames)
         if i >= warmup:
             parts.append(p), n_obs.append(n), good.append(g)
+    order = [(i % frames) for i in range(warmup, warmup + frames)]  # frame of each timed pass
+    by_frame = {f: (n, g) for f, n, g in zip(order, n_obs, good)}
+    cpp = _cpp_leg(c, maps, imus, inv_sigma2, [by_frame[f][0] for f in range(frames)],
+                   [by_frame[f][1] for f in range(frames)], warmup) if cpp_host else None
     med = lambda a: float(np.median(a)) * 1e3  # noqa: E731
     cols = list(zip(*parts))
     tot = [sum(p) for p in parts]
-    out = {
-        "workload": "stereo-inertial tracking after IMU init, one 752x480 frame at a time through "
-                    "the host ABI: 2-thread extraction (1000 kp, 8 levels) + ComputeStereoMatches + "
-                    "SearchLocalPoints (isInFrustum + SearchByProjection th 6, nn 0.8) + "
-                    f"PoseInertialOptimizationLastFrame; median of {frames} frames",
+    py = {
+        "host": "Python (ctypes) through the C ABI",
         "gpu_ms_per_frame": round(med(tot), 3),
         "gpu_extract_ms": round(med(cols[0]), 3),
         "gpu_stereo_ms": round(med(cols[1]), 3),
         "gpu_search_local_ms": round(med(cols[2]), 3),
         "gpu_pose_inertial_ms": round(med(cols[3]), 3),
+    }
+    out = {
+        "workload": "stereo-inertial tracking after IMU init, one 752x480 frame at a time through "
+                    "the host ABI: 2-thread extraction (1000 kp, 8 levels) + ComputeStereoMatches + "
+                    "SearchLocalPoints (isInFrustum + SearchByProjection th 6, nn 0.8) + "
+                    f"PoseInertialOptimizationLastFrame; median of {frames} frames",
         "observations_per_frame": round(float(np.mean(n_obs)), 1),
         "inliers_per_frame": round(float(np.mean(good)), 1),
     }
+    # headline: the C++ caller (the drop-ins are C++); the Python leg beside it
+    out.update({k: v for k, v in (cpp or py).items() if k.startswith("gpu_") or k == "host"})
+    if cpp is not None:
+        out["same_work_as_python_leg"] = cpp["same_work_as_python_leg"]
+        out["python_host"] = py
     if cpu_frames > 0:
         sys.path.insert(0, str(REPO / "oracle"))
         import binding as oracle  # cpu baseline leg only
@@ -167,6 +241,7 @@ def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4) -> dict:
                     "cpu_stereo_ms": round(med(cc[1]), 3), "cpu_search_local_ms": round(med(cc[2]), 3),
                     "cpu_pose_inertial_ms": round(med(cc[3]), 3), "cpu_cores": 2,
                     "speedup_vs_cpu": round(cpu / out["gpu_ms_per_frame"], 2),
+                    "speedup_vs_cpu_python_host": round(cpu / py["gpu_ms_per_frame"], 2),
                     "speedup_extract_plus_pose": round(
                         (med(cc[0]) + med(cc[3])) / (out["gpu_extract_ms"] + out["gpu_pose_inertial_ms"]),
                         2)})
@@ -179,5 +254,6 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--cpu-frames", type=int, default=4)
+    ap.add_argument("--no-cpp", action="store_true", help="skip the C++ host leg")
     a = ap.parse_args()
-    print(json.dumps(measure(a.frames, cpu_frames=a.cpu_frames)))
+    print(json.dumps(measure(a.frames, cpu_frames=a.cpu_frames, cpp_host=not a.no_cpp)))
