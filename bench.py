@@ -130,6 +130,16 @@ def load_profile():
         return None
 
 
+def load_fast_stamps():
+    """k_fast_cells phase stamps (tools/stamps.py on the ORB_STAMPS build):
+    the share of cells that ran the minTh fallback pass."""
+    f = REPO / "profiles" / PROFILE_ROUND / "fast_stamps.json"
+    try:
+        return json.loads(f.read_text()) if f.exists() else None
+    except ValueError:
+        return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -312,6 +322,14 @@ def main() -> int:
             for key in ("valu_busy", "rocprof_avg_ms_per_launch", "bound"):
                 if p.get(key) is not None:
                     row[key] = p[key]
+            if p.get("insts_valu_per_launch") is not None and prof.get("images_per_launch"):
+                row["valu_insts_per_64_images"] = round(p["insts_valu_per_launch"] * 64 /
+                                                        prof["images_per_launch"])
+        if st == "fast_cells":
+            fs = load_fast_stamps()
+            if fs:  # minTh fallback cells (stamp counters 10/11, tools/stamps.py)
+                row["fallback_cell_share"] = round(fs["fallback_frac"], 4)
+                row["fallback_source"] = f"profiles/{PROFILE_ROUND}/fast_stamps.json"
         kernels[st] = row
     roofline = {
         "bound": "hbm",

@@ -74,6 +74,16 @@ __device__ __forceinline__ void polar3(double* X) {
   }
 }
 
+// below this squared angle the SO(3) coefficients come from series, not sincos
+constexpr double kSeriesD2 = 0.0025;
+
+// profiling hook of the inertial kernel's stamps build (phase marks inside
+// the IMU edge); empty elsewhere
+#ifndef IMU_EDGE_MARK
+#define IMU_EDGE_MARK(i) (void)0
+#define IMU_EDGE_MARK_INIT (void)0
+#endif
+
 // ExpSO3 (g2o_types.cc:783-796)
 __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   const double d2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
@@ -85,6 +95,11 @@ __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) {
     s = 1.0;
     c = 0.5;
+  } else if (__builtin_amdgcn_readfirstlane(d2 < kSeriesD2 ? 1 : 0)) {
+    // sin(d)/d and (1 - cos d)/d^2 by their Taylor series (truncation
+    // < 1e-20 below d = 0.05; the updates near convergence all land here)
+    s = 1.0 + d2 * (-1.0 / 6 + d2 * (1.0 / 120 + d2 * (-1.0 / 5040 + d2 * (1.0 / 362880))));
+    c = 0.5 + d2 * (-1.0 / 24 + d2 * (1.0 / 720 + d2 * (-1.0 / 40320 + d2 * (1.0 / 3628800))));
   } else {
     double sn, cs;
     sincos(d, &sn, &cs);
@@ -121,17 +136,29 @@ __device__ __forceinline__ void right_j(const double* v, double* J) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) J[i] = i % 4 == 0 ? 1.0 : 0.0;
   if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) return;
-  double W[9], WW[9], sn, cs;
+  double W[9], WW[9];
   m3_hat(v, W);
   m3_mul(W, W, WW);
-  sincos(d, &sn, &cs);
   double a, b;
-  if (kInv) {
-    a = 0.5;
-    b = 1.0 / d2 - (1.0 + cs) / (2.0 * d * sn);
+  if (__builtin_amdgcn_readfirstlane(d2 < kSeriesD2 ? 1 : 0)) {
+    // the coefficients' Taylor series in d^2 (truncation < 1e-20 below 0.05)
+    if (kInv) {  // 1/d^2 - (1 + cos d) / (2 d sin d)
+      a = 0.5;
+      b = 1.0 / 12 + d2 * (1.0 / 720 + d2 * (1.0 / 30240 + d2 * (1.0 / 1209600 + d2 * (1.0 / 47900160))));
+    } else {  // -(1 - cos d) / d^2, (d - sin d) / d^3
+      a = -(0.5 + d2 * (-1.0 / 24 + d2 * (1.0 / 720 + d2 * (-1.0 / 40320 + d2 * (1.0 / 3628800)))));
+      b = 1.0 / 6 + d2 * (-1.0 / 120 + d2 * (1.0 / 5040 + d2 * (-1.0 / 362880 + d2 * (1.0 / 39916800))));
+    }
   } else {
-    a = -(1.0 - cs) / d2;
-    b = (d - sn) / (d2 * d);
+    double sn, cs;
+    sincos(d, &sn, &cs);
+    if (kInv) {
+      a = 0.5;
+      b = 1.0 / d2 - (1.0 + cs) / (2.0 * d * sn);
+    } else {
+      a = -(1.0 - cs) / d2;
+      b = (d - sn) / (d2 * d);
+    }
   }
 #pragma unroll
   for (int i = 0; i < 9; ++i) J[i] += W[i] * a + WW[i] * b;
@@ -227,6 +254,7 @@ __device__ __forceinline__ void pose_update(StateD& s, const double* u, const Ca
 __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const StateD& s2,
                                                    const orbgpu_imu_preint& pi, double dt, int lane,
                                                    double* J, double* ei) {
+  IMU_EDGE_MARK_INIT;
   float bg[3], ba[3], dbg[3], dba[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -239,6 +267,7 @@ __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const State
   delta_rotation(pi, dbg, dR);
   delta_lin(pi.dV, pi.JVg, pi.JVa, dbg, dba, dV);
   delta_lin(pi.dP, pi.JPg, pi.JPa, dbg, dba, dP);
+  IMU_EDGE_MARK(7);
   const double g2 = -(double)9.81f;  // g = (0, 0, -GRAVITY_VALUE)
   double Rbw1[9], dRt[9], T[9], eR[9];
   m3_tr(s1.Rwb, Rbw1);
@@ -247,6 +276,7 @@ __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const State
   m3_mul(T, s2.Rwb, eR);
   double er[3];
   log_so3(eR, er);
+  IMU_EDGE_MARK(9);
   double dv[3], dp[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -297,6 +327,7 @@ __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const State
     m3_mul(Rbw1, s2.Rwb, R12);
     put(6, 18, R12, 1.0);
   }
+  IMU_EDGE_MARK(15);
   double invJr[9];
   right_j<true>(er, invJr);
   put(0, 15, invJr, 1.0);

@@ -29,6 +29,21 @@
 // extractor, whose TUs keep -ffp-contract=off): let products fuse into FMAs.
 #pragma clang fp contract(fast)
 
+#ifdef ORB_STAMPS
+namespace orbgpu {
+extern __device__ unsigned long long g_in_stamps[64 * 16];
+}
+// IMU-edge sub-phases (thread 0): slot i += time since the previous mark
+#define IMU_EDGE_MARK(i)                                                                   \
+  do {                                                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                          \
+    if (threadIdx.x == 0 && blockIdx.x < 64) {                                             \
+      atomicAdd(&orbgpu::g_in_stamps[blockIdx.x * 16 + (i)], now_ - ie_prev_); \
+    }                                                                                      \
+    ie_prev_ = now_;                                                                       \
+  } while (0)
+#define IMU_EDGE_MARK_INIT unsigned long long ie_prev_ = __builtin_amdgcn_s_memtime()
+#endif
 #include "imu_math_dev.h"
 
 namespace orbgpu {
@@ -53,7 +68,15 @@ __device__ unsigned long long g_in_stamps[64 * 16];
         if (ist_acc_[i_]) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + i_], ist_acc_[i_]); \
   } while (0)
 #define ISTAMP_ADD_ITER (ist_acc_[8] += 1)
+// a sub-phase of thread 0 (wave 0) straight into slot i
+#define ISTAMP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define ISTAMP_SUB(i, a, b) \
+  do {                      \
+    if (threadIdx.x == 0) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + (i)], (b) - (a)); \
+  } while (0)
 #else
+#define ISTAMP_T(v) (void)0
+#define ISTAMP_SUB(i, a, b) (void)0
 #define ISTAMP_ADD_ITER (void)0
 #define ISTAMP_INIT (void)0
 #define ISTAMP(i) (void)0
@@ -68,11 +91,17 @@ constexpr int kInLdsObs = 2048;  // observations staged in LDS (the rest re-read
 constexpr int kLd = 31;          // padded row stride of the n x n system
 
 // ---- LDS ----------------------------------------------------------------------
+struct PriorState {  // == the head of orbgpu_imu_prior
+  double Rwb[9], twb[3], vwb[3], bg[3], ba[3];
+};
+static_assert(offsetof(orbgpu_imu_preint, info) == 68 * sizeof(float), "preint float part");
+static_assert(offsetof(orbgpu_imu_prior, H) == sizeof(PriorState), "prior head");
+
 struct InShared {
   StateD cur, prev;
   double ev_Rcw[9], ev_tcw[3];  // current camera pose at the last computeActiveErrors
   CalibD cal;
-  double H[30 * kLd];           // the system (full, row-major, padded)
+  double H[31 * kLd];           // the system (full, row-major, padded) + a zero row
   double b[30];
   double x[30];                 // solver x, persists over the call
   double Ji[9 * 24], ei[9];     // EdgeInertial Jacobian / error
@@ -81,6 +110,11 @@ struct InShared {
   double OJp[15 * 15], Oep[15];
   double wp;                    // prior Huber weight
   double info[81], info_g[9], info_a[9], pH[225];  // edge informations (LDS copies)
+  // the preintegration's float part and the prior's state (LDS copies: read
+  // from global memory they were hoisted into SGPRs over the whole loop and
+  // spilled)
+  orbgpu_imu_preint pre;  // dT .. ba valid (the doubles are the fields above)
+  PriorState prs;
   double vis[27];               // visual 6x6 (lower, 21) + gradient (6)
   double red[kInWaves * 4 * 27];
   double temp[32];
@@ -238,7 +272,7 @@ __device__ void inertial_edge_const(InShared& sh, const orbgpu_imu_preint& pi, i
 
 // EdgePriorPoseImu::computeError / linearizeOplus (g2o_types.cc:739-764) on
 // the previous frame's vertices, and its Huber weight (delta 5)
-__device__ void prior_edge(InShared& sh, const orbgpu_imu_prior* pr, bool prior_kernel, int lane) {
+__device__ void prior_edge(InShared& sh, const PriorState* pr, bool prior_kernel, int lane) {
   const StateD& s1 = sh.prev;
   {
     double PRt[9], Q[9], epr[15], dt3[3], et[3];
@@ -298,48 +332,96 @@ __device__ __forceinline__ int ei_col(int s) {
   return MODE == ORBGPU_INERTIAL_LAST_FRAME ? s - 15 : -1;  // VPk VVk VGk VAk
 }
 
-// The n x n system from the edge pieces: thread-owned entries.
+// sh.vis[k] from the visual waves' row partials (k < 27)
+__device__ __forceinline__ void vis_sum(InShared& sh, int k) {
+  double s = 0;
+#pragma unroll
+  for (int r = kVisWave0 * 4; r < kInWaves * 4; ++r) s += sh.red[r * 27 + k];
+  sh.vis[k] = s;
+}
+
+// Row blocks (bit b: rows 3b..3b+2) of EdgeInertial's Jacobian column c that
+// are not structural zeros (inertial_edge_core / inertial_edge_const).  The
+// dot products below skip only exact zeros, keep the order of the others and
+// so leave every sum unchanged; a block is issued when any lane of the wave
+// needs it (unrolled, its loads batched).
+__device__ __forceinline__ int ji_blocks(int c) {
+  constexpr unsigned kMask = 07 | 04 << 3 | 06 << 6 | 07 << 9 | 06 << 12 | 01 << 15 | 04 << 18 | 02 << 21;
+  return (kMask >> (3 * (c / 3))) & 7;
+}
+// sum_r A[r * lda] * B[r * ldb] over the rows of blocks m (ascending)
+__device__ __forceinline__ double dot_blocks(int m, const double* A, int lda, const double* B, int ldb) {
+  double h = 0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    if (m & (1 << b))
+#pragma unroll
+      for (int r = 3 * b; r < 3 * b + 3; ++r) h += A[r * lda] * B[r * ldb];
+  return h;
+}
+// the same over EdgePriorPoseImu's Jacobian diag(InvJr, Q, I9) (prior_edge):
+// column c < 6 has rows 3(c/3)..+2, column c >= 6 only row c
+__device__ __forceinline__ double dot_prior(int c, const double* A, int lda, const double* B, int ldb) {
+  double h = 0;
+  if (c < 6) {
+    const int r0 = c < 3 ? 0 : 3;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) h += A[(r0 + r) * lda] * B[(r0 + r) * ldb];
+  } else {
+    h += A[c * lda] * B[c * ldb];
+  }
+  return h;
+}
+
+// The n x n system from the edge pieces: thread-owned entries.  Pass 1 runs
+// its three jobs on disjoint threads (Omega J, the prior's Omega J, the visual
+// block's final sums); pass 2 writes both triangles, so the solve reads rows.
 template <int MODE>
 __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu_imu_prior* pr,
                          int t) {
   constexpr int n = MODE == ORBGPU_INERTIAL_LAST_FRAME ? 30 : 15;
   // pass 1: Omega * J and -Omega * e
-  for (int k = t; k < 9 * 24 + 9; k += kInThreads) {
-    if (k < 9 * 24) {
-      const int r = k / 24, c = k % 24;
-      double s = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.Ji[q * 24 + c];
-      sh.OJ[k] = s;
+  ISTAMP_T(at0);
+  if (t < 9 * 24 + 9) {
+    if (t < 9 * 24) {
+      const int r = t / 24, c = t % 24;
+      sh.OJ[t] = dot_blocks(ji_blocks(c), sh.info + r * 9, 1, sh.Ji + c, 24);
     } else {
-      const int r = k - 9 * 24;
+      const int r = t - 9 * 24;
       double s = 0;
 #pragma unroll
       for (int q = 0; q < 9; ++q) s += sh.info[r * 9 + q] * sh.ei[q];
       sh.Oe[r] = -s;
     }
-  }
-  if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
-    for (int k = t; k < 225 + 15; k += kInThreads) {
-      const double w = sh.wp;
-      if (k < 225) {
-        const int r = k / 15, c = k % 15;
-        double s = 0;
+  } else if (t < 9 * 24 + 9 + 27) {
+    vis_sum(sh, t - (9 * 24 + 9));
+  } else if (MODE == ORBGPU_INERTIAL_LAST_FRAME && t >= 256 && t < 256 + 225 + 15) {
+    const int k = t - 256;
+    const double w = sh.wp;
+    if (k < 225) {
+      const int r = k / 15, c = k % 15;
+      double s = 0;  // sum_q (w pH_rq) Jp_qc over Jp's non-zero rows
+      if (c < 6) {
+        const int q0 = c < 3 ? 0 : 3;
 #pragma unroll
-        for (int q = 0; q < 15; ++q) s += (w * sh.pH[r * 15 + q]) * sh.Jp[q * 15 + c];
-        sh.OJp[k] = s;
+        for (int q = 0; q < 3; ++q) s += (w * sh.pH[r * 15 + q0 + q]) * sh.Jp[(q0 + q) * 15 + c];
       } else {
-        const int r = k - 225;
-        double s = 0;
-#pragma unroll
-        for (int q = 0; q < 15; ++q) s += sh.pH[r * 15 + q] * sh.epr[q];
-        sh.Oep[r] = -s * w;
+        s += (w * sh.pH[r * 15 + c]) * sh.Jp[c * 15 + c];
       }
+      sh.OJp[k] = s;
+    } else {
+      const int r = k - 225;
+      double s = 0;
+#pragma unroll
+      for (int q = 0; q < 15; ++q) s += sh.pH[r * 15 + q] * sh.epr[q];
+      sh.Oep[r] = -s * w;
     }
   }
   __syncthreads();
-  // pass 2: entry (i, j) = visual + EdgeInertial + random walks + prior
-  // the lower triangle (the LDLT reads no other entry) and b
+  ISTAMP_T(at1);
+  ISTAMP_SUB(14, at0, at1);
+  // pass 2: entry (i, j) = visual + EdgeInertial + random walks + prior,
+  // the lower triangle mirrored into the upper, and b
   constexpr int nl = n * (n + 1) / 2;
   for (int k = t; k < nl + n; k += kInThreads) {
     const bool isb = k >= nl;
@@ -353,12 +435,7 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
     if (!isb) {
       if (i < 6 && j < 6) s += sh.vis[i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i];
       const int ci = ei_col<MODE>(i), cj = ei_col<MODE>(j);
-      if (ci >= 0 && cj >= 0) {
-        double h = 0;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) h += sh.Ji[r * 24 + ci] * sh.OJ[r * 24 + cj];
-        s += h;
-      }
+      if (ci >= 0 && cj >= 0) s += dot_blocks(ji_blocks(ci), sh.Ji + ci, 24, sh.OJ + cj, 24);
       // random walks: VG (9..11) <-> VGk (24..26), VA (12..14) <-> VAk (27..29)
       const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
       const int rj = (j >= 9 && j < 15) ? j - 9 : (j >= 24 ? j - 24 : -1);
@@ -367,22 +444,14 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
         const double sg = ((i < 15) == (j < 15)) ? 1.0 : -1.0;
         s += sg * Om[(ri % 3) * 3 + rj % 3];
       }
-      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15 && j >= 15) {
-        double h = 0;
-#pragma unroll
-        for (int r = 0; r < 15; ++r) h += sh.Jp[r * 15 + i - 15] * sh.OJp[r * 15 + j - 15];
-        s += h;
-      }
+      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15 && j >= 15)
+        s += dot_prior(i - 15, sh.Jp + i - 15, 15, sh.OJp + j - 15, 15);
       sh.H[i * kLd + j] = s;
+      sh.H[j * kLd + i] = s;
     } else {
       if (i < 6) s += sh.vis[21 + i];
       const int ci = ei_col<MODE>(i);
-      if (ci >= 0) {
-        double h = 0;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) h += sh.Ji[r * 24 + ci] * sh.Oe[r];
-        s += h;
-      }
+      if (ci >= 0) s += dot_blocks(ji_blocks(ci), sh.Ji + ci, 24, sh.Oe, 1);
       const int ri = (i >= 9 && i < 15) ? i - 9 : (i >= 24 ? i - 24 : -1);
       if (ri >= 0) {  // b = -J^T Omega e with J = -I (previous) / +I (current), e = x2 - x1
         const double* Om = ri < 3 ? sh.info_g : sh.info_a;
@@ -394,12 +463,7 @@ __device__ void assemble(InShared& sh, const orbgpu_imu_preint& pi, const orbgpu
         for (int q = 0; q < 3; ++q) oe += Om[rr * 3 + q] * (x2[q] - x1[q]);
         s += i < 15 ? -oe : oe;
       }
-      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15) {
-        double h = 0;
-#pragma unroll
-        for (int r = 0; r < 15; ++r) h += sh.Jp[r * 15 + i - 15] * sh.Oep[r];
-        s += h;
-      }
+      if (MODE == ORBGPU_INERTIAL_LAST_FRAME && i >= 15) s += dot_prior(i - 15, sh.Jp + i - 15, 15, sh.Oep, 1);
       sh.b[i] = s;
     }
   }
@@ -489,13 +553,12 @@ __device__ bool ldlt_wave(InShared& sh, int lane) {
 // keeps Eigen's semantics for it.
 template <int n>
 __device__ bool gj_wave(InShared& sh, int lane) {
+  ISTAMP_T(gt0);
   const double dl = lane < n ? fabs(sh.H[lane * kLd + lane]) : -1.0;
-  if (lane < n) sh.temp[lane] = dl;
-  wave_sync();
-  int rank = 0;
+  int rank = 0;  // the diagonal broadcast from registers (v_readlane), no LDS round trips
 #pragma unroll
   for (int j = 0; j < n; ++j) {
-    const double dj = sh.temp[j];
+    const double dj = bcast(dl, j);
     rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
   }
   if (lane < n) sh.perm[rank] = lane;
@@ -503,17 +566,25 @@ __device__ bool gj_wave(InShared& sh, int lane) {
   const int pl = lane < n ? sh.perm[lane] : 0;
   const int li = lane & 15, ia = li, ib = li + 16;
   const int pa = ia < n ? sh.perm[ia] : 0, pb = ib < n ? sh.perm[ib] : 0;
+  // rows of the full symmetric system (assemble mirrors it); rows past n read
+  // the zero row 30, the columns are wave-uniform offsets
+  const double* hA = sh.H + (ia < n ? pa : 30) * kLd;
+  const double* hB = sh.H + (ib < n ? pb : 30) * kLd;
   double rA[n + 1], rB[n + 1];
 #pragma unroll
   for (int j = 0; j < n; ++j) {
     const int pj = __builtin_amdgcn_readlane(pl, j);
-    rA[j] = ia < n ? sh.H[max(pa, pj) * kLd + min(pa, pj)] : 0.0;
-    rB[j] = ib < n ? sh.H[max(pb, pj) * kLd + min(pb, pj)] : 0.0;
+    rA[j] = hA[pj];
+    rB[j] = hB[pj];
   }
   rA[n] = ia < n ? sh.b[pa] : 0.0;
   rB[n] = ib < n ? sh.b[pb] : 0.0;
   double dA = 1.0, dB = 1.0;
+  ISTAMP_T(gt1);
   const int f = gj_pivots<n>(rA, rB, li, dA, dB);
+  ISTAMP_T(gt2);
+  ISTAMP_SUB(12, gt0, gt1);
+  ISTAMP_SUB(13, gt1, gt2);
   if (f & 1) return false;
   if (f & 2) return ldlt_wave<n>(sh, lane);
   constexpr double kTiny = 1.0 / 1.79769313486231570815e+308;
@@ -545,19 +616,22 @@ __device__ __forceinline__ void load_state(StateD& s, const orbgpu_imu_state& g)
 template <typename W0, typename W1>
 __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, const VisObs* gobs,
                           const uint8_t* glv, int cap, int n, bool robust, int kind, int t,
-                          W0&& w0, W1&& w1) {
-  double acc[27];
-#pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0;
+                          bool sum_here, W0&& w0, W1&& w1) {
   const int wave = t >> 6, lane = t & 63;
 #ifdef ORB_STAMPS
   const unsigned long long vt0 = __builtin_amdgcn_s_memtime();
+  unsigned long long vt1 = vt0;
 #endif
   if (wave == 0) {
     w0();
   } else if (wave == 1) {
     w1();
   } else {
+    // the accumulators live in this branch only, so they add nothing to the
+    // register pressure of the IMU-edge waves' code
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] = 0;
     const int tv = t - 64 * kVisWave0;
     for (int i = tv; i < n; i += kVisThreads) {
       const bool in_lds = i < cap;
@@ -566,11 +640,10 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
       const VisObs o = in_lds ? ob[i] : gobs[i];
       vis_accumulate(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, kind == 0 && robust, 1.0, acc);
     }
-  }
 #ifdef ORB_STAMPS
-  const unsigned long long vt1 = __builtin_amdgcn_s_memtime();
+    vt1 = __builtin_amdgcn_s_memtime();
 #endif
-  if (wave >= kVisWave0) {  // DPP row sums; lane 15 of each row writes its partial
+    // DPP row sums; lane 15 of each row writes its partial
 #pragma unroll
     for (int k = 0; k < 27; ++k) {
       double x = acc[k];
@@ -592,12 +665,7 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
   }
 #endif
   __syncthreads();
-  if (t < 27) {
-    double s = 0;
-#pragma unroll
-    for (int r = kVisWave0 * 4; r < kInWaves * 4; ++r) s += sh.red[r * 27 + t];
-    sh.vis[t] = s;
-  }
+  if (sum_here && t < 27) vis_sum(sh, t);
 }
 
 template <int MODE>
@@ -609,7 +677,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
   constexpr int n = MODE == ORBGPU_INERTIAL_LAST_FRAME ? 30 : 15;
   __shared__ InShared sh;
   extern __shared__ __attribute__((aligned(16))) uint8_t in_lds[];
-  const int p = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int p = blockIdx.x;
+  int t = threadIdx.x, lane = t & 63, wave = t >> 6;  // laundered per iteration (below)
   const int nobs = max(0, min(g_nobs[p], obs_stride));
   const VisObs* gobs = g_obs + (size_t)p * obs_stride;
   uint8_t* glv = g_out + (size_t)p * obs_stride;
@@ -630,6 +699,10 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     load_state(sh.prev, g_prev[p]);
   }
   if (t < 30) sh.x[t] = 0;
+  if (t < kLd) sh.H[30 * kLd + t] = 0;  // gj_wave's zero row
+  if (t < 68) reinterpret_cast<float*>(&sh.pre)[t] = reinterpret_cast<const float*>(&pi)[t];
+  if (MODE == ORBGPU_INERTIAL_LAST_FRAME && t >= 128 && t < 128 + 21)
+    reinterpret_cast<double*>(&sh.prs)[t - 128] = reinterpret_cast<const double*>(pr)[t - 128];
   for (int k = t; k < 81 + 18 + 225; k += kInThreads) {
     if (k < 81)
       sh.info[k] = pi.info[k];
@@ -651,19 +724,27 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
   const int n_edges = nobs + (MODE == ORBGPU_INERTIAL_LAST_FRAME ? 4 : 3);
   bool robust = true;
   int nBad = 0, nInl = 0;
+  // (not unrolled: four copies of the round only multiplied the live uniform
+  // values, spilled to VGPR lanes)
+#pragma unroll 1
   for (int it = 0; it < 4; ++it) {
+#pragma unroll 1
     for (int iter = 0; iter < 10; ++iter) {
+      // the thread index is opaque to the optimiser from here: otherwise every
+      // thread-predicate compare of the loop body is hoisted out of it and its
+      // lane mask lives in (spilled) SGPRs for the whole loop
+      asm volatile("" : "+v"(t), "+v"(lane), "+v"(wave));
       // computeActiveErrors + buildSystem
+      // (the visual block's final sums happen in assemble's first pass)
       vis_sweep(
-          sh, ob, lv, gobs, glv, cap, nobs, robust, 0, t,
+          sh, ob, lv, gobs, glv, cap, nobs, robust, 0, t, false,
           [&] {
-            inertial_edge(sh, pi, dt, lane);
+            inertial_edge(sh, sh.pre, dt, lane);
             ISTAMP(6);
           },
           [&] {
-            if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, pr, true, lane);
+            if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, &sh.prs, true, lane);
           });
-      __syncthreads();
       ISTAMP(0);
       assemble<MODE>(sh, pi, pr, t);
       __syncthreads();
@@ -778,9 +859,9 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
   // ---- the Hessian for the new ConstraintPoseImu ------------------------------
   // visual inliers' J^T Omega J (waves 2..) while waves 0, 1 linearise the IMU edges
   vis_sweep(
-      sh, ob, lv, gobs, glv, cap, nobs, false, 1, t, [&] { inertial_edge(sh, pi, dt, lane); },
+      sh, ob, lv, gobs, glv, cap, nobs, false, 1, t, true, [&] { inertial_edge(sh, sh.pre, dt, lane); },
       [&] {
-        if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, pr, false, lane);
+        if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, &sh.prs, false, lane);
       });
   __syncthreads();
   orbgpu_inertial_result* res = g_res + p;

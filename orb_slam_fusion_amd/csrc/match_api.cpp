@@ -162,7 +162,7 @@ size_t in_bytes(int n, int n_pts, size_t pt_size) {
 }
 
 size_t out_bytes(int n, int n_pts) {
-  return align_up(4 * (size_t)n) + align_up(sizeof(int)) +
+  return align_up(sizeof(int)) + align_up(4 * (size_t)n) + align_up(sizeof(int)) +
          align_up(sizeof(orbgpu_track_view) * n_pts) + align_up(4 * (size_t)n_pts) + 4 * 256;
 }
 
@@ -174,6 +174,7 @@ struct HostCall {
   int* h_counts = nullptr;  // n, npts (staged)
   int32_t* d_match = nullptr;
   int* d_nm = nullptr;
+  int* d_call_err = nullptr;  // this call's error word: offset 0 of `out`, read back with the outputs
   orbgpu_track_view* d_views_out = nullptr;
   explicit HostCall(orbgpu_matcher* m_) : m(m_), bi{m_->in}, bo{m_->out} {}
 };
@@ -204,7 +205,8 @@ orbgpu_status stage_frame(HostCall& c, const orbgpu_keypoint* kps, const uint8_t
   c.L.pt_stride = n_pts > 0 ? n_pts : 1;
   c.L.max_pts = n_pts;
   c.L.n_frames = 1;
-  c.L.err = m->d_err;
+  c.d_call_err = c.bo.take<int>(1);
+  c.L.err = c.d_call_err;
   if (ensure_scratch(m, 1, c.L.kp_stride, c.L.pt_stride) != ORBGPU_OK) return ORBGPU_ERR_NOMEM;
   c.L.cell_start = m->d_cell_start;
   c.L.cell_idx = m->d_cell_idx;
@@ -221,19 +223,19 @@ orbgpu_status run_host(HostCall& c, int n, int32_t* match, int* nmatches,
                        orbgpu_track_view* views_out, int n_pts) {
   orbgpu_matcher* m = c.m;
   hipStream_t s = m->stream;
-  if (hipMemsetAsync(m->d_err, 0, sizeof(int), s) ||
+  if (hipMemsetAsync(c.d_call_err, 0, sizeof(int), s) ||
       hipMemcpyAsync(m->in.d, m->in.h, c.bi.off, hipMemcpyHostToDevice, s) ||
       orbgpu::launch_match(c.L, s) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
-  // outputs: match, nmatches (+ views) are contiguous at the front of `out`
+  // outputs: the error word, match, nmatches (+ views) are contiguous at the
+  // front of `out`: one copy back
   const size_t dl = views_out ? (size_t)((uint8_t*)c.d_views_out - m->out.d) +
                                     sizeof(orbgpu_track_view) * n_pts
                               : (size_t)((uint8_t*)c.d_nm - m->out.d) + sizeof(int);
-  int err = 0;
-  if (hipMemcpyAsync(m->out.h, m->out.d, dl, hipMemcpyDeviceToHost, s) ||
-      hipMemcpyAsync(&err, m->d_err, sizeof(int), hipMemcpyDeviceToHost, s) ||
-      hipStreamSynchronize(s))
+  if (hipMemcpyAsync(m->out.h, m->out.d, dl, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
     return ORBGPU_ERR_DEVICE;
+  int err = 0;
+  std::memcpy(&err, m->out.h + ((uint8_t*)c.d_call_err - m->out.d), sizeof(int));
   if (err) return ORBGPU_ERR_CAPACITY;
   if (n > 0) std::memcpy(match, m->out.h + ((uint8_t*)c.d_match - m->out.d), 4 * (size_t)n);
   std::memcpy(nmatches, m->out.h + ((uint8_t*)c.d_nm - m->out.d), sizeof(int));

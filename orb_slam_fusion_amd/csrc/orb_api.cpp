@@ -93,7 +93,10 @@ struct orbgpu_extractor {
   // host path's device outputs
   uint16_t* d_st_lists = nullptr;
   int *d_st_rowend = nullptr, *d_st_sad = nullptr;
+  // host path block [error word, pad x3 | uright x kcap | depth x kcap] on the
+  // device and its pinned mirror: one copy back per call
   float* d_st_out = nullptr;
+  float* h_st_out = nullptr;
   size_t st_lists = 0, st_rowend = 0, st_sad = 0, st_out = 0;
 
   // optional per-stage event profiling of batch calls (a ring of event sets)
@@ -433,6 +436,7 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_st_rowend);
   dfree(h->d_st_sad);
   dfree(h->d_st_out);
+  if (h->h_st_out) (void)hipHostFree(h->h_st_out);
   for (hipEvent_t e : h->prof_events) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -697,13 +701,21 @@ orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* righ
   const int kcap = P.kp_slots;
   orbgpu_status st = ensure_stereo(left, 1, kcap);
   if (st != ORBGPU_OK) return st;
-  if ((size_t)2 * kcap > left->st_out) {
+  const size_t need = 4 + (size_t)2 * kcap;
+  if (need > left->st_out) {
     dfree(left->d_st_out);
-    if (dalloc(&left->d_st_out, (size_t)2 * kcap)) return ORBGPU_ERR_NOMEM;
-    left->st_out = (size_t)2 * kcap;
+    if (left->h_st_out) (void)hipHostFree(left->h_st_out);
+    left->h_st_out = nullptr;
+    left->st_out = 0;
+    if (dalloc(&left->d_st_out, need) ||
+        hipHostMalloc(&left->h_st_out, need * sizeof(float)) != hipSuccess)
+      return ORBGPU_ERR_NOMEM;
+    left->st_out = need;
   }
-  StereoLaunch a = make_stereo(left, 1, kcap, bf, mb, left->d_st_out, left->d_st_out + kcap,
-                               (size_t)kcap);
+  float* dur = left->d_st_out + 4;
+  StereoLaunch a = make_stereo(left, 1, kcap, bf, mb, dur, dur + kcap, (size_t)kcap);
+  int* d_call_err = reinterpret_cast<int*>(left->d_st_out);  // this call's error word
+  a.err = d_call_err;
   for (int side = 0; side < 2; ++side) {
     orbgpu_extractor* h = side ? right : left;
     StereoSide& s = side ? a.R : a.L;
@@ -714,22 +726,23 @@ orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* righ
     s.desc = h->d_descs;
     s.n = h->d_nm;
   }
-  int n = 0, err = 0;
-  if (launch_stereo(a, left->stream) != hipSuccess ||
-      hipMemcpyAsync(&n, left->d_nm, sizeof(int), hipMemcpyDeviceToHost, left->stream) ||
-      hipMemcpyAsync(&err, left->d_err, sizeof(int), hipMemcpyDeviceToHost, left->stream) ||
+  // the left call's keypoint count (its pinned output block, already synchronised)
+  const int n = std::min(left->h_small[0], kcap);
+  if (n > cap) return ORBGPU_ERR_CAPACITY;
+  // error word, uright[0, kcap), depth[0, n): one copy back
+  const size_t bytes = (4 + (size_t)kcap + (size_t)n) * sizeof(float);
+  if (hipMemsetAsync(d_call_err, 0, sizeof(int), left->stream) ||
+      launch_stereo(a, left->stream) != hipSuccess ||
+      hipMemcpyAsync(left->h_st_out, left->d_st_out, bytes, hipMemcpyDeviceToHost, left->stream) ||
       hipStreamSynchronize(left->stream))
     return ORBGPU_ERR_DEVICE;
-  if (err) {
-    (void)hipMemset(left->d_err, 0, sizeof(int));
-    return ORBGPU_ERR_CAPACITY;
+  int err = 0;
+  std::memcpy(&err, left->h_st_out, sizeof(int));
+  if (err) return ORBGPU_ERR_CAPACITY;
+  if (n > 0) {
+    std::memcpy(uright, left->h_st_out + 4, (size_t)n * sizeof(float));
+    std::memcpy(depth, left->h_st_out + 4 + kcap, (size_t)n * sizeof(float));
   }
-  n = std::min(n, kcap);
-  if (n > cap) return ORBGPU_ERR_CAPACITY;
-  if (n > 0 && (hipMemcpy(uright, left->d_st_out, (size_t)n * sizeof(float), hipMemcpyDeviceToHost) ||
-                hipMemcpy(depth, left->d_st_out + kcap, (size_t)n * sizeof(float),
-                          hipMemcpyDeviceToHost)))
-    return ORBGPU_ERR_DEVICE;
   return ORBGPU_OK;
 }
 

@@ -35,9 +35,13 @@ def main(mode: int):
     runs = P * (calls + 3)
     names = {6: "imu_edges (wave 0)", 0: "visual sweep wait + reduce", 1: "assemble",
              2: "ldlt", 3: "update", 4: "classify", 5: "final hessian + marginalise"}
+    sub = {10: "visual loop (wave 2)", 11: "visual DPP reduce + store (wave 2)",
+           12: "solve: order + loads", 13: "solve: pivots", 14: "assemble pass 1 (+barrier)",
+           7: "imu: preintegration deltas", 9: "imu: error (LogSO3)", 15: "imu: linear blocks"}
     tot = sum(v[i] for i in names)
     print(json.dumps({"ticks_per_problem": tot / runs, "iterations_per_problem": v[8] / runs,
-                      "ticks_per_phase_per_problem": {names[i]: round(v[i] / runs) for i in names}}))
+                      "ticks_per_phase_per_problem": {names[i]: round(v[i] / runs) for i in names},
+                      "sub_phases_per_problem": {sub[i]: round(v[i] / runs) for i in sub}}))
 
 
 if __name__ == "__main__":
