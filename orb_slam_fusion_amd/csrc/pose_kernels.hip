@@ -299,9 +299,11 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     int lds_obs) {
   constexpr int NT = kPoseThreads * G, NW = NT / 64;
   __shared__ PoseShared<G> sh;
-  const int p = blockIdx.x, t = threadIdx.x;
-  const int grp = __builtin_amdgcn_readfirstlane(t >> 8), tg = t & (kPoseThreads - 1);
-  const int lane = t & 63, gw = (t >> 6) & (kPoseWaves - 1);
+  const int p = blockIdx.x;
+  int t = threadIdx.x;  // t, tg, lane, gw: laundered per LM trial round (below)
+  const int grp = __builtin_amdgcn_readfirstlane(t >> 8);
+  int tg = t & (kPoseThreads - 1);
+  int lane = t & 63, gw = (t >> 6) & (kPoseWaves - 1);
   const int n = nobs[p];
   const PoseObsDev* obs = obs_all + (size_t)p * obs_stride;
   uint8_t* level = outlier_all + (size_t)p * obs_stride;
@@ -452,6 +454,10 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
       int q = 0;
       bool accepted = false, done = false;
       do {
+        // the thread indices are opaque to the optimiser here, so the loop
+        // body's thread-predicate compares are not hoisted into long-lived
+        // SGPR lane masks
+        asm volatile("" : "+v"(t), "+v"(tg), "+v"(lane), "+v"(gw));
         // this group's trial (q + grp): the lambda the sequential loop would
         // reach after grp more rejections
         double lg = lambda, ng = ni;
