@@ -546,12 +546,6 @@ __device__ __forceinline__ ushort2_t compass2(ushort2_t v, ushort2_t u, ushort2_
   const ushort2_t hi = min2(max2(u, d), max2(l, r));
   return max2(sub_sat2(v, lo), sub_sat2(hi, v));
 }
-__device__ __forceinline__ ushort2_t even_bytes(uint32_t w) {  // (b0, b2)
-  return as_us2(__builtin_amdgcn_perm(0u, w, 0x0c020c00u));
-}
-__device__ __forceinline__ ushort2_t odd_bytes(uint32_t w) {  // (b1, b3)
-  return as_us2(__builtin_amdgcn_perm(0u, w, 0x0c030c01u));
-}
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
 }
@@ -595,7 +589,31 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   {
     const uint8_t* Sa = S - lead;  // rows stay dword-aligned iff sp is; else unaligned loads
     const int ndw = (lead + c.cols + 3) >> 2;
-    if (ndw <= 16) {
+    if (ndw <= 16 && (sp & 3) == 0) {
+      // dword-aligned rows: raw buffer loads, the row step in the scalar
+      // offset (no per-load address arithmetic), rows past the ROI read 0
+      // (buffer bound) and only the last step's stores are predicated.
+      // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
+      // rows r0, r0 + 4, ...; lanes past the ROI width copy its last dword.
+      const uint32_t q4 = 4u * (uint32_t)min(lane & 15, ndw - 1), r0 = (uint32_t)lane >> 4;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint8_t*>(Sa), (short)0, (int)((uint32_t)c.rows * (uint32_t)sp), kBufRsrcWord3);
+      const int nst = (c.rows + 3) >> 2;                    // row steps
+      const bool last_ok = (int)r0 + 4 * (nst - 1) < c.rows;  // this lane's row of the last step
+      const uint32_t vo = __umul24(r0, (uint32_t)sp) + q4;
+      uint8_t* ld = roi + __umul24(r0, (uint32_t)ls) + q4;
+      for (int k0 = 0; k0 < nst; k0 += kFastPf) {
+        uint32_t v[kFastPf];
+#pragma unroll
+        for (int u = 0; u < kFastPf; ++u)
+          if (k0 + u < nst)
+            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vo, 4 * (k0 + u) * sp, 0);
+#pragma unroll
+        for (int u = 0; u < kFastPf; ++u)
+          if (k0 + u < nst && (k0 + u < nst - 1 || last_ok))
+            *reinterpret_cast<uint32_t*>(ld + 4 * (k0 + u) * ls) = v[u];
+      }
+    } else if (ndw <= 16) {
       // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
       // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight.
       // Lanes past the ROI width or height are clamped onto its last dword /
@@ -637,35 +655,49 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
 
   // One threshold pass; returns the number of keypoints, leaves the survivor
   // list (raster order, kp flag in bit 15) in sv[0..*n_sv).
+  // v_perm selectors of the compass windows (row bytes lead + 3: centre, up,
+  // down; lead: left; lead + 6: right): pair (2j, 2j + 1) of a window at byte
+  // offset s within its first dword is bytes s + 2j, s + 2j + 1 zero-extended
+  auto psel = [](int b) {
+    return (uint32_t)b | 0x0c00u | ((uint32_t)(b + 1) << 16) | 0x0c000000u;
+  };
+  const int s_v = (lead + 3) & 3, s_l = lead & 3, s_r = (lead + 6) & 3;
+  const uint2 sel_v = make_uint2(psel(s_v), psel(s_v + 2));
+  const uint2 sel_l = make_uint2(psel(s_l), psel(s_l + 2));
+  const uint2 sel_r = make_uint2(psel(s_r), psel(s_r + 2));
+
   auto pass = [&](int th, int* n_sv) -> int {
     // compass pre-test on 8 pixels per lane in packed u16 pairs; the window
     // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
-    const ushort2_t th2 = as_us2((uint32_t)th * 0x10001u);
     int ns = 0;
     auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
     for (int r = g_r0, g = g_q0;;) {
       const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
       if (mrv == 0) break;
       const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 8 * g;
-      // 8 window bytes at row byte o: (lo, hi) dwords
-      auto win = [&](const uint8_t* row, int o, uint32_t& lo, uint32_t& hi) {
+      // window of 8 centre-relative pixels at row byte o as four u16 pairs
+      // (pixels 2j, 2j + 1): one two-source v_perm each straight from the
+      // three dwords covering the window (wave-uniform selectors, no align)
+      auto win = [&](const uint8_t* row, int o, uint32_t sa, uint32_t sb, uint32_t (&q)[4]) {
         const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (o & ~3));
-        lo = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3);
-        hi = __builtin_amdgcn_alignbyte(w[2], w[1], o & 3);
+        const uint32_t a = w[0], b = w[1], c = w[2];
+        q[0] = __builtin_amdgcn_perm(b, a, sa);
+        q[1] = __builtin_amdgcn_perm(b, a, sb);
+        q[2] = __builtin_amdgcn_perm(c, b, sa);
+        q[3] = __builtin_amdgcn_perm(c, b, sb);
       };
-      uint32_t v0, v1, l0, l1, r0, r1, u0, u1, d0, d1;
-      win(C, lead + 3, v0, v1);
-      win(C, lead, l0, l1);
-      win(C, lead + 6, r0, r1);
-      win(C - 3 * ls, lead + 3, u0, u1);
-      win(C + 3 * ls, lead + 3, d0, d1);
-      auto test = [&](ushort2_t (*pick)(uint32_t), uint32_t v, uint32_t u, uint32_t d, uint32_t l, uint32_t rr) {
-        return __builtin_bit_cast(uint32_t, sub_sat2(compass2(pick(v), pick(u), pick(d), pick(l), pick(rr)), th2));
-      };
-      const uint32_t te0 = test(even_bytes, v0, u0, d0, l0, r0);  // pixels 0, 2
-      const uint32_t to0 = test(odd_bytes, v0, u0, d0, l0, r0);   // pixels 1, 3
-      const uint32_t te1 = test(even_bytes, v1, u1, d1, l1, r1);  // pixels 4, 6
-      const uint32_t to1 = test(odd_bytes, v1, u1, d1, l1, r1);   // pixels 5, 7
+      uint32_t qv[4], ql[4], qr[4], qu[4], qd[4];
+      win(C, lead + 3, sel_v.x, sel_v.y, qv);
+      win(C, lead, sel_l.x, sel_l.y, ql);
+      win(C, lead + 6, sel_r.x, sel_r.y, qr);
+      win(C - 3 * ls, lead + 3, sel_v.x, sel_v.y, qu);
+      win(C + 3 * ls, lead + 3, sel_v.x, sel_v.y, qd);
+      // compass value per pixel pair; corner at th => value > th
+      uint32_t tv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        tv[j] = __builtin_bit_cast(uint32_t, compass2(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]),
+                                                      as_us2(ql[j]), as_us2(qr[j])));
       // pixel k of the group is valid iff its row is (rv) and, for the row's
       // tail group (tl), k < tail; g < gpr - 1 groups are whole.  Both masks
       // come from one compare each, the per-pixel masks from scalar ANDs
@@ -674,17 +706,19 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint64_t mwhole = mrv & ~bal(tl);
       auto ok = [&](int k) { return rv && (k < tail || !tl); };
       auto okm = [&](int k) { return k < tail ? mrv : mwhole; };
-      const bool f0 = ok(0) && (te0 & 0xffffu), f1 = ok(1) && (to0 & 0xffffu);
-      const bool f2 = ok(2) && (te0 >> 16), f3 = ok(3) && (to0 >> 16);
-      const bool f4 = ok(4) && (te1 & 0xffffu), f5 = ok(5) && (to1 & 0xffffu);
-      const bool f6 = ok(6) && (te1 >> 16), f7 = ok(7) && (to1 >> 16);
+      auto pass_lo = [&](uint32_t x) { return (x & 0xffffu) > (uint32_t)th; };
+      auto pass_hi = [&](uint32_t x) { return (x >> 16) > (uint32_t)th; };
+      const bool f0 = ok(0) && pass_lo(tv[0]), f1 = ok(1) && pass_hi(tv[0]);
+      const bool f2 = ok(2) && pass_lo(tv[1]), f3 = ok(3) && pass_hi(tv[1]);
+      const bool f4 = ok(4) && pass_lo(tv[2]), f5 = ok(5) && pass_hi(tv[2]);
+      const bool f6 = ok(6) && pass_lo(tv[3]), f7 = ok(7) && pass_hi(tv[3]);
       // the masks as ANDs of single-compare ballots (scalar ANDs of the
       // compares' lane masks): a ballot of an && rematerialises the bool with
       // a v_cndmask + v_cmp pair per pixel
-      const uint64_t m0 = okm(0) & bal(te0 & 0xffffu), m1 = okm(1) & bal(to0 & 0xffffu);
-      const uint64_t m2 = okm(2) & bal(te0 >> 16), m3 = okm(3) & bal(to0 >> 16);
-      const uint64_t m4 = okm(4) & bal(te1 & 0xffffu), m5 = okm(5) & bal(to1 & 0xffffu);
-      const uint64_t m6 = okm(6) & bal(te1 >> 16), m7 = okm(7) & bal(to1 >> 16);
+      const uint64_t m0 = okm(0) & bal(pass_lo(tv[0])), m1 = okm(1) & bal(pass_hi(tv[0]));
+      const uint64_t m2 = okm(2) & bal(pass_lo(tv[1])), m3 = okm(3) & bal(pass_hi(tv[1]));
+      const uint64_t m4 = okm(4) & bal(pass_lo(tv[2])), m5 = okm(5) & bal(pass_hi(tv[2]));
+      const uint64_t m6 = okm(6) & bal(pass_lo(tv[3])), m7 = okm(7) & bal(pass_hi(tv[3]));
       int pos = ns + (int)mbcnt64(m7, mbcnt64(m6, mbcnt64(m5, mbcnt64(m4, mbcnt64(m3, mbcnt64(m2,
                          mbcnt64(m1, mbcnt64(m0, 0u))))))));
       const int i0 = (r << 7) | (8 * g);
