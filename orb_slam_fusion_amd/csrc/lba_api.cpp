@@ -255,7 +255,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_work = take(solve_lds ? 2 : (size_t)npad * (npad + 1) + (size_t)(npad / 16) * 272),  // S + the L_KK^-1 tiles (16 x 17)
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
-               c_itot = take(2);
+               c_itot = take(2 + ORBGPU_LIA_MAX_IMU_LINKS);  // [0] total, [2 + l] per link
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory

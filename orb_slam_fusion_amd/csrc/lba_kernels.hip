@@ -1498,17 +1498,17 @@ __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* _
 }
 
 // ---- LocalInertialBA's IMU links ------------------------------------------
-// One workgroup, a wave per link (links strided over the waves): the
+// One 64-thread workgroup (one wave) per link, all links in parallel: the
 // EdgeInertial error (and, building, its Jacobian) at the current or trial
 // state, every lane computing the same values (inertial_edge_core); the
 // link's robust chi2 (Huber sqrt(16.92) on flagged links, the information
 // x1e-2 on the window's last link) plus EdgeGyroRW / EdgeAccRW.  Building, it
 // writes the link's quadratic form over the 30 dims (kf1 VP VV VG VA | kf2 VP
 // VV VG VA; EdgeInertial's 24 columns are the first 24) and the gradient
-// -J^T W e.  Thread 0 sums the links' chi2 in link order into imu_tot.
-constexpr int kImuThreads = 256;
-constexpr int kImuWaves = kImuThreads / 64;
-
+// -J^T W e.  Evaluating, each link's chi2 goes to imu_tot[2 + l] and the last
+// workgroup sums them in link order into imu_tot[0].  (Round 2 ran the links
+// on the four waves of one workgroup, three in a row: 36 µs per build.)
+constexpr int kImuThreads = 64;
 
 __device__ __forceinline__ void load_state(StateD& s, const double* p) {
 #pragma unroll
@@ -1530,18 +1530,22 @@ template <bool kBuild>
 __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done || (kBuild && !c.need_build)) return;
-  __shared__ double sJ[kImuWaves][9 * 24];
-  __shared__ double sOJ[kImuWaves][9 * 24];
-  __shared__ double sE[kImuWaves][9];  // the link's error (inertial_edge_core, lane 0)
-  __shared__ double chis[kMaxImuLinks];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ double sJ[9 * 24];
+  __shared__ double sOJ[9 * 24];
+  __shared__ double sE[9];       // the link's error (inertial_edge_core, lane 0)
+  __shared__ double sInfo[81];   // the link's information (x1e-2 when downweighted)
+  const int lane = threadIdx.x;
+  const int l = blockIdx.x;      // (grid max(n_imu, 1): block 0 alone when there is no link)
   const double* st = a.poses[trial ? c.state ^ 1 : c.state];
-  for (int l = wave; l < a.n_imu; l += kImuWaves) {
+  double chi_link = 0;
+  if (l < a.n_imu) {
     const LiaImuDev& E = a.imu[l];
+    const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
+    for (int k = lane; k < 81; k += 64) sInfo[k] = E.pi.info[k] * isc;
     StateD s1, s2;
     load_state(s1, st + kImuStateStride * E.kf1);
     load_state(s2, st + kImuStateStride * E.kf2);
-    double* J = sJ[wave];
+    double* J = sJ;
     if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
       for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
       wave_lds_sync();
@@ -1554,18 +1558,17 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
         J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
       }
     }
-    inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sE[wave]);
+    inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sE);
     wave_lds_sync();
     double e[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) e[k] = sE[wave][k];
-    const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
+    for (int k = 0; k < 9; ++k) e[k] = sE[k];
     // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
     double part = 0;
     if (lane < 9) {
       double t = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) t += (E.pi.info[lane * 9 + q] * isc) * e[q];
+      for (int q = 0; q < 9; ++q) t += sInfo[lane * 9 + q] * e[q];
       double el = 0;
 #pragma unroll
       for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
@@ -1590,68 +1593,69 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
       cg += eg[i] * Og[i];
       ca += ea[i] * Oa[i];
     }
-    if (lane == 0) chis[l] = (rho0 + cg) + ca;
-    if (!kBuild) continue;
-    // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
-    for (int k = lane; k < 9 * 24; k += 64) {
-      const int r = k / 24, col = k - 24 * r;
-      double v = 0;
+    chi_link = (rho0 + cg) + ca;
+    if (kBuild) {
+      // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
+      for (int k = lane; k < 9 * 24; k += 64) {
+        const int r = k / 24, col = k - 24 * r;
+        double v = 0;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) v += (w * (E.pi.info[r * 9 + q] * isc)) * J[q * 24 + col];
-      sOJ[wave][k] = v;
-    }
-    double We[9];
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      double v = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) v += (w * (E.pi.info[r * 9 + q] * isc)) * e[q];
-      We[r] = v;
-    }
-    wave_lds_sync();
-    double* Q = a.imu_q + (size_t)kImuPairQ * l;
-    for (int k = lane; k < 900; k += 64) {
-      const int p = k / 30, q = k - 30 * p;
-      double v = 0;
-      if (p < 24 && q < 24) {
-#pragma unroll
-        for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sOJ[wave][r * 24 + q];
+        for (int q = 0; q < 9; ++q) v += (w * sInfo[r * 9 + q]) * J[q * 24 + col];
+        sOJ[k] = v;
       }
-      // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
-      const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
-      if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
-        if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
-      const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
-      if ((p >= 12 && p < 15) || (p >= 27))
-        if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
-      Q[k] = v;
-    }
-    if (lane < 30) {
-      const int p = lane;
-      double g = 0;
-      if (p < 24) {
+      double We[9];
 #pragma unroll
-        for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
-      }
-      double og = 0, oa = 0;
+      for (int r = 0; r < 9; ++r) {
+        double v = 0;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        og = p - 9 == i || p - 24 == i ? Og[i] : og;
-        oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
+        for (int q = 0; q < 9; ++q) v += (w * sInfo[r * 9 + q]) * e[q];
+        We[r] = v;
       }
-      if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
-      if (p >= 24 && p < 27) g -= og;
-      if (p >= 12 && p < 15) g += oa;
-      if (p >= 27) g -= oa;
-      Q[900 + p] = g;
+      wave_lds_sync();
+      double* Q = a.imu_q + (size_t)kImuPairQ * l;
+      for (int k = lane; k < 900; k += 64) {
+        const int p = k / 30, q = k - 30 * p;
+        double v = 0;
+        if (p < 24 && q < 24) {
+#pragma unroll
+          for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sOJ[r * 24 + q];
+        }
+        // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
+        const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
+        if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
+          if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
+        const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
+        if ((p >= 12 && p < 15) || (p >= 27))
+          if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
+        Q[k] = v;
+      }
+      if (lane < 30) {
+        const int p = lane;
+        double g = 0;
+        if (p < 24) {
+#pragma unroll
+          for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
+        }
+        double og = 0, oa = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          og = p - 9 == i || p - 24 == i ? Og[i] : og;
+          oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
+        }
+        if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
+        if (p >= 24 && p < 27) g -= og;
+        if (p >= 12 && p < 15) g += oa;
+        if (p >= 27) g -= oa;
+        Q[900 + p] = g;
+      }
     }
-    wave_lds_sync();  // J / sOJ are rewritten by this wave's next link
   }
   if (kBuild) return;
-  __syncthreads();
+  if (lane == 0) a.imu_tot[2 + l] = chi_link;
+  if (!last_block(a.counter + 3)) return;
   if (threadIdx.x == 0) {
     double tot = 0;
-    for (int l = 0; l < a.n_imu; ++l) tot += chis[l];
+    for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
     a.imu_tot[0] = tot;
   }
 }
@@ -1743,7 +1747,7 @@ size_t lba_solve_lds_bytes(int n_pad) {
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
-    hipLaunchKernelGGL(k_lia_imu<false>, dim3(1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
     hipLaunchKernelGGL(k_lba_begin<kModelImu>, g, dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_lba_begin<kModelSe3>, g, dim3(kThreads), 0, st, a);
@@ -1760,7 +1764,7 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
   }
   if (imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
-    hipLaunchKernelGGL(k_lia_imu<true>, dim3(1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
     hipLaunchKernelGGL(k_lia_assemble, dim3(blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads)),
                        dim3(kThreads), 0, st, a);
   }
@@ -1791,7 +1795,7 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
     hipLaunchKernelGGL(k_lia_trial_states, dim3(a.n_kf), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_lia_imu<false>, dim3(1), dim3(kImuThreads), 0, st, a, 1);
+    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 1);
     hipLaunchKernelGGL(k_lba_trial<kModelImu>, g, dim3(kThreads), 0, st, a);
   } else {
     if (a.n_kf > kMaxKfLds)
