@@ -589,31 +589,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   {
     const uint8_t* Sa = S - lead;  // rows stay dword-aligned iff sp is; else unaligned loads
     const int ndw = (lead + c.cols + 3) >> 2;
-    if (ndw <= 16 && (sp & 3) == 0) {
-      // dword-aligned rows: raw buffer loads, the row step in the scalar
-      // offset (no per-load address arithmetic), rows past the ROI read 0
-      // (buffer bound) and only the last step's stores are predicated.
-      // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
-      // rows r0, r0 + 4, ...; lanes past the ROI width copy its last dword.
-      const uint32_t q4 = 4u * (uint32_t)min(lane & 15, ndw - 1), r0 = (uint32_t)lane >> 4;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint8_t*>(Sa), (short)0, (int)((uint32_t)c.rows * (uint32_t)sp), kBufRsrcWord3);
-      const int nst = (c.rows + 3) >> 2;                    // row steps
-      const bool last_ok = (int)r0 + 4 * (nst - 1) < c.rows;  // this lane's row of the last step
-      const uint32_t vo = __umul24(r0, (uint32_t)sp) + q4;
-      uint8_t* ld = roi + __umul24(r0, (uint32_t)ls) + q4;
-      for (int k0 = 0; k0 < nst; k0 += kFastPf) {
-        uint32_t v[kFastPf];
-#pragma unroll
-        for (int u = 0; u < kFastPf; ++u)
-          if (k0 + u < nst)
-            v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vo, 4 * (k0 + u) * sp, 0);
-#pragma unroll
-        for (int u = 0; u < kFastPf; ++u)
-          if (k0 + u < nst && (k0 + u < nst - 1 || last_ok))
-            *reinterpret_cast<uint32_t*>(ld + 4 * (k0 + u) * ls) = v[u];
-      }
-    } else if (ndw <= 16) {
+    if (ndw <= 16) {
       // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
       // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight.
       // Lanes past the ROI width or height are clamped onto its last dword /
