@@ -251,6 +251,50 @@ __device__ __forceinline__ void pose_update(StateD& s, const double* u, const Ca
 // estimate-dependent Jacobian blocks to J[9][24] (columns VP1 VV1 VG1 VA1 VP2
 // VV2).  The constant blocks (-I, -JVg, -JPg, -JVa, -JPa) and the zeros are
 // the caller's (written once).
+// The Jacobian blocks of EdgeInertial that depend on the two states only
+// (not on the preintegration): -Rbw1 (VV1 rows 3-5 and, x dt, 6-8), Rbw1
+// (VV2), [Rbw1 dv]x and [Rbw1 dp]x (VP1 rotation), Rbw1 Rwb2 (VP2
+// translation).  inertial_edge_core<false> leaves them to this function, so
+// another wave can form them at the same time.
+__device__ __forceinline__ void inertial_edge_lin(const StateD& s1, const StateD& s2, double dt, int lane,
+                                                  double* J) {
+  const double g2 = -(double)9.81f;
+  double Rbw1[9];
+  m3_tr(s1.Rwb, Rbw1);
+  auto put = [&](int r0, int c0, const double* m, double sc) {
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) J[(r0 + i) * 24 + c0 + j] = sc * m[3 * i + j];
+  };
+  put(3, 6, Rbw1, -1.0);
+  put(6, 6, Rbw1, -dt);
+  put(3, 21, Rbw1, 1.0);
+  {
+    double dv[3], rv[3], hv[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dv[i] = s2.v[i] - s1.v[i] - (i == 2 ? g2 * dt : 0.0);
+    m3_mv(Rbw1, dv, rv);
+    m3_hat(rv, hv);
+    put(3, 0, hv, 1.0);
+  }
+  {
+    double dp2[3], rp2[3], hp[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dp2[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? 0.5 * g2 * dt * dt : 0.0);
+    m3_mv(Rbw1, dp2, rp2);
+    m3_hat(rp2, hp);
+    put(6, 0, hp, 1.0);
+  }
+  {
+    double R12[9];
+    m3_mul(Rbw1, s2.Rwb, R12);
+    put(6, 18, R12, 1.0);
+  }
+}
+
+template <bool kLin = true>
 __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const StateD& s2,
                                                    const orbgpu_imu_preint& pi, double dt, int lane,
                                                    double* J, double* ei) {
@@ -306,27 +350,7 @@ __device__ __forceinline__ void inertial_edge_core(const StateD& s1, const State
   if (lane == 0)
 #pragma unroll
     for (int i = 0; i < 9; ++i) ei[i] = e[i];
-  put(3, 6, Rbw1, -1.0);
-  put(6, 6, Rbw1, -dt);
-  put(3, 21, Rbw1, 1.0);
-  {
-    double hv[9];
-    m3_hat(rv, hv);
-    put(3, 0, hv, 1.0);
-  }
-  {
-    double dp2[3], rp2[3], hp[9];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) dp2[i] = s2.twb[i] - s1.twb[i] - s1.v[i] * dt - (i == 2 ? 0.5 * g2 * dt * dt : 0.0);
-    m3_mv(Rbw1, dp2, rp2);
-    m3_hat(rp2, hp);
-    put(6, 0, hp, 1.0);
-  }
-  {
-    double R12[9];
-    m3_mul(Rbw1, s2.Rwb, R12);
-    put(6, 18, R12, 1.0);
-  }
+  if constexpr (kLin) inertial_edge_lin(s1, s2, dt, lane, J);
   IMU_EDGE_MARK(15);
   double invJr[9];
   right_j<true>(er, invJr);

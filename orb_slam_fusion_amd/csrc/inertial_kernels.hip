@@ -251,7 +251,11 @@ __device__ __forceinline__ void vis_accumulate(const VisObs& o, const double* Rc
 
 // ---- the IMU edges (one wave each, every lane the same values; lane 0 stores)
 __device__ void inertial_edge(InShared& sh, const orbgpu_imu_preint& pi, double dt, int lane) {
-  inertial_edge_core(sh.prev, sh.cur, pi, dt, lane, sh.Ji, sh.ei);
+  inertial_edge_core<false>(sh.prev, sh.cur, pi, dt, lane, sh.Ji, sh.ei);
+}
+// the state-only Jacobian blocks, on another wave meanwhile
+__device__ void inertial_edge_states(InShared& sh, double dt, int lane) {
+  inertial_edge_lin(sh.prev, sh.cur, dt, lane, sh.Ji);
 }
 
 // The parts of EdgeInertial's Jacobian that do not depend on the estimates
@@ -613,10 +617,15 @@ __device__ __forceinline__ void load_state(StateD& s, const orbgpu_imu_state& g)
 // meanwhile runs `imu` (its own work).  kind 0: Gauss-Newton system (Huber
 // weights where robust); kind 1: unweighted J^T Omega J of the inlier edges
 // (GetHessian) at the current pose.
-template <typename W0, typename W1>
+// Waves 2..7 take the visual edges; wave kLinWave first forms the IMU
+// edge's state-only Jacobian blocks (`w3`), off wave 0's critical path.
+// (Handing the edges past kVisThreads to wave 1 after the prior edge instead
+// of a second pass of wave 2 measured slower: wave 1 became the last.)
+constexpr int kLinWave = 3;
+template <typename W0, typename W1, typename W3>
 __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, const VisObs* gobs,
                           const uint8_t* glv, int cap, int n, bool robust, int kind, int t,
-                          bool sum_here, W0&& w0, W1&& w1) {
+                          bool sum_here, W0&& w0, W1&& w1, W3&& w3) {
   const int wave = t >> 6, lane = t & 63;
 #ifdef ORB_STAMPS
   const unsigned long long vt0 = __builtin_amdgcn_s_memtime();
@@ -624,38 +633,40 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
 #endif
   if (wave == 0) {
     w0();
-  } else if (wave == 1) {
-    w1();
   } else {
-    // the accumulators live in this branch only, so they add nothing to the
-    // register pressure of the IMU-edge waves' code
-    double acc[27];
+    if (wave == 1) w1();
+    if (wave == kLinWave) w3();
+    if (wave >= kVisWave0) {
+      // the accumulators live in this branch only, so they add nothing to the
+      // register pressure of the IMU-edge wave's code
+      double acc[27];
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] = 0;
-    const int tv = t - 64 * kVisWave0;
-    for (int i = tv; i < n; i += kVisThreads) {
-      const bool in_lds = i < cap;
-      const uint8_t l = in_lds ? lv[i] : glv[i];
-      if (l) continue;
-      const VisObs o = in_lds ? ob[i] : gobs[i];
-      vis_accumulate(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, kind == 0 && robust, 1.0, acc);
-    }
+      for (int k = 0; k < 27; ++k) acc[k] = 0;
+      const int tv = t - 64 * kVisWave0;
+      for (int i = tv; i < n; i += kVisThreads) {
+        const bool in_lds = i < cap;
+        const uint8_t l = in_lds ? lv[i] : glv[i];
+        if (l) continue;
+        const VisObs o = in_lds ? ob[i] : gobs[i];
+        vis_accumulate(o, sh.cur.Rcw, sh.cur.tcw, sh.cal, kind == 0 && robust, 1.0, acc);
+      }
 #ifdef ORB_STAMPS
-    vt1 = __builtin_amdgcn_s_memtime();
+      vt1 = __builtin_amdgcn_s_memtime();
 #endif
-    // DPP row sums; lane 15 of each row writes its partial
+      // DPP row sums; lane 15 of each row writes its partial
 #pragma unroll
-    for (int k = 0; k < 27; ++k) {
-      double x = acc[k];
-      x += dpp_d<0x111, 0xf>(x);
-      x += dpp_d<0x112, 0xf>(x);
-      x += dpp_d<0x114, 0xf>(x);
-      x += dpp_d<0x118, 0xf>(x);
-      acc[k] = x;
+      for (int k = 0; k < 27; ++k) {
+        double x = acc[k];
+        x += dpp_d<0x111, 0xf>(x);
+        x += dpp_d<0x112, 0xf>(x);
+        x += dpp_d<0x114, 0xf>(x);
+        x += dpp_d<0x118, 0xf>(x);
+        acc[k] = x;
+      }
+      if ((lane & 15) == 15)
+#pragma unroll
+        for (int k = 0; k < 27; ++k) sh.red[(wave * 4 + (lane >> 4)) * 27 + k] = acc[k];
     }
-    if ((lane & 15) == 15)
-#pragma unroll
-      for (int k = 0; k < 27; ++k) sh.red[(wave * 4 + (lane >> 4)) * 27 + k] = acc[k];
   }
 #ifdef ORB_STAMPS
   if (t == 64 * kVisWave0) {
@@ -744,7 +755,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
           },
           [&] {
             if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, &sh.prs, true, lane);
-          });
+          },
+          [&] { inertial_edge_states(sh, dt, lane); });
       ISTAMP(0);
       assemble<MODE>(sh, pi, pr, t);
       __syncthreads();
@@ -862,7 +874,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       sh, ob, lv, gobs, glv, cap, nobs, false, 1, t, true, [&] { inertial_edge(sh, sh.pre, dt, lane); },
       [&] {
         if (MODE == ORBGPU_INERTIAL_LAST_FRAME) prior_edge(sh, &sh.prs, false, lane);
-      });
+      },
+      [&] { inertial_edge_states(sh, dt, lane); });
   __syncthreads();
   orbgpu_inertial_result* res = g_res + p;
   if (MODE == ORBGPU_INERTIAL_LAST_FRAME) {
