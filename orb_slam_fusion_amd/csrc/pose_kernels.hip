@@ -66,11 +66,31 @@ struct CamDev {
 constexpr int kPoseThreads = 256;  // threads per trial group
 constexpr int kPoseWaves = kPoseThreads / 64;
 
-__device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3& T, const CamDev& c,
+// A sweep's pose as a rotation matrix (Eigen's toRotationMatrix of the unit
+// quaternion) + translation: the per-edge map is then 9 FMAs instead of the
+// quaternion form's cross products (same value to rounding).
+struct Se3R {
+  double R[9], t[3];
+};
+__device__ __forceinline__ Se3R se3r(const Se3& T) {
+  const double tx = 2 * T.qx, ty = 2 * T.qy, tz = 2 * T.qz;
+  const double twx = tx * T.qw, twy = ty * T.qw, twz = tz * T.qw;
+  const double txx = tx * T.qx, txy = ty * T.qx, txz = tz * T.qx;
+  const double tyy = ty * T.qy, tyz = tz * T.qy, tzz = tz * T.qz;
+  return Se3R{{1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
+               txz - twy, tyz + twx, 1 - (txx + tyy)},
+              {T.t[0], T.t[1], T.t[2]}};
+}
+__device__ __forceinline__ void pose_map(const Se3R& T, const double X[3], double p[3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p[i] = T.R[3 * i] * X[0] + T.R[3 * i + 1] * X[1] + T.R[3 * i + 2] * X[2] + T.t[i];
+}
+
+__device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3R& T, const CamDev& c,
                                            double e[3], bool& stereo) {
   const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
   double p[3];
-  se3_map(T, X, p);
+  pose_map(T, X, p);
   stereo = o.ur >= 0.f;
   if (!stereo) {  // EdgeSE3ProjectXYZOnlyPose + Pinhole::Project
     e[0] = (double)o.u - (c.fx * p[0] / p[2] + c.cx);
@@ -92,11 +112,11 @@ __device__ __forceinline__ double edge_chi2(const double e[3], double info, bool
   return s;
 }
 
-__device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3& T, const CamDev& c,
+__device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3R& T, const CamDev& c,
                                               bool stereo, double J[3][6]) {
   const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
   double p[3];
-  se3_map(T, X, p);
+  pose_map(T, X, p);
   const double x = p[0], y = p[1], z = p[2];
   if (!stereo) {
     const double pj00 = -(c.fx / z), pj02 = -(-c.fx * x / (z * z));
@@ -246,7 +266,7 @@ constexpr int kPoseLdsObs = 4096;  // observations staged in LDS (the rest re-re
 // BlockSolver::buildSystem's H (lower triangle, 21) and b (6) into
 // acc[1..27].  Every sweep visits a thread's edges in the same order, so the
 // sums are reproducible.
-__device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3& T, const CamDev& cam,
+__device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3R& T, const CamDev& cam,
                                                 bool robust, double dmono, double dstereo,
                                                 bool build, double (&acc)[28]) {
   double e[3];
@@ -381,7 +401,8 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   // chains, ILP), the accumulation stays in edge order; the wave sums land in
   // dst[wave of the group] (added in wave order by the readers).
   constexpr int kU = 3;  // (ILP only: the sums are the same for any kU)
-  auto chi_sweep = [&](const Se3& X, double* dst) {
+  auto chi_sweep = [&](const Se3& Xq, double* dst) {
+    const Se3R X = se3r(Xq);
     double acc[28];
     acc[0] = 0;
     for (int i0 = tg; i0 < cap; i0 += kU * kPoseThreads) {
@@ -411,7 +432,8 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   // computeActiveErrors + buildSystem at pose X -> sh.hb (chi2, H, b); one
   // edge at a time straight into the accumulators (three in flight held 84
   // partials: 306 VGPRs and 0.312 ms per 64 problems; one: 185 VGPRs, 0.296)
-  auto build_sweep = [&](const Se3& X) {
+  auto build_sweep = [&](const Se3& Xq) {
+    const Se3R X = se3r(Xq);
     double acc[28];
 #pragma unroll
     for (int k = 0; k < 28; ++k) acc[k] = 0;
@@ -549,11 +571,11 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     // classify (optimizer.cc:966-1037): level-1 edges recompute at T, level-0
     // edges keep the error of the last sweep (at Teval)
     int bad = 0;
-    const Se3 Teval = pose_at(teval);
+    const Se3R TR = se3r(T), TevalR = se3r(pose_at(teval));
     auto classify = [&](const PoseObsDev& o, uint8_t& l) {
       double e[3];
       bool st;
-      edge_error(o, l ? T : Teval, cam, e, st);
+      edge_error(o, l ? TR : TevalR, cam, e, st);
       const float chi2 = (float)edge_chi2(e, (double)o.inv_sigma2, st);
       const bool out = chi2 > (st ? 7.815f : 5.991f);
       l = out ? 1 : 0;
