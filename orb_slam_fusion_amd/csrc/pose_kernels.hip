@@ -185,9 +185,21 @@ __device__ __forceinline__ double uniform_f64(double v) {  // wave-uniform value
 // block in LDS, then (NW == 4) thread k adds value k's 16 partials in row
 // order, or (NW > 4) 16-row slices first, the slices next.  Only LDS
 // consumers need the result (the build sweep's system): no broadcast.
+// (hf != nullptr, NV == 28: the H entries out[1..21] also land in hf as the
+// full row-major 6x6, for the solves' row gathers)
+__device__ __forceinline__ void mirror_h(int k, double a, double* hf) {
+  if (k >= 1 && k < 22) {
+    int r = 0;
+#pragma unroll
+    for (int q = 1; q < 6; ++q) r += (k - 1 >= q * (q + 1) / 2) ? 1 : 0;
+    const int c = k - 1 - r * (r + 1) / 2;
+    hf[r * 6 + c] = a;
+    hf[c * 6 + r] = a;
+  }
+}
 template <int NV, int NW>
 __device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, double* red2,
-                                                 double* out) {
+                                                 double* out, double* hf = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -208,6 +220,7 @@ __device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, d
 #pragma unroll
       for (int r = 0; r < 16; ++r) a += red[r * NV + threadIdx.x];
       out[threadIdx.x] = a;
+      if (hf) mirror_h(threadIdx.x, a, hf);
     }
   } else {
     constexpr int S = NW / 4;  // 16-row slices
@@ -224,6 +237,7 @@ __device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, d
 #pragma unroll
       for (int sl = 1; sl < S; ++sl) a += red2[sl * NV + threadIdx.x];
       out[threadIdx.x] = a;
+      if (hf) mirror_h(threadIdx.x, a, hf);
     }
   }
   __syncthreads();
@@ -253,6 +267,7 @@ struct PoseShared {
   double red[G * kPoseWaves * 4 * 28];
   double red2[G * 28];
   double hb[28];                        // chi2, H (lower, 21), b (6) at the current pose
+  double hf[36];                        // H as the full row-major 6x6 (the solves' gathers)
   double chi[2][G][kPoseWaves];         // trial chi2 wave partials, double-buffered by round
   double trial[2][G][14];               // x (6), Tn (qx qy qz qw t0 t1 t2), ok
   double init[7];                       // the input pose (qx qy qz qw t0 t1 t2)
@@ -443,7 +458,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
       if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
     for (int i = cap + t; i < n; i += NT)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
-    block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb);
+    block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb, sh.hf);
   };
 
   const double* hb = sh.hb;
@@ -491,7 +506,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
         // broadcast barrier
         double x[6];
         PSTAMP(0);
-        const bool ok = ldlt6_gj(hb, lg, x);
+        const bool ok = ldlt6_gj(hb, sh.hf, lg, x);
         PSTAMP(2);
         const Se3 Tn = se3_compose(se3_exp(x), T);
         PSTAMP(3);

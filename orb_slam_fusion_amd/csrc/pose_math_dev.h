@@ -405,7 +405,8 @@ __device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmin
   }
 }
 
-__device__ __forceinline__ bool ldlt6_gj(const double* hb, double lambda, double (&x)[6]) {
+__device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, double lambda,
+                                         double (&x)[6]) {
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int l6 = lane < 6 ? lane : 0;
   const double dl = lane < 6 ? fabs(hb[1 + l6 * (l6 + 1) / 2 + l6] + lambda) : -1.0;
@@ -418,12 +419,15 @@ __device__ __forceinline__ bool ldlt6_gj(const double* hb, double lambda, double
   int pi = 0;  // the original index at permuted position li
 #pragma unroll
   for (int j = 0; j < 6; ++j) pi = __builtin_amdgcn_readlane(rank, j) == li ? j : pi;
+  // row pi of the full matrix (hf, mirrored by the build's reduction), its
+  // columns in pivot order: a wave-uniform offset per column
   double w[12];
+  const double* row = hf + 6 * (li < 6 ? pi : 0);
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     const int pj = __builtin_amdgcn_readlane(pi, j);
-    const int r = max(pi, pj), c = min(pi, pj);
-    w[j] = li < 6 ? hb[1 + r * (r + 1) / 2 + c] + (r == c ? lambda : 0.0) : 0.0;
+    const double h = row[pj];
+    w[j] = li < 6 ? (pi == pj ? h + lambda : h) : 0.0;
   }
   w[6] = li < 6 ? hb[22 + pi] : 0.0;
 #pragma unroll
