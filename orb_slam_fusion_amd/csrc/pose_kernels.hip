@@ -17,6 +17,8 @@
 #include "lds_optin.h"
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "pose_math_dev.h"
 
 // fp64 solver arithmetic, parity by tolerance (not bit-exact like the
@@ -197,6 +199,44 @@ __device__ __forceinline__ void mirror_h(int k, double a, double* hf) {
     hf[c * 6 + r] = a;
   }
 }
+// The build's 28 sums over one 256-thread group mostly through LDS instead of
+// DPP trees: one DPP step adds lane pairs (2i, 2i + 1), the odd lanes store
+// the 28 pair sums (thread-major, 14 b128 writes), thread (k, c) = (t & 31,
+// t >> 5) adds value k of pairs 16c .. 16c + 15 in order (k < 28), and thread
+// k adds the 8 chunk sums in order.  Fixed order (reproducible); 84 VALU + 30
+// LDS instructions a thread instead of 336 VALU.  T: 128 x 28 doubles of
+// dynamic LDS (kPoseRedT), P: 224 doubles.
+constexpr size_t kPoseRedT = 128 * 28 * sizeof(double);
+__device__ __forceinline__ void block_sum28_lds_t(const double (&v)[28], double* T, double* P,
+                                                  double* out, double* hf) {
+  const int t = threadIdx.x;
+  double w[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) w[k] = v[k] + dpp_f64<0x111, 0xf>(v[k]);  // lane i: v_i + v_(i-1)
+  if (t & 1)
+#pragma unroll
+    for (int k = 0; k < 28; k += 2)
+      *reinterpret_cast<double2*>(T + (t >> 1) * 28 + k) = make_double2(w[k], w[k + 1]);
+  __syncthreads();
+  const int k = t & 31, c = t >> 5;
+  if (k < 28) {
+    const double* col = T + (16 * c) * 28 + k;
+    double a = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a += col[j * 28];
+    P[k * 8 + c] = a;
+  }
+  __syncthreads();
+  if (t < 28) {
+    double a = P[t * 8];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) a += P[t * 8 + q];
+    out[t] = a;
+    mirror_h(t, a, hf);
+  }
+  __syncthreads();
+}
+
 template <int NV, int NW>
 __device__ __forceinline__ void block_sum_to_lds(double (&v)[NV], double* red, double* red2,
                                                  double* out, double* hf = nullptr) {
@@ -359,6 +399,10 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   PoseObsDev* ob = reinterpret_cast<PoseObsDev*>(pose_lds);
   uint8_t* lv = pose_lds + (size_t)lds_obs * sizeof(PoseObsDev);
   uint16_t* pm = reinterpret_cast<uint16_t*>(lv + ((lds_obs + 1) & ~1));
+  // (G == 1) the build reduction's transpose buffer, 16-byte aligned after pm
+  double* tred = reinterpret_cast<double*>(
+      pose_lds + ((((size_t)lds_obs * sizeof(PoseObsDev) + ((lds_obs + 1) & ~1) + 2 * (size_t)lds_obs) + 15) &
+                  ~(size_t)15));
   {
     int c = 0;
     for (int i = t; i < cap; i += NT) c += obs[i].ur >= 0.f ? 1 : 0;
@@ -458,7 +502,10 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
       if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
     for (int i = cap + t; i < n; i += NT)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
-    block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb, sh.hf);
+    if constexpr (G == 1)
+      block_sum28_lds_t(acc, tred, sh.red, sh.hb, sh.hf);
+    else
+      block_sum_to_lds<28, NW>(acc, sh.red, sh.red2, sh.hb, sh.hf);
   };
 
   const double* hb = sh.hb;
@@ -630,12 +677,17 @@ static hipError_t launch_pose_opt_g(const CamDev& c, const float* d_pose_in, con
                                     const int* d_nobs, int obs_stride, int n_problems,
                                     float* d_pose_out, uint8_t* d_outlier, int* d_inliers,
                                     double* d_pose_out_d, hipStream_t st) {
-  const int lds_obs = obs_stride < kPoseLdsObs ? obs_stride : kPoseLdsObs;
+  // observations staged in LDS: up to kPoseLdsObs, and what fits beside the
+  // static part and (G == 1) the reduction buffer in 160 KB
+  const size_t fixed = sizeof(PoseShared<G>) + (G == 1 ? kPoseRedT : 0) + 64;
+  const int fit = (int)((160 * 1024 - fixed) / (sizeof(PoseObsDev) + 3));
+  const int lds_obs = std::min(std::min(obs_stride, kPoseLdsObs), fit);
   // observations, levels, slot -> observation index (k_pose_opt)
-  const size_t lds = ((size_t)lds_obs * sizeof(PoseObsDev) + (((size_t)lds_obs + 1) & ~(size_t)1) +
-                      2 * (size_t)lds_obs + 15) & ~(size_t)15;
+  const size_t lds = (((size_t)lds_obs * sizeof(PoseObsDev) + (((size_t)lds_obs + 1) & ~(size_t)1) +
+                       2 * (size_t)lds_obs + 15) & ~(size_t)15) +
+                     (G == 1 ? kPoseRedT : 0);  // + the build reduction's transpose buffer
   if (lds + sizeof(PoseShared<G>) > 64 * 1024) {
-    if (lds_optin(reinterpret_cast<const void*>(&k_pose_opt<G>), 150 * 1024) != hipSuccess)
+    if (lds_optin(reinterpret_cast<const void*>(&k_pose_opt<G>), (int)lds) != hipSuccess)
       return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(k_pose_opt<G>, dim3(n_problems), dim3(kPoseThreads * G), lds, st, c,
