@@ -548,41 +548,32 @@ __device__ bool ldlt_wave(InShared& sh, int lane) {
 #include "inertial_gj.inc"
 
 // The same system by Gauss-Jordan elimination (tools/gen_inertial_gj.py):
-// wave 0, lane li of each 16-lane row owns permuted rows li and li + 16 with
-// b appended, pivot k's row read by DPP64 row broadcast (one v_fmac_f64_dpp
-// per entry, no v_readlane chains, no substitution passes).  Same pivot order
-// and pivots as ldlt_wave (the rows below a pivot are eliminated alike; the
-// rows above cost nothing extra in this layout), x_i = b'_i / D_i with Eigen's
-// tolerance.  A negative pivot: not positive; a zero pivot: ldlt_wave, which
-// keeps Eigen's semantics for it.
+// wave 0, lane li of each 16-lane row owns rows li and li + 16 with b
+// appended, pivot k's row read by DPP64 row broadcast (one v_fmac_f64_dpp
+// per entry, no v_readlane chains, no substitution passes), every row but the
+// pivot's eliminated (the rows above cost nothing extra in this layout), x_i
+// = b'_i / D_i with Eigen's tolerance.  Pivots in natural order: the system
+// is symmetric positive definite whenever the step succeeds, where
+// elimination needs no pivoting and Eigen's diagonal pivot order changes
+// only the rounding, and the signs of the pivots (isPositive) do not depend
+// on the order; rows load with compile-time column offsets (the permuted
+// gather cost a tenth of the kernel).  A negative pivot: not positive; a
+// zero pivot: ldlt_wave, which keeps Eigen's pivoting and semantics for it.
 template <int n>
 __device__ bool gj_wave(InShared& sh, int lane) {
   ISTAMP_T(gt0);
-  const double dl = lane < n ? fabs(sh.H[lane * kLd + lane]) : -1.0;
-  int rank = 0;  // the diagonal broadcast from registers (v_readlane), no LDS round trips
-#pragma unroll
-  for (int j = 0; j < n; ++j) {
-    const double dj = bcast(dl, j);
-    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
-  }
-  if (lane < n) sh.perm[rank] = lane;
-  wave_sync();
-  const int pl = lane < n ? sh.perm[lane] : 0;
   const int li = lane & 15, ia = li, ib = li + 16;
-  const int pa = ia < n ? sh.perm[ia] : 0, pb = ib < n ? sh.perm[ib] : 0;
-  // rows of the full symmetric system (assemble mirrors it); rows past n read
-  // the zero row 30, the columns are wave-uniform offsets
-  const double* hA = sh.H + (ia < n ? pa : 30) * kLd;
-  const double* hB = sh.H + (ib < n ? pb : 30) * kLd;
+  // rows past n read the zero row 30
+  const double* hA = sh.H + (ia < n ? ia : 30) * kLd;
+  const double* hB = sh.H + (ib < n ? ib : 30) * kLd;
   double rA[n + 1], rB[n + 1];
 #pragma unroll
   for (int j = 0; j < n; ++j) {
-    const int pj = __builtin_amdgcn_readlane(pl, j);
-    rA[j] = hA[pj];
-    rB[j] = hB[pj];
+    rA[j] = hA[j];
+    rB[j] = hB[j];
   }
-  rA[n] = ia < n ? sh.b[pa] : 0.0;
-  rB[n] = ib < n ? sh.b[pb] : 0.0;
+  rA[n] = ia < n ? sh.b[ia] : 0.0;
+  rB[n] = ib < n ? sh.b[ib] : 0.0;
   double dA = 1.0, dB = 1.0;
   ISTAMP_T(gt1);
   const int f = gj_pivots<n>(rA, rB, li, dA, dB);
@@ -593,8 +584,8 @@ __device__ bool gj_wave(InShared& sh, int lane) {
   if (f & 2) return ldlt_wave<n>(sh, lane);
   constexpr double kTiny = 1.0 / 1.79769313486231570815e+308;
   if (lane < 16) {
-    if (ia < n) sh.x[pa] = fabs(dA) > kTiny ? rA[n] / dA : 0.0;
-    if (ib < n) sh.x[pb] = fabs(dB) > kTiny ? rB[n] / dB : 0.0;
+    if (ia < n) sh.x[ia] = fabs(dA) > kTiny ? rA[n] / dA : 0.0;
+    if (ib < n) sh.x[ib] = fabs(dB) > kTiny ? rB[n] / dB : 0.0;
   }
   return true;
 }
