@@ -407,29 +407,20 @@ __device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmin
 
 __device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, double lambda,
                                          double (&x)[6]) {
+  // pivots in natural order: H + lambda I is symmetric positive definite
+  // whenever the trial succeeds, where elimination needs no pivoting and
+  // Eigen's diagonal pivot order changes only the rounding (and not the pivot
+  // signs, so not isPositive()); rows of the full mirror (hf) load with
+  // compile-time offsets.  A zero pivot takes ldlt6_wave (Eigen's pivoting).
   const int lane = threadIdx.x & 63, li = lane & 15;
-  const int l6 = lane < 6 ? lane : 0;
-  const double dl = lane < 6 ? fabs(hb[1 + l6 * (l6 + 1) / 2 + l6] + lambda) : -1.0;
-  int rank = 0;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const double dj = readlane_f64(dl, j);
-    rank += (dj > dl || (dj == dl && j < lane)) ? 1 : 0;
-  }
-  int pi = 0;  // the original index at permuted position li
-#pragma unroll
-  for (int j = 0; j < 6; ++j) pi = __builtin_amdgcn_readlane(rank, j) == li ? j : pi;
-  // row pi of the full matrix (hf, mirrored by the build's reduction), its
-  // columns in pivot order: a wave-uniform offset per column
+  const double* row = hf + 6 * (li < 6 ? li : 0);
   double w[12];
-  const double* row = hf + 6 * (li < 6 ? pi : 0);
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    const int pj = __builtin_amdgcn_readlane(pi, j);
-    const double h = row[pj];
-    w[j] = li < 6 ? (pi == pj ? h + lambda : h) : 0.0;
+    const double h = row[j];
+    w[j] = li < 6 ? (li == j ? h + lambda : h) : 0.0;
   }
-  w[6] = li < 6 ? hb[22 + pi] : 0.0;
+  w[6] = li < 6 ? hb[22 + li] : 0.0;
 #pragma unroll
   for (int j = 7; j < 12; ++j) w[j] = 0.0;
   double dmine = 1.0;
@@ -438,7 +429,8 @@ __device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, dou
   if (flags & 2) return ldlt6_wave(hb, lambda, x);
   const double z = li < 6 && fabs(dmine) > 1.0 / 1.79769313486231570815e+308 ? w[6] / dmine : 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, __builtin_amdgcn_readlane(rank, k));
+  for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, k);
+  (void)lane;
   return !(flags & 1);
 }
 
