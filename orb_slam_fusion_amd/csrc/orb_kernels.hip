@@ -550,6 +550,20 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
 }
 
+// In-wave inclusive integer scan by DPP (row_shr 1,2,4,8 within each 16-lane
+// row, then row_bcast 15/31 carry the row totals): lane 63 holds the total.
+// Full-mask steps read 0 out of range (bound_ctrl), so they need no zeroed
+// destination.  The whole wave must be active.
+__device__ __forceinline__ int wave_iscan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 constexpr int kFastPf = 12;  // ROI dwords in flight per lane (one round trip up to 768)
 
 __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict__ P,
@@ -573,13 +587,15 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   }
   // LDS (fast_cell_lds_bytes): ROI rows of ls bytes (ROI column x at row byte
   // lead + x), score map of the detection area with a zero border (row pitch
-  // dw + 2), u16 survivor list.  A survivor is r << 7 | q (detection row,
-  // column; dw < 128, dh < 256 by the planner), bit 15 = keypoint flag.
+  // dw + 2), u16 survivor list, u32 list of the 8-pixel groups holding a
+  // survivor.  A survivor is r << 7 | q (detection row, column; dw < 128,
+  // dh < 256 by the planner), bit 15 = keypoint flag.
   const int ls = (c.cols + 6) & ~3;
   const int sp2 = dw + 2, nsc = sp2 * (dh + 2);
   uint8_t* roi = lds;
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
   uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
+  uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) + ((2 * nd + 15) & ~15));
   auto sci = [&](int i) { return ((i >> 7) + 1) * sp2 + (i & 127) + 1; };
 
   // ---- ROI -> LDS: raw dwords, all loads in flight before the first store
@@ -642,10 +658,13 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   const uint2 sel_l = make_uint2(psel(s_l), psel(s_l + 2));
   const uint2 sel_r = make_uint2(psel(s_r), psel(s_r + 2));
 
+  const uint32_t tail_mask = (1u << tail) - 1u;  // valid pixels of a row's tail group
+
   auto pass = [&](int th, int* n_sv) -> int {
     // compass pre-test on 8 pixels per lane in packed u16 pairs; the window
     // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
-    int ns = 0;
+    int ng = 0;
+    const ushort2_t thv = {(unsigned short)(0x7fff - th), (unsigned short)(0x7fff - th)};
     auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
     for (int r = g_r0, g = g_q0;;) {
       const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
@@ -674,43 +693,52 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       for (int j = 0; j < 4; ++j)
         tv[j] = __builtin_bit_cast(uint32_t, compass2(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]),
                                                       as_us2(ql[j]), as_us2(qr[j])));
-      // pixel k of the group is valid iff its row is (rv) and, for the row's
-      // tail group (tl), k < tail; g < gpr - 1 groups are whole.  Both masks
-      // come from one compare each, the per-pixel masks from scalar ANDs
-      // (per-pixel nv > k compares cost 8 VALU a group)
-      const bool rv = r < dh, tl = g == gpr - 1;
-      const uint64_t mwhole = mrv & ~bal(tl);
-      auto ok = [&](int k) { return rv && (k < tail || !tl); };
-      auto okm = [&](int k) { return k < tail ? mrv : mwhole; };
-      auto pass_lo = [&](uint32_t x) { return (x & 0xffffu) > (uint32_t)th; };
-      auto pass_hi = [&](uint32_t x) { return (x >> 16) > (uint32_t)th; };
-      const bool f0 = ok(0) && pass_lo(tv[0]), f1 = ok(1) && pass_hi(tv[0]);
-      const bool f2 = ok(2) && pass_lo(tv[1]), f3 = ok(3) && pass_hi(tv[1]);
-      const bool f4 = ok(4) && pass_lo(tv[2]), f5 = ok(5) && pass_hi(tv[2]);
-      const bool f6 = ok(6) && pass_lo(tv[3]), f7 = ok(7) && pass_hi(tv[3]);
-      // the masks as ANDs of single-compare ballots (scalar ANDs of the
-      // compares' lane masks): a ballot of an && rematerialises the bool with
-      // a v_cndmask + v_cmp pair per pixel
-      const uint64_t m0 = okm(0) & bal(pass_lo(tv[0])), m1 = okm(1) & bal(pass_hi(tv[0]));
-      const uint64_t m2 = okm(2) & bal(pass_lo(tv[1])), m3 = okm(3) & bal(pass_hi(tv[1]));
-      const uint64_t m4 = okm(4) & bal(pass_lo(tv[2])), m5 = okm(5) & bal(pass_hi(tv[2]));
-      const uint64_t m6 = okm(6) & bal(pass_lo(tv[3])), m7 = okm(7) & bal(pass_hi(tv[3]));
-      int pos = ns + (int)mbcnt64(m7, mbcnt64(m6, mbcnt64(m5, mbcnt64(m4, mbcnt64(m3, mbcnt64(m2,
-                         mbcnt64(m1, mbcnt64(m0, 0u))))))));
-      const int i0 = (r << 7) | (8 * g);
-      if (f0) sv[pos++] = (uint16_t)i0;
-      if (f1) sv[pos++] = (uint16_t)(i0 + 1);
-      if (f2) sv[pos++] = (uint16_t)(i0 + 2);
-      if (f3) sv[pos++] = (uint16_t)(i0 + 3);
-      if (f4) sv[pos++] = (uint16_t)(i0 + 4);
-      if (f5) sv[pos++] = (uint16_t)(i0 + 5);
-      if (f6) sv[pos++] = (uint16_t)(i0 + 6);
-      if (f7) sv[pos] = (uint16_t)(i0 + 7);
-      ns += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3) + __popcll(m4) + __popcll(m5) +
-            __popcll(m6) + __popcll(m7);
+      // value > th  <=>  bit 15 of the u16 value + (0x7fff - th) (value, th
+      // <= 255: no carry out); one packed add per pixel pair, then the flag
+      // bits 15 / 31 of the four pairs gathered by two v_perm into bits
+      // 7, 15, 23, 31 of A (pixels 0-3) and B (pixels 4-7)
+      uint32_t fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = __builtin_bit_cast(uint32_t, as_us2(tv[j]) + thv);
+      const uint32_t A = __builtin_amdgcn_perm(fb[1], fb[0], 0x07050301u) & 0x80808080u;
+      const uint32_t B = __builtin_amdgcn_perm(fb[3], fb[2], 0x07050301u) & 0x80808080u;
+      // group mask (pixel k at bit 7 + k) by two v_dot4 with per-pixel weights
+      // 2^k.  Pixels past the detection width in a row's tail group are
+      // dropped at the expansion (once per entry, not once per group here).
+      const uint32_t m7 = __builtin_amdgcn_udot4(A, 0x08040201u, __builtin_amdgcn_udot4(B, 0x80402010u, 0u, false),
+                                                 false);
+      // groups with a survivor append (r << 7 | 8 g) | mask << 16 in raster
+      // order; the per-pixel list is expanded below, once per 64 entries
+      const bool has = r < dh && m7 != 0;
+      const uint64_t mg = bal(has);
+      if (has) ge[mbcnt64(mg, (uint32_t)ng)] = (uint32_t)((r << 7) | (8 * g)) | (m7 << 9);
+      ng += __popcll(mg);
       g += g_dq;
       r += g_dr;
       if (g >= gpr) g -= gpr, ++r;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // expand the group entries into the per-pixel survivor list: lane j of a
+    // 64-entry chunk writes its entry's pixels from the wave's inclusive scan
+    // of the entries' popcounts (raster order kept: entries in order, pixels
+    // LSB-first)
+    int ns = 0;
+    for (int b0 = 0; b0 < ng; b0 += 64) {
+      const int j = b0 + lane;
+      const uint32_t e = j < ng ? ge[j] : 0u;
+      const int i0 = (int)(e & 0xffffu);
+      // the row's tail group keeps its first `tail` pixels
+      uint32_t m = (e >> 16) & (((i0 >> 3) & 15) == gpr - 1 ? tail_mask : 0xffu);
+      const int cnt = __popc(m);
+      const int incl = wave_iscan(cnt);
+      int pos = ns + incl - cnt;
+      while (m) {
+        sv[pos++] = (uint16_t)(i0 + __builtin_ctz(m));
+        m &= m - 1;
+      }
+      ns += __builtin_amdgcn_readlane(incl, 63);
     }
     __syncthreads();
     STAMP(0);
@@ -1228,18 +1256,6 @@ constexpr int kRawW = 36, kRawH = 31;   // 31x31 patch + dword alignment slack
 constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slack
 constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
 
-// In-wave integer sum by DPP (row_shr 1,2,4,8 + row_bcast 15/31): lane 63
-// holds the total.  Full-mask steps read 0 out of range (bound_ctrl), so they
-// need no zeroed destination.
-__device__ __forceinline__ int wave_isum_to_lane63(int v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-  return v;
-}
 
 // IC_Angle by v_dot4_u32_u8 over the staged 31-row patch: item t = (row
 // t / 9, dword t % 9) of the patch rows; for the patch's alignment offset o =
@@ -1353,9 +1369,9 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
       B = __builtin_amdgcn_udot4(val, w.y, B, false);
       S = __builtin_amdgcn_udot4(val, w.z, S, false);
     }
-    const int a = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)A), 63);
-    const int b = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)B), 63);
-    const int s = __builtin_amdgcn_readlane(wave_isum_to_lane63((int)S), 63);
+    const int a = __builtin_amdgcn_readlane(wave_iscan((int)A), 63);
+    const int b = __builtin_amdgcn_readlane(wave_iscan((int)B), 63);
+    const int s = __builtin_amdgcn_readlane(wave_iscan((int)S), 63);
     m10 = a - 15 * s;
     m01 = b - 15 * s;
   }
