@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "pose_math_dev.h"
 
@@ -88,24 +89,28 @@ __device__ __forceinline__ void pose_map(const Se3R& T, const double X[3], doubl
   for (int i = 0; i < 3; ++i) p[i] = T.R[3 * i] * X[0] + T.R[3 * i + 1] * X[1] + T.R[3 * i + 2] * X[2] + T.t[i];
 }
 
-__device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3R& T, const CamDev& c,
-                                           double e[3], bool& stereo) {
-  const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
-  double p[3];
-  pose_map(T, X, p);
-  stereo = o.ur >= 0.f;
+__device__ __forceinline__ void edge_error_p(const PoseObsDev& o, const double p[3], const RcpF64& rz,
+                                             const CamDev& c, double e[3], bool stereo) {
   if (!stereo) {  // EdgeSE3ProjectXYZOnlyPose + Pinhole::Project
-    e[0] = (double)o.u - (c.fx * p[0] / p[2] + c.cx);
-    e[1] = (double)o.v - (c.fy * p[1] / p[2] + c.cy);
+    e[0] = (double)o.u - (div_f64(c.fx * p[0], rz) + c.cx);
+    e[1] = (double)o.v - (div_f64(c.fy * p[1], rz) + c.cy);
     e[2] = 0;
   } else {  // EdgeStereoSE3ProjectXYZOnlyPose::cam_project (float invz)
-    const float invz = (float)(1.0 / p[2]);
+    const float invz = (float)div_f64(1.0, rz);
     const double u = p[0] * (double)invz * c.fx + c.cx;
     const double v = p[1] * (double)invz * c.fy + c.cy;
     e[0] = (double)o.u - u;
     e[1] = (double)o.v - v;
     e[2] = (double)o.ur - (u - c.bf * (double)invz);
   }
+}
+__device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3R& T, const CamDev& c,
+                                           double e[3], bool& stereo) {
+  const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
+  double p[3];
+  pose_map(T, X, p);
+  stereo = o.ur >= 0.f;
+  edge_error_p(o, p, rcp_f64(p[2]), c, e, stereo);
 }
 
 __device__ __forceinline__ double edge_chi2(const double e[3], double info, bool stereo) {
@@ -114,15 +119,13 @@ __device__ __forceinline__ double edge_chi2(const double e[3], double info, bool
   return s;
 }
 
-__device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3R& T, const CamDev& c,
-                                              bool stereo, double J[3][6]) {
-  const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
-  double p[3];
-  pose_map(T, X, p);
+__device__ __forceinline__ void edge_jacobian_p(const double p[3], const RcpF64& rz, const CamDev& c,
+                                                bool stereo, double J[3][6]) {
   const double x = p[0], y = p[1], z = p[2];
   if (!stereo) {
-    const double pj00 = -(c.fx / z), pj02 = -(-c.fx * x / (z * z));
-    const double pj11 = -(c.fy / z), pj12 = -(-c.fy * y / (z * z));
+    const RcpF64 rzz = rcp_f64(z * z);
+    const double pj00 = -div_f64(c.fx, rz), pj02 = -div_f64(-c.fx * x, rzz);
+    const double pj11 = -div_f64(c.fy, rz), pj12 = -div_f64(-c.fy * y, rzz);
     const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -131,7 +134,7 @@ __device__ __forceinline__ void edge_jacobian(const PoseObsDev& o, const Se3R& T
       J[2][k] = 0;
     }
   } else {
-    const double invz = 1.0 / z, invz2 = invz * invz;
+    const double invz = div_f64(1.0, rz), invz2 = invz * invz;
     J[0][0] = x * y * invz2 * c.fx;
     J[0][1] = -(1 + (x * x * invz2)) * c.fx;
     J[0][2] = y * invz * c.fx;
@@ -320,13 +323,20 @@ constexpr int kPoseLdsObs = 4096;  // observations staged in LDS (the rest re-re
 // One edge's contribution to a sweep at pose T: robust chi2 into acc[0] and
 // BlockSolver::buildSystem's H (lower triangle, 21) and b (6) into
 // acc[1..27].  Every sweep visits a thread's edges in the same order, so the
-// sums are reproducible.
+// sums are reproducible.  ST: the edge type when the caller knows it for the
+// whole wave (1 EdgeStereo, 0 EdgeMono: only that projection is compiled),
+// -1 to take it from the observation (both, selected per lane).
+template <int ST = -1>
 __device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3R& T, const CamDev& cam,
                                                 bool robust, double dmono, double dstereo,
                                                 bool build, double (&acc)[28]) {
+  const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
+  double p[3];
+  pose_map(T, X, p);
+  const RcpF64 rz = rcp_f64(p[2]);
   double e[3];
-  bool st;
-  edge_error(o, T, cam, e, st);
+  const bool st = ST < 0 ? o.ur >= 0.f : ST == 1;
+  edge_error_p(o, p, rz, cam, e, st);
   const double info = (double)o.inv_sigma2;
   const double c2 = edge_chi2(e, info, st);
   double w = 1.0;
@@ -339,7 +349,7 @@ __device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3R&
   }
   if (!build) return;
   double J[3][6];
-  edge_jacobian(o, T, cam, st, J);
+  edge_jacobian_p(p, rz, cam, st, J);
   const double wi = w * info;
   int hk = 1;
 #pragma unroll
@@ -403,10 +413,11 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   double* tred = reinterpret_cast<double*>(
       pose_lds + ((((size_t)lds_obs * sizeof(PoseObsDev) + ((lds_obs + 1) & ~1) + 2 * (size_t)lds_obs) + 15) &
                   ~(size_t)15));
+  int n_st;
   {
     int c = 0;
     for (int i = t; i < cap; i += NT) c += obs[i].ur >= 0.f ? 1 : 0;
-    const int n_st = block_sum_i<NW>(c, sh.ired);
+    n_st = block_sum_i<NW>(c, sh.ired);
     const int w = t >> 6;
     int base_s = 0, base_m = n_st;
     for (int i0 = 0; i0 < cap; i0 += NT) {
@@ -460,10 +471,59 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   // chains, ILP), the accumulation stays in edge order; the wave sums land in
   // dst[wave of the group] (added in wave order by the readers).
   constexpr int kU = 3;  // (ILP only: the sums are the same for any kU)
+  // Typed waves: when the stereo block [0, n_st) and the mono block
+  // [n_st, cap) fit in the group's 4 waves at kU x 64 edges a wave, wave gw
+  // takes one contiguous run of a single edge type (edges wbeg + lane + 64 u)
+  // and runs only that projection; otherwise (wtype < 0) every wave takes
+  // edges tg + 256 j and selects the projection per lane.  Wave-uniform.
+  int wtype = -1, wbeg = 0, wend = 0;
+  {
+    constexpr int per = kU * 64;
+    const int ws = (n_st + per - 1) / per, wm = (cap - n_st + per - 1) / per;
+    if (ws + wm <= kPoseWaves) {
+      const int gwu = __builtin_amdgcn_readfirstlane(gw);
+      if (gwu < ws) {
+        wtype = 1;
+        wbeg = gwu * per;
+        wend = min(wbeg + per, n_st);
+      } else if (gwu - ws < wm) {
+        wtype = 0;
+        wbeg = n_st + (gwu - ws) * per;
+        wend = min(wbeg + per, cap);
+      } else {
+        wtype = 2;  // no edges
+      }
+    }
+  }
+  auto chi_typed = [&](auto stc, const Se3R& X, double& acc0) {
+    constexpr int ST = decltype(stc)::value;
+    PoseObsDev o[kU];
+    bool live[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = wbeg + lane + 64 * u;
+      live[u] = i < wend && !lv[min(i, wend - 1)];
+      o[u] = ob[min(i, wend - 1)];
+    }
+    double part[kU][28];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      part[u][0] = 0;
+      edge_accumulate<ST>(o[u], X, cam, robust, dmono, dstereo, false, part[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (live[u]) acc0 += part[u][0];
+  };
   auto chi_sweep = [&](const Se3& Xq, double* dst) {
     const Se3R X = se3r(Xq);
     double acc[28];
     acc[0] = 0;
+    if (wtype == 1)
+      chi_typed(std::integral_constant<int, 1>{}, X, acc[0]);
+    else if (wtype == 0)
+      chi_typed(std::integral_constant<int, 0>{}, X, acc[0]);
+    else if (wtype < 0)
     for (int i0 = tg; i0 < cap; i0 += kU * kPoseThreads) {
       PoseObsDev o[kU];
       bool live[kU];
@@ -498,8 +558,16 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     for (int k = 0; k < 28; ++k) acc[k] = 0;
     // g2o adds each edge's block into H/b in edge order, the chi2 term first
     // as in computeActiveErrors
-    for (int i = t; i < cap; i += NT)
-      if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
+    if (G == 1 && wtype == 1) {
+      for (int i = wbeg + lane; i < wend; i += 64)
+        if (!lv[i]) edge_accumulate<1>(ob[i], X, cam, robust, dmono, dstereo, true, acc);
+    } else if (G == 1 && wtype == 0) {
+      for (int i = wbeg + lane; i < wend; i += 64)
+        if (!lv[i]) edge_accumulate<0>(ob[i], X, cam, robust, dmono, dstereo, true, acc);
+    } else if (G > 1 || wtype < 0) {
+      for (int i = t; i < cap; i += NT)
+        if (!lv[i]) edge_accumulate(ob[i], X, cam, robust, dmono, dstereo, true, acc);
+    }
     for (int i = cap + t; i < n; i += NT)
       if (!level[i]) edge_accumulate(obs[i], X, cam, robust, dmono, dstereo, true, acc);
     if constexpr (G == 1)
