@@ -44,6 +44,7 @@ extern __device__ unsigned long long g_in_stamps[64 * 16];
   } while (0)
 #define IMU_EDGE_MARK_INIT unsigned long long ie_prev_ = __builtin_amdgcn_s_memtime()
 #endif
+#include "f64_math_dev.h"
 #include "imu_math_dev.h"
 
 namespace orbgpu {
@@ -171,11 +172,12 @@ __device__ __forceinline__ void vis_error(const VisObs& o, const double* Rcw, co
   Xc[0] += tcw[0];
   Xc[1] += tcw[1];
   Xc[2] += tcw[2];
-  const double u = c.fx * Xc[0] / Xc[2] + c.cx;
-  const double v = c.fy * Xc[1] / Xc[2] + c.cy;
+  const RecipF64 rz = recip_f64(Xc[2]);  // (f64_math_dev.h: the IEEE quotients)
+  const double u = div_by(c.fx * Xc[0], rz) + c.cx;
+  const double v = div_by(c.fy * Xc[1], rz) + c.cy;
   e[0] = (double)o.u - u;
   e[1] = (double)o.v - v;
-  e[2] = o.ur >= 0.f ? (double)o.ur - (u - c.bf * (1 / Xc[2])) : 0.0;
+  e[2] = o.ur >= 0.f ? (double)o.ur - (u - c.bf * div_by(1.0, rz)) : 0.0;
 }
 
 __device__ __forceinline__ double vis_chi2(const double e[3], double info, bool stereo) {
@@ -192,14 +194,15 @@ __device__ __forceinline__ void vis_jacobian(const double Xc[3], const CalibD& c
   Xb[0] += c.tbc[0];
   Xb[1] += c.tbc[1];
   Xb[2] += c.tbc[2];
-  const double iz = 1.0 / Xc[2];
-  double pj[3][3] = {{c.fx * iz, 0, -c.fx * Xc[0] / (Xc[2] * Xc[2])},
-                     {0, c.fy * iz, -c.fy * Xc[1] / (Xc[2] * Xc[2])},
+  const RecipF64 rz = recip_f64(Xc[2]), rzz = recip_f64(Xc[2] * Xc[2]);
+  const double iz = div_by(1.0, rz);
+  double pj[3][3] = {{c.fx * iz, 0, div_by(-c.fx * Xc[0], rzz)},
+                     {0, c.fy * iz, div_by(-c.fy * Xc[1], rzz)},
                      {0, 0, 0}};
   if (stereo) {
     pj[2][0] = pj[0][0];
     pj[2][1] = pj[0][1];
-    pj[2][2] = pj[0][2] + c.bf * (1.0 / (Xc[2] * Xc[2]));
+    pj[2][2] = pj[0][2] + c.bf * div_by(1.0, rzz);
   }
   const double x = Xb[0], y = Xb[1], z = Xb[2];
   const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
@@ -215,7 +218,8 @@ __device__ __forceinline__ void vis_jacobian(const double Xc[3], const CalibD& c
 
 // Huber (robust_kernel_impl.cpp): rho'(e2)
 __device__ __forceinline__ double huber_w(double e2, double delta) {
-  return e2 <= delta * delta ? 1.0 : delta / sqrt(e2);
+  // delta >= 1: the sqrt / division branch sees e2 > 1 only
+  return e2 <= delta * delta ? 1.0 : div_by(delta, recip_f64(sqrt_f64(e2)));
 }
 
 // One visual edge's weighted 6x6 (lower, 21) + gradient (6) into acc[0..26].

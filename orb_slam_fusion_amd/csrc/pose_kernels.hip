@@ -89,14 +89,14 @@ __device__ __forceinline__ void pose_map(const Se3R& T, const double X[3], doubl
   for (int i = 0; i < 3; ++i) p[i] = T.R[3 * i] * X[0] + T.R[3 * i + 1] * X[1] + T.R[3 * i + 2] * X[2] + T.t[i];
 }
 
-__device__ __forceinline__ void edge_error_p(const PoseObsDev& o, const double p[3], const RcpF64& rz,
+__device__ __forceinline__ void edge_error_p(const PoseObsDev& o, const double p[3], const RecipF64& rz,
                                              const CamDev& c, double e[3], bool stereo) {
   if (!stereo) {  // EdgeSE3ProjectXYZOnlyPose + Pinhole::Project
-    e[0] = (double)o.u - (div_f64(c.fx * p[0], rz) + c.cx);
-    e[1] = (double)o.v - (div_f64(c.fy * p[1], rz) + c.cy);
+    e[0] = (double)o.u - (div_by(c.fx * p[0], rz) + c.cx);
+    e[1] = (double)o.v - (div_by(c.fy * p[1], rz) + c.cy);
     e[2] = 0;
   } else {  // EdgeStereoSE3ProjectXYZOnlyPose::cam_project (float invz)
-    const float invz = (float)div_f64(1.0, rz);
+    const float invz = (float)div_by(1.0, rz);
     const double u = p[0] * (double)invz * c.fx + c.cx;
     const double v = p[1] * (double)invz * c.fy + c.cy;
     e[0] = (double)o.u - u;
@@ -110,7 +110,7 @@ __device__ __forceinline__ void edge_error(const PoseObsDev& o, const Se3R& T, c
   double p[3];
   pose_map(T, X, p);
   stereo = o.ur >= 0.f;
-  edge_error_p(o, p, rcp_f64(p[2]), c, e, stereo);
+  edge_error_p(o, p, recip_f64(p[2]), c, e, stereo);
 }
 
 __device__ __forceinline__ double edge_chi2(const double e[3], double info, bool stereo) {
@@ -119,13 +119,13 @@ __device__ __forceinline__ double edge_chi2(const double e[3], double info, bool
   return s;
 }
 
-__device__ __forceinline__ void edge_jacobian_p(const double p[3], const RcpF64& rz, const CamDev& c,
+__device__ __forceinline__ void edge_jacobian_p(const double p[3], const RecipF64& rz, const CamDev& c,
                                                 bool stereo, double J[3][6]) {
   const double x = p[0], y = p[1], z = p[2];
   if (!stereo) {
-    const RcpF64 rzz = rcp_f64(z * z);
-    const double pj00 = -div_f64(c.fx, rz), pj02 = -div_f64(-c.fx * x, rzz);
-    const double pj11 = -div_f64(c.fy, rz), pj12 = -div_f64(-c.fy * y, rzz);
+    const RecipF64 rzz = recip_f64(z * z);
+    const double pj00 = -div_by(c.fx, rz), pj02 = -div_by(-c.fx * x, rzz);
+    const double pj11 = -div_by(c.fy, rz), pj12 = -div_by(-c.fy * y, rzz);
     const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -134,7 +134,7 @@ __device__ __forceinline__ void edge_jacobian_p(const double p[3], const RcpF64&
       J[2][k] = 0;
     }
   } else {
-    const double invz = div_f64(1.0, rz), invz2 = invz * invz;
+    const double invz = div_by(1.0, rz), invz2 = invz * invz;
     J[0][0] = x * y * invz2 * c.fx;
     J[0][1] = -(1 + (x * x * invz2)) * c.fx;
     J[0][2] = y * invz * c.fx;
@@ -333,7 +333,7 @@ __device__ __forceinline__ void edge_accumulate(const PoseObsDev& o, const Se3R&
   const double X[3] = {o.Xw[0], o.Xw[1], o.Xw[2]};
   double p[3];
   pose_map(T, X, p);
-  const RcpF64 rz = rcp_f64(p[2]);
+  const RecipF64 rz = recip_f64(p[2]);
   double e[3];
   const bool st = ST < 0 ? o.ur >= 0.f : ST == 1;
   edge_error_p(o, p, rz, cam, e, st);

@@ -6,6 +6,7 @@
 //                                   used by LinearSolverDense (linear_solver_dense.h:56-104)
 //   RobustKernelHuber::robustify    core/robust_kernel_impl.cpp:72-85
 #pragma once
+#include "f64_math_dev.h"
 #include <hip/hip_runtime.h>
 
 namespace orbgpu {
@@ -434,40 +435,6 @@ __device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, dou
   return !(flags & 1);
 }
 
-// f64 division as the compiler lowers it (v_rcp_f64, two Newton steps, one
-// residual correction), minus its v_div_scale / v_div_fmas scaling and
-// v_div_fixup special cases: the same value for the normal, finite operands
-// of a projection, and the reciprocal is computed once for every division
-// by the same denominator (an edge divides by z up to three times).
-struct RcpF64 {
-  double d, r;
-};
-__device__ __forceinline__ RcpF64 rcp_f64(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(r, fma(-d, r, 1.0), r);
-  r = fma(r, fma(-d, r, 1.0), r);
-  return RcpF64{d, r};
-}
-__device__ __forceinline__ double div_f64(double n, const RcpF64& q) {
-  const double m = n * q.r;
-  return fma(fma(-q.d, m, n), q.r, m);
-}
-
-// f64 sqrt as the compiler lowers it (v_rsq_f64, then the Goldschmidt /
-// Newton refinement), minus its v_ldexp range scaling for x < 2^-767 and the
-// zero / infinity class check: the same value for the normal, finite x here.
-__device__ __forceinline__ double sqrt_f64(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  double s = x * y, h = y * 0.5;
-  const double r = fma(-h, s, 0.5);
-  s = fma(s, r, s);
-  const double d0 = fma(-s, s, x);
-  h = fma(h, r, h);
-  s = fma(d0, h, s);
-  const double d1 = fma(-s, s, x);
-  return fma(d1, h, s);
-}
-
 // g2o RobustKernelHuber::robustify; e2 > delta^2 >= 1 in the sqrt branch
 __device__ __forceinline__ void huber_rho(double e2, double delta, double& rho0, double& rho1) {
   const double dsqr = delta * delta;
@@ -477,7 +444,7 @@ __device__ __forceinline__ void huber_rho(double e2, double delta, double& rho0,
   } else {
     const double s = sqrt_f64(e2);
     rho0 = 2 * s * delta - dsqr;
-    rho1 = div_f64(delta, rcp_f64(s));
+    rho1 = div_by(delta, recip_f64(s));
   }
 }
 
