@@ -84,8 +84,9 @@ __device__ __forceinline__ bool lba_error(const LbaEdgeDev& e, const Se3& T, con
   double p[3];
   se3_map(T, X, p);
   if (e.ur < 0.f) {
-    err[0] = (double)e.u - (c.fx * p[0] / p[2] + c.cx);
-    err[1] = (double)e.v - (c.fy * p[1] / p[2] + c.cy);
+    const RecipF64 rz = recip_f64(p[2]);  // (f64_math_dev.h: the IEEE quotients)
+    err[0] = (double)e.u - (div_by(c.fx * p[0], rz) + c.cx);
+    err[1] = (double)e.v - (div_by(c.fy * p[1], rz) + c.cy);
     err[2] = 0;
   } else {
     const float invz = 1.0f / (float)p[2];
@@ -127,9 +128,11 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
       R[r][2] = c2[r];
     }
   }
+  // one reciprocal per denominator (z, z^2) for the IEEE quotients below
+  const RecipF64 rz = recip_f64(z), rzz = recip_f64(z * z);
   if (e.ur < 0.f) {  // optimizable_types.cc:134-155
-    const double pj[2][3] = {{-(c.fx / z), 0.0, -(-c.fx * x / (z * z))},
-                             {0.0, -(c.fy / z), -(-c.fy * y / (z * z))}};
+    const double pj[2][3] = {{-div_by(c.fx, rz), 0.0, -div_by(-c.fx * x, rzz)},
+                             {0.0, -div_by(c.fy, rz), -div_by(-c.fy * y, rzz)}};
     const double S[3][6] = {{0, z, -y, 1, 0, 0}, {-z, 0, x, 0, 1, 0}, {y, -x, 0, 0, 0, 1}};
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -143,31 +146,31 @@ __device__ __forceinline__ void lba_jacobians(const LbaEdgeDev& e, const Se3& T,
 #pragma unroll
     for (int k = 0; k < 6; ++k) Jp[2][k] = 0;
   } else {  // types_six_dof_expmap.cpp:211-257
-    const double z_2 = z * z, fx = c.fx, fy = c.fy, bf = c.bf;
+    const double fx = c.fx, fy = c.fy, bf = c.bf;  // q / z and q / z_2 by div_by
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      Jl[0][k] = -fx * R[0][k] / z + fx * x * R[2][k] / z_2;
-      Jl[1][k] = -fy * R[1][k] / z + fy * y * R[2][k] / z_2;
-      Jl[2][k] = Jl[0][k] - bf * R[2][k] / z_2;
+      Jl[0][k] = div_by(-fx * R[0][k], rz) + div_by(fx * x * R[2][k], rzz);
+      Jl[1][k] = div_by(-fy * R[1][k], rz) + div_by(fy * y * R[2][k], rzz);
+      Jl[2][k] = Jl[0][k] - div_by(bf * R[2][k], rzz);
     }
-    Jp[0][0] = x * y / z_2 * fx;
-    Jp[0][1] = -(1 + (x * x / z_2)) * fx;
-    Jp[0][2] = y / z * fx;
-    Jp[0][3] = -1. / z * fx;
+    Jp[0][0] = div_by(x * y, rzz) * fx;
+    Jp[0][1] = -(1 + div_by(x * x, rzz)) * fx;
+    Jp[0][2] = div_by(y, rz) * fx;
+    Jp[0][3] = div_by(-1., rz) * fx;
     Jp[0][4] = 0;
-    Jp[0][5] = x / z_2 * fx;
-    Jp[1][0] = (1 + y * y / z_2) * fy;
-    Jp[1][1] = -x * y / z_2 * fy;
-    Jp[1][2] = -x / z * fy;
+    Jp[0][5] = div_by(x, rzz) * fx;
+    Jp[1][0] = (1 + div_by(y * y, rzz)) * fy;
+    Jp[1][1] = div_by(-x * y, rzz) * fy;
+    Jp[1][2] = div_by(-x, rz) * fy;
     Jp[1][3] = 0;
-    Jp[1][4] = -1. / z * fy;
-    Jp[1][5] = y / z_2 * fy;
-    Jp[2][0] = Jp[0][0] - bf * y / z_2;
-    Jp[2][1] = Jp[0][1] + bf * x / z_2;
+    Jp[1][4] = div_by(-1., rz) * fy;
+    Jp[1][5] = div_by(y, rzz) * fy;
+    Jp[2][0] = Jp[0][0] - div_by(bf * y, rzz);
+    Jp[2][1] = Jp[0][1] + div_by(bf * x, rzz);
     Jp[2][2] = Jp[0][2];
     Jp[2][3] = Jp[0][3];
     Jp[2][4] = 0;
-    Jp[2][5] = Jp[0][5] - bf / z_2;
+    Jp[2][5] = Jp[0][5] - div_by(bf, rzz);
   }
 }
 
@@ -214,11 +217,12 @@ __device__ __forceinline__ bool vis_error(const LbaArgs& a, const LbaEdgeDev& e,
   } else {
     double Xc[3];
     imu_cam_point(ks, X, Xc);
-    const double u = a.cam.fx * Xc[0] / Xc[2] + a.cam.cx;
-    const double v = a.cam.fy * Xc[1] / Xc[2] + a.cam.cy;
+    const RecipF64 rz = recip_f64(Xc[2]);
+    const double u = div_by(a.cam.fx * Xc[0], rz) + a.cam.cx;
+    const double v = div_by(a.cam.fy * Xc[1], rz) + a.cam.cy;
     err[0] = (double)e.u - u;
     err[1] = (double)e.v - v;
-    err[2] = e.ur >= 0.f ? (double)e.ur - (u - a.cam.bf * (1 / Xc[2])) : 0.0;
+    err[2] = e.ur >= 0.f ? (double)e.ur - (u - a.cam.bf * div_by(1.0, rz)) : 0.0;
     return Xc[2] > 0.0;
   }
 }
@@ -236,13 +240,14 @@ __device__ __forceinline__ void vis_jacobians(const LbaArgs& a, const LbaEdgeDev
     imu_cam_point(ks, X, Xc);
     const double* R = ks + 12;
     const bool st = e.ur >= 0.f;
-    double pj[3][3] = {{c.fx / Xc[2], 0, -c.fx * Xc[0] / (Xc[2] * Xc[2])},
-                       {0, c.fy / Xc[2], -c.fy * Xc[1] / (Xc[2] * Xc[2])},
+    const RecipF64 rz = recip_f64(Xc[2]), rzz = recip_f64(Xc[2] * Xc[2]);
+    double pj[3][3] = {{div_by(c.fx, rz), 0, div_by(-c.fx * Xc[0], rzz)},
+                       {0, div_by(c.fy, rz), div_by(-c.fy * Xc[1], rzz)},
                        {0, 0, 0}};
     if (st) {
       pj[2][0] = pj[0][0];
       pj[2][1] = pj[0][1];
-      pj[2][2] = pj[0][2] + c.bf * (1.0 / (Xc[2] * Xc[2]));
+      pj[2][2] = pj[0][2] + c.bf * div_by(1.0, rzz);
     }
     double Xb[3];
 #pragma unroll
