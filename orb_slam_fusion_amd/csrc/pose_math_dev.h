@@ -42,11 +42,12 @@ __device__ __forceinline__ void se3_normalize(Se3& T) {
     T.qy = -T.qy;
     T.qz = -T.qz;
   }
-  const double n = sqrt(T.qx * T.qx + T.qy * T.qy + T.qz * T.qz + T.qw * T.qw);
-  T.qw /= n;
-  T.qx /= n;
-  T.qy /= n;
-  T.qz /= n;
+  // |q| ~ 1: the IEEE sqrt and quotients by f64_math_dev.h (one reciprocal)
+  const RecipF64 n = recip_f64(sqrt_f64(T.qx * T.qx + T.qy * T.qy + T.qz * T.qz + T.qw * T.qw));
+  T.qw = div_by(T.qw, n);
+  T.qx = div_by(T.qx, n);
+  T.qy = div_by(T.qy, n);
+  T.qz = div_by(T.qz, n);
 }
 
 // a * b
@@ -137,30 +138,30 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   const int qc = t > 0 ? 0 : R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0]) ? 1 : R[1][1] > R[0][0] ? 2 : 3;
   const int qcase = kUniform ? __builtin_amdgcn_readfirstlane(qc) : qc;
   if (qcase == 0) {
-    t = sqrt(t + 1.0);
+    t = sqrt_f64(t + 1.0);  // the chosen pivot's argument is >= 1
     e.qw = 0.5 * t;
-    t = 0.5 / t;
+    t = div_by(0.5, recip_f64(t));
     e.qx = (R[2][1] - R[1][2]) * t;
     e.qy = (R[0][2] - R[2][0]) * t;
     e.qz = (R[1][0] - R[0][1]) * t;
   } else if (qcase == 1) {  // i = 2, j = 0, k = 1
-    t = sqrt(R[2][2] - R[0][0] - R[1][1] + 1.0);
+    t = sqrt_f64(R[2][2] - R[0][0] - R[1][1] + 1.0);
     e.qz = 0.5 * t;
-    t = 0.5 / t;
+    t = div_by(0.5, recip_f64(t));
     e.qw = (R[1][0] - R[0][1]) * t;
     e.qx = (R[0][2] + R[2][0]) * t;
     e.qy = (R[1][2] + R[2][1]) * t;
   } else if (qcase == 2) {  // i = 1, j = 2, k = 0
-    t = sqrt(R[1][1] - R[2][2] - R[0][0] + 1.0);
+    t = sqrt_f64(R[1][1] - R[2][2] - R[0][0] + 1.0);
     e.qy = 0.5 * t;
-    t = 0.5 / t;
+    t = div_by(0.5, recip_f64(t));
     e.qw = (R[0][2] - R[2][0]) * t;
     e.qz = (R[2][1] + R[1][2]) * t;
     e.qx = (R[0][1] + R[1][0]) * t;
   } else {  // i = 0, j = 1, k = 2
-    t = sqrt(R[0][0] - R[1][1] - R[2][2] + 1.0);
+    t = sqrt_f64(R[0][0] - R[1][1] - R[2][2] + 1.0);
     e.qx = 0.5 * t;
-    t = 0.5 / t;
+    t = div_by(0.5, recip_f64(t));
     e.qw = (R[2][1] - R[1][2]) * t;
     e.qy = (R[1][0] + R[0][1]) * t;
     e.qz = (R[2][0] + R[0][2]) * t;
