@@ -6,6 +6,7 @@
 // evaluate the same rotation.  Include after `#pragma clang fp contract(fast)`
 // (fp64 solver TUs, parity by tolerance).
 #pragma once
+#include "f64_math_dev.h"
 #include <hip/hip_runtime.h>
 
 #include "../../include/orbgpu.h"
@@ -68,7 +69,8 @@ __device__ __forceinline__ void polar3(double* X) {
     C[6] = X[1] * X[5] - X[2] * X[4];
     C[7] = X[2] * X[3] - X[0] * X[5];
     C[8] = X[0] * X[4] - X[1] * X[3];
-    const double rdet = 1.0 / (X[0] * C[0] + X[1] * C[1] + X[2] * C[2]);
+    // det ~ 1: the IEEE quotient by f64_math_dev.h (no range steps)
+    const double rdet = div_by(1.0, recip_f64(X[0] * C[0] + X[1] * C[1] + X[2] * C[2]));
 #pragma unroll
     for (int i = 0; i < 9; ++i) X[i] = 0.5 * (X[i] + C[i] * rdet);
   }
@@ -122,7 +124,7 @@ __device__ __forceinline__ void log_so3(const double* R, double* w) {
   const double th = acos(ct);
   const double s = sin(th);
   if (__builtin_amdgcn_readfirstlane(fabs(s) < 1e-5 ? 1 : 0)) return;
-  const double f = th / s;
+  const double f = div_by(th, recip_f64(s));  // |s| >= 1e-5 here
   w[0] *= f;
   w[1] *= f;
   w[2] *= f;
