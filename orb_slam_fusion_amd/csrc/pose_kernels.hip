@@ -589,6 +589,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     double lambda = 0, ni = 2;
     int nbad = 0;
     for (int iter = 0; iter < 10; ++iter) {
+      asm volatile("" : "+s"(wtype), "+s"(wbeg), "+s"(wend));
       const double ini = cur;
       if (iter == 0) {  // computeLambdaInit: tau * max diag
         double mx = 0;
@@ -610,6 +611,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
         // body's thread-predicate compares are not hoisted into long-lived
         // SGPR lane masks
         asm volatile("" : "+v"(t), "+v"(tg), "+v"(lane), "+v"(gw));
+        asm volatile("" : "+s"(wtype), "+s"(wbeg), "+s"(wend));
         // this group's trial (q + grp): the lambda the sequential loop would
         // reach after grp more rejections
         double lg = lambda, ng = ni;
