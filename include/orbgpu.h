@@ -22,9 +22,7 @@ typedef int orbgpu_status;
 #define ORBGPU_ERR_EMPTY (-2)    /* empty image: reference operator() returns -1 */
 #define ORBGPU_ERR_CAPACITY (-3) /* caller buffer or internal bound too small  */
 #define ORBGPU_ERR_DEVICE (-4)   /* HIP runtime error                          */
-#define ORBGPU_ERR_NOMEM (-5)
-#define ORBGPU_ERR_UNSUPPORTED (-6) /* valid for the reference, outside what the GPU path
-                                       implements: the caller runs the CPU code instead */
+#define ORBGPU_ERR_NOMEM (-5)     /* device or pinned host memory exhausted   */
 
 /* OrbExtractor(int num_feats, float scale_factor, int num_levs,
  *              int ini_th_fast, int min_th_fast)
@@ -255,13 +253,24 @@ void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c);
  * (sum)), and the same number of trials, so the collectives stay matched. */
 orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered);
 
-/* Bounds of the device solver: the reduced camera system of 6 rows per free
- * key frame is factorised by one workgroup, packed in LDS up to 160 rows and
- * in HBM beyond, with D and the right-hand side in LDS (16 bytes per row of
- * the 16-padded system, at most 160 KB).  A window with more free key frames
- * returns ORBGPU_ERR_CAPACITY before any device work (the C++ drop-in then
- * runs the reference's CPU LocalBundleAdjustment). */
-#define ORBGPU_LBA_MAX_FREE_KF 1706 /* 6 * 1706 <= 10240 reduced rows */
+/* The reduced-camera-system path (default AUTO: by size, see below).  LDS:
+ * packed tiles in one workgroup's LDS; BLOCK: one workgroup, the matrix in
+ * HBM; GRID: tile steps over the whole device.  A forced path a window does
+ * not fit returns ORBGPU_ERR_CAPACITY from the optimise call.  BLOCK and GRID
+ * perform the same tile operations in the same order (identical results). */
+#define ORBGPU_LBA_SOLVER_AUTO (-1)
+#define ORBGPU_LBA_SOLVER_LDS 0
+#define ORBGPU_LBA_SOLVER_BLOCK 1
+#define ORBGPU_LBA_SOLVER_GRID 2
+orbgpu_status orbgpu_lba_ctx_set_solver(orbgpu_lba_ctx* c, int solver);
+
+/* Window size: the reduced camera system (6 rows per free key frame) is
+ * factorised packed in LDS by one workgroup up to 160 rows, from HBM by one
+ * workgroup below 224 rows, and by tile steps spread over the whole device
+ * beyond (every factor in HBM): any
+ * window the reference accepts runs on the device; only exhausted device
+ * memory (ORBGPU_ERR_NOMEM, about 16 n^2 bytes for n reduced rows) or more
+ * than INT_MAX / 2 rows (ORBGPU_ERR_CAPACITY) is refused. */
 
 /* One window from host buffers.  Keyframe k is fixed iff fixed[k] (the map's
  * initial keyframe, :1161, and every fixed camera, :1169-1183).  Points
@@ -730,14 +739,13 @@ typedef struct orbgpu_lia_imu_edge {
  * stats (optional, 7 doubles): err = the robust chi2 before optimize()
  * (:2790-2791), err_end = the robust chi2 of the last computed errors
  * (:2793), LM iterations, trials, final lambda, outliers, accepted chi2. */
-/* Bounds of orbgpu_lia_optimize: 15 reduced rows per free key frame
- * (ORBGPU_LIA_MAX_FREE_KF, the solver bound above) and at most
- * ORBGPU_LIA_MAX_IMU_LINKS inertial links -> ORBGPU_ERR_CAPACITY; a free key
- * frame without IMU vertices (imu[k] == 0: the reference's VertexPose-only
- * key frame, optimizer.cc:2466-2484) -> ORBGPU_ERR_UNSUPPORTED.  Both are
- * reported before any device work; the drop-in runs the CPU optimiser. */
-#define ORBGPU_LIA_MAX_FREE_KF 682
-#define ORBGPU_LIA_MAX_IMU_LINKS 64
+/* A free key frame owns 15 reduced rows (VP VV VG VA); one without IMU data
+ * (imu[k] == 0: the reference's VertexPose-only key frame,
+ * optimizer.cc:2466-2484) has only its pose vertex, and no link may touch it
+ * (:2503: an EdgeInertial needs bImu on both key frames; such a link is
+ * ORBGPU_ERR_INVALID).  Its 9 inertial rows stay structurally zero with a
+ * zero right-hand side, so the step leaves v / bg / ba as given.  Window size
+ * and link count are bounded only by device memory (the solver paths above). */
 orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* c, const orbgpu_imu_calib* calib, int n_kf,
                                   const orbgpu_imu_state* kfs, const uint8_t* fixed,
                                   const uint8_t* imu, int n_pts, const float* pts_in,

@@ -531,7 +531,8 @@ def lia_system(pb):
     frames' 15-blocks (VP VV VG VA) first, then 3 rows per point; Huber
     weights from the initial errors."""
     n_kf, n_p, ne, ni = len(pb.kfs), len(pb.pts_init), len(pb.edges), len(pb.imu_edges)
-    n = 15 * int((pb.fixed == 0).sum()) + 3 * n_p
+    free = pb.fixed == 0
+    n = int(np.where(pb.imu[free] != 0, 15, 6).sum()) + 3 * n_p
     H = np.zeros((n, n))
     b = np.zeros(n)
     r = lib().orc_lia_system(_p(pb.calib), n_kf, _p(pb.kfs), _p(pb.fixed), _p(pb.imu), n_p,

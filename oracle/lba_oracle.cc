@@ -156,29 +156,41 @@ bool inv3(const double A[3][3], double Ai[3][3]) {
 // SimplicialLDLT (linear_solver_eigen.h:101-104) reports NumericalIssue only
 // for D(k,k) == 0 (SimplicialCholesky_impl.h, the DoLDLT branch); a negative
 // pivot factorises and the LM step is judged by rho.
+// Row i's entries left of its first structural non-zero (fst[i]) stay zero
+// through the factorisation, so every sum runs from max(fst[i], fst[k]): the
+// terms left out are exact zeros, and the result is the full loop's (a large
+// banded window factorises in O(n b^2)).
 bool ldlt_dense(std::vector<double>& S, int n, const double* b, double* x) {
   std::vector<double> d(n);
+  std::vector<int> fst(n);
+  for (int i = 0; i < n; ++i) {
+    int j = 0;
+    while (j < i && S[(size_t)i * n + j] == 0.0) ++j;
+    fst[i] = j;
+  }
   bool ok = true;
   for (int k = 0; k < n; ++k) {
     double dk = S[(size_t)k * n + k];
-    for (int j = 0; j < k; ++j) dk -= S[(size_t)k * n + j] * S[(size_t)k * n + j] * d[j];
+    for (int j = fst[k]; j < k; ++j) dk -= S[(size_t)k * n + j] * S[(size_t)k * n + j] * d[j];
     d[k] = dk;
     if (dk == 0) ok = false;
     for (int i = k + 1; i < n; ++i) {
+      if (fst[i] > k) continue;  // S(i, k) = 0 and stays 0
       double s = S[(size_t)i * n + k];
-      for (int j = 0; j < k; ++j) s -= S[(size_t)i * n + j] * S[(size_t)k * n + j] * d[j];
+      for (int j = std::max(fst[i], fst[k]); j < k; ++j) s -= S[(size_t)i * n + j] * S[(size_t)k * n + j] * d[j];
       S[(size_t)i * n + k] = dk != 0 ? s / dk : 0.0;
     }
   }
   for (int i = 0; i < n; ++i) {
     double s = b[i];
-    for (int j = 0; j < i; ++j) s -= S[(size_t)i * n + j] * x[j];
+    for (int j = fst[i]; j < i; ++j) s -= S[(size_t)i * n + j] * x[j];
     x[i] = s;
   }
   for (int i = 0; i < n; ++i) x[i] = d[i] != 0 ? x[i] / d[i] : 0.0;
   for (int i = n - 1; i >= 0; --i) {
     double s = x[i];
-    for (int j = i + 1; j < n; ++j) s -= S[(size_t)j * n + i] * x[j];
+    for (int j = i + 1; j < n; ++j)
+      if (fst[j] <= i) s -= S[(size_t)j * n + i] * x[j];
     x[i] = s;
   }
   return ok;

@@ -21,8 +21,13 @@
 //             mono edges also on !isDepthPositive) on the errors of the last
 //             computeActiveErrors, and err / err_end of :2790-2793.
 //
-// Layout of the reduced system: free key frame f owns rows [15f, 15f + 15),
-// VP(6) VV(3) VG(3) VA(3).  Parity with the GPU path is by tolerance
+// Layout of the reduced system: the free key frames in window order, each
+// owning its vertices' rows -- VP(6) VV(3) VG(3) VA(3) for a key frame with
+// IMU data, VP(6) alone for one without (`!pKFi->bImu`: optimizer.cc:
+// 2466-2484 adds only the VertexPose; no inertial edge reaches it, :2503).
+// The factorisation is the dense natural-order LDLT restricted to the
+// envelope of S (ldlt_dense): the same operations on the same values, the
+// products with structural zeros left out.  Parity with the GPU path is by tolerance
 // (states) and exact on outlier flags away from the thresholds.
 #include <algorithm>
 #include <cfloat>
@@ -42,7 +47,8 @@ using namespace oracle::inertial;
 
 namespace {
 
-constexpr int kDim = 15;
+constexpr int kDimImu = 15;  // VP VV VG VA
+constexpr int kDimPose = 6;  // VP
 
 struct VisEdge {  // == orbgpu_lba_edge
   int32_t point, kf;
@@ -130,29 +136,40 @@ bool inv3(const double A[3][3], double Ai[3][3]) {  // Eigen compute_inverse_siz
 
 // Dense LDLT (natural order) of S, solve S x = b; false on a zero pivot
 // (SimplicialLDLT's only NumericalIssue, linear_solver_eigen.h:101-104).
+// Row i's entries left of its first structural non-zero (fst[i]) stay zero
+// through the factorisation, so every sum runs from max(fst[i], fst[k]):
+// the terms left out are exact zeros, and the result is the full loop's.
 bool ldlt_dense(std::vector<double>& S, int n, const double* b, double* x) {
   std::vector<double> d(n);
+  std::vector<int> fst(n);
+  for (int i = 0; i < n; ++i) {
+    int j = 0;
+    while (j < i && S[(size_t)i * n + j] == 0.0) ++j;
+    fst[i] = j;
+  }
   bool ok = true;
   for (int k = 0; k < n; ++k) {
     double dk = S[(size_t)k * n + k];
-    for (int j = 0; j < k; ++j) dk -= S[(size_t)k * n + j] * S[(size_t)k * n + j] * d[j];
+    for (int j = fst[k]; j < k; ++j) dk -= S[(size_t)k * n + j] * S[(size_t)k * n + j] * d[j];
     d[k] = dk;
     if (dk == 0) ok = false;
     for (int i = k + 1; i < n; ++i) {
+      if (fst[i] > k) continue;  // S(i, k) = 0 and stays 0
       double s = S[(size_t)i * n + k];
-      for (int j = 0; j < k; ++j) s -= S[(size_t)i * n + j] * S[(size_t)k * n + j] * d[j];
+      for (int j = std::max(fst[i], fst[k]); j < k; ++j) s -= S[(size_t)i * n + j] * S[(size_t)k * n + j] * d[j];
       S[(size_t)i * n + k] = dk != 0 ? s / dk : 0.0;
     }
   }
   for (int i = 0; i < n; ++i) {
     double s = b[i];
-    for (int j = 0; j < i; ++j) s -= S[(size_t)i * n + j] * x[j];
+    for (int j = fst[i]; j < i; ++j) s -= S[(size_t)i * n + j] * x[j];
     x[i] = s;
   }
   for (int i = 0; i < n; ++i) x[i] = d[i] != 0 ? x[i] / d[i] : 0.0;
   for (int i = n - 1; i >= 0; --i) {
     double s = x[i];
-    for (int j = i + 1; j < n; ++j) s -= S[(size_t)j * n + i] * x[j];
+    for (int j = i + 1; j < n; ++j)
+      if (fst[j] <= i) s -= S[(size_t)j * n + i] * x[j];
     x[i] = s;
   }
   return ok;
@@ -183,8 +200,9 @@ double imu_chi2(const ImuEdge& E, const State& s1, const State& s2, const V3& g)
   return chi;
 }
 
-void add_update(State& s, const double* u, const Calib& c) {
+void add_update(State& s, const double* u, const Calib& c, bool imu) {
   pose_update(s, u, c);
+  if (!imu) return;  // VertexPose only
   for (int i = 0; i < 3; ++i) {
     s.v[i] += u[6 + i];
     s.bg[i] += u[9 + i];
@@ -206,14 +224,13 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
   if (n_kf <= 0 || n_pts < 0 || n_edges < 0 || n_imu < 0 || !(lambda_init > 0)) return -1;
   const Calib c = load_calib(cb);
   const V3 g = gravity();
-  std::vector<int> hidx(n_kf, -1);
-  int nf = 0;
+  std::vector<int> hidx(n_kf, -1);  // first reduced-system row of a free key frame
+  int n = 0;
   for (int k = 0; k < n_kf; ++k)
     if (!fixed[k]) {
-      if (!imu[k]) return -1;
-      hidx[k] = nf++;
+      hidx[k] = n;
+      n += imu[k] ? kDimImu : kDimPose;
     }
-  const int n = kDim * nf;
   std::vector<State> S(n_kf);
   for (int k = 0; k < n_kf; ++k) S[k] = load_state(kfs[k]);
   std::vector<double> X((size_t)3 * n_pts);
@@ -291,7 +308,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
         }
         const int hk = hidx[e.kf];
         if (hk < 0) continue;
-        const int o = kDim * hk;
+        const int o = hk;
         for (int a = 0; a < 6; ++a) {
           for (int r = 0; r < D; ++r) bp[o + a] += Jp[r][a] * om_r[r];
           for (int q = 0; q < 6; ++q) {
@@ -309,8 +326,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
     // the inertial edges (no points: straight into the camera-side system)
     for (const ImuEdge& E : IE) {
       const State &s1 = S[E.kf1], &s2 = S[E.kf2];
-      const int o1 = hidx[E.kf1] >= 0 ? kDim * hidx[E.kf1] : -1;
-      const int o2 = hidx[E.kf2] >= 0 ? kDim * hidx[E.kf2] : -1;
+      const int o1 = hidx[E.kf1], o2 = hidx[E.kf2];
       auto at = [](int o, int d) { return o >= 0 ? o + d : -1; };
       double e[9], J[9][24];
       inertial_edge_error(s1, s2, E.pi, E.dt, g, e);
@@ -355,8 +371,8 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
         for (int a = 0; a < 6; ++a)
           for (int q = 0; q < 3; ++q) {
             const double h = Hpl[(size_t)18 * i + 3 * a + q];
-            sys_H[(size_t)(kDim * hi + a) * m + o + q] += h;
-            sys_H[(size_t)(o + q) * m + kDim * hi + a] += h;
+            sys_H[(size_t)(hi + a) * m + o + q] += h;
+            sys_H[(size_t)(o + q) * m + hi + a] += h;
           }
       }
     }
@@ -400,14 +416,14 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
             for (int b2 = 0; b2 < 3; ++b2)
               W[a][b2] = Bi[3 * a] * Di[0][b2] + Bi[3 * a + 1] * Di[1][b2] + Bi[3 * a + 2] * Di[2][b2];
           for (int a = 0; a < 6; ++a)
-            bs[kDim * hi + a] -= W[a][0] * blp[0] + W[a][1] * blp[1] + W[a][2] * blp[2];
+            bs[hi + a] -= W[a][0] * blp[0] + W[a][1] * blp[1] + W[a][2] * blp[2];
           for (int j : pe[p]) {
             const int hj = hidx[edges[j].kf];
             if (hj < 0) continue;
             const double* Bj = &Hpl[(size_t)18 * j];
             for (int a = 0; a < 6; ++a)
               for (int b2 = 0; b2 < 6; ++b2)
-                Sm[(size_t)(kDim * hi + a) * n + kDim * hj + b2] -=
+                Sm[(size_t)(hi + a) * n + hj + b2] -=
                     W[a][0] * Bj[3 * b2] + W[a][1] * Bj[3 * b2 + 1] + W[a][2] * Bj[3 * b2 + 2];
           }
         }
@@ -422,7 +438,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
           if (hi < 0) continue;
           const double* Bi = &Hpl[(size_t)18 * i];
           for (int b2 = 0; b2 < 3; ++b2)
-            for (int a = 0; a < 6; ++a) cp[b2] -= Bi[3 * a + b2] * xp[kDim * hi + a];
+            for (int a = 0; a < 6; ++a) cp[b2] -= Bi[3 * a + b2] * xp[hi + a];
         }
         const double* Di = &Dinv[(size_t)9 * p];
         for (int a = 0; a < 3; ++a) {
@@ -433,7 +449,7 @@ int lia_optimize(const orbgpu_imu_calib& cb, int n_kf, const orbgpu_imu_state* k
       }
       for (int k = 0; k < n_kf; ++k) {
         Sn[k] = S[k];
-        if (hidx[k] >= 0) add_update(Sn[k], &xp[kDim * hidx[k]], c);
+        if (hidx[k] >= 0) add_update(Sn[k], &xp[hidx[k]], c, imu[k] != 0);
       }
       double tmp = active_chi2(Sn, Xn);
       last = tmp;

@@ -22,12 +22,12 @@ ORBGPU_ERR_EMPTY = -2
 ORBGPU_ERR_CAPACITY = -3
 ORBGPU_ERR_DEVICE = -4
 ORBGPU_ERR_NOMEM = -5
-ORBGPU_ERR_UNSUPPORTED = -6
 ORBGPU_RESIZE_SSE = 0
+ORBGPU_LBA_SOLVER_AUTO = -1
+ORBGPU_LBA_SOLVER_LDS = 0
+ORBGPU_LBA_SOLVER_BLOCK = 1
+ORBGPU_LBA_SOLVER_GRID = 2
 ORBGPU_RESIZE_SCALAR = 1
-ORBGPU_LBA_MAX_FREE_KF = 1706
-ORBGPU_LIA_MAX_FREE_KF = 682
-ORBGPU_LIA_MAX_IMU_LINKS = 64
 
 STATUS_NAMES = {
     ORBGPU_OK: "OK",
@@ -36,7 +36,6 @@ STATUS_NAMES = {
     ORBGPU_ERR_CAPACITY: "CAPACITY",
     ORBGPU_ERR_DEVICE: "DEVICE",
     ORBGPU_ERR_NOMEM: "NOMEM",
-    ORBGPU_ERR_UNSUPPORTED: "UNSUPPORTED",
 }
 
 
@@ -261,6 +260,7 @@ SIGNATURES = {
     ),
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "orbgpu_lba_ctx_set_reduce_ordered": (_I, [_P, _I]),
+    "orbgpu_lba_ctx_set_solver": (_I, [_P, _I]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (
         _I,

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -26,12 +27,15 @@
 #include "../../include/orbgpu.h"
 #include "lba_launch.h"
 
+static_assert(ORBGPU_LBA_SOLVER_LDS == orbgpu::kSolveLds && ORBGPU_LBA_SOLVER_BLOCK == orbgpu::kSolveBlock &&
+                  ORBGPU_LBA_SOLVER_GRID == orbgpu::kSolveGrid,
+              "solver path ids");
+
 using namespace orbgpu;
 
 namespace {
 
-constexpr int kAhead = 2;            // LM steps queued ahead of the device
-constexpr size_t kLdsBudget = 160 * 1024;
+constexpr int kAhead = 2;  // LM steps queued ahead of the device
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -40,6 +44,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct orbgpu_lba_ctx {
   int device = 0;
   int reduce_ordered = 0;  // orbgpu_lba_ctx_set_reduce_ordered
+  int solver = ORBGPU_LBA_SOLVER_AUTO;  // orbgpu_lba_ctx_set_solver
   hipStream_t stream = nullptr;
   char* arena = nullptr;  // device
   size_t arena_cap = 0;
@@ -104,6 +109,12 @@ orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered) 
   return ORBGPU_OK;
 }
 
+orbgpu_status orbgpu_lba_ctx_set_solver(orbgpu_lba_ctx* c, int solver) {
+  if (!c || solver < ORBGPU_LBA_SOLVER_AUTO || solver > ORBGPU_LBA_SOLVER_GRID) return ORBGPU_ERR_INVALID;
+  c->solver = solver;
+  return ORBGPU_OK;
+}
+
 void orbgpu_lba_ctx_destroy(orbgpu_lba_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
@@ -156,10 +167,11 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       hidx[k] = nf++;
       free_kf.push_back(k);
     }
+  if ((long long)m.pdim * nf > INT_MAX / 2) return ORBGPU_ERR_CAPACITY;  // row indices are int
   const int n = m.pdim * nf;
   const int npad = (n + 15) / 16 * 16;
-  // the solver keeps D and the right-hand side in LDS (16 B per padded row)
-  if (16 * (size_t)npad > kLdsBudget) return ORBGPU_ERR_CAPACITY;
+  // a sharded rank all-reduces [S | b_s | b_p] through an int-counted callback
+  if (reduce && (size_t)n * n + 2 * (size_t)n > (size_t)INT_MAX) return ORBGPU_ERR_CAPACITY;
   const int np = pt_end - pt_begin;
   std::vector<int> cnt(np + 1, 0);
   for (int i = 0; i < n_edges; ++i) {
@@ -248,14 +260,18 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     cz = align_up(cz + sizeof(double) * doubles, 256);
     return o;
   };
-  const bool solve_lds = lba_solve_lds_bytes(npad) <= kLdsBudget;
+  int solve_mode = lba_solve_mode(npad);
+  if (h->solver != ORBGPU_LBA_SOLVER_AUTO) {  // a forced path must hold the window
+    if (!lba_solve_mode_fits(h->solver, npad)) return ORBGPU_ERR_CAPACITY;
+    solve_mode = h->solver;
+  }
   const size_t c_err = take(3 * E), c_hpl = take(18 * E), c_hppe = take(27 * E), c_hlle = take(12 * E),
                c_hll = take(9 * P), c_bl = take(3 * P), c_hpp = take(36 * F), c_bp = take(6 * F),
                c_diag = take(n + 2), c_sys = take((size_t)n * n + 2 * n + 2),
-               c_work = take(solve_lds ? 2 : (size_t)npad * (npad + 1) + (size_t)(npad / 16) * 272),  // S + the L_KK^-1 tiles (16 x 17)
+               c_work = take(lba_solve_work_doubles(solve_mode, npad)),
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
-               c_itot = take(2 + ORBGPU_LIA_MAX_IMU_LINKS);  // [0] total, [2 + l] per link
+               c_itot = take(2 + NI);  // [0] total, [2 + l] per link
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
@@ -340,7 +356,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.n_sys = n;
   a.n_pairs = n_pairs;
   a.sharded = reduce ? 1 : 0;
-  a.solve_lds = solve_lds ? 1 : 0;
+  a.solve_mode = solve_mode;
   a.n_pad = npad;
   a.n_edgeless = n_edgeless;
   a.edges = reinterpret_cast<const LbaEdgeDev*>(A + u_edges);
@@ -531,11 +547,6 @@ orbgpu_status orbgpu_lba_optimize(orbgpu_lba_ctx* h, const orbgpu_camera* cam, i
   ModelIn m;
   m.state0 = s0.data();
   WindowOut wo;
-  static_assert(6 * ORBGPU_LBA_MAX_FREE_KF <= kLdsBudget / 16 && 6 * (ORBGPU_LBA_MAX_FREE_KF + 1) > kLdsBudget / 16,
-                "ORBGPU_LBA_MAX_FREE_KF is the solver's bound");
-  static_assert(15 * ORBGPU_LIA_MAX_FREE_KF <= kLdsBudget / 16 && 15 * (ORBGPU_LIA_MAX_FREE_KF + 1) > kLdsBudget / 16,
-                "ORBGPU_LIA_MAX_FREE_KF is the solver's bound");
-  static_assert(ORBGPU_LIA_MAX_IMU_LINKS == kMaxImuLinks, "link bound");
   const orbgpu_status r = run_window(h, cam, n_kf, fixed, n_pts, pts_in, n_edges, edges, pt_begin, pt_end,
                                      iterations, lambda_init, stop_flag, reduce, user, m, pts_out, outlier, wo);
   if (r != ORBGPU_OK) return r;
@@ -573,14 +584,6 @@ orbgpu_status orbgpu_lia_optimize(orbgpu_lba_ctx* h, const orbgpu_imu_calib* cal
       (n_imu > 0 && !imu_edges) || iterations < 0 || !(lambda_init > 0) || !kfs_out ||
       (n_edges > 0 && !outlier))
     return ORBGPU_ERR_INVALID;
-  if (n_imu > kMaxImuLinks) return ORBGPU_ERR_CAPACITY;
-  int n_free = 0;
-  for (int k = 0; k < n_kf; ++k) {
-    n_free += !fixed[k];
-    // a free key frame without IMU vertices (VertexPose only, optimizer.cc:2466-2484)
-    if (!fixed[k] && !imu[k]) return ORBGPU_ERR_UNSUPPORTED;
-  }
-  if (n_free > ORBGPU_LIA_MAX_FREE_KF) return ORBGPU_ERR_CAPACITY;
   for (int l = 0; l < n_imu; ++l) {
     const orbgpu_lia_imu_edge& e = imu_edges[l];
     if (e.kf1 < 0 || e.kf1 >= n_kf || e.kf2 < 0 || e.kf2 >= n_kf || e.kf1 == e.kf2 || !imu[e.kf1] ||

@@ -905,6 +905,49 @@ __device__ __forceinline__ void diag_chain(double (&aug)[32], double& y, double 
   }
 }
 
+// The diagonal tile K by elimination of the augmented rows [A_KK | I | y_K]
+// (one wave; lane li of every 16-lane row owns row li): pivot c subtracts
+// l_i = a_ic / d_c times row c from the rows below it, which leaves D_K on
+// the diagonal, L_KK^-1 in the identity's place and L_KK^-1 y_K in y -- the
+// factorisation, the inverse and the tile's forward substitution in one pass
+// of 16 row-broadcast FMAs per pivot.  SKK: the tile (row stride ts), yk: y_K
+// (read), then L_KK^-1 -> li_out (16 x kTileLd), D_K -> d_out, the
+// substituted y_K -> y_out; a zero pivot sets *bad.
+__device__ __forceinline__ void diag_tile_factor(const double* SKK, int ts, const double* yk, double* li_out,
+                                                 double* d_out, double* y_out, int* bad, int lane) {
+  const int li = lane & 15;
+  double aug[32];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) aug[j] = SKK[li * ts + j];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
+  double yv = yk[li];
+  double dmine = 0;
+  int zero = 0;
+  {
+    const double d0 = row_bcast_f64<0>(aug[0]);
+    dmine = li == 0 ? d0 : 0.0;
+    diag_chain<0>(aug, yv, (li > 0 ? aug[0] : 0.0) * rcp_f64(d0), dmine, li);
+  }
+  if (__builtin_amdgcn_ballot_w64(lane < 16 && dmine == 0.0) != 0) {
+    // a zero pivot (Eigen: NumericalIssue): the guarded elimination of the
+    // tile from its original rows (SKK and y_K are not written above)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aug[j] = SKK[li * ts + j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
+    yv = yk[li];
+    diag_pivots<0>(aug, yv, dmine, zero, li);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) li_out[li * kTileLd + j] = aug[16 + j];
+    d_out[li] = dmine;
+    y_out[li] = yv;
+  }
+  if (lane == 0 && zero) *bad = 1;
+}
+
 #ifdef LBA_SOLVE_STAMPS
 __device__ unsigned long long g_lba_stamps[16];
 #define LBA_STAMP(k)                                                  \
@@ -1036,46 +1079,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   __syncthreads();
   LBA_STAMP(0);
 
-  // 1-3. the diagonal tile K by elimination of the augmented rows
-  // [A_KK | I | y_K] (lane li of every 16-lane row owns row li): pivot c
-  // subtracts l_i = a_ic / d_c times row c from the rows below it, which
-  // leaves D_K on the diagonal, L_KK^-1 in the identity's place and
-  // L_KK^-1 y_K in y -- the factorisation, the inverse and the tile's
-  // forward substitution in one pass of 16 row-broadcast FMAs per pivot.
-  // One wave.
+  // 1-3. the diagonal tile K (diag_tile_factor): one wave
   auto diag_tile = [&](int K) {
     const int k0 = 16 * K;
-    const double* const SKK = tile(K, K);
-    double aug[32];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) aug[j] = SKK[li * TS + j];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
-    double yv = y[k0 + li];
-    double dmine = 0;
-    int zero = 0;
-    {
-      const double d0 = row_bcast_f64<0>(aug[0]);
-      dmine = li == 0 ? d0 : 0.0;
-      diag_chain<0>(aug, yv, (li > 0 ? aug[0] : 0.0) * rcp_f64(d0), dmine, li);
-    }
-    if (__builtin_amdgcn_ballot_w64(lane < 16 && dmine == 0.0) != 0) {
-      // a zero pivot (Eigen: NumericalIssue): the guarded elimination of the
-      // tile from its original rows (SKK and y_K are not written above)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) aug[j] = SKK[li * TS + j];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) aug[16 + j] = j == li ? 1.0 : 0.0;
-      yv = y[k0 + li];
-      diag_pivots<0>(aug, yv, dmine, zero, li);
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) Li[(size_t)K * kTileSz + li * kTileLd + j] = aug[16 + j];
-      Dg[k0 + li] = dmine;
-      y[k0 + li] = yv;
-    }
-    if (lane == 0 && zero) bad = 1;
+    diag_tile_factor(tile(K, K), TS, y + k0, Li + (size_t)K * kTileSz, Dg + k0, y + k0, &bad, lane);
   };
 
   if constexpr (kLds) {
@@ -1314,6 +1321,201 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     a.scal[1] = bad;
   }
   LBA_STAMP(7);
+}
+
+// ---- the reduced camera system of a large window (kSolveGrid): the same
+// tiled L D L^T and substitutions as k_lba_solve<false>, spread over the
+// whole device.  Everything lives in a.work (hbm_solve): S row-major (stride
+// n_pad + 1, lower tiles only), the L_KK^-1 tiles, D, y and the zero-pivot
+// flag -- no LDS bound on the window.  Per tile step K two launches:
+//   k_lba_ldl_panel   every block factors diagonal tile K into LDS
+//                     (diag_tile_factor, block 0 also stores it), then a wave
+//                     per block row I > K: L_IK = A_IK L_KK^-T D_K^-1 (MFMA)
+//                     and y_I -= L_IK y_K
+//   k_lba_ldl_update  a wave per trailing tile (I, J), K < J <= I:
+//                     A_IJ -= L_IK D_K L_JK^T (MFMA)
+// after k_lba_ldl_stage (S + lambda I, y = b_s) and before k_lba_ldl_back
+// (D^-1, backward substitution, x_p and computeScale on one block).  The
+// arithmetic per entry is k_lba_solve<false>'s (same tile operations in the
+// same order), so both paths give the same x_p.
+struct HbmSolve {
+  double* S;
+  double* Li;
+  double* Dg;
+  double* y;   // the right-hand side, rows below the current step updated in place
+  double* ys;  // L^-1 y after the forward substitution (written per diagonal tile)
+  int* bad;
+};
+
+__device__ __forceinline__ HbmSolve hbm_solve(const LbaArgs& a) {
+  const size_t N = a.n_pad, T = N >> 4;
+  HbmSolve h;
+  h.S = a.work;
+  h.Li = h.S + N * (N + 1);
+  h.Dg = h.Li + T * kTileSz;
+  h.y = h.Dg + N;
+  h.ys = h.y + N;
+  h.bad = reinterpret_cast<int*>(h.ys + N);
+  return h;
+}
+
+// one block per padded row r: its lower-tile entries of S + lambda I (identity
+// padding past n_sys), y_r = b_s (+ the IMU links' gradient), the flag cleared
+__global__ __launch_bounds__(kThreads) void k_lba_ldl_stage(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const HbmSolve h = hbm_solve(a);
+  const double lambda = c.lambda;
+  const int n = a.n_sys, N = a.n_pad, r = blockIdx.x;
+  const size_t LD = (size_t)N + 1;
+  const double* src = a.sys;
+  const double* hm = a.himu;
+  const int cend = 16 * ((r >> 4) + 1);
+  for (int cc = threadIdx.x; cc < cend; cc += kThreads) {
+    const bool in = r < n && cc < n;
+    const size_t o = (size_t)r * n + cc;
+    double x = in ? src[o] : 0.0;
+    if (hm && in) x += hm[o];
+    h.S[(size_t)r * LD + cc] = x + (r == cc ? (r < n ? lambda : 1.0) : 0.0);
+  }
+  if (threadIdx.x == 0) {
+    h.y[r] = r < n ? src[(size_t)n * n + r] + (hm ? hm[(size_t)n * n + r] : 0.0) : 0.0;
+    if (r == 0) *h.bad = 0;
+  }
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_panel(LbaArgs a, int K) {
+  __shared__ double sLi[kTileSz];
+  __shared__ double sD[16], sY[16];
+  __shared__ int sbad;
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const HbmSolve h = hbm_solve(a);
+  const int T = a.n_pad >> 4, k0 = 16 * K;
+  const size_t LD = (size_t)a.n_pad + 1;
+  const int t = threadIdx.x, lane = t & 63, li = lane & 15, lk = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (t == 0) sbad = 0;
+  __syncthreads();
+  if (wave == 0) diag_tile_factor(h.S + (size_t)k0 * LD + k0, (int)LD, h.y + k0, sLi, sD, sY, &sbad, lane);
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int q = t; q < kTileSz; q += kSolveThreads) h.Li[(size_t)K * kTileSz + q] = sLi[q];
+    if (t < 16) {  // (every block reads y_K: the substituted values go to ys)
+      h.Dg[k0 + t] = sD[t];
+      h.ys[k0 + t] = sY[t];
+    }
+    if (t == 0 && sbad) *h.bad = 1;
+  }
+  const int I = K + 1 + (int)blockIdx.x * kSolveWaves + wave;
+  if (I >= T) return;
+  const int i0 = 16 * I;
+  double* const SIK = h.S + (size_t)i0 * LD + k0;
+  d4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    const int kk = 4 * kc + lk;
+    const double av = SIK[li * LD + kk];
+    const double bv = sLi[li * kTileLd + kk];  // (L^-1)^T[kk][li]
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+  const double dinv = rcp_f64(sD[li]);
+  const double ykl = sY[li];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const double l = acc[rr] * dinv;
+    SIK[(lk + 4 * rr) * LD + li] = l;
+    double p = l * ykl;
+    p += dpp_f64<0x111, 0xf>(p);
+    p += dpp_f64<0x112, 0xf>(p);
+    p += dpp_f64<0x114, 0xf>(p);
+    p += dpp_f64<0x118, 0xf>(p);
+    if (li == 15) h.y[i0 + lk + 4 * rr] -= p;
+  }
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_update(LbaArgs a, int K) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const HbmSolve h = hbm_solve(a);
+  const int T = a.n_pad >> 4, k0 = 16 * K, m = T - K - 1;
+  const size_t LD = (size_t)a.n_pad + 1;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int q = (int)blockIdx.x * kSolveWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  if (q >= m * (m + 1) / 2) return;
+  // q -> (I, J), J <= I, row-major over the trailing triangle
+  int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= q) ++I;
+  while (I * (I + 1) / 2 > q) --I;
+  const int J = q - I * (I + 1) / 2;
+  const size_t r0 = (size_t)16 * (K + 1 + I), c0 = (size_t)16 * (K + 1 + J);
+  double* const SIJ = h.S + r0 * LD + c0;
+  const double* const SIK = h.S + r0 * LD + k0;
+  const double* const SJK = h.S + c0 * LD + k0;
+  d4 acc;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) acc[rr] = SIJ[(lk + 4 * rr) * LD + li];
+#pragma unroll
+  for (int kc = 0; kc < 4; ++kc) {
+    const int kk = 4 * kc + lk;
+    const double av = -SIK[li * LD + kk];
+    const double bv = SJK[li * LD + kk] * h.Dg[k0 + kk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) SIJ[(lk + 4 * rr) * LD + li] = acc[rr];
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_back(LbaArgs a) {
+  __shared__ double red[kSolveWaves];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const HbmSolve h = hbm_solve(a);
+  const double lambda = c.lambda;
+  const int n = a.n_sys, N = a.n_pad, T = N >> 4;
+  const size_t LD = (size_t)N + 1;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double* const y = h.ys;
+  for (int r = t; r < N; r += kSolveThreads) y[r] = y[r] * rcp_f64(h.Dg[r]);
+  __syncthreads();
+  for (int K = T - 1; K >= 0; --K) {
+    const int k0 = 16 * K;
+    if (t < 16) {
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s = fma(h.Li[(size_t)K * kTileSz + k * kTileLd + t], y[k0 + k], s);
+      __builtin_amdgcn_wave_barrier();
+      y[k0 + t] = s;
+    }
+    __syncthreads();
+    const double* const rowK = h.S + (size_t)k0 * LD;
+    for (int r = t; r < k0; r += kSolveThreads) {
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s = fma(rowK[k * LD + r], y[k0 + k], s);
+      y[r] -= s;
+    }
+    __syncthreads();
+  }
+  const double* src = a.sys;
+  const double* hm = a.himu;
+  double sc = 0;
+  for (int r = t; r < n; r += kSolveThreads) {
+    const double xv = y[r];
+    a.xp[r] = xv;
+    sc += xv * (lambda * xv + src[(size_t)n * n + n + r] + (hm ? hm[(size_t)n * n + r] : 0.0));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sc += __shfl_xor(sc, o, 64);
+  if (lane == 0) red[wave] = sc;
+  __syncthreads();
+  if (t == 0) {
+    double v = 0;
+#pragma unroll
+    for (int w = 0; w < kSolveWaves; ++w) v += red[w];
+    a.scal[0] = v;
+    a.scal[1] = *h.bad;
+  }
 }
 
 // ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
@@ -1749,6 +1951,47 @@ size_t lba_solve_lds_bytes(int n_pad) {
   return 8 * (T * (T + 1) / 2 * kTileSz + T * kTileSz + 2 * (size_t)n_pad + (size_t)kSolveWaves * kTileSz);
 }
 
+// LDS a workgroup may hold, less a margin for the solve kernels' static
+// __shared__ arrays (red[kSolveWaves] and a flag: < 100 B) next to the
+// dynamic block
+constexpr size_t kLdsBudget = 160 * 1024;
+constexpr size_t kStaticLdsMargin = 1024;
+static_assert(sizeof(double) * kSolveWaves + sizeof(int) <= kStaticLdsMargin, "static LDS margin");
+
+// One block factorises up to this many padded rows from HBM (kSolveBlock);
+// larger systems take the device-wide path (orbgpu_lba_ctx_set_solver forces
+// either for A/B timing).
+constexpr int kGridMinPad = 224;  // tools/lba_solver_ab.py: block wins at 176 rows, grid at 272
+
+bool lba_solve_mode_fits(int mode, int n_pad) {
+  switch (mode) {
+    case kSolveLds:
+      return lba_solve_lds_bytes(n_pad) + kStaticLdsMargin <= kLdsBudget;
+    case kSolveBlock:
+      return 16 * (size_t)n_pad + kStaticLdsMargin <= kLdsBudget;
+    default:
+      return true;
+  }
+}
+
+int lba_solve_mode(int n_pad) {
+  if (lba_solve_mode_fits(kSolveLds, n_pad)) return kSolveLds;
+  if (n_pad < kGridMinPad && lba_solve_mode_fits(kSolveBlock, n_pad)) return kSolveBlock;
+  return kSolveGrid;
+}
+
+size_t lba_solve_work_doubles(int mode, int n_pad) {
+  const size_t N = n_pad, T = N / 16;
+  switch (mode) {
+    case kSolveLds:
+      return 2;
+    case kSolveBlock:
+      return N * (N + 1) + T * kTileSz;  // S + the L_KK^-1 tiles
+    default:
+      return N * (N + 1) + T * kTileSz + 3 * N + 2;  // S, L_KK^-1 tiles, D, y, ys, flag (hbm_solve)
+  }
+}
+
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
@@ -1784,18 +2027,30 @@ hipError_t lba_schur(const LbaArgs& a, hipStream_t st) {
 }
 
 hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
-  if (a.solve_lds) {
+  if (a.solve_mode == kSolveLds) {
     const size_t lds = lba_solve_lds_bytes(a.n_pad);
     if (lds > 64 * 1024 &&
         lds_optin(reinterpret_cast<const void*>(&k_lba_solve<true>), (int)lds) != hipSuccess)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_lba_solve<true>, dim3(1), dim3(kSolveThreads), lds, st, a);
-  } else {
-    const size_t lds = 16 * (size_t)a.n_pad;  // D and y (the API bounds it by 160 KB)
+  } else if (a.solve_mode == kSolveBlock) {
+    const size_t lds = 16 * (size_t)a.n_pad;  // D and y (lba_solve_mode bounds it)
     if (lds > 64 * 1024 &&
         lds_optin(reinterpret_cast<const void*>(&k_lba_solve<false>), (int)lds) != hipSuccess)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_lba_solve<false>, dim3(1), dim3(kSolveThreads), lds, st, a);
+  } else {
+    const int T = a.n_pad >> 4;
+    hipLaunchKernelGGL(k_lba_ldl_stage, dim3(a.n_pad), dim3(kThreads), 0, st, a);
+    for (int K = 0; K < T; ++K) {
+      const int m = T - K - 1;
+      hipLaunchKernelGGL(k_lba_ldl_panel, dim3(m > 0 ? blocks(m, kSolveWaves) : 1), dim3(kSolveThreads), 0, st,
+                         a, K);
+      if (m > 0)
+        hipLaunchKernelGGL(k_lba_ldl_update, dim3(blocks((long)m * (m + 1) / 2, kSolveWaves)),
+                           dim3(kSolveThreads), 0, st, a, K);
+    }
+    hipLaunchKernelGGL(k_lba_ldl_back, dim3(1), dim3(kSolveThreads), 0, st, a);
   }
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {

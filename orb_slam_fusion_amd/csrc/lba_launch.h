@@ -24,7 +24,6 @@ enum LbaModel { kModelSe3 = 0, kModelImu = 1 };
 constexpr int kImuStateStride = 33;
 constexpr int kImuDim = 15;
 constexpr int kImuPairQ = 30 * 30 + 30;  // per IMU link: 30 x 30 form + gradient
-constexpr int kMaxImuLinks = 64;
 
 struct LiaCalibDev {  // == CalibD (imu_math_dev.h)
   double fx, fy, cx, cy, bf;
@@ -58,6 +57,11 @@ struct LbaCtrl {
   int lambda_due;  // sharded: the first build's lambda init waits for the all-reduce (k_lba_ctl)
 };
 
+// The reduced-camera-system factorisation (lba_kernels.hip): the packed
+// lower-triangle tiles in LDS (one block), S in HBM with D and y in LDS (one
+// block), or every piece in HBM over the whole device (any window size).
+enum LbaSolveMode { kSolveLds = 0, kSolveBlock = 1, kSolveGrid = 2 };
+
 // LM decision points whose inputs a point-sharded run all-reduces first
 enum LbaCtlMode { kCtlInit = 0, kCtlLambda = 1, kCtlDecide = 2 };
 
@@ -72,7 +76,7 @@ struct LbaArgs {
   LbaCamDev cam;
   int n_kf, n_pts, n_edges, n_free, n_sys, n_pairs;
   int sharded;               // 1: LM decisions wait for the host's all-reduce (k_lba_ctl)
-  int solve_lds;             // 1: the reduced system is factorised in LDS
+  int solve_mode;            // LbaSolveMode: where the reduced system is factorised
   int n_pad;                 // n_sys rounded up to the 16-wide MFMA tile
   int n_edgeless;            // points of the shard with no edge (their Hll is 0)
   const LbaEdgeDev* edges;   // [n_edges]
@@ -134,5 +138,9 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
 // outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles)
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
+// the solver path for an n_pad-row system, and the doubles of a.work it needs
+int lba_solve_mode(int n_pad);
+bool lba_solve_mode_fits(int mode, int n_pad);
+size_t lba_solve_work_doubles(int mode, int n_pad);
 
 }  // namespace orbgpu

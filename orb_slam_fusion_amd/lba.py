@@ -100,6 +100,11 @@ class LocalBundleAdjuster:
         except Exception:
             pass
 
+    def set_solver(self, solver: int) -> None:
+        """Forces the reduced-system path (_lib.ORBGPU_LBA_SOLVER_*; AUTO by
+        default): A/B timing and the path-equivalence tests."""
+        check(lib().orbgpu_lba_ctx_set_solver(self._h, int(solver)), "orbgpu_lba_ctx_set_solver")
+
     def optimize(self, problem, iterations: int = 10, pt_range=None, group=None,
                  stop_flag: Optional[ctypes.c_uint8] = None, lambda_init: float = 0.0,
                  ordered: bool = False) -> dict:

@@ -1,7 +1,7 @@
 // Optimizer::LocalBundleAdjustment over the gfx950 C ABI.
 // Compiled inside the reference build (its include paths: keyframe.h,
-// mappoint.h, map.h, Sophus, Eigen); the original definition in
-// optimizer.cc:1053-1441 is guarded with ORBGPU_LBA.
+// mappoint.h, map.h, Sophus, Eigen) in place of the original definition in
+// optimizer.cc:1053-1441.
 // The window gather and the write-back keep the reference's semantics
 // (:1057-1124 and :1362-1441: local keyframes = pKF + its non-bad covisible
 // keyframes of the same map, local map points = their non-bad points of that
@@ -12,6 +12,7 @@
 #include <list>
 #include <mutex>
 #include <stdexcept>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -22,14 +23,6 @@
 #include "solver/g2o_solver/optimizer.h"
 
 namespace ORB_SLAM_FUSION {
-
-// The reference's own LocalBundleAdjustment, compiled from optimizer.cc under
-// this name when ORBGPU_LBA is defined: the fallback for a
-// window beyond the device solver (ORBGPU_LBA_MAX_FREE_KF free key frames).
-namespace orbgpu_cpu {
-void LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int &num_fixedKF, int &num_OptKF,
-                           int &num_MPs, int &num_edges);
-}  // namespace orbgpu_cpu
 
 namespace {
 // LocalMapping calls this; keep one context per calling thread.
@@ -63,17 +56,6 @@ void Optimizer::LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap
   for (KeyFrame *k : pKF->GetVectorCovisibleKeyFrames()) {
     k->mnBALocalForKF = pKF->id_;
     if (!k->isBad() && k->GetMap() == pCurrentMap) local_kfs.push_back(k);
-  }
-  {
-    // beyond the device solver: the reference's CPU path, decided before the
-    // map-point marks below are set (its own gather repeats the key-frame
-    // marks above, which are idempotent)
-    int n_free = 0;
-    for (KeyFrame *k : local_kfs) n_free += k->id_ != pMap->GetInitKFid();
-    if (n_free > ORBGPU_LBA_MAX_FREE_KF) {
-      orbgpu_cpu::LocalBundleAdjustment(pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_MPs, num_edges);
-      return;
-    }
   }
   num_fixedKF = 0;
   std::list<MapPoint *> local_mps;
@@ -141,13 +123,16 @@ void Optimizer::LocalBundleAdjustment(KeyFrame *pKF, bool *pbStopFlag, Map *pMap
   std::vector<float> pts_out(pts);
   std::vector<uint8_t> outlier(edges.size());
   static_assert(sizeof(bool) == 1, "pbStopFlag is read as one byte by the ABI");
-  if (orbgpu_lba_optimize(lba_thread_ctx(), &cam, (int)kfs.size(), poses.data(), fixed.data(),
-                          (int)mps.size(), pts.data(), (int)edges.size(), edges.data(), 0,
-                          (int)mps.size(), 10, pMap->IsInertial() ? 100.0 : 0.0,  // :1137
+  // every window runs on the device (any size: orbgpu.h); a failure -- only
+  // exhausted device memory remains -- is an error, never a CPU fallback
+  const orbgpu_status st =
+      orbgpu_lba_optimize(lba_thread_ctx(), &cam, (int)kfs.size(), poses.data(), fixed.data(), (int)mps.size(),
+                          pts.data(), (int)edges.size(), edges.data(), 0, (int)mps.size(), 10,
+                          pMap->IsInertial() ? 100.0 : 0.0,  // :1137
                           reinterpret_cast<const volatile uint8_t *>(pbStopFlag), nullptr, nullptr,
-                          poses_out.data(), nullptr, pts_out.data(), outlier.data(),
-                          nullptr) != ORBGPU_OK)
-    throw std::runtime_error("orbgpu_lba_optimize failed");
+                          poses_out.data(), nullptr, pts_out.data(), outlier.data(), nullptr);
+  if (st != ORBGPU_OK)
+    throw std::runtime_error("orbgpu_lba_optimize failed with status " + std::to_string(st));
 
   // ---- outliers and write-back (:1362-1441)
   std::vector<std::pair<KeyFrame *, MapPoint *>> to_erase;

@@ -1,7 +1,8 @@
 // Optimizer::LocalInertialBA over the gfx950 C ABI.  Compiled inside the
 // reference build (keyframe.h, mappoint.h, map.h, imu_types.h, g2o_types.h,
-// Eigen, Sophus); the original definition in optimizer.cc:2329-2902 is
-// guarded with ORBGPU_INERTIAL_LBA.  The temporal window
+// Eigen, Sophus) in place of the original definition in
+// optimizer.cc:2329-2902.  Key frames without IMU data
+// (VertexPose only, :2466-2484) and windows of any size run on the device.  The temporal window
 // (:2332-2436), the graph (:2461-2781), the FAIL test and the write-back
 // (:2832-2901) keep the reference's semantics; the optimisation and the
 // outlier test run on the GPU (orbgpu_lia_optimize).  Pinhole rigs only (the
@@ -13,6 +14,7 @@
 #include <list>
 #include <mutex>
 #include <stdexcept>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -24,15 +26,6 @@
 #include "solver/g2o_solver/optimizer.h"
 
 namespace ORB_SLAM_FUSION {
-
-// The reference's own LocalInertialBA, compiled from optimizer.cc under this
-// name when ORBGPU_INERTIAL_LBA is defined: the fallback for
-// windows the device path does not take (a free key frame without IMU
-// vertices, more than ORBGPU_LIA_MAX_FREE_KF free key frames).
-namespace orbgpu_cpu {
-void LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int &num_fixedKF, int &num_OptKF,
-                     int &num_MPs, int &num_edges, bool bLarge, bool bRecInit);
-}  // namespace orbgpu_cpu
 
 namespace {
 
@@ -67,7 +60,12 @@ void Optimizer::LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int 
                                 int &num_OptKF, int &num_MPs, int &num_edges, bool bLarge,
                                 bool bRecInit) {
   // pbStopFlag: attached after optimize() in the reference (:2794), never stops it;
-  // the counters are the reference's out-params (set only on its CPU path here)
+  // the counters are the reference's out-params, which it leaves unwritten
+  (void)pbStopFlag;
+  (void)num_fixedKF;
+  (void)num_OptKF;
+  (void)num_MPs;
+  (void)num_edges;
   if (pKF->cam2_) throw std::logic_error("orbgpu LocalInertialBA: fisheye rig not supported");
   Map *pCurrentMap = pKF->GetMap();
   const int maxOpt = bLarge ? 25 : 10, opt_it = bLarge ? 4 : 10;
@@ -80,18 +78,6 @@ void Optimizer::LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int 
     if (!opt.back()->mPrevKF) break;
     opt.push_back(opt.back()->mPrevKF);
     opt.back()->mnBALocalForKF = pKF->id_;
-  }
-  {
-    // windows the device path does not take go to the reference's CPU code,
-    // decided before the map-point marks below are set (the key-frame marks
-    // above are repeated identically by its own gather)
-    bool cpu = (int)opt.size() > ORBGPU_LIA_MAX_FREE_KF;
-    for (KeyFrame *k : opt) cpu = cpu || !k->bImu;  // VertexPose-only key frame (:2466-2484)
-    if (cpu) {
-      orbgpu_cpu::LocalInertialBA(pKF, pbStopFlag, pMap, num_fixedKF, num_OptKF, num_MPs, num_edges, bLarge,
-                                  bRecInit);
-      return;
-    }
   }
   std::list<MapPoint *> local_mps;
   for (KeyFrame *k : opt)
@@ -190,11 +176,13 @@ void Optimizer::LocalInertialBA(KeyFrame *pKF, bool *pbStopFlag, Map *pMap, int 
   std::vector<float> pts_out(pts);
   std::vector<uint8_t> outlier(edges.size() + 1);
   double stats[7];
-  if (orbgpu_lia_optimize(lia_thread_ctx(), &calib, (int)kfs.size(), states.data(), fixed.data(), imu.data(),
+  const orbgpu_status st =
+      orbgpu_lia_optimize(lia_thread_ctx(), &calib, (int)kfs.size(), states.data(), fixed.data(), imu.data(),
                           (int)mps.size(), pts.data(), close.data(), (int)edges.size(), edges.data(),
                           (int)links.size(), links.data(), opt_it, bLarge ? 1e-2 : 1e0, out_states.data(),
-                          nullptr, pts_out.data(), outlier.data(), stats) != ORBGPU_OK)
-    throw std::runtime_error("orbgpu_lia_optimize failed");
+                          nullptr, pts_out.data(), outlier.data(), stats);
+  if (st != ORBGPU_OK)  // exhausted device memory: an error, never a CPU fallback
+    throw std::runtime_error("orbgpu_lia_optimize failed with status " + std::to_string(st));
 
   // ---- FAIL test, erase, write-back (:2796-2901)
   std::vector<std::pair<KeyFrame *, MapPoint *>> to_erase;

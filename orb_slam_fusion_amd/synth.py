@@ -198,7 +198,14 @@ class LiaProblem:
 
 def lia_problem(seed: int = LIA_SEED, n_opt: int = 10, n_fixed_cov: int = 10, n_pts: int = 2000,
                 max_obs: int = 8, outlier_frac: float = 0.05, stereo_frac: float = 0.5,
-                b_large: bool = False, rec_init: bool = False, perturb: float = 1.0) -> LiaProblem:
+                b_large: bool = False, rec_init: bool = False, perturb: float = 1.0,
+                no_imu: tuple = (), max_depth: float = 40.0, consecutive: bool = False) -> LiaProblem:
+    """no_imu: window indices of key frames without IMU data (`!pKFi->bImu`:
+    VertexPose only, optimizer.cc:2466-2484) -- the temporal links touching
+    them are left out, as :2503 skips them.  max_depth: farthest visible
+    depth.  consecutive: a point's observers are max_obs consecutive key
+    frames of those that see it (a banded window) instead of a random
+    subset."""
     rng = np.random.default_rng(seed)
     c = lia_calib()
     fx, fy, cx, cy, bf = LIA_CAM
@@ -234,26 +241,35 @@ def lia_problem(seed: int = LIA_SEED, n_opt: int = 10, n_fixed_cov: int = 10, n_
                                bg_true[k] + rng.normal(0, 1e-3 * s, 3),
                                ba_true[k] + rng.normal(0, 5e-3 * s, 3))
     imu = np.ones(n_tot, np.uint8)
+    for i in no_imu:
+        assert 0 <= i < n_opt
+        imu[i] = 0
     # points ahead of the flight, observed by the key frames that see them
     span = times[-1]
     P = np.stack([rng.uniform(3.0, span + 22.0, 4 * n_pts), rng.uniform(-8, 8, 4 * n_pts),
                   rng.uniform(-3, 3, 4 * n_pts)], 1)
     Rcw_t = [kfs_true[i]["Rcw"].astype(float).reshape(3, 3) for i in range(n_tot)]
     tcw_t = [kfs_true[i]["tcw"].astype(float) for i in range(n_tot)]
+    # visibility of every candidate from every key frame, one key frame at a time
+    vis_of = [[] for _ in range(len(P))]
+    for i in range(n_tot):
+        Xc = P @ Rcw_t[i].T + tcw_t[i]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = fx * Xc[:, 0] / Xc[:, 2] + cx
+            v = fy * Xc[:, 1] / Xc[:, 2] + cy
+        ok = (Xc[:, 2] >= 0.5) & (Xc[:, 2] <= max_depth) & (u >= 0) & (u < 752) & (v >= 0) & (v < 480)
+        for j in np.nonzero(ok)[0]:
+            vis_of[j].append((i, Xc[j, 2], u[j], v[j]))
     pts, obs_lists = [], []
-    for X in P:
-        vis = []
-        for i in range(n_tot):
-            Xc = Rcw_t[i] @ X + tcw_t[i]
-            if Xc[2] < 0.5 or Xc[2] > 40:
-                continue
-            u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
-            if 0 <= u < 752 and 0 <= v < 480:
-                vis.append((i, Xc[2], u, v))
+    for X, vis in zip(P, vis_of):
         if len(vis) < 2 or not any(i < n_opt for i, *_ in vis):
             continue
         if len(vis) > max_obs:
-            keep = np.sort(rng.choice(len(vis), max_obs, replace=False))
+            if consecutive:
+                j0 = int(rng.integers(0, len(vis) - max_obs + 1))
+                keep = np.arange(j0, j0 + max_obs)
+            else:
+                keep = np.sort(rng.choice(len(vis), max_obs, replace=False))
             vis = [vis[j] for j in keep]
             if not any(i < n_opt for i, *_ in vis):
                 continue
@@ -309,6 +325,7 @@ def lia_problem(seed: int = LIA_SEED, n_opt: int = 10, n_fixed_cov: int = 10, n_
         ie[i]["kf1"], ie[i]["kf2"] = i + 1, i
         ie[i]["flags"] = ((LIA_ROBUST | LIA_DOWNWEIGHT) if i == n_opt - 1 else 0) | \
             (LIA_ROBUST if rec_init else 0)
+    ie = ie[[bool(imu[i] and imu[i + 1]) for i in range(n_opt)]]  # pKFi->bImu && mPrevKF->bImu
     return LiaProblem(calib=c, kfs=kfs, kfs_true=kfs_true, fixed=fixed, imu=imu,
                       pts_init=pts_init, pts_true=pts_true.astype(np.float32), close=close,
                       edges=edges, imu_edges=ie, outliers=np.array(bad, bool),

@@ -93,8 +93,16 @@ class Window:
         self.init = [s for s in pb.kfs]  # camera pose of a not-yet-updated vertex
         self.X = [p.astype(float) for p in pb.pts_init]
         self.free = [k for k in range(len(pb.kfs)) if not pb.fixed[k]]
-        self.col = {k: 15 * i for i, k in enumerate(self.free)}
-        self.n = 15 * len(self.free) + 3 * len(self.X)
+        # a key frame's vertices: VP VV VG VA, or VP alone without IMU data
+        # (optimizer.cc:2466-2484)
+        self.blocks = {k: (("P", 0, 6), ("V", 6, 3), ("G", 9, 3), ("A", 12, 3)) if pb.imu[k] else (("P", 0, 6),)
+                       for k in self.free}
+        self.col, o = {}, 0
+        for k in self.free:
+            self.col[k] = o
+            o += 15 if pb.imu[k] else 6
+        self.n_kf_rows = o
+        self.n = o + 3 * len(self.X)
 
     def errors(self, x=None, X=None, init=None):
         """[(error, Omega, delta)] visual edges in order, then per IMU link its three edges."""
@@ -120,7 +128,7 @@ class Window:
         base = self.errors()
         Js = [np.zeros((len(e), self.n)) for e, _, _ in base]
         for k in self.free:
-            for blk, off, dim in (("P", 0, 6), ("V", 6, 3), ("G", 9, 3), ("A", 12, 3)):
+            for blk, off, dim in self.blocks[k]:
                 for j in range(dim):
                     d = np.zeros(dim)
                     d[j] = h
@@ -134,7 +142,7 @@ class Window:
                         res.append(self.errors(x=x, init=init))
                     for i, (ep, em) in enumerate(zip(*res)):
                         Js[i][:, self.col[k] + off + j] = (ep[0] - em[0]) / (2 * h)
-        o0 = 15 * len(self.free)
+        o0 = self.n_kf_rows
         for p in range(len(self.X)):
             for j in range(3):
                 res = []
@@ -160,10 +168,10 @@ class Window:
         x = list(self.x)
         for k in self.free:
             o = self.col[k]
-            xk = update21(self.x[k], dx[o:o + 6], "P")
-            xk = update21(xk, dx[o + 6:o + 9], "V")
-            xk = update21(xk, dx[o + 9:o + 12], "G")
-            x[k] = update21(xk, dx[o + 12:o + 15], "A")
-        o0 = 15 * len(self.free)
+            xk = self.x[k]
+            for blk, off, dim in self.blocks[k]:
+                xk = update21(xk, dx[o + off:o + off + dim], blk)
+            x[k] = xk
+        o0 = self.n_kf_rows
         X = [self.X[p] + dx[o0 + 3 * p:o0 + 3 * p + 3] for p in range(len(self.X))]
         return x, X

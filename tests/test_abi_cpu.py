@@ -104,11 +104,11 @@ def test_inertial_mode_and_prior_checked_with_a_handle():
 
 def test_local_inertial_ba_checked_with_a_handle():
     """orbgpu_lia_optimize's argument checks (lba_api.cpp) return before the
-    context is dereferenced: a link to a key frame without IMU vertices, a
-    self link and a non-positive user lambda are INVALID; a free key frame
-    without IMU vertices (the reference's VertexPose-only key frame) is
-    UNSUPPORTED and more links than the kernel's bound CAPACITY -- the two
-    statuses on which the C++ drop-in runs the reference's CPU code."""
+    context is dereferenced: a link to a key frame without IMU vertices (free
+    or fixed: optimizer.cc:2503 adds an EdgeInertial only between two bImu
+    key frames), a self link and a non-positive user lambda are INVALID.  A
+    free key frame without IMU vertices and no link is valid (VertexPose
+    only), and so is any link count -- tests/test_gpu_lia.py runs both."""
     from orb_slam_fusion_amd import synth
     from orb_slam_fusion_amd.lba import LocalBundleAdjuster
 
@@ -131,17 +131,14 @@ def test_local_inertial_ba_checked_with_a_handle():
 
     try:
         imu = pb.imu.copy()
-        imu[0] = 0  # a free key frame
-        assert status(imu=imu) == _lib.ORBGPU_ERR_UNSUPPORTED
+        imu[0] = 0  # a free key frame that link 0 still touches
+        assert status(imu=imu) == INV
         imu = pb.imu.copy()
         imu[int((pb.fixed == 0).sum())] = 0  # the key frame before the window (a link's kf1)
         assert status(imu=imu) == INV
         links = pb.imu_edges.copy()
         links[0]["kf1"] = links[0]["kf2"]
         assert status(imu_edges=links) == INV
-        many = np.repeat(pb.imu_edges, 30)  # 90 links > the 64-link bound
-        assert len(many) > _lib.ORBGPU_LIA_MAX_IMU_LINKS
-        assert status(imu_edges=many) == _lib.ORBGPU_ERR_CAPACITY
         assert status(lambda_init=0.0) == INV
         assert so.orbgpu_lia_optimize(None, None, 0, None, None, None, 0, None, None, 0, None, 0,
                                       None, 10, 1.0, None, None, None, None, None) == INV

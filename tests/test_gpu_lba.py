@@ -78,16 +78,51 @@ def test_lba_window_past_2048_rows(gpu_available):
     _compare(synth.lba_problem(seed=21, n_kf=346, n_pts=3460, obs_per_pt=6, n_fixed=2), iters=1)
 
 
-def test_lba_capacity_bound(gpu_available):
-    """One free key frame past ORBGPU_LBA_MAX_FREE_KF: ORBGPU_ERR_CAPACITY before
-    any device work (the C++ drop-in then runs the reference's CPU code)."""
+def test_lba_window_past_old_lds_bound(gpu_available):
+    """1710 free key frames (a 10260-row reduced system: past the round-3 bound
+    of 1706, where D and the right-hand side no longer fit LDS) on the
+    device-wide solver -- one LM iteration against the oracle.  No window
+    size is refused and no CPU code runs (the drop-in has no fallback)."""
+    p = synth.lba_problem(seed=23, n_kf=1712, n_pts=4 * 1712, obs_per_pt=4, n_fixed=2)
+    _compare(p, iters=1)
+
+
+def test_lba_lds_path_at_its_bound(gpu_available):
+    """26 free key frames: 156 rows, n_pad 160 -- the largest system the packed
+    LDS solve takes (its dynamic block plus the kernel's static LDS within
+    160 KB); 27 take the one-block HBM path."""
     from orb_slam_fusion_amd import _lib
 
-    nf = _lib.ORBGPU_LBA_MAX_FREE_KF + 1
-    p = synth.lba_problem(seed=22, n_kf=nf + 1, n_pts=nf, obs_per_pt=2, n_fixed=1)
+    p = synth.lba_problem(seed=24, n_kf=28, n_pts=1400, obs_per_pt=5, n_fixed=2)
+    got, _ = _compare(p)
+    adj = LocalBundleAdjuster()
+    adj.set_solver(_lib.ORBGPU_LBA_SOLVER_LDS)
+    forced = adj.optimize(p)
+    assert np.array_equal(forced["poses_d"], got["poses_d"])  # AUTO took the LDS path
+    q = synth.lba_problem(seed=24, n_kf=29, n_pts=1400, obs_per_pt=5, n_fixed=2)
     with pytest.raises(_lib.OrbGpuError) as e:
-        LocalBundleAdjuster().optimize(p, iterations=1)
+        adj.optimize(q)  # 162 rows: past the LDS path
     assert e.value.status == _lib.ORBGPU_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("n_kf", [30, 60])
+def test_lba_block_and_grid_solvers_identical(gpu_available, n_kf):
+    """The one-workgroup HBM solve and the device-wide one run the same tile
+    operations in the same order: bit-identical LM paths and states."""
+    from orb_slam_fusion_amd import _lib
+
+    p = synth.lba_problem(seed=25, n_kf=n_kf, n_pts=40 * n_kf, obs_per_pt=5, n_fixed=2)
+    res = {}
+    for mode in (_lib.ORBGPU_LBA_SOLVER_BLOCK, _lib.ORBGPU_LBA_SOLVER_GRID):
+        adj = LocalBundleAdjuster()
+        adj.set_solver(mode)
+        res[mode] = adj.optimize(p)
+    a, b = res[_lib.ORBGPU_LBA_SOLVER_BLOCK], res[_lib.ORBGPU_LBA_SOLVER_GRID]
+    assert np.array_equal(a["stats"], b["stats"])
+    assert np.array_equal(a["poses_d"], b["poses_d"])
+    assert np.array_equal(a["pts"], b["pts"])
+    assert np.array_equal(a["outlier"], b["outlier"])
+    _compare(p)
 
 
 def test_lba_all_fixed_and_empty(gpu_available):

@@ -77,6 +77,29 @@ def test_lia_outlier_heavy(gpu_available):
     _compare(synth.lia_problem(12, n_opt=8, n_pts=1000, outlier_frac=0.2))
 
 
+def test_lia_vertex_pose_only_keyframes(gpu_available):
+    """Free key frames without IMU data (`!pKFi->bImu`: VertexPose only,
+    optimizer.cc:2466-2484; no EdgeInertial touches them, :2503) on the
+    device, against the oracle that gives them 6 rows: same LM path, states
+    within tolerance, their velocity and biases untouched."""
+    pb = synth.lia_problem(16, n_opt=8, n_fixed_cov=3, n_pts=900, no_imu=(2, 5))
+    assert len(pb.imu_edges) == 8 - 4
+    got, _ = _compare(pb)
+    for k in (2, 5):
+        for f in ("v", "bg", "ba"):
+            assert np.array_equal(got["kfs"][f][k], pb.kfs[f][k])
+
+
+def test_lia_many_links_grid_solver(gpu_available):
+    """72 temporal key frames (71 IMU links, past the round-3 64-link bound; a
+    1080-row reduced system on the device-wide solver) with two VertexPose-only
+    key frames, against the oracle."""
+    pb = synth.lia_problem(17, n_opt=72, n_fixed_cov=4, n_pts=1500, max_obs=3, max_depth=10.0,
+                           consecutive=True, no_imu=(30, 31))
+    assert len(pb.imu_edges) > 64
+    _compare(pb)
+
+
 def test_lia_then_lba_on_one_context(gpu_available):
     """Both windows share the context's arena: an LBA call after a LocalInertialBA
     call (and back) gives the standalone results."""

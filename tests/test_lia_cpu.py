@@ -133,8 +133,52 @@ def test_recovers_truth(b_large):
     assert out.mean() < 0.2
 
 
-def test_rejects_free_keyframe_without_imu():
-    pb = small()
-    pb.imu[0] = 0
-    with pytest.raises(AssertionError):
-        oracle.lia(pb)
+def test_vertex_pose_only_keyframes_system():
+    """Free key frames without IMU data (`!pKFi->bImu`, optimizer.cc:2466-2484):
+    a VertexPose alone (6 rows), no temporal link touching it (:2503) -- the
+    oracle's system against the numpy model's central differences."""
+    pb = small(11, n_opt=5, no_imu=(1, 3))
+    assert list(pb.imu[:5]) == [1, 0, 1, 0, 1]
+    assert all(pb.imu[e["kf1"]] and pb.imu[e["kf2"]] for e in pb.imu_edges)
+    H, b = oracle.lia_system(pb)
+    w = lm.Window(pb)
+    assert w.n_kf_rows == 15 * 3 + 6 * 2
+    Hn, bn = w.system()
+    assert H.shape == Hn.shape
+    assert np.abs(H - Hn).max() <= 1e-6 * np.abs(Hn).max()
+    assert np.abs(b - bn).max() <= 1e-6 * np.abs(bn).max()
+
+
+def test_vertex_pose_only_keyframes_lm_step():
+    """One LM trial with VertexPose-only key frames against the dense solve of
+    the oracle's full system: their velocity and biases are not vertices and
+    stay as given."""
+    pb = small(12, n_opt=5, no_imu=(0, 2))
+    r = oracle.lia(pb, iterations=1, lambda_init=1.0)
+    assert r["stats"][3] == 1
+    w = lm.Window(pb)
+    x, X = w.step(1.0, system=oracle.lia_system(pb))
+    for k in w.free:
+        assert np.abs(r["kfs21"][k] - x[k]).max() <= 1e-9 * max(1.0, np.abs(x[k]).max())
+        if not pb.imu[k]:
+            assert np.array_equal(r["kfs21"][k, 12:], lm.state21(pb.kfs[k])[12:])
+    assert np.abs(r["pts"] - np.array(X)).max() <= 1e-9 * np.abs(np.array(X)).max()
+
+
+def test_vertex_pose_only_recovers_truth():
+    pb = synth.lia_problem(14, n_opt=10, no_imu=(4,))
+    r = oracle.lia(pb)
+    assert r["stats"][1] < 0.6 * r["stats"][0]
+    for k in range(10):
+        assert np.linalg.norm(r["kfs21"][k, 9:12] - pb.kfs_true[k]["twb"]) < 1.5e-2
+
+
+def test_banded_window_generator():
+    """consecutive observers: every point's key frames are adjacent in the
+    window order (a banded reduced system)."""
+    pb = synth.lia_problem(15, n_opt=12, n_fixed_cov=2, n_pts=300, max_obs=3, consecutive=True)
+    kfs_of = {}
+    for e in pb.edges:
+        kfs_of.setdefault(int(e["point"]), []).append(int(e["kf"]))
+    span = np.array([max(v) - min(v) for v in kfs_of.values()])
+    assert (span == 2).mean() > 0.95 and span.max() <= 10
