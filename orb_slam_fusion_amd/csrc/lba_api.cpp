@@ -20,6 +20,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <thread>
 #include <vector>
@@ -146,6 +147,55 @@ struct WindowOut {
   int n_out = 0;
 };
 
+// The point-major Schur layout (LbaArgs::sc_*, k_lba_schur_band): the
+// shard's points with a free edge ordered by their lowest free pose (a stable
+// counting sort), cut greedily into chunks whose free poses span at most
+// kSchurBandMax poses and whose W_all + H_all (64 bytes x points x padded band
+// rows) fit kSchurChunkLds.  O(points + edges); ok = false (the pair kernel)
+// when one point alone spans a wider band.
+struct SchurChunks {
+  std::vector<int> order, tile0{0};
+  std::vector<int4> chunk;
+  bool ok = false;
+};
+
+void build_schur_chunks(int np, int nf, const std::vector<int>& cnt, const std::vector<int>& pf,
+                        SchurChunks& sc) {
+  if (nf == 0) return;
+  std::vector<int> lo(np, -1), hi(np, -1), start(nf + 1, 0);
+  for (int p = 0; p < np; ++p) {
+    for (int u = cnt[p]; u < cnt[p + 1]; ++u)
+      if (pf[u] >= 0) {
+        lo[p] = lo[p] < 0 ? pf[u] : std::min(lo[p], pf[u]);
+        hi[p] = std::max(hi[p], pf[u]);
+      }
+    if (lo[p] >= 0) {
+      if (hi[p] - lo[p] + 1 > kSchurBandMax) return;
+      ++start[lo[p] + 1];
+    }
+  }
+  for (int f = 0; f < nf; ++f) start[f + 1] += start[f];
+  sc.order.resize(start[nf]);
+  for (int p = 0; p < np; ++p)
+    if (lo[p] >= 0) sc.order[start[lo[p]]++] = p;
+  for (size_t i = 0; i < sc.order.size();) {
+    const int b0 = lo[sc.order[i]];
+    int top = hi[sc.order[i]];
+    size_t j = i + 1;
+    for (; j < sc.order.size(); ++j) {
+      const int t = std::max(top, hi[sc.order[j]]);
+      if (t - b0 + 1 > kSchurBandMax || 64 * (int)(j - i + 1) * schur_band_rows(t - b0 + 1) > kSchurChunkLds)
+        break;
+      top = t;
+    }
+    const int w = top - b0 + 1, T = schur_band_rows(w) / 16;
+    sc.chunk.push_back(make_int4((int)i, (int)(j - i), b0, w));
+    sc.tile0.push_back(sc.tile0.back() + T * (T + 1) / 2);
+    i = j;
+  }
+  sc.ok = true;
+}
+
 // The shared body of orbgpu_lba_optimize / orbgpu_lia_optimize: layout,
 // one upload, the device LM loop (or the host-in-the-loop sharded form), the
 // outlier classification and one download.
@@ -189,8 +239,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // when some point of the shard is seen by both (the other blocks stay the
   // zeros the per-call clear leaves; a sharded rank's zeros add nothing)
   std::vector<int> pair_list;
+  std::vector<int> pf(std::max(ne, 1));  // free-pose index of each point-major edge (-1: fixed)
   {
-    std::vector<int> pf(std::max(ne, 1)), fill(cnt.begin(), cnt.end() - 1);
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
     for (int i = 0; i < n_edges; ++i) {
       const orbgpu_lba_edge& e = edges[i];
       if (e.point >= pt_begin && e.point < pt_end) pf[fill[e.point - pt_begin]++] = hidx[e.kf];
@@ -211,6 +262,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
         }
   }
   const int n_pairs = (int)pair_list.size() / 2;
+  SchurChunks sc;
+  build_schur_chunks(np, nf, cnt, pf, sc);
   std::vector<int> gidx(ne);  // shard edge -> caller's edge index
   std::vector<int> pose_cnt(nf + 1, 0);
   // IMU links incident to each free key frame (link order)
@@ -233,6 +286,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const int nblk = (int)((std::max(std::max(ne, np), 1) + 255) / 256) + nf + 1;
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)1);
+  // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order
+  const size_t n_sc = sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1;
   size_t up = 0;
   const size_t u_ctrl = up;
   up += 128;
@@ -242,6 +297,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   up = align_up(up + sizeof(LbaEdgeDev) * E, 256);
   const size_t u_ints = up;
   up = align_up(up + sizeof(int) * n_ints, 256);
+  const size_t u_sc = up;
+  up = align_up(up + sizeof(int) * n_sc, 256);
   const size_t u_state = up;
   up = align_up(up + sizeof(double) * (2 * KS + 2 * P3), 256);
   const size_t u_imu = up;
@@ -271,7 +328,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_work = take(lba_solve_work_doubles(solve_mode, npad)),
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
-               c_itot = take(2 + NI);  // [0] total, [2 + l] per link
+               c_itot = take(2 + NI),  // [0] total, [2 + l] per link
+               c_scp = take(sc.ok ? 256 * (size_t)sc.tile0.back() : 1);
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
@@ -330,6 +388,12 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::copy(free_kf.begin(), free_kf.end(), I_fk);
   std::copy(inc.begin(), inc.end(), I_inc);
   std::copy(inc_list.begin(), inc_list.end(), I_incl);
+  int* const SC = reinterpret_cast<int*>(U + u_sc);
+  if (sc.ok) {
+    std::memcpy(SC, sc.chunk.data(), sizeof(int4) * sc.chunk.size());
+    std::memcpy(SC + 4 * sc.chunk.size(), sc.tile0.data(), sizeof(int) * sc.tile0.size());
+    std::memcpy(SC + 4 * sc.chunk.size() + sc.tile0.size(), sc.order.data(), sizeof(int) * sc.order.size());
+  }
   auto* S0 = reinterpret_cast<double*>(U + u_state);
   std::copy(m.state0, m.state0 + KS, S0);
   std::copy(m.state0, m.state0 + KS, S0 + KS);
@@ -355,6 +419,14 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.n_free = nf;
   a.n_sys = n;
   a.n_pairs = n_pairs;
+  if (sc.ok) {
+    const int* dS = reinterpret_cast<const int*>(A + u_sc);
+    a.n_chunks = (int)sc.chunk.size();
+    a.sc_chunk = reinterpret_cast<const int4*>(dS);
+    a.sc_tile0 = dS + 4 * sc.chunk.size();
+    a.sc_order = dS + 4 * sc.chunk.size() + sc.tile0.size();
+    a.sc_part = dp(c_scp);
+  }
   a.sharded = reduce ? 1 : 0;
   a.solve_mode = solve_mode;
   a.n_pad = npad;

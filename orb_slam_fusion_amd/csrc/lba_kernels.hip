@@ -777,6 +777,186 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
   }
 }
 
+// ---- Schur complement, point-major (block_solver.hpp:392-460 visits each
+// landmark once): one block per chunk of points (lba_api.cpp orders the points
+// by their lowest free pose and cuts chunks spanning <= kSchurBandMax poses).
+// The chunk's part of S_ij = sum_p W_pi Hpl_pj^T (W = Hpl (Hll + lambda I)^-1)
+// and of b_s = sum_p W_pi bl_p is one matrix product over the chunk:
+//   W_all (band rows x 4 per point) . H_all^T,
+// row 6 (f - b0) + s of point p's slice holding W_pe[s] (H: Hpl_pe[s]) for
+// its edge e to free pose f, zeros for the band's other poses, and one more H
+// row holding bl_p (so the product's last column is W bl).
+//   1. a thread per point: (Hll + lambda I)^-1 once, W for each of its free
+//      edges, both slices into LDS (component-major: conflict-free MFMA reads);
+//   2. a wave per upper 16 x 16 tile of the product: one
+//      v_mfma_f64_16x16x4f64 per point (k-step = the point's 3 components +
+//      a zero), two accumulators for the even / odd points (ILP), added at
+//      the end -- a fixed order, reproducible run to run;
+//   3. the upper tiles to HBM; k_lba_schur_sum adds each pose pair's entries
+//      over the chunks covering it, in chunk order.
+// Each edge's Hll / Hpl / bl are read once per trial (the pair kernel below
+// re-reads a pose's edges for every pair it is in).
+constexpr int kBandThreads = 256;
+constexpr int kBandWaves = kBandThreads / 64;
+
+__global__ __launch_bounds__(kBandThreads) void k_lba_schur_band(LbaArgs a) {
+  extern __shared__ double sb[];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const double lambda = c.lambda;
+  const int4 ch = a.sc_chunk[blockIdx.x];  // {first in sc_order, points, b0, w}
+  const int P = ch.y, b0 = ch.z, w = ch.w;
+  const int NB = schur_band_rows(w), T = NB >> 4;
+  double* const sW = sb;                        // [P][4][NB]
+  double* const sH = sb + (size_t)P * 4 * NB;   // [P][4][NB]
+  const int t = threadIdx.x;
+  {
+    double2* z = reinterpret_cast<double2*>(sb);
+    const int n2 = P * 4 * NB;  // (2 * P * 4 * NB doubles)
+    for (int k = t; k < n2; k += kBandThreads) z[k] = make_double2(0.0, 0.0);
+  }
+  __syncthreads();
+  for (int k = t; k < P; k += kBandThreads) {
+    const int p = a.sc_order[ch.x + k];
+    double hll[9], bl[3];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) hll[q] = a.hll[9 * (size_t)p + q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) bl[q] = a.bl[3 * (size_t)p + q];
+    double Di[9];
+    inv3_lambda(hll, lambda, Di);
+    double* const wk = sW + (size_t)k * 4 * NB;
+    double* const hk = sH + (size_t)k * 4 * NB;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) hk[q * NB + 6 * w] = bl[q];
+    const int u0 = a.pt_begin[p], u1 = a.pt_begin[p + 1];
+    for (int ub = u0; ub < u1; ub += 4) {  // four edges' loads in flight
+      int fs[4];
+      double B[4][18];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) fs[v] = ub + v < u1 ? a.ef[ub + v] : -1;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int q = 0; q < 18; ++q) B[v][q] = fs[v] >= 0 ? a.hpl[18 * (size_t)(ub + v) + q] : 0.0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if (fs[v] < 0) continue;
+        const int r0 = 6 * (fs[v] - b0);
+#pragma unroll
+        for (int s6 = 0; s6 < 6; ++s6)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            hk[q * NB + r0 + s6] = B[v][3 * s6 + q];
+            wk[q * NB + r0 + s6] =
+                B[v][3 * s6] * Di[q] + B[v][3 * s6 + 1] * Di[3 + q] + B[v][3 * s6 + 2] * Di[6 + q];
+          }
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = t & 63, li = lane & 15, lk = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  double* const part = a.sc_part + 256 * (size_t)a.sc_tile0[blockIdx.x];
+  for (int q = wave, I = 0, J = wave; q < T * (T + 1) / 2; q += kBandWaves) {
+    while (J >= T) {  // tile q -> (I, J), J >= I, row-major over the upper triangle
+      J -= T - I;
+      ++I;
+      J += 1;
+    }
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+    int k = 0;
+    for (; k + 1 < P; k += 2) {
+      const double a0 = sW[((size_t)k * 4 + lk) * NB + 16 * I + li];
+      const double c0 = sH[((size_t)k * 4 + lk) * NB + 16 * J + li];
+      const double a1 = sW[((size_t)(k + 1) * 4 + lk) * NB + 16 * I + li];
+      const double c1 = sH[((size_t)(k + 1) * 4 + lk) * NB + 16 * J + li];
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, c0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, c1, acc1, 0, 0, 0);
+    }
+    if (k < P) {
+      const double a0 = sW[((size_t)k * 4 + lk) * NB + 16 * I + li];
+      const double c0 = sH[((size_t)k * 4 + lk) * NB + 16 * J + li];
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, c0, acc0, 0, 0, 0);
+    }
+    // C[lk + 4 rr][li] of tile q
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) part[256 * (size_t)q + (lk + 4 * rr) * 16 + li] = acc0[rr] + acc1[rr];
+    J += kBandWaves;
+  }
+}
+
+// one wave per pose pair (fi <= fj): the entries of its block (and, for a
+// diagonal pair, of b_s) summed over the chunks whose band covers both poses,
+// in chunk order, then written as k_lba_schur writes them (a diagonal block
+// from its upper entries, mirrored: exactly symmetric)
+constexpr int kSumChunksLds = 1024;
+
+__global__ __launch_bounds__(64) void k_lba_schur_sum(LbaArgs a) {
+  __shared__ int4 sch[kSumChunksLds];
+  __shared__ int st0[kSumChunksLds];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const int pr = blockIdx.x, t = threadIdx.x;
+  const int fi = a.pair_i[pr], fj = a.pair_j[pr];
+  const bool diag = fi == fj;
+  const int s = t < 36 ? t / 6 : t - 36, q = t < 36 ? t - 6 * (t / 6) : 0;
+  const bool live = t < 36 ? (!diag || s <= q) : (diag && t < 42);
+  // covering chunks have b0 in [fj - kSchurBandMax + 1, fi] (chunks sorted by b0)
+  int lo = 0, hi = a.n_chunks;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a.sc_chunk[mid].z < fj - kSchurBandMax + 1)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  double sum = 0;
+  for (int c0 = lo; c0 < a.n_chunks; c0 += kSumChunksLds) {
+    const int nc = min(kSumChunksLds, a.n_chunks - c0);
+    __syncthreads();
+    for (int k = t; k < nc; k += 64) {
+      sch[k] = a.sc_chunk[c0 + k];
+      st0[k] = a.sc_tile0[c0 + k];
+    }
+    __syncthreads();
+    bool past = false;
+    for (int k = 0; k < nc; k += 4) {  // four chunks' loads in flight, summed in order
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = 0.0;
+        if (k + u >= nc) continue;
+        const int4 ck = sch[k + u];
+        if (ck.z > fi) {
+          past = true;
+          continue;
+        }
+        if (!live || fj >= ck.z + ck.w) continue;
+        const int T = schur_band_rows(ck.w) >> 4;
+        const int row = 6 * (fi - ck.z) + s, col = t < 36 ? 6 * (fj - ck.z) + q : 6 * ck.w;
+        const int I = row >> 4, J = col >> 4;  // I <= J: fi < fj, s <= q on the diagonal, or the bl column
+        const int tile = I * T - I * (I - 1) / 2 + (J - I);
+        v[u] = a.sc_part[256 * ((size_t)st0[k + u] + tile) + (row & 15) * 16 + (col & 15)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sum += v[u];
+      if (__builtin_amdgcn_readfirstlane(past ? 1 : 0)) break;
+    }
+    if (past) break;
+  }
+  const int n = a.n_sys, P = a.pdim;
+  if (!live) return;
+  if (t < 36) {
+    const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
+    a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
+    a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
+  } else {
+    a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
+    a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
+  }
+}
+
 // ---- reduced camera system (S + lambda I) x = b_s: L D L^T by 16 x 16 tiles
 // (linear_solver_eigen.h:93-126 factorises the same matrix with
 // SimplicialLDLT; the factorisation order here is natural, tiled).
@@ -1198,7 +1378,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
     for (int q = 0; q < 7; ++q)
       if (kRowWave[q] == wave) slot = q;
-    if (wave == 0) diag_tile(0);
+    if (wave == 0 && T > 0) diag_tile(0);  // (T == 0: every key frame fixed, nothing to factor)
     __syncthreads();
     LBA_STAMP(1);
     for (int K = 0; K < T - 1; ++K) {
@@ -1741,17 +1921,44 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   __shared__ double sOJ[9 * 24];
   __shared__ double sE[9];       // the link's error (inertial_edge_core, lane 0)
   __shared__ double sInfo[81];   // the link's information (x1e-2 when downweighted)
+  __shared__ LiaImuDev sL;       // the link (preintegration) and the two key-frame states,
+  __shared__ double sS[2 * kImuStateStride];  // staged in one round trip
   const int lane = threadIdx.x;
   const int l = blockIdx.x;      // (grid max(n_imu, 1): block 0 alone when there is no link)
   const double* st = a.poses[trial ? c.state ^ 1 : c.state];
   double chi_link = 0;
   if (l < a.n_imu) {
-    const LiaImuDev& E = a.imu[l];
+    {
+      // every load in flight before the first store: the edge chain below
+      // then reads LDS, not one HBM round trip per field it reaches
+      constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
+      static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
+      const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
+      uint32_t w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
+      double sv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
+        sv[u] = k < 2 * kImuStateStride ? st[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
+      }
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&sL);
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (lane + 64 * u < 2 * kImuStateStride) sS[lane + 64 * u] = sv[u];
+      wave_lds_sync();
+    }
+    const LiaImuDev& E = sL;
     const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
     for (int k = lane; k < 81; k += 64) sInfo[k] = E.pi.info[k] * isc;
     StateD s1, s2;
-    load_state(s1, st + kImuStateStride * E.kf1);
-    load_state(s2, st + kImuStateStride * E.kf2);
+    load_state(s1, sS);
+    load_state(s2, sS + kImuStateStride);
     double* J = sJ;
     if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
       for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
@@ -2022,7 +2229,15 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
 }
 
 hipError_t lba_schur(const LbaArgs& a, hipStream_t st) {
-  if (a.n_pairs > 0) hipLaunchKernelGGL(k_lba_schur, dim3(a.n_pairs), dim3(kSchurThreads), 0, st, a);
+  if (a.n_pairs <= 0) return hipSuccess;
+  if (a.n_chunks > 0) {
+    if (lds_optin(reinterpret_cast<const void*>(&k_lba_schur_band), kSchurChunkLds) != hipSuccess)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_lba_schur_band, dim3(a.n_chunks), dim3(kBandThreads), kSchurChunkLds, st, a);
+    hipLaunchKernelGGL(k_lba_schur_sum, dim3(a.n_pairs), dim3(64), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_lba_schur, dim3(a.n_pairs), dim3(kSchurThreads), 0, st, a);
+  }
   return hipGetLastError();
 }
 

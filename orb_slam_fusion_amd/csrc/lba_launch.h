@@ -87,6 +87,21 @@ struct LbaArgs {
   const int* ef;             // [n_edges] free-pose index of each edge (edges[i].f, packed)
   const int* pair_i;         // [n_pairs] free-pose pairs (i <= j), row-major upper triangle
   const int* pair_j;
+  // point-major Schur complement (k_lba_schur_band + k_lba_schur_sum): the
+  // shard's points with a free edge, ordered by their lowest free pose (a
+  // counting sort), cut into chunks whose free poses span a band of at most
+  // kSchurBandMax poses [b0, b0 + w).  A chunk's part of the Schur complement
+  // is the MFMA product W_all H_all^T over its points (W_all / H_all: the
+  // band's 6 w rows x 4 columns per point, each point's W = Hpl (Hll +
+  // lambda I)^-1 / Hpl in its poses' rows, zeros elsewhere; one more H row
+  // holds bl, so the product also carries W bl).  n_chunks == 0: one block
+  // per pose pair (k_lba_schur) -- a point whose free poses span more than
+  // kSchurBandMax.
+  int n_chunks;
+  const int* sc_order;   // [points with a free edge] shard point index, chunk order
+  const int4* sc_chunk;  // [n_chunks] {first in sc_order, points, b0, w}
+  const int* sc_tile0;   // [n_chunks + 1] first partial tile of each chunk (256 doubles a tile)
+  double* sc_part;       // the chunks' upper product tiles
   double* poses[2];          // [7 n_kf] current / trial state (ctrl.state selects)
   double* pts[2];            // [3 n_pts]
   double* err;               // [3 E] errors of the last computeActiveErrors
@@ -138,6 +153,12 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
 // outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles)
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
+constexpr int kSchurBandMax = 15;        // free poses a Schur chunk spans (6 w + 1 <= 96 rows)
+constexpr int kSchurChunkLds = 120 * 1024;  // W_all + H_all of a chunk: 64 x points x padded rows bytes
+
+// padded product rows of a band of w poses (6 w rows + the bl row, to the 16-row MFMA tile)
+__host__ __device__ inline int schur_band_rows(int w) { return (6 * w + 1 + 15) / 16 * 16; }
+
 // the solver path for an n_pad-row system, and the doubles of a.work it needs
 int lba_solve_mode(int n_pad);
 bool lba_solve_mode_fits(int mode, int n_pad);

@@ -502,12 +502,16 @@ __device__ __forceinline__ ushort2_t max2(ushort2_t a, ushort2_t b) {
   return __builtin_elementwise_max(a, b);
 }
 
-// S(p) for the pixel at p (ROI bytes, row stride ls), clamped below at 0.
-// Dark and bright arcs run together as a packed f16 pair: a byte b becomes the
-// f16 1024 + b (bit pattern 0x6400 | b, ulp 1 on [1024, 2048)), so
-// x_k = (v - p_k, p_k - v) is exact, and the 9-arc minima and their maximum
-// are v_pk_minimum3_f16 / v_pk_maximum3_f16 on exact integers:
-// m3_k = min(x_k..x_k+2), arc_k = min(m3_k, m3_k+3, m3_k+6), 40 packed ops.
+// The FAST score of the pixel at p (ROI bytes, row stride ls) as the larger
+// of the dark / bright arc maxima m = S + 1 (cornerScore<16>'s b0 negated).
+// Dark and bright arcs run together as a packed f16 pair: a byte b loaded
+// zero-extended is the f16 denormal b * 2^-24, so x_k = (p_k - v, v - p_k)
+// is ONE v_pk_add_f16 of the two loaded registers (op_sel picks both low
+// halves for both results, neg the other source per half) and exact, and the
+// 9-arc minima and their maximum are v_pk_minimum3_f16 / v_pk_maximum3_f16 on
+// exact multiples of 2^-24 (the kernel keeps f16 denormals: the default
+// denorm mode 16/64 = 3): m3_k = min(x_k..x_k+2), arc_k = min(m3_k, m3_k+3,
+// m3_k+6), 40 packed ops.  The bit pattern of a non-negative m is m * 2^24.
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2_t hmin3(half2_t a, half2_t b, half2_t c) {
   return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
@@ -515,18 +519,18 @@ __device__ __forceinline__ half2_t hmin3(half2_t a, half2_t b, half2_t c) {
 __device__ __forceinline__ half2_t hmax3(half2_t a, half2_t b, half2_t c) {
   return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
-__device__ __forceinline__ int fast_score(const uint8_t* p, int ls) {
+__device__ __forceinline__ half2_t ring_diff(uint32_t pk, uint32_t v) {
+  half2_t x;
+  asm("v_pk_add_f16 %0, %1, %2 op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(x) : "v"(pk), "v"(v));
+  return x;
+}
+__device__ __forceinline__ _Float16 fast_arc_max(const uint8_t* p, int ls) {
   constexpr int cx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
   constexpr int cy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-  const uint32_t vb = (uint32_t)p[0] | 0x64006400u;
+  const uint32_t vb = (uint32_t)p[0];
   half2_t x[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    // (vb.b0, 0x64, p_k, 0x64): one v_perm_b32
-    const half2_t r = __builtin_bit_cast(
-        half2_t, __builtin_amdgcn_perm((uint32_t)p[cx[k] + cy[k] * ls], vb, 0x03040100u));
-    x[k] = r - r.yx;
-  }
+  for (int k = 0; k < 16; ++k) x[k] = ring_diff((uint32_t)p[cx[k] + cy[k] * ls], vb);
   half2_t m3[16], a[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) m3[k] = hmin3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
@@ -536,7 +540,7 @@ __device__ __forceinline__ int fast_score(const uint8_t* p, int ls) {
 #pragma unroll
   for (int k = 3; k < 15; k += 2) b = hmax3(b, a[k], a[k + 1]);
   b = __builtin_elementwise_maximum(b, a[15]);
-  return max((int)__builtin_fmaxf((float)b.x, (float)b.y) - 1, 0);
+  return __builtin_fmaxf16(b.x, b.y);
 }
 
 // compass value of 4 pixels (two u16 pairs): corner at th => value > th
@@ -566,6 +570,14 @@ __device__ __forceinline__ int wave_iscan(int v) {
 
 constexpr int kFastPf = 12;  // ROI dwords in flight per lane (one round trip up to 768)
 
+// LS > 0: the plan's LDS row pitch for every cell (PlanHeader::fast_pitch:
+// the smallest of 48..64 that holds each cell's ROI row and score-map row;
+// 48 at 752 x 480).  The ROI and the score map then share that compile-time
+// pitch and a survivor is its own pixel offset r * LS + q -- every ring / NMS
+// neighbour address is base + immediate, the score-map index i + LS + 1 (no
+// per-survivor row multiplies or offset adds).  LS = 0: pitches per cell,
+// survivors r << 7 | q.
+template <int LS>
 __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict__ P,
                                                    const Cell* __restrict__ cells, ImgSrc src,
                                                    const uint8_t* __restrict__ pyr,
@@ -590,13 +602,22 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   // dw + 2), u16 survivor list, u32 list of the 8-pixel groups holding a
   // survivor.  A survivor is r << 7 | q (detection row, column; dw < 128,
   // dh < 256 by the planner), bit 15 = keypoint flag.
-  const int ls = (c.cols + 6) & ~3;
-  const int sp2 = dw + 2, nsc = sp2 * (dh + 2);
+  constexpr int QB = 7, QM = (1 << QB) - 1;  // (LS == 0) survivor index r << QB | q
+  const int ls = LS ? LS : (c.cols + 6) & ~3;
+  const int sp2 = LS ? LS : dw + 2, nsc = sp2 * (dh + 2);
   uint8_t* roi = lds;
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
   uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
   uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) + ((2 * nd + 15) & ~15));
-  auto sci = [&](int i) { return ((i >> 7) + 1) * sp2 + (i & 127) + 1; };
+  auto sci = [&](int i) {
+    if constexpr (LS != 0) return i + LS + 1;
+    return ((i >> QB) + 1) * sp2 + (i & QM) + 1;
+  };
+  // a survivor's pixel in the ROI, relative to detection pixel (0, 0)
+  auto px = [&](int i) -> int {
+    if constexpr (LS != 0) return i;
+    return (int)__umul24((uint32_t)i >> QB, (uint32_t)ls) + (i & QM);
+  };
 
   // ---- ROI -> LDS: raw dwords, all loads in flight before the first store
   int sp;
@@ -623,7 +644,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
           v[u] = *reinterpret_cast<const uint32_t*>(Sa + (__umul24(rr[u], (uint32_t)sp) + q4));
 #pragma unroll
         for (int u = 0; u < kFastPf; ++u)
-          *reinterpret_cast<uint32_t*>(roi + (__umul24(rr[u], (uint32_t)ls) + q4)) = v[u];
+          *reinterpret_cast<uint32_t*>(roi + ((LS ? rr[u] * (uint32_t)LS : __umul24(rr[u], (uint32_t)ls)) + q4)) = v[u];
       }
     } else {
       for (int i = lane; i < c.rows * ndw; i += 64) {
@@ -665,11 +686,13 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
     int ng = 0;
     const ushort2_t thv = {(unsigned short)(0x7fff - th), (unsigned short)(0x7fff - th)};
+    const _Float16 thp1 = __builtin_bit_cast(_Float16, (uint16_t)(th + 1));  // (th + 1) * 2^-24, exact
     auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
     for (int r = g_r0, g = g_q0;;) {
       const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
       if (mrv == 0) break;
-      const uint8_t* C = roi + __umul24((uint32_t)(min(r, dh - 1) + 3), (uint32_t)ls) + 8 * g;
+      const uint32_t cr = (uint32_t)(min(r, dh - 1) + 3);
+      const uint8_t* C = roi + (LS ? cr * (uint32_t)LS : __umul24(cr, (uint32_t)ls)) + 8 * g;
       // window of 8 centre-relative pixels at row byte o as four u16 pairs
       // (pixels 2j, 2j + 1): one two-source v_perm each straight from the
       // three dwords covering the window (wave-uniform selectors, no align)
@@ -711,7 +734,13 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       // order; the per-pixel list is expanded below, once per 64 entries
       const bool has = r < dh && m7 != 0;
       const uint64_t mg = bal(has);
-      if (has) ge[mbcnt64(mg, (uint32_t)ng)] = (uint32_t)((r << 7) | (8 * g)) | (m7 << 9);
+      if (has) {
+        // LS > 0: the row's tail group keeps its first `tail` pixels here (the
+        // entry then holds only valid pixels); LS == 0 drops them at the expansion
+        const uint32_t mv = LS ? (g == gpr - 1 ? m7 & (tail_mask << 7) : m7) : m7;
+        const uint32_t i0 = LS ? (uint32_t)(r * LS + 8 * g) : (uint32_t)((r << QB) | (8 * g));
+        ge[mbcnt64(mg, (uint32_t)ng)] = i0 | (mv << 9);
+      }
       ng += __popcll(mg);
       g += g_dq;
       r += g_dr;
@@ -730,7 +759,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint32_t e = j < ng ? ge[j] : 0u;
       const int i0 = (int)(e & 0xffffu);
       // the row's tail group keeps its first `tail` pixels
-      uint32_t m = (e >> 16) & (((i0 >> 3) & 15) == gpr - 1 ? tail_mask : 0xffu);
+      uint32_t m = LS ? (e >> 16) & 0xffu : (e >> 16) & (((i0 >> 3) & ((1 << (QB - 3)) - 1)) == gpr - 1 ? tail_mask : 0xffu);
       const int cnt = __popc(m);
       const int incl = wave_iscan(cnt);
       int pos = ns + incl - cnt;
@@ -744,8 +773,11 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     STAMP(0);
     for (int j = lane; j < ns; j += 64) {
       const int i = sv[j];
-      const int s = fast_score(base + __umul24((uint32_t)i >> 7, (uint32_t)ls) + (i & 127), ls);
-      sc[sci(i)] = (uint8_t)(s >= th ? s : 0);
+      // S = max(m - 1, 0) is a corner's score iff m >= th + 1 (then m > 0
+      // and its bit pattern is the integer m)
+      const _Float16 m = fast_arc_max(base + px(i), ls);
+      const uint16_t bits = __builtin_bit_cast(uint16_t, m);
+      sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
     }
     __syncthreads();
     STAMP(1);
@@ -794,7 +826,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     const uint64_t m = __ballot(k);
     if (k) {
       const int i = e & 0x7fff;
-      const int r = i >> 7, q = i & 127;
+      const int r = LS ? i / LS : i >> QB, q = LS ? i - r * LS : i & QM;
       const int pos = written + __popcll(m & lt);
       if (pos < c.slot_cap)
         out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)sc[sci(i)] << 24);
@@ -1531,7 +1563,13 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   hipLaunchKernelGGL(k_blur, dim3(n * H.blur_tiles), dim3(256), 0, st, a.plan, src,
                      (const uint8_t*)a.pyr, a.blur);
   mark(2);
-  hipLaunchKernelGGL(k_fast_cells, dim3(n * H.n_cells), dim3(64), H.max_roi_lds, st, a.plan,
+  auto fast = H.fast_pitch == 48   ? k_fast_cells<48>
+              : H.fast_pitch == 52 ? k_fast_cells<52>
+              : H.fast_pitch == 56 ? k_fast_cells<56>
+              : H.fast_pitch == 60 ? k_fast_cells<60>
+              : H.fast_pitch == 64 ? k_fast_cells<64>
+                                   : k_fast_cells<0>;
+  hipLaunchKernelGGL(fast, dim3(n * H.n_cells), dim3(64), H.max_roi_lds, st, a.plan,
                      a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count);
   mark(3);
   hipLaunchKernelGGL(k_octree, dim3(n * H.levels), dim3(kOctThreads), a.octree_lds, st, a.plan,

@@ -78,7 +78,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   out.cells.clear();
   out.rs_tab.clear();
   int pyr = 0, blur = 0, slots = 0, kps = 0, tiles = 0, max_roi = 0, node_cap = 64, rs_lds = 0;
-  int max_roi_lds = 0;
+  int max_roi_lds = 0, need_pitch = 0;
   for (int l = 0; l < L; ++l) {
     LevelGeom& g = P.lev[l];
     g.w = cv_round((float)W * out.inv_scale[l]);  // :1096
@@ -186,6 +186,8 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         slots += c.slot_cap;
         max_roi = std::max(max_roi, c.cols * c.rows);
         max_roi_lds = std::max(max_roi_lds, fast_cell_lds_bytes(c.cols, c.rows));
+        // the ROI row (lead <= 3 + cols) and the score-map row (dw + 2) in one pitch
+        need_pitch = std::max(need_pitch, std::max(c.cols + 3, dw + 2));
         if (dw > 127 || dh > 255)  // k_fast_cells survivor encoding r << 7 | q
           return why = "FAST cell too large", false;
         out.cells.push_back(c);
@@ -214,6 +216,16 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   P.node_cap = (node_cap + 63) & ~63;
   P.blur_tiles = tiles;
   P.max_roi = (max_roi + 15) & ~15;
+  P.fast_pitch = 0;
+  for (int pt = 48; pt <= 64; pt += 4)
+    if (need_pitch <= pt) {
+      P.fast_pitch = pt;
+      break;
+    }
+  if (P.fast_pitch) {
+    max_roi_lds = 0;
+    for (const Cell& c : out.cells) max_roi_lds = std::max(max_roi_lds, fast_cell_lds_bytes_pitch(c.cols, c.rows, P.fast_pitch));
+  }
   P.max_roi_lds = (max_roi_lds + 15) & ~15;
   P.rs_lds = (rs_lds + 15) & ~15;
   if (P.rs_lds > 160 * 1024) return why = "scale factor too large for the resize tile", false;
@@ -232,6 +244,15 @@ int fast_cell_lds_bytes(int cols, int rows) {
   const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
   const int nsc = std::max(cols - 4, 0) * std::max(rows - 4, 0);
   return ((ls * rows + 15) & ~15) + ((nsc + 15) & ~15) + ((2 * nd + 15) & ~15) + 4 * ng + 16;
+}
+
+// The same with the plan's fixed pitch for the ROI and the score-map rows
+// (k_fast_cells<pitch>), plus slack for the compass windows' reads past a
+// row's last group.
+int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch) {
+  const int dw = std::max(cols - 6, 0), dh = std::max(rows - 6, 0);
+  const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
+  return ((pitch * rows + 15) & ~15) + ((pitch * (dh + 2) + 15) & ~15) + ((2 * nd + 15) & ~15) + 4 * ng + 16 + 16;
 }
 
 size_t octree_lds_bytes(const PlanHeader& P) {

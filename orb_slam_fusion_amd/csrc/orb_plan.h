@@ -62,6 +62,7 @@ struct PlanHeader {
   int blur_tiles;   // per image
   int max_roi;      // largest cell ROI (bytes)
   int max_roi_lds;  // LDS bytes of one FAST cell (staged ROI + score map + lists)
+  int fast_pitch;   // 48..64: the LDS row pitch of every FAST cell (k_fast_cells<pitch>); 0 = per cell
   int rs_lds;       // LDS bytes of one resize tile
   int umax[16];     // circular patch extents (:452-464)
   LevelGeom lev[kMaxLevels];

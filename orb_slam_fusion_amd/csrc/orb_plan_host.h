@@ -24,5 +24,6 @@ bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out,
                int resize_rounding = 0);
 size_t octree_lds_bytes(const PlanHeader& P);
 int fast_cell_lds_bytes(int cols, int rows);
+int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch);
 
 }  // namespace orbgpu

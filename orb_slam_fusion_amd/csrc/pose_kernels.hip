@@ -312,7 +312,7 @@ struct PoseShared {
   double hb[28];                        // chi2, H (lower, 21), b (6) at the current pose
   double hf[36];                        // H as the full row-major 6x6 (the solves' gathers)
   double chi[2][G][kPoseWaves];         // trial chi2 wave partials, double-buffered by round
-  double trial[2][G][14];               // x (6), Tn (qx qy qz qw t0 t1 t2), ok
+  double trial[16][14];                 // an iteration's trials q < 10: x (6), Tn (qx qy qz qw t0 t1 t2), ok
   double init[7];                       // the input pose (qx qy qz qw t0 t1 t2)
   int ired[G * kPoseWaves];
   int pcnt[2][G * kPoseWaves];          // observation partition: stereo / mono per wave
@@ -606,30 +606,29 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
       double rho = 0;
       int q = 0;
       bool accepted = false, done = false;
-      do {
-        // the thread indices are opaque to the optimiser here, so the loop
-        // body's thread-predicate compares are not hoisted into long-lived
-        // SGPR lane masks
-        asm volatile("" : "+v"(t), "+v"(tg), "+v"(lane), "+v"(gw));
-        asm volatile("" : "+s"(wtype), "+s"(wbeg), "+s"(wend));
-        // this group's trial (q + grp): the lambda the sequential loop would
-        // reach after grp more rejections
-        double lg = lambda, ng = ni;
-        for (int k = 0; k < grp; ++k) {
-          lg *= ng;
-          ng *= 2;
+      // Every trial of this iteration up front: g2o retries a rejected step on
+      // the same system with lambda *= ni, ni *= 2, so trial q solves
+      // H + lambda_q I with the lambda the sequential loop holds after q
+      // rejections (the same products in the same order).  The 16-lane rows of
+      // the block's waves take trials q = 4 wave + row at once (ldlt6_gj_rows,
+      // then the exp per row), so an iteration pays one solve + exp instead of
+      // one per trial; the sweeps below read trial[q].
+      PSTAMP(0);
+      __syncthreads();  // the previous iteration's readers of sh.trial are done
+      {
+        const int qq = (t >> 4) & (4 * NW - 1);
+        double lq = lambda, nq = ni;
+        for (int k = 0; k < min(qq, 10); ++k) {
+          lq *= nq;
+          nq *= 2;
         }
-        // each wave solves the (identical) 6x6 system lane-parallel: no
-        // broadcast barrier
         double x[6];
-        PSTAMP(0);
-        const bool ok = ldlt6_gj(hb, sh.hf, lg, x);
+        const bool ok = ldlt6_gj_rows(hb, sh.hf, lq, x);
         PSTAMP(2);
-        const Se3 Tn = se3_compose(se3_exp(x), T);
+        const Se3 Tn = se3_compose(se3_exp<false>(x), T);
         PSTAMP(3);
-        chi_sweep(Tn, sh.chi[buf][grp]);
-        if (tg == 0) {
-          double* tr = sh.trial[buf][grp];
+        if ((t & 15) == 0 && qq < 10) {
+          double* tr = sh.trial[qq];
 #pragma unroll
           for (int j = 0; j < 6; ++j) tr[j] = x[j];
           tr[6] = Tn.qx;
@@ -641,13 +640,25 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
           tr[12] = Tn.t[2];
           tr[13] = ok ? 1.0 : 0.0;
         }
+      }
+      __syncthreads();
+      do {
+        // the thread indices are opaque to the optimiser here, so the loop
+        // body's thread-predicate compares are not hoisted into long-lived
+        // SGPR lane masks
+        asm volatile("" : "+v"(t), "+v"(tg), "+v"(lane), "+v"(gw));
+        asm volatile("" : "+s"(wtype), "+s"(wbeg), "+s"(wend));
+        // this group's trial q + grp (precomputed above; past trial 9 the
+        // group idles: the sequential loop stops at 10)
+        PSTAMP(0);
+        if (q + grp < 10) chi_sweep(pose_at(sh.trial[q + grp] + 6), sh.chi[buf][grp]);
         __syncthreads();
         PSTAMP(4);
         PSTAMP_ADD(10, 1);
         // the outcomes in trial order, exactly as the sequential do-while
         const int gn = min(G, 10 - q);
         for (int g = 0; g < gn; ++g) {
-          const double* tr = sh.trial[buf][g];
+          const double* tr = sh.trial[q];
           const double* cg = sh.chi[buf][g];
           double tmp = cg[0];
 #pragma unroll

@@ -407,6 +407,51 @@ __device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmin
   }
 }
 
+// ldlt6_gj with a lambda per 16-lane row: the four rows of a wave solve four
+// systems H + lambda_r I at once (the row broadcasts never leave a row).  A
+// row with a zero pivot is redone alone by ldlt6_wave (Eigen's pivoting).
+// Every lane of row r returns row r's x and isPositive().
+__device__ __forceinline__ bool ldlt6_gj_rows(const double* hb, const double* hf, double lambda,
+                                              double (&x)[6]) {
+  const int lane = threadIdx.x & 63, li = lane & 15;
+  const double* row = hf + 6 * (li < 6 ? li : 0);
+  double w[12];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double h = row[j];
+    w[j] = li < 6 ? (li == j ? h + lambda : h) : 0.0;
+  }
+  w[6] = li < 6 ? hb[22 + li] : 0.0;
+#pragma unroll
+  for (int j = 7; j < 12; ++j) w[j] = 0.0;
+  double dmine = 1.0;
+  int flags = 0;
+  gj6_pivots<0>(w, li, dmine, flags);
+  const double z = li < 6 && fabs(dmine) > 1.0 / 1.79769313486231570815e+308 ? w[6] / dmine : 0.0;
+  x[0] = row16_bcast_f64<0>(z);
+  x[1] = row16_bcast_f64<1>(z);
+  x[2] = row16_bcast_f64<2>(z);
+  x[3] = row16_bcast_f64<3>(z);
+  x[4] = row16_bcast_f64<4>(z);
+  x[5] = row16_bcast_f64<5>(z);
+  bool ok = !(flags & 1);
+  const uint64_t zero = __builtin_amdgcn_ballot_w64((flags & 2) != 0);
+  if (zero) {
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r)
+      if ((zero >> (16 * r)) & 0xffffu) {
+        double xr[6];
+        const bool okr = ldlt6_wave(hb, readlane_f64(lambda, 16 * r), xr);
+        if ((lane >> 4) == r) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) x[k] = xr[k];
+          ok = okr;
+        }
+      }
+  }
+  return ok;
+}
+
 __device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, double lambda,
                                          double (&x)[6]) {
   // pivots in natural order: H + lambda I is symmetric positive definite

@@ -125,6 +125,14 @@ def test_lba_block_and_grid_solvers_identical(gpu_available, n_kf):
     _compare(p)
 
 
+def test_lba_point_seen_by_many_keyframes(gpu_available):
+    """Points observed by more free key frames than a Schur chunk holds (390 >
+    kSchurChunkEdges = 384): the one-block-per-pose-pair Schur kernel takes the
+    window -- one LM iteration against the oracle."""
+    p = synth.lba_problem(seed=26, n_kf=392, n_pts=12, obs_per_pt=390, n_fixed=2)
+    _compare(p, iters=1)
+
+
 def test_lba_all_fixed_and_empty(gpu_available):
     p = synth.lba_problem(seed=4, n_kf=4, n_pts=50, obs_per_pt=3, n_fixed=4)
     got = LocalBundleAdjuster().optimize(p)
