@@ -549,6 +549,9 @@ __device__ bool ldlt_wave(InShared& sh, int lane) {
   return true;
 }
 
+// relative size of a pivot treated as (near) zero by the natural-order solves
+constexpr double kGjNearZero = 1e-12;
+
 #include "inertial_gj.inc"
 
 // The same system by Gauss-Jordan elimination (tools/gen_inertial_gj.py):
@@ -560,9 +563,12 @@ __device__ bool ldlt_wave(InShared& sh, int lane) {
 // is symmetric positive definite whenever the step succeeds, where
 // elimination needs no pivoting and Eigen's diagonal pivot order changes
 // only the rounding, and the signs of the pivots (isPositive) do not depend
-// on the order; rows load with compile-time column offsets (the permuted
-// gather cost a tenth of the kernel).  A negative pivot: not positive; a
-// zero pivot: ldlt_wave, which keeps Eigen's pivoting and semantics for it.
+// on the order -- in exact arithmetic.  A pivot within kGjNearZero of the
+// largest diagonal entry (a zero or nearly singular system, where rounding
+// in another order could flip a pivot's sign) takes ldlt_wave, Eigen's own
+// pivot order and semantics, before any sign is judged; otherwise a negative
+// pivot: not positive.  Rows load with compile-time column offsets (the
+// permuted gather cost a tenth of the kernel).
 template <int n>
 __device__ bool gj_wave(InShared& sh, int lane) {
   ISTAMP_T(gt0);
@@ -579,13 +585,16 @@ __device__ bool gj_wave(InShared& sh, int lane) {
   rA[n] = ia < n ? sh.b[ia] : 0.0;
   rB[n] = ib < n ? sh.b[ib] : 0.0;
   double dA = 1.0, dB = 1.0;
+  double dmax = 0;  // the largest |diagonal entry| (uniform LDS reads)
+#pragma unroll
+  for (int j = 0; j < n; ++j) dmax = fmax(dmax, fabs(sh.H[j * kLd + j]));
   ISTAMP_T(gt1);
-  const int f = gj_pivots<n>(rA, rB, li, dA, dB);
+  const int f = gj_pivots<n>(rA, rB, li, dA, dB, kGjNearZero * dmax);
   ISTAMP_T(gt2);
   ISTAMP_SUB(12, gt0, gt1);
   ISTAMP_SUB(13, gt1, gt2);
-  if (f & 1) return false;
   if (f & 2) return ldlt_wave<n>(sh, lane);
+  if (f & 1) return false;
   constexpr double kTiny = 1.0 / 1.79769313486231570815e+308;
   if (lane < 16) {
     if (ia < n) sh.x[ia] = fabs(dA) > kTiny ? rA[n] / dA : 0.0;

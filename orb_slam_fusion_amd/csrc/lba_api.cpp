@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -262,8 +263,23 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
         }
   }
   const int n_pairs = (int)pair_list.size() / 2;
+  // Schur path: point ranges (k_lba_schur_split), S of them so that a
+  // (pair, range) block gets about kSchurSplitEdges of its pose's edges.
+  // ORBGPU_SCHUR=pair|band|split picks a path for A/B runs (tools/).
+  int n_free_edges = 0;
+  for (int u = 0; u < ne; ++u) n_free_edges += pf[u] >= 0;
+  int sc_split = nf > 0 ? (n_free_edges + nf * kSchurSplitEdges - 1) / (nf * kSchurSplitEdges) : 0;
+  sc_split = std::min(std::max(sc_split, 1), kSchurSplitMax);
   SchurChunks sc;
-  build_schur_chunks(np, nf, cnt, pf, sc);
+  if (const char* e = std::getenv("ORBGPU_SCHUR")) {
+    if (std::strcmp(e, "split") != 0) sc_split = 0;
+    if (std::strcmp(e, "band") == 0) build_schur_chunks(np, nf, cnt, pf, sc);
+  }
+  if (nf == 0 || n_pairs == 0) sc_split = 0;
+  // range x = points [pbx[x], pbx[x + 1]), cut at about x ne / S edges
+  std::vector<int> pbx(sc_split + 1, np);
+  for (int x = 0; x < sc_split; ++x)
+    pbx[x] = (int)(std::lower_bound(cnt.begin(), cnt.end() - 1, (int)((long long)x * ne / sc_split)) - cnt.begin());
   std::vector<int> gidx(ne);  // shard edge -> caller's edge index
   std::vector<int> pose_cnt(nf + 1, 0);
   // IMU links incident to each free key frame (link order)
@@ -287,7 +303,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)1);
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order
-  const size_t n_sc = sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1;
+  const size_t n_sc = (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1) +
+                      (size_t)nf * (sc_split + 1);
   size_t up = 0;
   const size_t u_ctrl = up;
   up += 128;
@@ -329,7 +346,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
                c_itot = take(2 + NI),  // [0] total, [2 + l] per link
-               c_scp = take(sc.ok ? 256 * (size_t)sc.tile0.back() : 1);
+               c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
+                                     sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
@@ -389,6 +407,15 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::copy(inc.begin(), inc.end(), I_inc);
   std::copy(inc_list.begin(), inc_list.end(), I_incl);
   int* const SC = reinterpret_cast<int*>(U + u_sc);
+  int* const SP = SC + (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1);
+  // per free pose, where each point range starts in its (point-ordered) slots
+  for (int f = 0; f < nf && sc_split > 0; ++f) {
+    int k = pose_cnt[f];
+    for (int x = 0; x <= sc_split; ++x) {
+      while (k < pose_cnt[f + 1] && I_slot[4 * (size_t)k + 1] < pbx[x]) ++k;
+      SP[(size_t)f * (sc_split + 1) + x] = x == sc_split ? pose_cnt[f + 1] : k;
+    }
+  }
   if (sc.ok) {
     std::memcpy(SC, sc.chunk.data(), sizeof(int4) * sc.chunk.size());
     std::memcpy(SC + 4 * sc.chunk.size(), sc.tile0.data(), sizeof(int) * sc.tile0.size());
@@ -419,6 +446,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.n_free = nf;
   a.n_sys = n;
   a.n_pairs = n_pairs;
+  a.sc_split = sc_split;
+  a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
+  if (sc_split > 1) a.sc_part = dp(c_scp);
   if (sc.ok) {
     const int* dS = reinterpret_cast<const int*>(A + u_sc);
     a.n_chunks = (int)sc.chunk.size();

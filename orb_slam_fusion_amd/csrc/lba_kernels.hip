@@ -777,6 +777,149 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
   }
 }
 
+// ---- Schur complement by point range (k_lba_schur_split + k_lba_schur_fold):
+// the shard's points cut into a.sc_split contiguous ranges of about equal edge
+// counts (lba_api.cpp), one 128-thread block per (pose pair, range) -- blocks
+// pair * S + x, so with S = 8 the blocks of range x share blockIdx % 8 and
+// (under the round-robin dispatch, for speed only) one XCD: every byte of a
+// range's points is then fetched into one XCD's L2, not all eight.  Each
+// thread takes one of pose fi's edges in the range (a.pose_split bounds them
+// in the point-ordered pslot list), looks up the point's edge to pose fj
+// FIRST and loads Hll / Hpl_i / Hpl_j only for a hit (about one edge in four
+// at C4), so the HBM bytes are those of the hits.  The block's partial of S_ij
+// (and, diagonal pairs, of W bl) goes to a.sc_part in a fixed DPP / LDS tree;
+// k_lba_schur_fold adds the S partials of each pair in range order (S = 1:
+// the block writes the system itself).  Deterministic run to run.
+constexpr int kSplitThreads = 128;
+constexpr int kSplitWaves = kSplitThreads / 64;
+
+__device__ __forceinline__ void schur_write(const LbaArgs& a, int fi, int fj, int t, double sum) {
+  const bool diag = fi == fj;
+  const int n = a.n_sys, P = a.pdim;  // P: the pose block's rows (VP first in a kModelImu key frame)
+  if (t < 36) {
+    const int s = t / 6, q = t - 6 * s;
+    if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
+    const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
+    a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
+    a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
+  } else {
+    const int s = t - 36;
+    a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
+    a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
+  }
+}
+
+__global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
+  __shared__ double red[kSplitWaves * 4 * 42];
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const double lambda = c.lambda;
+  const int S = a.sc_split;
+  const int pr = blockIdx.x / S, x = blockIdx.x - pr * S;
+  const int fi = a.pair_i[pr], fj = a.pair_j[pr];
+  const bool diag = fi == fj;
+  const int* ps = a.pose_split + (size_t)fi * (S + 1);
+  const int k1 = ps[x + 1];
+  double acc[42];
+#pragma unroll
+  for (int k = 0; k < 42; ++k) acc[k] = 0;
+  for (int k = ps[x] + threadIdx.x; k < k1; k += kSplitThreads) {
+    const int4 sl = a.pslot[k];  // {edge, point, first edge of the point, end}
+    const int ei = sl.x, p = sl.y;
+    int fs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) fs[u] = sl.z + u < sl.w ? a.ef[sl.z + u] : -2;
+    int uj = -1;  // the point's first edge to pose fj among its first 8
+#pragma unroll
+    for (int u = 7; u >= 0; --u)
+      if (fs[u] == fj) uj = u;
+    if (uj < 0 && sl.w - sl.z <= 8) continue;  // not seen by pose fj: adds nothing
+    // a hit (or a point seen by more than 8 key frames): its data, the first
+    // matching Hpl_j in the same batch of loads
+    double hll[9], B[18], Bj[18], blp[3] = {0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 9; ++q) hll[q] = a.hll[9 * (size_t)p + q];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) B[q] = a.hpl[18 * (size_t)ei + q];
+    const size_t ej = 18 * (size_t)(sl.z + (uj < 0 ? 0 : uj));
+#pragma unroll
+    for (int q = 0; q < 18; ++q) Bj[q] = a.hpl[ej + q];
+    if (diag)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) blp[q] = a.bl[3 * (size_t)p + q];
+    double Di[9];
+    inv3_lambda(hll, lambda, Di);
+    double W[6][3];
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) W[s][q] = B[3 * s] * Di[q] + B[3 * s + 1] * Di[3 + q] + B[3 * s + 2] * Di[6 + q];
+    auto add = [&](const double* Bq) {
+#pragma unroll
+      for (int s = 0; s < 6; ++s)
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          acc[6 * s + q] += W[s][0] * Bq[3 * q] + W[s][1] * Bq[3 * q + 1] + W[s][2] * Bq[3 * q + 2];
+    };
+    // the point's edges to pose fj in edge order (normally exactly one)
+    for (int base = sl.z;;) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (fs[u] != fj) continue;
+        if (base == sl.z && u == uj)
+          add(Bj);
+        else
+          add(a.hpl + 18 * (size_t)(base + u));
+      }
+      base += 8;
+      if (base >= sl.w) break;  // points seen by more than 8 keyframes: next chunk
+#pragma unroll
+      for (int u = 0; u < 8; ++u) fs[u] = base + u < sl.w ? a.ef[base + u] : -2;
+    }
+    if (diag)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) acc[36 + s] += W[s][0] * blp[0] + W[s][1] * blp[1] + W[s][2] * blp[2];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 42; ++k) {
+    double v = acc[k];
+    v += dpp_f64<0x111, 0xf>(v);
+    v += dpp_f64<0x112, 0xf>(v);
+    v += dpp_f64<0x114, 0xf>(v);
+    v += dpp_f64<0x118, 0xf>(v);
+    if ((lane & 15) == 15) red[(wave * 4 + (lane >> 4)) * 42 + k] = v;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= (diag ? 42 : 36)) return;
+  double sum = 0;
+#pragma unroll
+  for (int r = 0; r < kSplitWaves * 4; ++r) sum += red[r * 42 + t];
+  if (S == 1)
+    schur_write(a, fi, fj, t, sum);
+  else
+    a.sc_part[42 * (size_t)blockIdx.x + t] = sum;
+}
+
+// each pair's S range partials added in range order, then written as above
+__global__ __launch_bounds__(64) void k_lba_schur_fold(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  if (c.done) return;
+  const int pr = blockIdx.x, t = threadIdx.x, S = a.sc_split;
+  const int fi = a.pair_i[pr], fj = a.pair_j[pr];
+  if (t >= (fi == fj ? 42 : 36)) return;
+  const double* part = a.sc_part + 42 * (size_t)pr * S + t;
+  double v[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) v[x] = x < S ? part[42 * x] : 0.0;
+  double sum = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+    if (x < S) sum += v[x];
+  schur_write(a, fi, fj, t, sum);
+}
+
 // ---- Schur complement, point-major (block_solver.hpp:392-460 visits each
 // landmark once): one block per chunk of points (lba_api.cpp orders the points
 // by their lowest free pose and cuts chunks spanning <= kSchurBandMax poses).
@@ -1721,8 +1864,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial_poses(LbaArgs a) {
 }
 
 // ---- one LM trial, edge side: back-substitution x_l = Dinv (b_l - sum
-// Hpl^T x_p) of the edge's point (recomputed by each of its edges; the first
-// edge writes the point), the edge's error and robust chi2 at the trial state
+// Hpl^T x_p) of the block's points (a thread per point; the block holding a
+// point's first edge writes it), each edge's error and robust chi2 at the trial state
 // (computeActiveErrors), the landmark part of computeScale; the last block
 // sums the partials in block order and takes the LM decision.
 // kModelImu: the trial key-frame states come from k_lia_trial_states.
@@ -1749,9 +1892,22 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   }
   const int i = blockIdx.x * kThreads + threadIdx.x;
   double part[3] = {0, 0, 0};  // robust chi2, landmark scale, singular landmark blocks
-  if (i < a.n_edges) {
-    const LbaEdgeDev e = a.edges[i];
-    const int p = e.point;
+  // the points of this block's edges (a contiguous range: edges are point-
+  // major), each back-substituted once by one thread into LDS -- not once per
+  // edge; the block holding a point's first edge writes it and adds its
+  // landmark scale and failure
+  // (points past the first kThreads of the range -- only edgeless points
+  // between can make it longer -- are read back from pts[s1]: every point
+  // but the first has its first edge here, so this block wrote it)
+  __shared__ double sX[kThreads * 3];
+  const int i_first = blockIdx.x * kThreads;
+  int pA = 0, n_bp = 0;
+  if (i_first < a.n_edges) {
+    pA = a.edges[i_first].point;
+    n_bp = a.edges[min(i_first + kThreads, a.n_edges) - 1].point - pA + 1;
+  }
+  for (int k = threadIdx.x; k < n_bp; k += kThreads) {
+    const int p = pA + k;
     const int e0 = a.pt_begin[p], e1 = a.pt_begin[p + 1];
     const double* blp = a.bl + 3 * (size_t)p;
     double cp[3] = {blp[0], blp[1], blp[2]};
@@ -1784,8 +1940,9 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     for (int r = 0; r < 3; ++r) {
       v[r] = Di[3 * r] * cp[0] + Di[3 * r + 1] * cp[1] + Di[3 * r + 2] * cp[2];
       X[r] = X0[r] + v[r];
+      if (k < kThreads) sX[3 * k + r] = X[r];
     }
-    if (i == e0) {
+    if (e0 >= i_first) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         a.pts[s1][3 * (size_t)p + r] = X[r];
@@ -1793,6 +1950,13 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
       }
       part[2] = det == 0 ? 1.0 : 0.0;
     }
+  }
+  __syncthreads();
+  if (i < a.n_edges) {
+    const LbaEdgeDev e = a.edges[i];
+    const int k = e.point - pA;
+    const double* xs = k < kThreads ? sX + 3 * k : a.pts[s1] + 3 * (size_t)e.point;
+    const double X[3] = {xs[0], xs[1], xs[2]};
     double err[3];
     vis_error<M>(a, e, tposes + a.pstride * e.kf, X, err);
     a.err[3 * i] = err[0];
@@ -2230,7 +2394,10 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
 
 hipError_t lba_schur(const LbaArgs& a, hipStream_t st) {
   if (a.n_pairs <= 0) return hipSuccess;
-  if (a.n_chunks > 0) {
+  if (a.sc_split > 0) {
+    hipLaunchKernelGGL(k_lba_schur_split, dim3(a.n_pairs * a.sc_split), dim3(kSplitThreads), 0, st, a);
+    if (a.sc_split > 1) hipLaunchKernelGGL(k_lba_schur_fold, dim3(a.n_pairs), dim3(64), 0, st, a);
+  } else if (a.n_chunks > 0) {
     if (lds_optin(reinterpret_cast<const void*>(&k_lba_schur_band), kSchurChunkLds) != hipSuccess)
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_lba_schur_band, dim3(a.n_chunks), dim3(kBandThreads), kSchurChunkLds, st, a);

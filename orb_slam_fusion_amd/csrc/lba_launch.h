@@ -97,11 +97,16 @@ struct LbaArgs {
   // holds bl, so the product also carries W bl).  n_chunks == 0: one block
   // per pose pair (k_lba_schur) -- a point whose free poses span more than
   // kSchurBandMax.
+  // Schur complement by point range (k_lba_schur_split): sc_split ranges of
+  // the shard's points (1..kSchurSplitMax; 0 = the band / pair kernels), and
+  // per free pose the pslot offsets where each range starts
+  int sc_split;
+  const int* pose_split;  // [n_free * (sc_split + 1)]
   int n_chunks;
-  const int* sc_order;   // [points with a free edge] shard point index, chunk order
+  const int* sc_order;  // [points with a free edge] shard point index, chunk order
   const int4* sc_chunk;  // [n_chunks] {first in sc_order, points, b0, w}
   const int* sc_tile0;   // [n_chunks + 1] first partial tile of each chunk (256 doubles a tile)
-  double* sc_part;       // the chunks' upper product tiles
+  double* sc_part;       // the chunks' upper product tiles | split: [n_pairs * sc_split * 42]
   double* poses[2];          // [7 n_kf] current / trial state (ctrl.state selects)
   double* pts[2];            // [3 n_pts]
   double* err;               // [3 E] errors of the last computeActiveErrors
@@ -153,7 +158,9 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
 // outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles)
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
-constexpr int kSchurBandMax = 15;        // free poses a Schur chunk spans (6 w + 1 <= 96 rows)
+constexpr int kSchurSplitMax = 8;        // point ranges of k_lba_schur_split (one per XCD)
+constexpr int kSchurSplitEdges = 128;    // target pose edges per (pair, range) block
+constexpr int kSchurBandMax = 15;       // free poses a Schur chunk spans (6 w + 1 <= 96 rows)
 constexpr int kSchurChunkLds = 120 * 1024;  // W_all + H_all of a chunk: 64 x points x padded rows bytes
 
 // padded product rows of a band of w poses (6 w rows + the bl row, to the 16-row MFMA tile)

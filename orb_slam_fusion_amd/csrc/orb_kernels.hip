@@ -569,6 +569,7 @@ __device__ __forceinline__ int wave_iscan(int v) {
 }
 
 constexpr int kFastPf = 12;  // ROI dwords in flight per lane (one round trip up to 768)
+constexpr int kFastSvChunk = 512;  // survivors of 64 group entries (the list is expanded per 64 entries)
 
 // LS > 0: the plan's LDS row pitch for every cell (PlanHeader::fast_pitch:
 // the smallest of 48..64 that holds each cell's ROI row and score-map row;
@@ -597,18 +598,21 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     if (lane == 0) cell_count[(size_t)img * P->n_cells + ci] = 0;
     return;
   }
-  // LDS (fast_cell_lds_bytes): ROI rows of ls bytes (ROI column x at row byte
-  // lead + x), score map of the detection area with a zero border (row pitch
-  // dw + 2), u16 survivor list, u32 list of the 8-pixel groups holding a
-  // survivor.  A survivor is r << 7 | q (detection row, column; dw < 128,
-  // dh < 256 by the planner), bit 15 = keypoint flag.
+  // LDS (fast_cell_lds_bytes[_pitch]): ROI rows of ls bytes (ROI column x at
+  // row byte lead + x), score map of the detection area with a zero border
+  // (row pitch sp2), the u16 survivors of 64 group entries (kFastSvChunk; the
+  // list is expanded per 64 entries, twice: scores, then NMS -- never held
+  // whole, which keeps a cell wave's LDS and so the occupancy down), u32 list
+  // of the 8-pixel groups holding a survivor.  A survivor is r * LS + q (LS >
+  // 0) or r << 7 | q (detection row, column; dw < 128, dh < 256 by the
+  // planner).
   constexpr int QB = 7, QM = (1 << QB) - 1;  // (LS == 0) survivor index r << QB | q
   const int ls = LS ? LS : (c.cols + 6) & ~3;
   const int sp2 = LS ? LS : dw + 2, nsc = sp2 * (dh + 2);
   uint8_t* roi = lds;
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
   uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
-  uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) + ((2 * nd + 15) & ~15));
+  uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) + 2 * kFastSvChunk);
   auto sci = [&](int i) {
     if constexpr (LS != 0) return i + LS + 1;
     return ((i >> QB) + 1) * sp2 + (i & QM) + 1;
@@ -681,6 +685,9 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
 
   const uint32_t tail_mask = (1u << tail) - 1u;  // valid pixels of a row's tail group
 
+  const int xrel0 = c.x0 + 3 - kFastBorder, yrel0 = c.y0 + 3 - kFastBorder;
+  // One threshold pass: the compass, the scores, NMS; the keypoints go to the
+  // cell's slots (raster order); returns how many were found (*n_sv: survivors).
   auto pass = [&](int th, int* n_sv) -> int {
     // compass pre-test on 8 pixels per lane in packed u16 pairs; the window
     // of centres q..q+7 starts at row byte lead + q + 3 (wave-uniform shifts)
@@ -692,7 +699,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
       if (mrv == 0) break;
       const uint32_t cr = (uint32_t)(min(r, dh - 1) + 3);
-      const uint8_t* C = roi + (LS ? cr * (uint32_t)LS : __umul24(cr, (uint32_t)ls)) + 8 * g;
+      const uint8_t* C = roi + __umul24(cr, (uint32_t)(LS ? LS : ls)) + 8 * g;  // (24-bit: full-rate)
       // window of 8 centre-relative pixels at row byte o as four u16 pairs
       // (pixels 2j, 2j + 1): one two-source v_perm each straight from the
       // three dwords covering the window (wave-uniform selectors, no align)
@@ -738,7 +745,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         // LS > 0: the row's tail group keeps its first `tail` pixels here (the
         // entry then holds only valid pixels); LS == 0 drops them at the expansion
         const uint32_t mv = LS ? (g == gpr - 1 ? m7 & (tail_mask << 7) : m7) : m7;
-        const uint32_t i0 = LS ? (uint32_t)(r * LS + 8 * g) : (uint32_t)((r << QB) | (8 * g));
+        const uint32_t i0 = LS ? __umul24((uint32_t)r, (uint32_t)LS) + 8 * g : (uint32_t)((r << QB) | (8 * g));
         ge[mbcnt64(mg, (uint32_t)ng)] = i0 | (mv << 9);
       }
       ng += __popcll(mg);
@@ -749,89 +756,87 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // expand the group entries into the per-pixel survivor list: lane j of a
-    // 64-entry chunk writes its entry's pixels from the wave's inclusive scan
-    // of the entries' popcounts (raster order kept: entries in order, pixels
-    // LSB-first)
-    int ns = 0;
-    for (int b0 = 0; b0 < ng; b0 += 64) {
+    STAMP(0);
+    // survivors, 64 group entries at a time: lane j expands entry b0 + j into
+    // sv[] from the wave's inclusive scan of the entries' popcounts (raster
+    // order: entries in order, pixels LSB-first), at most kFastSvChunk
+    auto expand = [&](int b0) -> int {
       const int j = b0 + lane;
       const uint32_t e = j < ng ? ge[j] : 0u;
       const int i0 = (int)(e & 0xffffu);
-      // the row's tail group keeps its first `tail` pixels
+      // (LS == 0) the row's tail group keeps its first `tail` pixels
       uint32_t m = LS ? (e >> 16) & 0xffu : (e >> 16) & (((i0 >> 3) & ((1 << (QB - 3)) - 1)) == gpr - 1 ? tail_mask : 0xffu);
       const int cnt = __popc(m);
       const int incl = wave_iscan(cnt);
-      int pos = ns + incl - cnt;
+      int pos = incl - cnt;
       while (m) {
         sv[pos++] = (uint16_t)(i0 + __builtin_ctz(m));
         m &= m - 1;
       }
-      ns += __builtin_amdgcn_readlane(incl, 63);
-    }
-    __syncthreads();
-    STAMP(0);
-    for (int j = lane; j < ns; j += 64) {
-      const int i = sv[j];
-      // S = max(m - 1, 0) is a corner's score iff m >= th + 1 (then m > 0
-      // and its bit pattern is the integer m)
-      const _Float16 m = fast_arc_max(base + px(i), ls);
-      const uint16_t bits = __builtin_bit_cast(uint16_t, m);
-      sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
-    }
-    __syncthreads();
-    STAMP(1);
-    // NMS: a corner is kept iff its score beats all 8 neighbours' (0 for
-    // non-corners and for the zero border outside the detection area)
-    int nk = 0;
-    for (int b0 = 0; b0 < ns; b0 += 64) {
-      const int j = b0 + lane;
-      bool kp = false;
-      if (j < ns) {
+      __syncthreads();
+      return __builtin_amdgcn_readlane(incl, 63);
+    };
+    // scores of every survivor into the map
+    for (int b0 = 0; b0 < ng; b0 += 64) {
+      const int ns = expand(b0);
+      *n_sv += ns;
+      for (int j = lane; j < ns; j += 64) {
         const int i = sv[j];
-        const uint8_t* m = sc + sci(i);
-        const int s = m[0];
-        const int n = max(max(max(m[-sp2 - 1], m[-sp2]), max(m[-sp2 + 1], m[-1])),
-                          max(max(m[1], m[sp2 - 1]), max(m[sp2], m[sp2 + 1])));
-        kp = s > n;
-        if (kp) sv[j] = (uint16_t)(i | 0x8000);
+        // S = max(m - 1, 0) is a corner's score iff m >= th + 1 (then m > 0
+        // and its bit pattern is the integer m)
+        const _Float16 m = fast_arc_max(base + px(i), ls);
+        const uint16_t bits = __builtin_bit_cast(uint16_t, m);
+        sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
       }
-      nk += __popcll(__ballot(kp));
+      __syncthreads();  // sv is rewritten by the next chunk
     }
-    __syncthreads();
+    STAMP(1);
+    // NMS over the survivors again (re-expanded: the list is never held
+    // whole), keypoints straight to the cell's slots in raster order: a corner
+    // is kept iff its score beats all 8 neighbours' (0 for non-corners and
+    // for the zero border outside the detection area)
+    int written = 0;
+    for (int b0 = 0; b0 < ng; b0 += 64) {
+      const int ns = expand(b0);
+      for (int jb = 0; jb < ns; jb += 64) {
+        const int j = jb + lane;
+        bool kp = false;
+        int i = 0, s = 0;
+        if (j < ns) {
+          i = sv[j];
+          const uint8_t* mp = sc + sci(i);
+          s = mp[0];
+          const int n = max(max(max(mp[-sp2 - 1], mp[-sp2]), max(mp[-sp2 + 1], mp[-1])),
+                            max(max(mp[1], mp[sp2 - 1]), max(mp[sp2], mp[sp2 + 1])));
+          kp = s > n;
+        }
+        const uint64_t km = __ballot(kp);
+        if (kp) {
+          const int r = LS ? i / LS : i >> QB, q = LS ? i - r * LS : i & QM;
+          const int pos = written + __popcll(km & lt);
+          if (pos < c.slot_cap)
+            out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
+        }
+        written += __popcll(km);
+      }
+      __syncthreads();
+    }
     STAMP(2);
-    *n_sv = ns;
-    return nk;
+    return written;
   };
 
   int ns = 0;
-  int nk = pass(P->ini_th, &ns);
+  int written = pass(P->ini_th, &ns);
   STAMP_ADD(12, ns);
-  if (nk == 0) {
+  if (written == 0) {
     STAMP_ADD(10, 1);
-    for (int j = lane; j < ns; j += 64) sc[sci(sv[j] & 0x7fff)] = 0;
+    for (int i = lane; i < ((nsc + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
     __syncthreads();
     STAMP(3);
-    nk = pass(P->min_th, &ns);
+    ns = 0;
+    written = pass(P->min_th, &ns);
     STAMP(4);
     STAMP_ADD(11, ns);
-  }
-
-  const int xrel0 = c.x0 + 3 - kFastBorder, yrel0 = c.y0 + 3 - kFastBorder;
-  int written = 0;
-  for (int b0 = 0; b0 < ns && written < nk; b0 += 64) {
-    const int j = b0 + lane;
-    const int e = j < ns ? sv[j] : 0;
-    const bool k = (e & 0x8000) != 0;
-    const uint64_t m = __ballot(k);
-    if (k) {
-      const int i = e & 0x7fff;
-      const int r = LS ? i / LS : i >> QB, q = LS ? i - r * LS : i & QM;
-      const int pos = written + __popcll(m & lt);
-      if (pos < c.slot_cap)
-        out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)sc[sci(i)] << 24);
-    }
-    written += __popcll(m);
   }
   if (lane == 0) cell_count[(size_t)img * P->n_cells + ci] = min(written, c.slot_cap);
   STAMP(5);

@@ -369,14 +369,19 @@ __device__ __forceinline__ bool ldlt6_wave(const double* hb, double lambda, doub
 }
 
 // The same system by Gauss-Jordan elimination with DPP64 row broadcasts: lane
-// li of every 16-lane row owns permuted row li (li < 6; the others zero) with
-// b appended; pivot K's row is read from lane K of the lane's own row by
-// v_fmac_f64_dpp row_newbcast, one instruction per entry (a fixed window of 6
-// entries after the pivot column: the row's rest, b, zero padding), every row
-// but the pivot's subtracting l_i times it.  Same pivot order and pivots as
-// ldlt6_wave, so the same isPositive(); x_i = b'_i / D_i with Eigen's
-// tolerance, solved even when a pivot is negative (as ldlt6_wave).  A zero
-// pivot takes ldlt6_wave, which keeps Eigen's semantics for it.
+// li of every 16-lane row owns row li (li < 6; the others zero) in the
+// natural order, with b appended; pivot K's row is read from lane K of the
+// lane's own row by v_fmac_f64_dpp row_newbcast, one instruction per entry (a
+// fixed window of 6 entries after the pivot column: the row's rest, b, zero
+// padding), every row but the pivot's subtracting l_i times it.  For a
+// symmetric positive definite system the pivot signs do not depend on the
+// order, so isPositive() is ldlt6_wave's; x_i = b'_i / D_i with Eigen's
+// tolerance, solved even when a pivot is negative (as ldlt6_wave).  A zero or
+// near-zero pivot (|d| <= kGj6NearZero x the largest diagonal entry, where
+// rounding in another order could flip a sign) takes ldlt6_wave: Eigen's
+// pivot order and semantics.  ldlt6_wave / ldlt_wave run only in that case.
+constexpr double kGj6NearZero = 1e-12;
+
 template <int N>
 __device__ __forceinline__ double row16_bcast_f64(double v) {
   double o;
@@ -395,19 +400,19 @@ __device__ __forceinline__ void gj6_pivot(double (&w)[12], double l) {
 }
 #undef POSE_FMC
 template <int K>
-__device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmine, int& flags) {
+__device__ __forceinline__ void gj6_pivots(double (&w)[12], int li, double& dmine, int& flags, double tiny) {
   if constexpr (K < 6) {
     const double d = row16_bcast_f64<K>(w[K]);
-    flags |= (d < 0.0 ? 1 : 0) | (d == 0.0 ? 2 : 0);
+    flags |= (d < 0.0 ? 1 : 0) | (fabs(d) <= tiny ? 2 : 0);
     double r = __builtin_amdgcn_rcp(d);
     r = fma(r, fma(-d, r, 1.0), r);
     dmine = li == K ? d : dmine;
     gj6_pivot<K>(w, li != K ? w[K] * r : 0.0);
-    gj6_pivots<K + 1>(w, li, dmine, flags);
+    gj6_pivots<K + 1>(w, li, dmine, flags, tiny);
   }
 }
 
-// ldlt6_gj with a lambda per 16-lane row: the four rows of a wave solve four
+// The Gauss-Jordan solve with a lambda per 16-lane row: the four rows of a wave solve four
 // systems H + lambda_r I at once (the row broadcasts never leave a row).  A
 // row with a zero pivot is redone alone by ldlt6_wave (Eigen's pivoting).
 // Every lane of row r returns row r's x and isPositive().
@@ -426,7 +431,10 @@ __device__ __forceinline__ bool ldlt6_gj_rows(const double* hb, const double* hf
   for (int j = 7; j < 12; ++j) w[j] = 0.0;
   double dmine = 1.0;
   int flags = 0;
-  gj6_pivots<0>(w, li, dmine, flags);
+  double dmax = 0;  // the largest |diagonal entry| of this row's system
+#pragma unroll
+  for (int j = 0; j < 6; ++j) dmax = fmax(dmax, fabs(hf[7 * j] + lambda));
+  gj6_pivots<0>(w, li, dmine, flags, kGj6NearZero * dmax);
   const double z = li < 6 && fabs(dmine) > 1.0 / 1.79769313486231570815e+308 ? w[6] / dmine : 0.0;
   x[0] = row16_bcast_f64<0>(z);
   x[1] = row16_bcast_f64<1>(z);
@@ -450,35 +458,6 @@ __device__ __forceinline__ bool ldlt6_gj_rows(const double* hb, const double* hf
       }
   }
   return ok;
-}
-
-__device__ __forceinline__ bool ldlt6_gj(const double* hb, const double* hf, double lambda,
-                                         double (&x)[6]) {
-  // pivots in natural order: H + lambda I is symmetric positive definite
-  // whenever the trial succeeds, where elimination needs no pivoting and
-  // Eigen's diagonal pivot order changes only the rounding (and not the pivot
-  // signs, so not isPositive()); rows of the full mirror (hf) load with
-  // compile-time offsets.  A zero pivot takes ldlt6_wave (Eigen's pivoting).
-  const int lane = threadIdx.x & 63, li = lane & 15;
-  const double* row = hf + 6 * (li < 6 ? li : 0);
-  double w[12];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const double h = row[j];
-    w[j] = li < 6 ? (li == j ? h + lambda : h) : 0.0;
-  }
-  w[6] = li < 6 ? hb[22 + li] : 0.0;
-#pragma unroll
-  for (int j = 7; j < 12; ++j) w[j] = 0.0;
-  double dmine = 1.0;
-  int flags = 0;
-  gj6_pivots<0>(w, li, dmine, flags);
-  if (flags & 2) return ldlt6_wave(hb, lambda, x);
-  const double z = li < 6 && fabs(dmine) > 1.0 / 1.79769313486231570815e+308 ? w[6] / dmine : 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) x[k] = readlane_f64(z, k);
-  (void)lane;
-  return !(flags & 1);
 }
 
 // g2o RobustKernelHuber::robustify; e2 > delta^2 >= 1 in the sqrt branch

@@ -80,6 +80,25 @@ def test_tiny_problems(gpu_available, n_obs):
         _check(res, out, ref, ref_out)
 
 
+@pytest.mark.parametrize("n_obs", [0, 40])
+def test_near_rank_deficient_last_keyframe(gpu_available, n_obs):
+    """Accelerometer bias all but unobservable: its random-walk information
+    scaled by 1e-14 and the preintegration's accelerometer Jacobians zeroed.
+    The ba pivots are ~1e-18 of the largest diagonal entry, below the
+    relative cutoff (kGjNearZero) that sends the Gauss-Jordan solve to the
+    pivoted LDLT (Eigen's order, as the reference's dense solver); results
+    must match the oracle as for any other problem."""
+    case = ic.make_case(41, mode=1, n_obs=n_obs)
+    pi = case["preint"]
+    pi["info_a"] = pi["info_a"] * 1e-14
+    pi["JVa"] = 0.0
+    pi["JPa"] = 0.0
+    ref, ref_out = oracle.pose_inertial(case)
+    ret, res, out = _gpu(case)
+    assert ret == int(ref["n_good"])
+    _check(res, out, ref, ref_out)
+
+
 def test_observations_beyond_lds(gpu_available):
     """More observations than the kernel stages in LDS (2048): the rest are
     re-read from HBM."""
