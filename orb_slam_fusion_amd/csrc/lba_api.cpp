@@ -17,7 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -208,6 +210,14 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
   hipStream_t st = h->stream;
   const bool imu = m.model == kModelImu;
+  // ORBGPU_LBA_TRACE=1: host phase times of the call to stderr (tools/)
+  static const bool trace = std::getenv("ORBGPU_LBA_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const auto t_enter = clk::now();
+  auto us = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+  };
+  int trace_steps = 0;
 
   // ---- graph layout of this shard, O(edges): free-pose indices, point-major
   // edges (insertion order kept inside a point), per-pose edge lists, pairs
@@ -301,7 +311,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const size_t NI = std::max(m.n_imu, 1);
   const int nblk = (int)((std::max(std::max(ne, np), 1) + 255) / 256) + nf + 1;
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
-                        F + (nf + 1) + std::max(inc_list.size(), (size_t)1);
+                        F + (nf + 1) + std::max(inc_list.size(), (size_t)1) + E;
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order
   const size_t n_sc = (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1) +
                       (size_t)nf * (sc_split + 1);
@@ -339,12 +349,12 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     if (!lba_solve_mode_fits(h->solver, npad)) return ORBGPU_ERR_CAPACITY;
     solve_mode = h->solver;
   }
-  const size_t c_err = take(3 * E), c_hpl = take(18 * E), c_hppe = take(27 * E), c_hlle = take(12 * E),
+  const size_t c_err = take(3 * E), c_hpl = take(2 * 18 * E), c_hppe = take(2 * 27 * E), c_hlle = take(2 * 12 * E),
                c_hll = take(9 * P), c_bl = take(3 * P), c_hpp = take(36 * F), c_bp = take(6 * F),
                c_diag = take(n + 2), c_sys = take((size_t)n * n + 2 * n + 2),
                c_work = take(lba_solve_work_doubles(solve_mode, npad)),
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
-               c_imuq = take(imu ? kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
+               c_imuq = take(imu ? 2 * kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
                c_itot = take(2 + NI),  // [0] total, [2 + l] per link
                c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
                                      sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));
@@ -357,6 +367,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   ctrl0.user_lambda = lambda_init;
   ctrl0.max_iters = iterations;
   ctrl0.need_build = 1;
+  ctrl0.lin_state = -1;
   std::memcpy(U + u_ctrl, &ctrl0, sizeof(ctrl0));
   std::memset(U + u_cnt, 0, 128);
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
@@ -382,6 +393,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   int* I_fk = I_pj + std::max(n_pairs, 1);
   int* I_inc = I_fk + F;
   int* I_incl = I_inc + (nf + 1);
+  int* I_es = I_incl + std::max(inc_list.size(), (size_t)1);
   std::copy(hidx.begin(), hidx.end(), I_hidx);
   std::copy(cnt.begin(), cnt.end(), I_pt);
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
@@ -390,7 +402,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     std::vector<int> fill(pose_cnt.begin(), pose_cnt.end() - 1);
     for (int j = 0; j < ne; ++j) {
       I_ef[j] = le[j].f;
+      I_es[j] = -1;
       if (le[j].f < 0) continue;
+      I_es[j] = fill[le[j].f];
       int* r = I_slot + 4 * (size_t)fill[le[j].f]++;
       const int p = le[j].point;
       r[0] = j;
@@ -432,6 +446,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     std::memcpy(U + u_imu, m.imu, sizeof(LiaImuDev) * m.n_imu);
     std::memcpy(U + u_close, m.close + pt_begin, np);
   }
+  const auto t_layout = clk::now();
   if (hipMemcpyAsync(h->arena, U, up, hipMemcpyHostToDevice, st) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
 
@@ -470,6 +485,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.ef = dI + (I_ef - I);
   a.pair_i = dI + (I_pi - I);
   a.pair_j = dI + (I_pj - I);
+  a.eslot = dI + (I_es - I);
+  a.n_slots = nf > 0 ? pose_cnt[nf] : 0;
   a.poses[0] = dp(u_state);
   a.poses[1] = dp(u_state) + KS;
   a.pts[0] = dp(u_state) + 2 * KS;
@@ -507,10 +524,6 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     a.himu = dp(c_himu);
     a.imu_tot = dp(c_itot);
   }
-  // blocks no launched pose pair writes (and, kModelImu, the IMU rows, which
-  // get no Schur terms) stay zero: clear the system once per call
-  if (hipMemsetAsync(a.sys, 0, sizeof(double) * ((size_t)n * n + 2 * n), st) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
 
   volatile LbaHostWords* hw = h->host;
   hw->progress = 0;
@@ -528,6 +541,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
         if (lba_step(a, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
         ++issued;
+        trace_steps = issued;
       } else {
         std::this_thread::yield();
       }
@@ -602,9 +616,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   }
 
   // ---- outliers, final state, one copy back
+  const auto t_loop = clk::now();
   char* D = A + d_begin;
-  if (hipMemcpyAsync(D, a.ctrl, sizeof(LbaCtrl), hipMemcpyDeviceToDevice, st) != hipSuccess ||
-      lba_classify(a, reinterpret_cast<uint8_t*>(D + d_outlier), reinterpret_cast<double*>(D + d_out), st) !=
+  if (lba_classify(a, reinterpret_cast<uint8_t*>(D + d_outlier), reinterpret_cast<double*>(D + d_out), D, st) !=
           hipSuccess ||
       hipMemcpyAsync(h->staging, D, dn, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
@@ -621,6 +635,13 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const double* xo = out + KS;
   for (int p = 0; p < np; ++p)
     for (int q = 0; q < 3; ++q) pts_out[3 * (size_t)(pt_begin + p) + q] = (float)xo[3 * (size_t)p + q];
+  if (trace) {
+    const auto t_end = clk::now();
+    std::fprintf(stderr, "{\"lba_trace\": 1, \"layout_us\": %.1f, \"loop_us\": %.1f, \"tail_us\": %.1f, "
+                 "\"steps_issued\": %d, \"trials\": %d, \"edges\": %d, \"pairs\": %d, \"sc_split\": %d}\n",
+                 us(t_enter, t_layout), us(t_layout, t_loop), us(t_loop, t_end), trace_steps, wo.ctrl.trials, ne,
+                 n_pairs, sc_split);
+  }
   return ORBGPU_OK;
 }
 

@@ -391,6 +391,7 @@ __device__ void ctl_init(const LbaArgs& a, double chi, int stop) {
   c.iters_done = 0;
   c.trials = 0;
   c.need_build = 1;
+  c.lin_state = -1;
   c.stopped = stop;
   // SparseOptimizer::optimize: for (i < iterations && !terminate() ...)
   c.done = (c.max_iters <= 0 || stop) ? 1 : 0;
@@ -421,6 +422,7 @@ __device__ void ctl_decide(const LbaArgs& a, double chi_trial, double scale_l, i
     c.ni = 2;
     c.cur = tmp;
     c.state ^= 1;  // discardTop: the trial state becomes current
+    c.lin_state = c.state;  // its per-edge terms were written by the trial
   } else {
     c.lambda *= c.ni;  // pop: the current state stays
     c.ni *= 2;
@@ -453,6 +455,11 @@ template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   __shared__ double red[4];
   const int i = blockIdx.x * kThreads + threadIdx.x;
+  // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
+  // which get no Schur terms) stay zero: clear it once per call
+  for (size_t k = i, nz = (size_t)a.n_sys * a.n_sys + 2 * (size_t)a.n_sys; k < nz;
+       k += (size_t)gridDim.x * kThreads)
+    a.sys[k] = 0.0;
   double r0 = 0;
   if (i < a.n_edges) {
     const LbaEdgeDev e = a.edges[i];
@@ -490,18 +497,27 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
 // The row loops run over 3 rows for mono edges too: their third Jacobian
 // row and error are zero, and adding an exact 0 changes no sum (constant
 // trip counts keep the Jacobians in registers, not in scratch).
+// The per-edge terms live in two copies, one per LM state (lin_of(a, s)):
+// the build at state s reads / writes copy s, and every trial writes the
+// terms of its trial state into the other copy as it evaluates the edges
+// (k_lba_trial), so an accepted trial leaves the next build nothing to
+// linearise (LbaCtrl::lin_state; the values are those k_lba_linearize would
+// compute from the same state and errors).
+struct LinPtr {
+  double* hpl;    // [18 E]
+  double* hpp_e;  // [27][n_slots]
+  double* hll_e;  // [12][E]
+};
+__device__ __forceinline__ LinPtr lin_of(const LbaArgs& a, int s) {
+  return LinPtr{a.hpl + (size_t)s * 18 * a.n_edges, a.hpp_e + (size_t)s * 27 * a.n_slots,
+                a.hll_e + (size_t)s * 12 * a.n_edges};
+}
+
 template <int M>
-__global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
-  const LbaCtrl& c = *a.ctrl;
-  if (c.done || !c.need_build) return;
-  const int i = blockIdx.x * kThreads + threadIdx.x;
-  if (i >= a.n_edges) return;
-  const LbaEdgeDev e = a.edges[i];
-  const double* x = a.pts[c.state] + 3 * e.point;
-  const double X[3] = {x[0], x[1], x[2]};
-  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
+__device__ __forceinline__ void lin_edge(const LbaArgs& a, const LbaEdgeDev& e, int i, const double* ks,
+                                         const double X[3], const double ev[3], const LinPtr& L) {
   double Jl[3][3], Jp[3][6];
-  vis_jacobians<M>(a, e, a.poses[c.state] + a.pstride * e.kf, X, Jl, Jp);
+  vis_jacobians<M>(a, e, ks, X, Jl, Jp);
   double r0, w;
   huber_rho(lba_chi2(e, ev), lba_delta(e), r0, w);
   const double info = (double)e.inv_sigma2, wi = w * info;
@@ -523,9 +539,9 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
       hl[3 * s + q] = h;
     }
   }
-  double* hlo = a.hll_e + 12 * (size_t)i;
+  double* hlo = L.hll_e + i;  // component-major: a wave's stores are contiguous
 #pragma unroll
-  for (int k = 0; k < 12; ++k) hlo[k] = hl[k];
+  for (int k = 0; k < 12; ++k) hlo[(size_t)k * a.n_edges] = hl[k];
   if (e.f < 0) return;
   double hp[27], hpl[18];  // 21 lower-triangle Hpp terms, 6 bp terms; Hpl 6 x 3
   int hk = 0;
@@ -550,12 +566,26 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
       hpl[3 * s + q] = h;
     }
   }
-  double* hpo = a.hpp_e + 27 * (size_t)i;
+  double* hpo = L.hpp_e + a.eslot[i];  // the edge's pose slot, component-major
 #pragma unroll
-  for (int k = 0; k < 27; ++k) hpo[k] = hp[k];
-  double* hplo = a.hpl + 18 * (size_t)i;
+  for (int k = 0; k < 27; ++k) hpo[(size_t)k * a.n_slots] = hp[k];
+  double* hplo = L.hpl + 18 * (size_t)i;
 #pragma unroll
   for (int k = 0; k < 18; ++k) hplo[k] = hpl[k];
+}
+
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
+  const LbaCtrl& c = *a.ctrl;
+  // nothing due, or the accepted trial already left this state's terms
+  if (c.done || !c.need_build || c.lin_state == c.state) return;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n_edges) return;
+  const LbaEdgeDev e = a.edges[i];
+  const double* x = a.pts[c.state] + 3 * e.point;
+  const double X[3] = {x[0], x[1], x[2]};
+  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
+  lin_edge<M>(a, e, i, a.poses[c.state] + a.pstride * e.kf, X, ev, lin_of(a, c.state));
 }
 
 // ---- buildSystem, vertex side.  Blocks [0, n_free): one free pose each,
@@ -568,6 +598,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   __shared__ double red[4 * 27];
   const LbaCtrl& c = *a.ctrl;
   if (c.done || !c.need_build) return;
+  const LinPtr L = lin_of(a, c.state);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double hmax = 0;
   if ((int)blockIdx.x < a.n_free) {
@@ -576,17 +607,20 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = 0;
     const int j0 = a.pose_begin[f], j1 = a.pose_begin[f + 1];
+    // the pose's slots are contiguous in hpp_e's component rows: every load
+    // of a wave reads 512 consecutive bytes (four slots' terms in flight)
     for (int jb = j0 + threadIdx.x; jb < j1; jb += 4 * kThreads) {
-      int ei[4];  // four edges' indices in flight before their terms
+      double hv[4][27];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) ei[u] = jb + u * kThreads < j1 ? a.pslot[jb + u * kThreads].x : -1;
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (ei[u] < 0) continue;
-        const double* hp = a.hpp_e + 27 * (size_t)ei[u];
+        for (int k = 0; k < 27; ++k)
+          hv[u][k] = jb + u * kThreads < j1 ? L.hpp_e[(size_t)k * a.n_slots + jb + u * kThreads] : 0.0;
 #pragma unroll
-        for (int k = 0; k < 27; ++k) acc[k] += hp[k];
-      }
+      for (int u = 0; u < 4; ++u)
+        if (jb + u * kThreads < j1)
+#pragma unroll
+          for (int k = 0; k < 27; ++k) acc[k] += hv[u][k];
     }
 #pragma unroll
     for (int k = 0; k < 27; ++k) {
@@ -622,7 +656,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int k = 0; k < 12; ++k) hl[u][k] = ib + u < i1 ? a.hll_e[12 * (size_t)(ib + u) + k] : 0.0;
+          for (int k = 0; k < 12; ++k) hl[u][k] = ib + u < i1 ? L.hll_e[(size_t)k * a.n_edges + ib + u] : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (ib + u < i1)
@@ -686,6 +720,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
   const double lambda = c.lambda;
+  const double* const hpl = lin_of(a, c.state).hpl;
   const int pr = blockIdx.x;
   const int fi = a.pair_i[pr], fj = a.pair_j[pr];
   const int n = a.n_sys;
@@ -700,7 +735,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
 #pragma unroll
     for (int q = 0; q < 9; ++q) hll[q] = a.hll[9 * (size_t)p + q];
 #pragma unroll
-    for (int q = 0; q < 18; ++q) B[q] = a.hpl[18 * (size_t)ei + q];
+    for (int q = 0; q < 18; ++q) B[q] = hpl[18 * (size_t)ei + q];
     double blp[3] = {0, 0, 0};
     if (diag)
 #pragma unroll
@@ -727,7 +762,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         if (fs[u] != fj) continue;
-        const double* Bj = a.hpl + 18 * (size_t)(base + u);
+        const double* Bj = hpl + 18 * (size_t)(base + u);
 #pragma unroll
         for (int s = 0; s < 6; ++s)
 #pragma unroll
@@ -814,6 +849,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
   const double lambda = c.lambda;
+  const double* const hpl = lin_of(a, c.state).hpl;
   const int S = a.sc_split;
   const int pr = blockIdx.x / S, x = blockIdx.x - pr * S;
   const int fi = a.pair_i[pr], fj = a.pair_j[pr];
@@ -840,10 +876,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
 #pragma unroll
     for (int q = 0; q < 9; ++q) hll[q] = a.hll[9 * (size_t)p + q];
 #pragma unroll
-    for (int q = 0; q < 18; ++q) B[q] = a.hpl[18 * (size_t)ei + q];
+    for (int q = 0; q < 18; ++q) B[q] = hpl[18 * (size_t)ei + q];
     const size_t ej = 18 * (size_t)(sl.z + (uj < 0 ? 0 : uj));
 #pragma unroll
-    for (int q = 0; q < 18; ++q) Bj[q] = a.hpl[ej + q];
+    for (int q = 0; q < 18; ++q) Bj[q] = hpl[ej + q];
     if (diag)
 #pragma unroll
       for (int q = 0; q < 3; ++q) blp[q] = a.bl[3 * (size_t)p + q];
@@ -869,7 +905,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
         if (base == sl.z && u == uj)
           add(Bj);
         else
-          add(a.hpl + 18 * (size_t)(base + u));
+          add(hpl + 18 * (size_t)(base + u));
       }
       base += 8;
       if (base >= sl.w) break;  // points seen by more than 8 keyframes: next chunk
@@ -947,6 +983,7 @@ __global__ __launch_bounds__(kBandThreads) void k_lba_schur_band(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
   const double lambda = c.lambda;
+  const double* const hpl = lin_of(a, c.state).hpl;
   const int4 ch = a.sc_chunk[blockIdx.x];  // {first in sc_order, points, b0, w}
   const int P = ch.y, b0 = ch.z, w = ch.w;
   const int NB = schur_band_rows(w), T = NB >> 4;
@@ -981,7 +1018,7 @@ __global__ __launch_bounds__(kBandThreads) void k_lba_schur_band(LbaArgs a) {
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int q = 0; q < 18; ++q) B[v][q] = fs[v] >= 0 ? a.hpl[18 * (size_t)(ub + v) + q] : 0.0;
+        for (int q = 0; q < 18; ++q) B[v][q] = fs[v] >= 0 ? hpl[18 * (size_t)(ub + v) + q] : 0.0;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         if (fs[v] < 0) continue;
@@ -1877,6 +1914,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   const double lambda = c.lambda;
   const int s0 = c.state, s1 = s0 ^ 1;
   const double* tposes = a.poses[s1];
+  const double* const hpl0 = lin_of(a, s0).hpl;
   if constexpr (M == kModelSe3) {
     __shared__ double tp[kMaxKfLds * 7];
     if (a.n_kf <= kMaxKfLds) {
@@ -1919,7 +1957,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int q = 0; q < 18; ++q) B[u][q] = fs[u] >= 0 ? a.hpl[18 * (size_t)(base + u) + q] : 0.0;
+        for (int q = 0; q < 18; ++q) B[u][q] = fs[u] >= 0 ? hpl0[18 * (size_t)(base + u) + q] : 0.0;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -1964,6 +2002,9 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     a.err[3 * i + 2] = err[2];
     double w;
     huber_rho(lba_chi2(e, err), lba_delta(e), part[0], w);
+    // the trial state's per-edge terms, for the build that follows if the
+    // trial is accepted (LinPtr above)
+    lin_edge<M>(a, e, i, tposes + a.pstride * e.kf, X, err, lin_of(a, s1));
   }
   block_sum<3>(part, red);
   if (threadIdx.x == 0)
@@ -2020,9 +2061,12 @@ __global__ void k_lba_ctl(LbaArgs a, int mode) {
 // only for mono edges.
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* __restrict__ outlier,
-                                                           double* __restrict__ out) {
+                                                           double* __restrict__ out,
+                                                           uint32_t* __restrict__ ctrl_out) {
   const int s = a.ctrl->state;
   const int i = blockIdx.x * kThreads + threadIdx.x;
+  // the final LM state for the host's one copy back
+  if (i < (int)(sizeof(LbaCtrl) / 4)) ctrl_out[i] = reinterpret_cast<const uint32_t*>(a.ctrl)[i];
   if (i < a.pstride * a.n_kf) out[i] = a.poses[s][i];
   if (i < 3 * a.n_pts) out[(size_t)a.pstride * a.n_kf + i] = a.pts[s][i];
   if (i >= a.n_edges) return;
@@ -2077,10 +2121,14 @@ __device__ __forceinline__ void load_state(StateD& s, const double* p) {
   }
 }
 
+// kBuild with trial = 0: the build's forms at the current state (skipped when
+// the accepted trial already left them); with trial = 1: the trial's errors
+// and chi2 and, speculatively, its forms into the other copy of imu_q (as
+// k_lba_trial does for the visual edges, lin_of).
 template <bool kBuild>
 __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   const LbaCtrl& c = *a.ctrl;
-  if (c.done || (kBuild && !c.need_build)) return;
+  if (c.done || (kBuild && !trial && (!c.need_build || c.lin_state == c.state))) return;
   __shared__ double sJ[9 * 24];
   __shared__ double sOJ[9 * 24];
   __shared__ double sE[9];       // the link's error (inertial_edge_core, lane 0)
@@ -2190,7 +2238,7 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
         We[r] = v;
       }
       wave_lds_sync();
-      double* Q = a.imu_q + (size_t)kImuPairQ * l;
+      double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * (trial ? c.state ^ 1 : c.state));
       for (int k = lane; k < 900; k += 64) {
         const int p = k / 30, q = k - 30 * p;
         double v = 0;
@@ -2228,7 +2276,7 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
       }
     }
   }
-  if (kBuild) return;
+  if (kBuild && !trial) return;
   if (lane == 0) a.imu_tot[2 + l] = chi_link;
   if (!last_block(a.counter + 3)) return;
   if (threadIdx.x == 0) {
@@ -2258,7 +2306,7 @@ __global__ __launch_bounds__(kThreads) void k_lia_assemble(LbaArgs a) {
     const int l = a.imu_inc_list[j];
     const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
     const int sr = k1 == kr ? 0 : 1;
-    const double* Q = a.imu_q + (size_t)kImuPairQ * l;
+    const double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * c.state);
     if (grad) {
       v += Q[900 + kImuDim * sr + dr];
     } else {
@@ -2437,7 +2485,7 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
     hipLaunchKernelGGL(k_lia_trial_states, dim3(a.n_kf), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 1);
+    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 1);
     hipLaunchKernelGGL(k_lba_trial<kModelImu>, g, dim3(kThreads), 0, st, a);
   } else {
     if (a.n_kf > kMaxKfLds)
@@ -2459,16 +2507,16 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st) {
+hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, void* ctrl_out, hipStream_t st) {
   long n = a.n_edges;
   if ((long)a.pstride * a.n_kf > n) n = (long)a.pstride * a.n_kf;
   if (3L * a.n_pts > n) n = 3L * a.n_pts;
   if (a.model == kModelImu)
     hipLaunchKernelGGL(k_lba_classify<kModelImu>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0,
-                       st, a, outlier, out);
+                       st, a, outlier, out, static_cast<uint32_t*>(ctrl_out));
   else
     hipLaunchKernelGGL(k_lba_classify<kModelSe3>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0,
-                       st, a, outlier, out);
+                       st, a, outlier, out, static_cast<uint32_t*>(ctrl_out));
   return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct LbaCtrl {
   double lambda, ni, cur, ini, chi_init, user_lambda;
   double last;  // robust chi2 of the last computeActiveErrors (LocalInertialBA's err_end)
   int it, q, nbad, need_build, done, state, iters_done, trials, max_iters, stopped;
+  int lin_state;   // the state whose per-edge terms (lin_of) are current; -1: none
   int lambda_due;  // sharded: the first build's lambda init waits for the all-reduce (k_lba_ctl)
 };
 
@@ -64,6 +65,8 @@ enum LbaSolveMode { kSolveLds = 0, kSolveBlock = 1, kSolveGrid = 2 };
 
 // LM decision points whose inputs a point-sharded run all-reduces first
 enum LbaCtlMode { kCtlInit = 0, kCtlLambda = 1, kCtlDecide = 2 };
+
+static_assert(sizeof(LbaCtrl) % 4 == 0 && sizeof(LbaCtrl) <= 128, "LbaCtrl: copied by dwords into 128 B");
 
 // host-mapped progress word: (done << 32) | trials completed
 struct LbaHostWords {
@@ -110,9 +113,13 @@ struct LbaArgs {
   double* poses[2];          // [7 n_kf] current / trial state (ctrl.state selects)
   double* pts[2];            // [3 n_pts]
   double* err;               // [3 E] errors of the last computeActiveErrors
-  double* hpl;               // [18 E] Hpl = Jp^T W Jl (6 x 3), free-pose edges only
-  double* hpp_e;             // [27 E] per-edge Hpp (lower, 21) + bp (6) terms
-  double* hll_e;             // [12 E] per-edge Hll (9) + bl (3) terms
+  // per-edge terms, two copies (one per LM state, lin_of in lba_kernels.hip):
+  double* hpl;               // 2 x [18 E] Hpl = Jp^T W Jl (6 x 3), free-pose edges only
+  double* hpp_e;             // 2 x [27][n_slots] per-edge Hpp (lower, 21) + bp (6) terms, component-
+                             //   major in pslot order (k_lba_sums reads a pose's run coalesced)
+  double* hll_e;             // 2 x [12][n_edges] per-edge Hll (9) + bl (3) terms, component-major
+  const int* eslot;          // [n_edges] pslot index of each free-pose edge (-1: fixed pose)
+  int n_slots;               // pslot entries (free-pose edges)
   double* hll;               // [9 P]
   double* bl;                // [3 P]
   double* hpp;               // [36 F] full 6 x 6 per free pose
@@ -138,7 +145,8 @@ struct LbaArgs {
   const int* free_kf;        // [n_free] key frame of each free index
   const int* imu_inc;        // [n_free + 1] CSR of the links incident to a free key frame,
   const int* imu_inc_list;   //   link ids ascending
-  double* imu_q;             // [n_imu * kImuPairQ] per link: form over (kf1 dims, kf2 dims) + gradient
+  double* imu_q;             // 2 x [n_imu * kImuPairQ] (one copy per LM state) per link: form over
+                             //   (kf1 dims, kf2 dims) + gradient
   double* himu;              // [n_sys^2 + n_sys] the links' part of the camera system | gradient
   double* imu_tot;           // [1] robust chi2 of the links at the last evaluation
 };
@@ -155,8 +163,9 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st);
 hipError_t lba_schur(const LbaArgs& a, hipStream_t st);
 hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st);
 hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
-// outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles)
-hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, hipStream_t st);
+// outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles),
+// and a copy of the LbaCtrl at ctrl_out
+hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, void* ctrl_out, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
 constexpr int kSchurSplitMax = 8;        // point ranges of k_lba_schur_split (one per XCD)
 constexpr int kSchurSplitEdges = 128;    // target pose edges per (pair, range) block

@@ -235,7 +235,8 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = min(i0 + 256 * u + (int)threadIdx.x, total - 1);
-        // i < 2^13, mg < 2^19: the 24-bit multiply's low word is the product
+        // i mg < rows 2^19 < 2^32: the 24-bit multiply's low word is the
+        // product, and the shift gives i / nq exactly (rows nq^2 < 2^19, planner)
         const int r = (int)(__umul24((uint32_t)i, mg) >> 19), q = i - __mul24(r, nq);
         const auto w = __builtin_amdgcn_raw_buffer_load_b128(
             srs, (int)(__umul24((uint32_t)(rr0 + r), (uint32_t)sp) + 16u * (uint32_t)q), 0, 0);

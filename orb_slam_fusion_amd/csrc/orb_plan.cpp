@@ -146,6 +146,12 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         g.rs_src_rows = std::max(g.rs_src_rows, r1 - r0 + 1);
       }
       rs_lds = std::max(rs_lds, g.rs_src_cols * g.rs_src_rows + 16);  // + k_resize's 3-dword overreach
+      // k_resize splits a staging index i < rows x nq by the multiply-shift
+      // (i * ceil(2^19 / nq)) >> 19, exact while rows x nq^2 < 2^19
+      {
+        const long long nq = g.rs_src_cols / 16;
+        if ((long long)g.rs_src_rows * nq * nq >= (1 << 19)) return why = "scale factor too large for the resize tile", false;
+      }
       int x = 0;
       for (; x <= g.w - 16; x += 16) {
       }

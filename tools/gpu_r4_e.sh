@@ -18,3 +18,6 @@ for r in csv.DictReader(open('$f')):
     n=re.sub(r'\(orbgpu::LbaArgs.*','',r['Name']).replace('void ','').replace('orbgpu::(anonymous namespace)::','')
     print('  %-40s n=%5s avg_us=%8.2f' % (n[:40], r['Calls'], float(r['AverageNs'])/1e3))"
 done
+for NF in 18 25; do timeout -k 10 60 ./build/lba_solve_bench $NF 200 || exit 1; done
+ORBGPU_LBA_TRACE=1 timeout -k 10 100 python tools/bench_lba.py --calls 5 --cpu-calls 0 2> gpurun_out/trace_lba.log > /dev/null || exit 1; tail -2 gpurun_out/trace_lba.log
+ORBGPU_LBA_TRACE=1 timeout -k 10 100 python tools/bench_lba.py --lia --calls 5 --cpu-calls 0 2> gpurun_out/trace_lia.log > /dev/null || exit 1; tail -2 gpurun_out/trace_lia.log
