@@ -50,6 +50,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxKfLds = 1024;  // trial poses staged in LDS up to this many keyframes
+constexpr int kMaxKfImuLds = 128;  // kModelImu trial states (33 doubles) likewise
 constexpr double kTau = 1e-5;    // OptimizationAlgorithmLevenberg _tau
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -1878,6 +1879,60 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_back(LbaArgs a) {
   }
 }
 
+__device__ __forceinline__ void load_state(StateD& s, const double* p) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s.Rwb[i] = p[i];
+    s.Rcw[i] = p[12 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.twb[i] = p[9 + i];
+    s.tcw[i] = p[21 + i];
+    s.v[i] = p[24 + i];
+    s.bg[i] = p[27 + i];
+    s.ba[i] = p[30 + i];
+  }
+}
+
+// Trial key-frame states: ImuCamPose::Update of VP (g2o_types.cc:192-216) and
+// the additive VV / VG / VA updates from the reduced solve (fixed key frames
+// copied); src: key frame k's current state (33 doubles), dst may be src.
+__device__ __forceinline__ void lia_trial_state(const LbaArgs& a, int k, const double* src, double* dst) {
+  const int h = a.hidx[k];
+  if (h < 0) {
+    if (dst != src)
+      for (int i = 0; i < kImuStateStride; ++i) dst[i] = src[i];
+    return;
+  }
+  StateD s;
+  load_state(s, src);
+  const double* u = a.xp + kImuDim * h;
+  double up[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) up[i] = u[i];
+  pose_update(s, up, calib_of(a), true);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.v[i] += u[6 + i];
+    s.bg[i] += u[9 + i];
+    s.ba[i] += u[12 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    dst[i] = s.Rwb[i];
+    dst[12 + i] = s.Rcw[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dst[9 + i] = s.twb[i];
+    dst[21 + i] = s.tcw[i];
+    dst[24 + i] = s.v[i];
+    dst[27 + i] = s.bg[i];
+    dst[30 + i] = s.ba[i];
+  }
+}
+
 // ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
 __device__ __forceinline__ void trial_pose(const LbaArgs& a, int s0, int k, double* out) {
   Se3 T = load_pose(a.poses[s0] + 7 * k);
@@ -1926,6 +1981,20 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
       }
       __syncthreads();
       tposes = tp;
+    }
+  } else {
+    // the trial key-frame states, every block its own copy in LDS (block 0
+    // also writes the state buffer); larger windows: k_lia_trial_states
+    __shared__ double ts[kMaxKfImuLds * kImuStateStride];
+    if (a.n_kf <= kMaxKfImuLds) {
+      for (int k = threadIdx.x; k < a.n_kf; k += kThreads) {
+        double* const d = ts + kImuStateStride * k;
+        lia_trial_state(a, k, a.poses[s0] + kImuStateStride * k, d);
+        if (blockIdx.x == 0)
+          for (int q = 0; q < kImuStateStride; ++q) a.poses[s1][kImuStateStride * k + q] = d[q];
+      }
+      __syncthreads();
+      tposes = ts;
     }
   }
   const int i = blockIdx.x * kThreads + threadIdx.x;
@@ -2105,22 +2174,6 @@ __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* _
 // on the four waves of one workgroup, three in a row: 36 µs per build.)
 constexpr int kImuThreads = 64;
 
-__device__ __forceinline__ void load_state(StateD& s, const double* p) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    s.Rwb[i] = p[i];
-    s.Rcw[i] = p[12 + i];
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    s.twb[i] = p[9 + i];
-    s.tcw[i] = p[21 + i];
-    s.v[i] = p[24 + i];
-    s.bg[i] = p[27 + i];
-    s.ba[i] = p[30 + i];
-  }
-}
-
 // kBuild with trial = 0: the build's forms at the current state (skipped when
 // the accepted trial already left them); with trial = 1: the trial's errors
 // and chi2 and, speculatively, its forms into the other copy of imu_q (as
@@ -2137,7 +2190,10 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   __shared__ double sS[2 * kImuStateStride];  // staged in one round trip
   const int lane = threadIdx.x;
   const int l = blockIdx.x;      // (grid max(n_imu, 1): block 0 alone when there is no link)
-  const double* st = a.poses[trial ? c.state ^ 1 : c.state];
+  // a trial of a window k_lba_trial stages (kMaxKfImuLds) forms the two trial
+  // states here from the current ones; larger windows read k_lia_trial_states'
+  const bool own_trial = trial && a.n_kf <= kMaxKfImuLds;
+  const double* st = a.poses[trial && !own_trial ? c.state ^ 1 : c.state];
   double chi_link = 0;
   if (l < a.n_imu) {
     {
@@ -2164,6 +2220,10 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
       for (int u = 0; u < 2; ++u)
         if (lane + 64 * u < 2 * kImuStateStride) sS[lane + 64 * u] = sv[u];
       wave_lds_sync();
+      if (own_trial) {  // lane 0: kf1, lane 1: kf2, in place
+        if (lane < 2) lia_trial_state(a, lane ? k2 : k1, sS + kImuStateStride * lane, sS + kImuStateStride * lane);
+        wave_lds_sync();
+      }
     }
     const LiaImuDev& E = sL;
     const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
@@ -2317,48 +2377,15 @@ __global__ __launch_bounds__(kThreads) void k_lia_assemble(LbaArgs a) {
   a.himu[idx] = v;
 }
 
-// Trial key-frame states: ImuCamPose::Update of VP (g2o_types.cc:192-216) and
-// the additive VV / VG / VA updates from the reduced solve; one wave per key
-// frame (the SO3 branches are wave-uniform), fixed key frames copied.
-__global__ __launch_bounds__(64) void k_lia_trial_states(LbaArgs a) {
+// windows with more key frames than k_lba_trial<kModelImu> stages in LDS
+// (kMaxKfImuLds): the trial states to the state buffer first, a thread per
+// key frame
+__global__ __launch_bounds__(kThreads) void k_lia_trial_states(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   if (c.done) return;
-  const int k = blockIdx.x, lane = threadIdx.x;
-  const double* src = a.poses[c.state] + kImuStateStride * k;
-  double* dst = a.poses[c.state ^ 1] + kImuStateStride * k;
-  const int h = a.hidx[k];
-  if (h < 0) {
-    if (lane < kImuStateStride) dst[lane] = src[lane];
-    return;
-  }
-  StateD s;
-  load_state(s, src);
-  const double* u = a.xp + kImuDim * h;
-  double up[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) up[i] = u[i];
-  pose_update(s, up, calib_of(a), true);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    s.v[i] += u[6 + i];
-    s.bg[i] += u[9 + i];
-    s.ba[i] += u[12 + i];
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      dst[i] = s.Rwb[i];
-      dst[12 + i] = s.Rcw[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      dst[9 + i] = s.twb[i];
-      dst[21 + i] = s.tcw[i];
-      dst[24 + i] = s.v[i];
-      dst[27 + i] = s.bg[i];
-      dst[30 + i] = s.ba[i];
-    }
-  }
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  if (k < a.n_kf)
+    lia_trial_state(a, k, a.poses[c.state] + kImuStateStride * k, a.poses[c.state ^ 1] + kImuStateStride * k);
 }
 
 inline unsigned blocks(long n, int t) { return (unsigned)((n + t - 1) / t); }
@@ -2484,7 +2511,8 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   }
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
-    hipLaunchKernelGGL(k_lia_trial_states, dim3(a.n_kf), dim3(64), 0, st, a);
+    if (a.n_kf > kMaxKfImuLds)
+      hipLaunchKernelGGL(k_lia_trial_states, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
     hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 1);
     hipLaunchKernelGGL(k_lba_trial<kModelImu>, g, dim3(kThreads), 0, st, a);
   } else {
