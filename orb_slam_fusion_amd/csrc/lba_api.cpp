@@ -309,7 +309,10 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const size_t KS = (size_t)m.pstride * n_kf, P3 = 3 * (size_t)std::max(np, 1);
   const size_t E = std::max(ne, 1), P = std::max(np, 1), F = std::max(nf, 1);
   const size_t NI = std::max(m.n_imu, 1);
-  const int nblk = (int)((std::max(std::max(ne, np), 1) + 255) / 256) + nf + 1;
+  // blocks of the widest grid that writes a.partials (k_lba_sums with, for
+  // kModelImu, its link-assembly blocks)
+  const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + nf + 1 +
+                    (imu ? ((long)n * n + n + 255) / 256 : 0);
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)1) + E;
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order

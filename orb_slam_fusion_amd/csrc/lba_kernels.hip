@@ -24,7 +24,7 @@
 // Jacobians (EdgeMono / EdgeStereo, g2o_types.cc:334-415), 15 reduced-system
 // rows per free key frame, and the IMU links (EdgeInertial + EdgeGyroRW +
 // EdgeAccRW, no points) evaluated by one workgroup (k_lia_imu) and added to
-// the camera-side system (k_lia_assemble) before the solve.
+// the camera-side system (lia_assemble_entry, in k_lba_sums) before the solve.
 //
 // Sums inside a launch have a fixed order (per-thread loops in edge order,
 // fixed trees, block partials summed by the last block in block order), so
@@ -589,6 +589,35 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   lin_edge<M>(a, e, i, a.poses[c.state] + a.pstride * e.kf, X, ev, lin_of(a, c.state));
 }
 
+// The links' part of the camera-side system: entry (r, c) of free key frames
+// (fr, fc) sums, over the links incident to fr in link order, the form
+// entries whose dims land on (r, c); the last n entries are the gradient.
+// Run by extra blocks of k_lba_sums (one launch for the build's sums).
+__device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, long idx) {
+  const int n = a.n_sys;
+  if (idx >= (long)n * n + n) return;
+  const bool grad = idx >= (long)n * n;
+  const int r = grad ? (int)(idx - (long)n * n) : (int)(idx / n);
+  const int cc = grad ? 0 : (int)(idx - (long)r * n);
+  const int fr = r / kImuDim, dr = r - kImuDim * fr;
+  const int fc = cc / kImuDim, dc = cc - kImuDim * fc;
+  const int kr = a.free_kf[fr], kc = a.free_kf[fc];
+  double v = 0;
+  for (int j = a.imu_inc[fr]; j < a.imu_inc[fr + 1]; ++j) {
+    const int l = a.imu_inc_list[j];
+    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
+    const int sr = k1 == kr ? 0 : 1;
+    const double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * state);
+    if (grad) {
+      v += Q[900 + kImuDim * sr + dr];
+    } else {
+      const int sc = k1 == kc ? 0 : (k2 == kc ? 1 : -1);
+      if (sc >= 0) v += Q[(kImuDim * sr + dr) * 30 + kImuDim * sc + dc];
+    }
+  }
+  a.himu[idx] = v;
+}
+
 // ---- buildSystem, vertex side.  Blocks [0, n_free): one free pose each,
 // its edges strided over the threads, a fixed tree per term -> Hpp (6 x 6
 // full), bp and the pose diagonal.  Blocks [n_free, ...): one point per
@@ -647,6 +676,10 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
         a.bp[6 * (size_t)f + (k - 21)] = v;
       }
     }
+  } else if ((int)blockIdx.x >= a.n_free + (max(a.n_pts, 1) + kThreads - 1) / kThreads) {
+    // kModelImu: the links' part of the system (lia_assemble_entry)
+    const long b = (long)blockIdx.x - a.n_free - (max(a.n_pts, 1) + kThreads - 1) / kThreads;
+    lia_assemble_entry(a, c.state, b * kThreads + threadIdx.x);
   } else {
     const int p = (blockIdx.x - a.n_free) * kThreads + threadIdx.x;
     if (p < a.n_pts) {
@@ -2346,37 +2379,6 @@ __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   }
 }
 
-// The links' part of the camera-side system: entry (r, c) of free key frames
-// (fr, fc) sums, over the links incident to fr in link order, the form
-// entries whose dims land on (r, c); the last n entries are the gradient.
-__global__ __launch_bounds__(kThreads) void k_lia_assemble(LbaArgs a) {
-  const LbaCtrl& c = *a.ctrl;
-  if (c.done || !c.need_build) return;
-  const int n = a.n_sys;
-  const long idx = (long)blockIdx.x * kThreads + threadIdx.x;
-  if (idx >= (long)n * n + n) return;
-  const bool grad = idx >= (long)n * n;
-  const int r = grad ? (int)(idx - (long)n * n) : (int)(idx / n);
-  const int cc = grad ? 0 : (int)(idx - (long)r * n);
-  const int fr = r / kImuDim, dr = r - kImuDim * fr;
-  const int fc = cc / kImuDim, dc = cc - kImuDim * fc;
-  const int kr = a.free_kf[fr], kc = a.free_kf[fc];
-  double v = 0;
-  for (int j = a.imu_inc[fr]; j < a.imu_inc[fr + 1]; ++j) {
-    const int l = a.imu_inc_list[j];
-    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
-    const int sr = k1 == kr ? 0 : 1;
-    const double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * c.state);
-    if (grad) {
-      v += Q[900 + kImuDim * sr + dr];
-    } else {
-      const int sc = k1 == kc ? 0 : (k2 == kc ? 1 : -1);
-      if (sc >= 0) v += Q[(kImuDim * sr + dr) * 30 + kImuDim * sc + dc];
-    }
-  }
-  a.himu[idx] = v;
-}
-
 // windows with more key frames than k_lba_trial<kModelImu> stages in LDS
 // (kMaxKfImuLds): the trial states to the state buffer first, a thread per
 // key frame
@@ -2459,10 +2461,10 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
   }
   if (imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
     hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
-    hipLaunchKernelGGL(k_lia_assemble, dim3(blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads)),
-                       dim3(kThreads), 0, st, a);
   }
-  hipLaunchKernelGGL(k_lba_sums, dim3(a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads)),
+  // kModelImu: extra blocks assemble the links' part of the system
+  const unsigned asm_blocks = imu && a.n_sys > 0 ? blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads) : 0;
+  hipLaunchKernelGGL(k_lba_sums, dim3(a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads) + asm_blocks),
                      dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
