@@ -542,7 +542,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       if (p >> 32) break;
       if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
-        if (lba_step(a, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
+        if (lba_step(a, st, issued == 0) != hipSuccess) return ORBGPU_ERR_DEVICE;
         ++issued;
         trace_steps = issued;
       } else {

@@ -2451,15 +2451,15 @@ hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t lba_build(const LbaArgs& a, hipStream_t st) {
+hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   const bool imu = a.model == kModelImu;
-  if (a.n_edges > 0) {
+  if (linearize && a.n_edges > 0) {
     if (imu)
       hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
     else
       hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
   }
-  if (imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
+  if (linearize && imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
     hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
   }
   // kModelImu: extra blocks assemble the links' part of the system
@@ -2525,8 +2525,8 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t lba_step(const LbaArgs& a, hipStream_t st) {
-  hipError_t e = lba_build(a, st);
+hipError_t lba_step(const LbaArgs& a, hipStream_t st, bool linearize) {
+  hipError_t e = lba_build(a, st, linearize);
   if (e == hipSuccess) e = lba_schur(a, st);
   if (e == hipSuccess) e = lba_solve_trial(a, st);
   return e;

@@ -157,9 +157,14 @@ struct LbaArgs {
 // trial key-frame states (ImuCamPose::Update + additive IMU vertices) before
 // the edge stage of a trial.
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st);   // initial errors + LM state
-hipError_t lba_step(const LbaArgs& a, hipStream_t st);    // build (if due) + one trial
+// linearize = false leaves out the edge / link linearisation launches: every
+// build after the first finds its state's terms already written by the
+// accepted trial (LbaCtrl::lin_state; an iteration that ends without
+// accepting a trial either ends the optimisation or rebuilds at a state whose
+// terms are current), so only the first step needs them.
+hipError_t lba_step(const LbaArgs& a, hipStream_t st, bool linearize);  // build (if due) + one trial
 // sharded pieces (the host all-reduces between them)
-hipError_t lba_build(const LbaArgs& a, hipStream_t st);
+hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize = true);
 hipError_t lba_schur(const LbaArgs& a, hipStream_t st);
 hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st);
 hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
