@@ -29,6 +29,17 @@ $(LIB)/liborbgpu.so: $(GPU_OBJS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_OBJS)
 
+# A/B variant of the library (tools/ab_fast.sh, tools/valu_ab.sh): the FAST
+# compass pre-test on four opposite ring pairs instead of two
+$(OBJDIR)/varB/orb_kernels.hip.o: $(CSRC)/orb_kernels.hip $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)/varB
+	$(HIPCC) $(HIPFLAGS) -DORB_FAST_PAIRS=4 -c -o $@ $<
+
+$(LIB)/liborbgpu_varB.so: $(OBJDIR)/varB/orb_kernels.hip.o $(filter-out $(OBJDIR)/orb_kernels.hip.o,$(GPU_OBJS))
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+
+varB: $(LIB)/liborbgpu_varB.so
+
 $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 	@mkdir -p $(LIB)
 	$(CXX) -std=c++17 -O2 -fPIC -shared -o $@ $<
@@ -57,4 +68,4 @@ stamps:
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
 
-.PHONY: all oracle clean stamps
+.PHONY: varB all oracle clean stamps

@@ -551,6 +551,21 @@ __device__ __forceinline__ ushort2_t compass2(ushort2_t v, ushort2_t u, ushort2_
   const ushort2_t hi = min2(max2(u, d), max2(l, r));
   return max2(sub_sat2(v, lo), sub_sat2(hi, v));
 }
+// the same over the four opposite pairs {0,8} {4,12} {6,14} {2,10}: a and b
+// the diagonal pairs ((2,-2), (-2,2)) and ((2,2), (-2,-2)) (x, y)
+__device__ __forceinline__ ushort2_t compass2x4(ushort2_t v, ushort2_t u, ushort2_t d, ushort2_t l,
+                                                ushort2_t r, ushort2_t a0, ushort2_t a1, ushort2_t b0,
+                                                ushort2_t b1) {
+  const ushort2_t lo = max2(max2(min2(u, d), min2(l, r)), max2(min2(a0, a1), min2(b0, b1)));
+  const ushort2_t hi = min2(min2(max2(u, d), max2(l, r)), min2(max2(a0, a1), max2(b0, b1)));
+  return max2(sub_sat2(v, lo), sub_sat2(hi, v));
+}
+
+// opposite ring pairs the compass pre-test checks (2 or 4; a build switch for
+// A/B runs: tools/ab_fast.sh)
+#ifndef ORB_FAST_PAIRS
+#define ORB_FAST_PAIRS 2
+#endif
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
 }
@@ -683,6 +698,12 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   const uint2 sel_v = make_uint2(psel(s_v), psel(s_v + 2));
   const uint2 sel_l = make_uint2(psel(s_l), psel(s_l + 2));
   const uint2 sel_r = make_uint2(psel(s_r), psel(s_r + 2));
+#if ORB_FAST_PAIRS == 4
+  // the diagonal windows: rows -2 / +2 at bytes lead + 1, lead + 5
+  const int s_1 = (lead + 1) & 3, s_5 = (lead + 5) & 3;
+  const uint2 sel_1 = make_uint2(psel(s_1), psel(s_1 + 2));
+  const uint2 sel_5 = make_uint2(psel(s_5), psel(s_5 + 2));
+#endif
 
   const uint32_t tail_mask = (1u << tail) - 1u;  // valid pixels of a row's tail group
 
@@ -720,10 +741,23 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       win(C + 3 * ls, lead + 3, sel_v.x, sel_v.y, qd);
       // compass value per pixel pair; corner at th => value > th
       uint32_t tv[4];
+#if ORB_FAST_PAIRS == 4
+      uint32_t qa0[4], qa1[4], qb0[4], qb1[4];
+      win(C - 2 * ls, lead + 5, sel_5.x, sel_5.y, qa0);  // ring 6: (2, -2)
+      win(C + 2 * ls, lead + 1, sel_1.x, sel_1.y, qa1);  // ring 14: (-2, 2)
+      win(C + 2 * ls, lead + 5, sel_5.x, sel_5.y, qb0);  // ring 2: (2, 2)
+      win(C - 2 * ls, lead + 1, sel_1.x, sel_1.y, qb1);  // ring 10: (-2, -2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        tv[j] = __builtin_bit_cast(uint32_t, compass2x4(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]), as_us2(ql[j]),
+                                                        as_us2(qr[j]), as_us2(qa0[j]), as_us2(qa1[j]),
+                                                        as_us2(qb0[j]), as_us2(qb1[j])));
+#else
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         tv[j] = __builtin_bit_cast(uint32_t, compass2(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]),
                                                       as_us2(ql[j]), as_us2(qr[j])));
+#endif
       // value > th  <=>  bit 15 of the u16 value + (0x7fff - th) (value, th
       // <= 255: no carry out); one packed add per pixel pair, then the flag
       // bits 15 / 31 of the four pairs gathered by two v_perm into bits
