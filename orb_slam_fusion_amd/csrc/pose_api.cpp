@@ -38,6 +38,13 @@ struct orbgpu_pose_ctx {
   uint8_t* h_out = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_out = nullptr;
+  // zero-copy single path (the default): the kernel reads h_in and writes
+  // h_out through their device mappings (fine-grained, uncached host memory),
+  // so a call is one kernel launch -- no copy commands, no graph replay.
+  // ORBGPU_POSE_IO=graph keeps the copy + graph path (A/B runs).
+  bool zero_copy = true;
+  uint8_t* h_in_dev = nullptr;
+  uint8_t* h_out_dev = nullptr;
   struct Graph {
     int bucket = 0, groups = 0;
     double cam[5] = {};
@@ -96,9 +103,14 @@ orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
   }
   const size_t in_bytes = kInObs + sizeof(orbgpu_pose_obs) * ((max_obs + kObsBucket - 1) / kObsBucket * kObsBucket);
   const size_t out_bytes = kOutFlags + (max_obs + kObsBucket - 1) / kObsBucket * kObsBucket;
+  if (const char* e = getenv("ORBGPU_POSE_IO")) c->zero_copy = strcmp(e, "graph") != 0;
+  const unsigned hflags = hipHostMallocMapped | hipHostMallocCoherent;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_in, in_bytes) != hipSuccess || hipMalloc(&c->d_out, out_bytes) != hipSuccess ||
-      hipHostMalloc(&c->h_in, in_bytes) != hipSuccess || hipHostMalloc(&c->h_out, out_bytes) != hipSuccess) {
+      hipHostMalloc(&c->h_in, in_bytes, hflags) != hipSuccess ||
+      hipHostMalloc(&c->h_out, out_bytes, hflags) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_in_dev), c->h_in, 0) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_out_dev), c->h_out, 0) != hipSuccess) {
     orbgpu_pose_ctx_destroy(c);
     return ORBGPU_ERR_DEVICE;
   }
@@ -144,6 +156,18 @@ orbgpu_status orbgpu_pose_opt(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
   if (n_obs > 0) memcpy(c->h_in + kInObs, obs, sizeof(orbgpu_pose_obs) * n_obs);
   const int bucket = std::min(c->max_obs, std::max(1, (n_obs + kObsBucket - 1) / kObsBucket) * kObsBucket);
   const int groups = c->groups_single;
+  if (c->zero_copy) {
+    const hipError_t ze = orbgpu::launch_pose_opt(
+        cd, reinterpret_cast<const float*>(c->h_in_dev + kInPose), c->h_in_dev + kInObs,
+        reinterpret_cast<const int*>(c->h_in_dev + kInN), bucket, 1,
+        reinterpret_cast<float*>(c->h_out_dev + kOutPose), c->h_out_dev + kOutFlags,
+        reinterpret_cast<int*>(c->h_out_dev + kOutInl), nullptr, c->stream, groups);
+    if (ze != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    memcpy(Tcw_out, c->h_out + kOutPose, sizeof(orbgpu_pose));
+    memcpy(n_inliers, c->h_out + kOutInl, sizeof(int));
+    if (n_obs > 0) memcpy(outlier, c->h_out + kOutFlags, n_obs);
+    return ORBGPU_OK;
+  }
   orbgpu_pose_ctx::Graph* g = nullptr;
   for (auto& x : c->graphs)
     if (x.bucket == bucket && x.groups == groups && memcmp(x.cam, cd, sizeof(cd)) == 0) g = &x;

@@ -389,8 +389,22 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   const int grp = __builtin_amdgcn_readfirstlane(t >> 8);
   int tg = t & (kPoseThreads - 1);
   int lane = t & 63, gw = (t >> 6) & (kPoseWaves - 1);
-  const int n = nobs[p];
   const PoseObsDev* obs = obs_all + (size_t)p * obs_stride;
+  // the observations up to the stride (in bounds whatever n is) are loaded
+  // with n in one round trip when they fit kHold per thread -- the single-
+  // problem path reads them straight from host memory (pose_api.cpp)
+  constexpr int kHold = 3;
+  const bool held = obs_stride <= NT * kHold;
+  float oh[kHold][7];
+  if (held) {
+#pragma unroll
+    for (int u = 0; u < kHold; ++u) {
+      const int i = t + NT * u;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) oh[u][k] = i < obs_stride ? reinterpret_cast<const float*>(obs + i)[k] : 0.f;
+    }
+  }
+  const int n = nobs[p];
   uint8_t* level = outlier_all + (size_t)p * obs_stride;
   const float* pin = pose_in + 7 * p;
   if (n < 3) {  // optimizer.cc:951
@@ -416,16 +430,19 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   int n_st;
   {
     int c = 0;
-    for (int i = t; i < cap; i += NT) c += obs[i].ur >= 0.f ? 1 : 0;
+    if (held) {
+#pragma unroll
+      for (int u = 0; u < kHold; ++u) c += t + NT * u < cap && oh[u][5] >= 0.f ? 1 : 0;
+    } else {
+      for (int i = t; i < cap; i += NT) c += obs[i].ur >= 0.f ? 1 : 0;
+    }
     n_st = block_sum_i<NW>(c, sh.ired);
     const int w = t >> 6;
     int base_s = 0, base_m = n_st;
-    for (int i0 = 0; i0 < cap; i0 += NT) {
+    // one NT-slot step of the stable partition (o: observation i0 + t)
+    auto part_step = [&](int i0, const float (&o)[7]) {
       const int i = i0 + t;
       const bool in = i < cap;
-      float o[7];  // PoseObsDev as 7 floats (no aggregate copy through scratch)
-#pragma unroll
-      for (int k = 0; k < 7; ++k) o[k] = reinterpret_cast<const float*>(obs + min(i, cap - 1))[k];
       const bool st = in && o[5] >= 0.f;  // ur
       const uint64_t bs = __ballot(st), bm = __ballot(in && !st);
       if (lane == 0) {
@@ -452,6 +469,18 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
       base_s += ts;
       base_m += tm;
       __syncthreads();
+    };
+    if (held) {
+#pragma unroll
+      for (int u = 0; u < kHold; ++u)
+        if (NT * u < cap) part_step(NT * u, oh[u]);
+    } else {
+      for (int i0 = 0; i0 < cap; i0 += NT) {
+        float o[7];  // PoseObsDev as 7 floats (no aggregate copy through scratch)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) o[k] = reinterpret_cast<const float*>(obs + min(i0 + t, cap - 1))[k];
+        part_step(i0, o);
+      }
     }
   }
   for (int i = cap + t; i < n; i += NT) level[i] = 0;
