@@ -465,6 +465,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.n_sys = n;
   a.n_pairs = n_pairs;
   a.sc_split = sc_split;
+  // the build re-linearises every iteration instead of taking the accepted
+  // trial's terms (same values; tests/test_gpu_lba.py compares the two)
+  a.force_lin = std::getenv("ORBGPU_LBA_RELINEARIZE") != nullptr;
   a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
   if (sc_split > 1) a.sc_part = dp(c_scp);
   if (sc.ok) {
@@ -542,7 +545,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       if (p >> 32) break;
       if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
-        if (lba_step(a, st, issued == 0) != hipSuccess) return ORBGPU_ERR_DEVICE;
+        if (lba_step(a, st, issued == 0 || a.force_lin) != hipSuccess) return ORBGPU_ERR_DEVICE;
         ++issued;
         trace_steps = issued;
       } else {

@@ -579,7 +579,7 @@ template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   // nothing due, or the accepted trial already left this state's terms
-  if (c.done || !c.need_build || c.lin_state == c.state) return;
+  if (c.done || !c.need_build || (c.lin_state == c.state && !a.force_lin)) return;
   const int i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n_edges) return;
   const LbaEdgeDev e = a.edges[i];
@@ -2214,7 +2214,7 @@ constexpr int kImuThreads = 64;
 template <bool kBuild>
 __global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
   const LbaCtrl& c = *a.ctrl;
-  if (c.done || (kBuild && !trial && (!c.need_build || c.lin_state == c.state))) return;
+  if (c.done || (kBuild && !trial && (!c.need_build || (c.lin_state == c.state && !a.force_lin)))) return;
   __shared__ double sJ[9 * 24];
   __shared__ double sOJ[9 * 24];
   __shared__ double sE[9];       // the link's error (inertial_edge_core, lane 0)

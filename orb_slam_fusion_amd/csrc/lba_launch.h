@@ -103,6 +103,7 @@ struct LbaArgs {
   // Schur complement by point range (k_lba_schur_split): sc_split ranges of
   // the shard's points (1..kSchurSplitMax; 0 = the band / pair kernels), and
   // per free pose the pslot offsets where each range starts
+  int force_lin;             // 1: every build re-linearises (ORBGPU_LBA_RELINEARIZE; tests compare)
   int sc_split;
   const int* pose_split;  // [n_free * (sc_split + 1)]
   int n_chunks;

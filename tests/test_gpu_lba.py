@@ -126,9 +126,9 @@ def test_lba_block_and_grid_solvers_identical(gpu_available, n_kf):
 
 
 def test_lba_point_seen_by_many_keyframes(gpu_available):
-    """Points observed by more free key frames than a Schur chunk holds (390 >
-    kSchurChunkEdges = 384): the one-block-per-pose-pair Schur kernel takes the
-    window -- one LM iteration against the oracle."""
+    """Points observed by 390 free key frames (past the 8 edges a Schur thread
+    looks up per batch: the lookup walks the rest in batches) -- one LM
+    iteration against the oracle."""
     p = synth.lba_problem(seed=26, n_kf=392, n_pts=12, obs_per_pt=390, n_fixed=2)
     _compare(p, iters=1)
 
@@ -292,3 +292,31 @@ def test_lba_two_ranks_one_gpu(gpu_available, tmp_path, ordered):
     owner = (p.edges["point"] >= cut[1]).astype(int)
     outl = np.where(owner == 0, r[0]["outlier"], r[1]["outlier"])
     assert (outl == single["outlier"]).all()
+
+
+def _same(a, b):
+    for k in ("stats", "poses_d", "pts", "outlier"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_lba_trial_terms_equal_relinearised(gpu_available, monkeypatch):
+    """An accepted trial leaves its state's per-edge terms for the next build
+    (lin_of / LbaCtrl::lin_state); re-linearising every build instead
+    (ORBGPU_LBA_RELINEARIZE) computes the same values: bit-identical runs."""
+    p = synth.lba_problem(seed=31, n_kf=12, n_pts=900, obs_per_pt=5, n_fixed=2, outlier_pct=5)
+    spec = LocalBundleAdjuster().optimize(p)
+    monkeypatch.setenv("ORBGPU_LBA_RELINEARIZE", "1")
+    relin = LocalBundleAdjuster().optimize(p)
+    _same(spec, relin)
+    assert spec["stats"][3] >= 3  # several accepted trials
+
+
+@pytest.mark.parametrize("mode", ["split", "pair", "band"])
+def test_lba_schur_paths(gpu_available, monkeypatch, mode):
+    """The Schur complement by point range (default), by pose pair and by
+    point band (ORBGPU_SCHUR; band falls back to pairs when a point spans more
+    than 15 free key frames) each match the oracle and repeat bit for bit."""
+    monkeypatch.setenv("ORBGPU_SCHUR", mode)
+    p = synth.lba_problem(seed=32)
+    got, _ = _compare(p)
+    _same(got, LocalBundleAdjuster().optimize(p))

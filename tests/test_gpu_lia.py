@@ -112,3 +112,25 @@ def test_lia_then_lba_on_one_context(gpu_available):
     b2 = LocalBundleAdjuster().optimize(pl)
     assert np.array_equal(a1["kfs21"], a2["kfs21"]) and np.array_equal(a1["outlier"], a2["outlier"])
     assert np.array_equal(b1["poses_d"], b2["poses_d"])
+
+
+def test_lia_trial_terms_equal_relinearised(gpu_available, monkeypatch):
+    """The accepted trial's visual terms and IMU link forms (written while the
+    trial is evaluated) equal a fresh linearisation at the accepted state
+    (ORBGPU_LBA_RELINEARIZE): bit-identical runs."""
+    pb = synth.lia_problem()
+    spec = LocalBundleAdjuster().optimize_inertial(pb)
+    monkeypatch.setenv("ORBGPU_LBA_RELINEARIZE", "1")
+    relin = LocalBundleAdjuster().optimize_inertial(pb)
+    for k in ("stats", "kfs21", "pts", "outlier"):
+        assert np.array_equal(spec[k], relin[k]), k
+
+
+def test_lia_trial_states_past_lds_table(gpu_available):
+    """More key frames than the trial kernel stages in LDS (kMaxKfImuLds =
+    128): the trial states go through k_lia_trial_states, against the
+    oracle."""
+    pb = synth.lia_problem(18, n_opt=131, n_fixed_cov=2, n_pts=2000, max_obs=3, max_depth=10.0,
+                           consecutive=True)
+    assert len(pb.kfs) > 128
+    _compare(pb)
