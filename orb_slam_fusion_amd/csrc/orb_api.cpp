@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -227,6 +228,13 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   a.host_plan = &h->plan.hdr;
   a.plan = h->d_plan;
   a.n_cu = h->n_cu;
+  // the resize chain as one launch (k_pyramid, a workgroup per image) when the
+  // batch fills the device, else per level; ORBGPU_RESIZE=levels|fused forces
+  {
+    const char* e = std::getenv("ORBGPU_RESIZE");
+    const bool fused = e ? std::strcmp(e, "fused") == 0 : n >= h->n_cu;
+    a.pyramid_groups = fused ? pyramid_groups_for((size_t)h->plan.hdr.rs_lds) : 0;
+  }
   a.cells = h->d_cells;
   a.rs_tab = h->d_rs;
   a.imgs = imgs;
@@ -316,7 +324,8 @@ static bool same_launch(const ExtractLaunch& x, const ExtractLaunch& y) {
          x.angle == y.angle && x.desc == y.desc && x.octree_lds == y.octree_lds &&
          x.lap0 == y.lap0 && x.lap1 == y.lap1 && x.kps_out == y.kps_out &&
          x.desc_out == y.desc_out && x.cap == y.cap && x.n_out == y.n_out &&
-         x.mono_out == y.mono_out && x.err == y.err && x.n_cu == y.n_cu && x.events == y.events;
+         x.mono_out == y.mono_out && x.err == y.err && x.n_cu == y.n_cu && x.events == y.events &&
+         x.pyramid_groups == y.pyramid_groups;
 }
 
 // Enqueue the single-image chain between its copies: the image from pinned

@@ -188,17 +188,16 @@ __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t
 // buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
 constexpr int kBufRsrcWord3 = 0x00020000;
 
-__global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
-                                                const int* __restrict__ rs_tab, ImgSrc src,
-                                                uint8_t* __restrict__ pyr, int l) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+// One output tile (tyx) of level l of image img by 256 threads (tid) with an
+// LDS slice of PlanHeader::rs_lds bytes; every thread of the workgroup passes
+// its one barrier.  live = false: the group takes part in the barrier and
+// writes nothing (k_pyramid's spare groups).
+__device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
+                                            const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
+                                            int tyx, uint8_t* __restrict__ lds, int tid, bool live) {
   constexpr int RW = kResizeTileH / 4;  // output rows per wave
   const LevelGeom& g = P->lev[l];
   const int sw = P->lev[l - 1].w;
-  const int nb = gridDim.x * gridDim.y * gridDim.z;
-  const int wid = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nb);
-  const int img = wid / (g.rs_tiles_x * g.rs_tiles_y);
-  const int tyx = wid - img * (g.rs_tiles_x * g.rs_tiles_y);
   const int x0 = (tyx % g.rs_tiles_x) * kResizeTileW, y0 = (tyx / g.rs_tiles_x) * kResizeTileH;
   const int xl = min(x0 + kResizeTileW, g.w) - 1, yl = min(y0 + kResizeTileH, g.h) - 1;
   const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
@@ -211,7 +210,7 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
 
   // taps, fetched up front (before any store, so no wait ever queues behind one)
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int x = x0 + 4 * lane;
   const int ys = y0 + RW * wave;  // wave-uniform first output row
   int2 xa[4];
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
       int at[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int i = min(i0 + 256 * u + (int)threadIdx.x, total - 1);
+        const int i = min(i0 + 256 * u + tid, total - 1);
         // i mg < rows 2^19 < 2^32: the 24-bit multiply's low word is the
         // product, and the shift gives i / nq exactly (rows nq^2 < 2^19, planner)
         const int r = (int)(__umul24((uint32_t)i, mg) >> 19), q = i - __mul24(r, nq);
@@ -247,7 +246,7 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
       for (int u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(lds + at[u]) = v[u];
     }
   } else {
-    for (int i = threadIdx.x; i < nrow * ncol; i += 256) {
+    for (int i = tid; i < nrow * ncol; i += 256) {
       const int r = i / ncol, c = i - r * ncol;
       lds[i] = S[(size_t)(rr0 + r) * sp + min(c0 + c, sw - 1)];
     }
@@ -277,7 +276,7 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
   const bool bytewise = __builtin_amdgcn_ballot_w64(active && hi - lo > 7) != 0;
   const bool any_tail = __builtin_amdgcn_ballot_w64(active && tail_k != 0) != 0;
   __syncthreads();
-  if (ys > yl) return;  // after the barrier: every wave staged its share
+  if (!live || ys > yl) return;  // after the barrier: every wave staged its share
 
   // stream the source rows: two register slots hold rows p and p+1 (slot sa
   // = row p; a wave-uniform flag, so advancing one row recomputes into the
@@ -342,6 +341,48 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
       out_row(y, h0, q0, h1, q1, b0, b1);
     } else {
       out_row(y, h1, q1, h0, q0, b0, b1);
+    }
+  }
+}
+
+// k_resize: one tile per workgroup, one launch per level (tiles of all the
+// batch's images).
+__global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
+                                                const int* __restrict__ rs_tab, ImgSrc src,
+                                                uint8_t* __restrict__ pyr, int l) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const LevelGeom& g = P->lev[l];
+  const int nb = gridDim.x * gridDim.y * gridDim.z;
+  const int wid = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nb);
+  const int img = wid / (g.rs_tiles_x * g.rs_tiles_y);
+  const int tyx = wid - img * (g.rs_tiles_x * g.rs_tiles_y);
+  resize_tile(P, rs_tab, src, pyr, l, img, tyx, lds, threadIdx.x, true);
+}
+
+// k_pyramid: the whole chain (levels 1 .. L-1) of one image per workgroup of
+// G x 256 threads in ONE launch: the G groups take a level's tiles G at a
+// time (each its own LDS slice, the same tile code as k_resize, so the same
+// bytes), and the workgroup barrier after a level's last round orders its
+// stores before the next level's loads -- no cross-workgroup dependency, so
+// no grid-wide flag or fence.  For batches of at least as many images as the
+// device has CUs (a workgroup per image then fills it); smaller batches take
+// the per-level launches, whose every launch spreads one level over the
+// whole device (latency).
+__global__ __launch_bounds__(1024) void k_pyramid(const PlanHeader* __restrict__ P,
+                                                  const int* __restrict__ rs_tab, ImgSrc src,
+                                                  uint8_t* __restrict__ pyr, int rs_lds) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int G = blockDim.x >> 8;
+  const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), tid = threadIdx.x & 255;
+  const int img = xcd_remap(blockIdx.x, gridDim.x);
+  uint8_t* const my = lds + grp * rs_lds;
+  for (int l = 1; l < P->levels; ++l) {
+    const LevelGeom& g = P->lev[l];
+    const int nt = g.rs_tiles_x * g.rs_tiles_y;
+    for (int t0 = 0; t0 < nt; t0 += G) {
+      const int tile = t0 + grp;
+      resize_tile(P, rs_tab, src, pyr, l, img, tile < nt ? tile : 0, my, tid, tile < nt);
+      __syncthreads();  // the slice is restaged by the group's next tile; the level is complete
     }
   }
 }
@@ -847,7 +888,8 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         }
         const uint64_t km = __ballot(kp);
         if (kp) {
-          const int r = LS ? i / LS : i >> QB, q = LS ? i - r * LS : i & QM;
+          constexpr int LSD = LS ? LS : 1;  // (no division by zero in the LS == 0 instance)
+          const int r = LS ? i / LSD : i >> QB, q = LS ? i - r * LS : i & QM;
           const int pos = written + __popcll(km & lt);
           if (pos < c.slot_cap)
             out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
@@ -1594,10 +1636,15 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     if (a.events) (void)hipEventRecord(a.events[i], st);
   };
   mark(0);
-  for (int l = 1; l < H.levels; ++l) {
-    const LevelGeom& g = H.lev[l];
-    dim3 grid(g.rs_tiles_x, g.rs_tiles_y, n);
-    hipLaunchKernelGGL(k_resize, grid, dim3(256), H.rs_lds, st, a.plan, a.rs_tab, src, a.pyr, l);
+  if (a.pyramid_groups > 0) {  // one launch: a workgroup per image (k_pyramid)
+    hipLaunchKernelGGL(k_pyramid, dim3(n), dim3(256 * a.pyramid_groups), (size_t)a.pyramid_groups * H.rs_lds, st,
+                       a.plan, a.rs_tab, src, a.pyr, H.rs_lds);
+  } else {
+    for (int l = 1; l < H.levels; ++l) {
+      const LevelGeom& g = H.lev[l];
+      dim3 grid(g.rs_tiles_x, g.rs_tiles_y, n);
+      hipLaunchKernelGGL(k_resize, grid, dim3(256), H.rs_lds, st, a.plan, a.rs_tab, src, a.pyr, l);
+    }
   }
   mark(1);
   hipLaunchKernelGGL(k_blur, dim3(n * H.blur_tiles), dim3(256), 0, st, a.plan, src,
@@ -1638,8 +1685,18 @@ hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes) {
     const hipError_t e = lds_optin((const void*)k_octree, (int)octree_bytes);
     if (e != hipSuccess) return e;
   }
-  if (resize_bytes > 64 * 1024) return lds_optin((const void*)k_resize, (int)resize_bytes);
+  if (resize_bytes > 64 * 1024) {
+    const hipError_t e = lds_optin((const void*)k_resize, (int)resize_bytes);
+    if (e != hipSuccess) return e;
+  }
+  const int G = pyramid_groups_for(resize_bytes);
+  if (G > 0 && (size_t)G * resize_bytes > 64 * 1024) return lds_optin((const void*)k_pyramid, (int)(G * resize_bytes));
   return hipSuccess;
+}
+
+int pyramid_groups_for(size_t resize_bytes) {
+  if (resize_bytes == 0) return 4;
+  return (int)std::min<size_t>(4, (160 * 1024) / resize_bytes);
 }
 
 }  // namespace orbgpu

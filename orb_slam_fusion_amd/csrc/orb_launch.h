@@ -36,6 +36,7 @@ struct ExtractLaunch {
   int* mono_out;
   int* err;
   int n_cu;            // compute units of the device (persistent grids)
+  int pyramid_groups;  // > 0: the resize chain as one k_pyramid launch, this many tile groups a workgroup
   hipEvent_t* events;  // optional: kStages + 1 events recorded around the stages
 };
 
@@ -44,5 +45,7 @@ enum Stage : int { kStResize, kStBlur, kStFast, kStOctree, kStDescribe, kStAssem
 
 hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st);
 hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes);
+// tile groups of a k_pyramid workgroup for the plan's resize tile LDS (0: none fits)
+int pyramid_groups_for(size_t resize_bytes);
 
 }  // namespace orbgpu

@@ -250,3 +250,33 @@ def test_handles_with_different_plans_coexist(gpu_available):
     again = big(left)
     assert ref[0] == again[0] and ref[1].tobytes() == again[1].tobytes()
     _compare((4000, 1.2, 8, 20, 7), left)
+
+
+@pytest.mark.parametrize("case", ["c2", "euroc", "odd", "scale2", "scale15", "rounding1"])
+def test_fused_pyramid_bit_exact(gpu_available, monkeypatch, case):
+    """The resize chain as ONE launch (k_pyramid: a workgroup per image whose
+    tile groups walk the levels, the same tile code as the per-level
+    launches), forced for single images by ORBGPU_RESIZE=fused -- batches of
+    at least as many images as the device has CUs take it by default."""
+    monkeypatch.setenv("ORBGPU_RESIZE", "fused")
+    if case == "c2":
+        assert _compare(C2, synth.stereo_frame(0)[0]) > 900
+    elif case == "euroc":
+        assert _compare(EUROC, synth.stereo_frame(10)[1]) > 1100
+    elif case == "odd":
+        full, _ = synth.stereo_frame(20, w=641, h=397)
+        _compare((1000, 1.2, 8, 20, 7), full)
+    elif case == "scale2":  # a wide resize window: fewer tile groups fit a workgroup's LDS
+        full, _ = synth.stereo_frame(21, w=1024, h=768)
+        _compare((1000, 2.0, 4, 20, 7), full)
+    elif case == "scale15":
+        full, _ = synth.stereo_frame(21, w=1024, h=768)
+        _compare((1000, 1.5, 6, 20, 7), full)
+    else:
+        assert _compare(C2, synth.stereo_frame(4)[0], rounding=1) > 900
+
+
+def test_fused_pyramid_batch(gpu_available, monkeypatch):
+    """A batch through the one-launch pyramid equals the oracle image by image."""
+    monkeypatch.setenv("ORBGPU_RESIZE", "fused")
+    test_batch_matches_single(gpu_available)
