@@ -8,5 +8,6 @@ bash tools/valu_ab.sh > gpurun_out/valu_ab.log 2>&1 || { tail -5 gpurun_out/valu
 grep -E "liborbgpu|k_fast|k_resize" gpurun_out/valu_ab.log
 bash tools/ab_fast.sh > gpurun_out/ab_fast.log 2>&1 || { tail -5 gpurun_out/ab_fast.log; exit 1; }
 cut -c1-300 gpurun_out/ab_fast.log
+for R in levels fused; do echo "== resize $R, 256 images"; ORBGPU_RESIZE=$R timeout -k 10 120 python tools/prof_stages.py --frames 128 --iters 20 --mode ext 2>/dev/null | tail -c 300 || exit 1; done
 echo "== pose single"; timeout -k 10 120 python tools/pose_single.py 2>/dev/null || exit 1
 bash tools/gpu_r4_e.sh

@@ -76,6 +76,8 @@ def main():
         for r in csv.DictReader(open(a.stats)):
             stats[short(r["Name"])] = (float(r["AverageNs"]), int(r["Calls"]))
     for st, (kname, per) in STAGES.items():
+        if st == "resize" and any("k_pyramid" in src for src in (tr, sq, stats)):
+            kname, per = "k_pyramid", 1  # the chain as one launch (batches that fill the device)
         row = {"kernel": kname, "dispatches_per_launch": per}
         t = tr.get(kname, {})
         if "FETCH_SIZE" in t and "WRITE_SIZE" in t:

@@ -16,7 +16,10 @@ export TMPDIR=/tmp
 R=${ROUND:-r02}
 O=gpurun_out/prof_$R
 rm -rf "$O"; mkdir -p "$O"
-WL="tools/prof_stages.py --frames 32 --iters 5 --mode both"
+# the bench's launch size: 128 stereo frames = 256 images a launch (the
+# resize chain then runs as one k_pyramid launch, as in the bench)
+FR=${FRAMES:-128}
+WL="tools/prof_stages.py --frames $FR --iters 5 --mode both"
 SQ="SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 180 rocprofv3 --pmc $c --kernel-trace -d $O/traffic -o $c --output-format csv \
@@ -35,7 +38,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/bench_prof -o be
 f=$(find $O/bench_prof -name '*kernel_stats.csv' | head -n1)
 cp "$f" $O/bench_kernel_stats.csv
 python3 tools/pmc_kernels.py --traffic $O/traffic --sq $O/sq --calib $O/calib \
-  --stats $O/bench_kernel_stats.csv --out $O/kernels.json > $O/kernels.log 2>&1 \
+  --stats $O/bench_kernel_stats.csv --images-per-launch $((2 * FR)) --out $O/kernels.json > $O/kernels.log 2>&1 \
   || { echo "summary failed"; tail -5 $O/kernels.log; exit 1; }
 echo "kernels.json ok"
 if [ "${RUN_BENCH:-1}" = "1" ]; then
