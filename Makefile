@@ -29,13 +29,16 @@ $(LIB)/liborbgpu.so: $(GPU_OBJS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(GPU_OBJS)
 
-# A/B variant of the library (tools/ab_fast.sh, tools/valu_ab.sh): the FAST
-# compass pre-test on four opposite ring pairs instead of two
-$(OBJDIR)/varB/orb_kernels.hip.o: $(CSRC)/orb_kernels.hip $(GPU_HDRS)
+# A/B variant of the library (tools/ab_fast.sh, tools/valu_ab.sh): FAST with
+# the survivor list held whole instead of expanded per 64 group entries
+VARB_DEF := -DORB_FAST_SV_FULL=1
+$(OBJDIR)/varB/%.o: $(CSRC)/% $(GPU_HDRS)
 	@mkdir -p $(OBJDIR)/varB
-	$(HIPCC) $(HIPFLAGS) -DORB_FAST_PAIRS=4 -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(VARB_DEF) -c -o $@ $<
 
-$(LIB)/liborbgpu_varB.so: $(OBJDIR)/varB/orb_kernels.hip.o $(filter-out $(OBJDIR)/orb_kernels.hip.o,$(GPU_OBJS))
+VARB_OBJS := $(OBJDIR)/varB/orb_kernels.hip.o $(OBJDIR)/varB/orb_plan.cpp.o \
+             $(filter-out $(OBJDIR)/orb_kernels.hip.o $(OBJDIR)/orb_plan.cpp.o,$(GPU_OBJS))
+$(LIB)/liborbgpu_varB.so: $(VARB_OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 varB: $(LIB)/liborbgpu_varB.so

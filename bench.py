@@ -288,7 +288,6 @@ def main() -> int:
     stage_avg["pose_opt"] = pose_ms
     dom = max(stage_avg, key=stage_avg.get)
     imgs_per_launch = 2 * Bp
-    n_cu = torch.cuda.get_device_properties(local).multi_processor_count
     prof = load_profile()
     pk = (prof or {}).get("stages", {})
 
@@ -306,8 +305,8 @@ def main() -> int:
     for st, ms in stage_avg.items():
         b = per_img.get(st, 0) * imgs_per_launch if st != "pose_opt" else 0
         kname = STAGE_KERNELS[st]
-        if st == "resize" and imgs_per_launch >= n_cu and os.environ.get("ORBGPU_RESIZE") != "levels":
-            kname = "k_pyramid"  # one launch for the chain when a launch fills the device (orb_api.cpp)
+        if st == "resize" and os.environ.get("ORBGPU_RESIZE") == "fused":
+            kname = "k_pyramid"  # the chain as one launch (orb_api.cpp, opt-in)
         row = {"kernel": kname, "avg_ms_per_launch": round(ms, 5),
                "algorithmic_bytes_per_launch": int(b)}
         if b:

@@ -228,11 +228,12 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   a.host_plan = &h->plan.hdr;
   a.plan = h->d_plan;
   a.n_cu = h->n_cu;
-  // the resize chain as one launch (k_pyramid, a workgroup per image) when the
-  // batch fills the device, else per level; ORBGPU_RESIZE=levels|fused forces
+  // the resize chain per level (default), or as one launch (k_pyramid, a
+  // workgroup per image) with ORBGPU_RESIZE=fused -- bit-identical, slower
+  // at every batch size measured
   {
     const char* e = std::getenv("ORBGPU_RESIZE");
-    const bool fused = e ? std::strcmp(e, "fused") == 0 : n >= h->n_cu;
+    const bool fused = e && std::strcmp(e, "fused") == 0;
     a.pyramid_groups = fused ? pyramid_groups_for((size_t)h->plan.hdr.rs_lds) : 0;
   }
   a.cells = h->d_cells;

@@ -364,10 +364,10 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
 // time (each its own LDS slice, the same tile code as k_resize, so the same
 // bytes), and the workgroup barrier after a level's last round orders its
 // stores before the next level's loads -- no cross-workgroup dependency, so
-// no grid-wide flag or fence.  For batches of at least as many images as the
-// device has CUs (a workgroup per image then fills it); smaller batches take
-// the per-level launches, whose every launch spreads one level over the
-// whole device (latency).
+// no grid-wide flag or fence.  Opt-in (ORBGPU_RESIZE=fused): at 256 images
+// a launch it took 0.28 ms against 0.22 ms for the seven per-level launches
+// (each of which spreads one level over the whole device at full occupancy),
+// DESIGN §4.
 __global__ __launch_bounds__(1024) void k_pyramid(const PlanHeader* __restrict__ P,
                                                   const int* __restrict__ rs_tab, ImgSrc src,
                                                   uint8_t* __restrict__ pyr, int rs_lds) {
@@ -592,20 +592,10 @@ __device__ __forceinline__ ushort2_t compass2(ushort2_t v, ushort2_t u, ushort2_
   const ushort2_t hi = min2(max2(u, d), max2(l, r));
   return max2(sub_sat2(v, lo), sub_sat2(hi, v));
 }
-// the same over the four opposite pairs {0,8} {4,12} {6,14} {2,10}: a and b
-// the diagonal pairs ((2,-2), (-2,2)) and ((2,2), (-2,-2)) (x, y)
-__device__ __forceinline__ ushort2_t compass2x4(ushort2_t v, ushort2_t u, ushort2_t d, ushort2_t l,
-                                                ushort2_t r, ushort2_t a0, ushort2_t a1, ushort2_t b0,
-                                                ushort2_t b1) {
-  const ushort2_t lo = max2(max2(min2(u, d), min2(l, r)), max2(min2(a0, a1), min2(b0, b1)));
-  const ushort2_t hi = min2(min2(max2(u, d), max2(l, r)), min2(max2(a0, a1), max2(b0, b1)));
-  return max2(sub_sat2(v, lo), sub_sat2(hi, v));
-}
-
-// opposite ring pairs the compass pre-test checks (2 or 4; a build switch for
-// A/B runs: tools/ab_fast.sh)
-#ifndef ORB_FAST_PAIRS
-#define ORB_FAST_PAIRS 2
+// A/B build switch (make varB): the survivor list expanded once and held
+// whole (LDS 2 bytes a detection pixel) instead of per 64 group entries
+#ifndef ORB_FAST_SV_FULL
+#define ORB_FAST_SV_FULL 0
 #endif
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m, uint32_t acc) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
@@ -669,7 +659,8 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   uint8_t* roi = lds;
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
   uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
-  uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) + 2 * kFastSvChunk);
+  uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) +
+                                             (ORB_FAST_SV_FULL ? ((2 * nd + 15) & ~15) : 2 * kFastSvChunk));
   auto sci = [&](int i) {
     if constexpr (LS != 0) return i + LS + 1;
     return ((i >> QB) + 1) * sp2 + (i & QM) + 1;
@@ -739,12 +730,6 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   const uint2 sel_v = make_uint2(psel(s_v), psel(s_v + 2));
   const uint2 sel_l = make_uint2(psel(s_l), psel(s_l + 2));
   const uint2 sel_r = make_uint2(psel(s_r), psel(s_r + 2));
-#if ORB_FAST_PAIRS == 4
-  // the diagonal windows: rows -2 / +2 at bytes lead + 1, lead + 5
-  const int s_1 = (lead + 1) & 3, s_5 = (lead + 5) & 3;
-  const uint2 sel_1 = make_uint2(psel(s_1), psel(s_1 + 2));
-  const uint2 sel_5 = make_uint2(psel(s_5), psel(s_5 + 2));
-#endif
 
   const uint32_t tail_mask = (1u << tail) - 1u;  // valid pixels of a row's tail group
 
@@ -782,23 +767,10 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       win(C + 3 * ls, lead + 3, sel_v.x, sel_v.y, qd);
       // compass value per pixel pair; corner at th => value > th
       uint32_t tv[4];
-#if ORB_FAST_PAIRS == 4
-      uint32_t qa0[4], qa1[4], qb0[4], qb1[4];
-      win(C - 2 * ls, lead + 5, sel_5.x, sel_5.y, qa0);  // ring 6: (2, -2)
-      win(C + 2 * ls, lead + 1, sel_1.x, sel_1.y, qa1);  // ring 14: (-2, 2)
-      win(C + 2 * ls, lead + 5, sel_5.x, sel_5.y, qb0);  // ring 2: (2, 2)
-      win(C - 2 * ls, lead + 1, sel_1.x, sel_1.y, qb1);  // ring 10: (-2, -2)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        tv[j] = __builtin_bit_cast(uint32_t, compass2x4(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]), as_us2(ql[j]),
-                                                        as_us2(qr[j]), as_us2(qa0[j]), as_us2(qa1[j]),
-                                                        as_us2(qb0[j]), as_us2(qb1[j])));
-#else
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         tv[j] = __builtin_bit_cast(uint32_t, compass2(as_us2(qv[j]), as_us2(qu[j]), as_us2(qd[j]),
                                                       as_us2(ql[j]), as_us2(qr[j])));
-#endif
       // value > th  <=>  bit 15 of the u16 value + (0x7fff - th) (value, th
       // <= 255: no carry out); one packed add per pixel pair, then the flag
       // bits 15 / 31 of the four pairs gathered by two v_perm into bits
@@ -833,6 +805,59 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(0);
+#if ORB_FAST_SV_FULL
+    // the whole survivor list, expanded once (raster order: entries in order,
+    // pixels LSB-first), then scores and NMS over it
+    int ns = 0;
+    for (int b0 = 0; b0 < ng; b0 += 64) {
+      const int j = b0 + lane;
+      const uint32_t e = j < ng ? ge[j] : 0u;
+      const int i0 = (int)(e & 0xffffu);
+      uint32_t m = LS ? (e >> 16) & 0xffu : (e >> 16) & (((i0 >> 3) & ((1 << (QB - 3)) - 1)) == gpr - 1 ? tail_mask : 0xffu);
+      const int cnt = __popc(m);
+      const int incl = wave_iscan(cnt);
+      int pos = ns + incl - cnt;
+      while (m) {
+        sv[pos++] = (uint16_t)(i0 + __builtin_ctz(m));
+        m &= m - 1;
+      }
+      ns += __builtin_amdgcn_readlane(incl, 63);
+    }
+    __syncthreads();
+    *n_sv += ns;
+    for (int j = lane; j < ns; j += 64) {
+      const int i = sv[j];
+      const _Float16 m = fast_arc_max(base + px(i), ls);
+      const uint16_t bits = __builtin_bit_cast(uint16_t, m);
+      sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
+    }
+    __syncthreads();
+    STAMP(1);
+    int written = 0;
+    for (int jb = 0; jb < ns; jb += 64) {
+      const int j = jb + lane;
+      bool kp = false;
+      int i = 0, s = 0;
+      if (j < ns) {
+        i = sv[j];
+        const uint8_t* mp = sc + sci(i);
+        s = mp[0];
+        const int n = max(max(max(mp[-sp2 - 1], mp[-sp2]), max(mp[-sp2 + 1], mp[-1])),
+                          max(max(mp[1], mp[sp2 - 1]), max(mp[sp2], mp[sp2 + 1])));
+        kp = s > n;
+      }
+      const uint64_t km = __ballot(kp);
+      if (kp) {
+        constexpr int LSD = LS ? LS : 1;
+        const int r = LS ? i / LSD : i >> QB, q = LS ? i - r * LS : i & QM;
+        const int pos = written + __popcll(km & lt);
+        if (pos < c.slot_cap)
+          out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
+      }
+      written += __popcll(km);
+    }
+    __syncthreads();
+#else
     // survivors, 64 group entries at a time: lane j expands entry b0 + j into
     // sv[] from the wave's inclusive scan of the entries' popcounts (raster
     // order: entries in order, pixels LSB-first), at most kFastSvChunk
@@ -898,6 +923,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       }
       __syncthreads();
     }
+#endif
     STAMP(2);
     return written;
   };

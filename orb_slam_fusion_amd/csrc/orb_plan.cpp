@@ -245,13 +245,16 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
 // (+3 lead bytes), a byte score map of the detection area with a zero border
 // the u16 survivors of 64 group entries and a u32 list of the 8-pixel
 // groups holding one.
+#ifndef ORB_FAST_SV_FULL
+#define ORB_FAST_SV_FULL 0  // A/B build switch, as in orb_kernels.hip
+#endif
 int fast_cell_lds_bytes(int cols, int rows) {
   const int ls = (cols + 3 + 3) & ~3;
   const int dw = std::max(cols - 6, 0), dh = std::max(rows - 6, 0);
   const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
   const int nsc = std::max(cols - 4, 0) * std::max(rows - 4, 0);
-  (void)nd;
-  return ((ls * rows + 15) & ~15) + ((nsc + 15) & ~15) + 2 * 512 + 4 * ng + 16;  // sv: kFastSvChunk u16
+  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * 512;  // u16 survivors (kFastSvChunk)
+  return ((ls * rows + 15) & ~15) + ((nsc + 15) & ~15) + sv + 4 * ng + 16;
 }
 
 // The same with the plan's fixed pitch for the ROI and the score-map rows
@@ -260,8 +263,8 @@ int fast_cell_lds_bytes(int cols, int rows) {
 int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch) {
   const int dw = std::max(cols - 6, 0), dh = std::max(rows - 6, 0);
   const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
-  (void)nd;
-  return ((pitch * rows + 15) & ~15) + ((pitch * (dh + 2) + 15) & ~15) + 2 * 512 + 4 * ng + 16 + 16;
+  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * 512;
+  return ((pitch * rows + 15) & ~15) + ((pitch * (dh + 2) + 15) & ~15) + sv + 4 * ng + 16 + 16;
 }
 
 size_t octree_lds_bytes(const PlanHeader& P) {

@@ -69,7 +69,7 @@ struct PlanHeader {
 };
 
 constexpr int kBlurTileW = 256, kBlurTileH = 128;   // 64 threads x 4 cols, 4 waves x 32 rows
-constexpr int kResizeTileW = 256, kResizeTileH = 64;  // 4 waves x 16 rows, 64 lanes x 4 px
+constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 4 waves x 8 rows, 64 lanes x 4 px
 constexpr int kLevelAlign = 16;
 constexpr int kOctreeLdsCand = 2048;  // octree candidates per (image, level) kept in LDS (rest in HBM)
 

@@ -256,8 +256,7 @@ def test_handles_with_different_plans_coexist(gpu_available):
 def test_fused_pyramid_bit_exact(gpu_available, monkeypatch, case):
     """The resize chain as ONE launch (k_pyramid: a workgroup per image whose
     tile groups walk the levels, the same tile code as the per-level
-    launches), forced for single images by ORBGPU_RESIZE=fused -- batches of
-    at least as many images as the device has CUs take it by default."""
+    launches; opt-in by ORBGPU_RESIZE=fused) gives the same bytes."""
     monkeypatch.setenv("ORBGPU_RESIZE", "fused")
     if case == "c2":
         assert _compare(C2, synth.stereo_frame(0)[0]) > 900

@@ -3,7 +3,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_lba.py tests/test_gpu_lia.py > gpurun_out/lba_r4e_tests.log 2>&1; rc=$?; tail -3 gpurun_out/lba_r4e_tests.log; [ $rc -eq 0 ] || exit $rc
 for W in lba lia; do
   X=""; [ $W = lia ] && X="--lia"
   for M in pair band split; do
