@@ -87,6 +87,9 @@ constexpr double kSeriesD2 = 0.0025;
 #endif
 
 // ExpSO3 (g2o_types.cc:783-796)
+// kUniform: every lane of the wave evaluates the same rotation (the branches
+// are taken by readfirstlane); false: each lane its own (divergent branches)
+template <bool kUniform = true>
 __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   const double d2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   const double d = sqrt(d2);
@@ -94,10 +97,11 @@ __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   m3_hat(w, W);
   m3_mul(W, W, WW);
   double s, c;
-  if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) {
+  auto uni = [](bool b) { return kUniform ? __builtin_amdgcn_readfirstlane(b ? 1 : 0) != 0 : b; };
+  if (uni(d < 1e-5)) {
     s = 1.0;
     c = 0.5;
-  } else if (__builtin_amdgcn_readfirstlane(d2 < kSeriesD2 ? 1 : 0)) {
+  } else if (uni(d2 < kSeriesD2)) {
     // sin(d)/d and (1 - cos d)/d^2 by their Taylor series (truncation
     // < 1e-20 below d = 0.05; the updates near convergence all land here)
     s = 1.0 + d2 * (-1.0 / 6 + d2 * (1.0 / 120 + d2 * (-1.0 / 5040 + d2 * (1.0 / 362880))));
@@ -217,12 +221,13 @@ __device__ __forceinline__ void delta_lin(const float* d0, const float* Jg, cons
 
 // ImuCamPose::Update (g2o_types.cc:192-214); the NormalizeRotation there
 // discards its result.
+template <bool kUniform = true>
 __device__ __forceinline__ void pose_update(StateD& s, const double* u, const CalibD& c, bool store) {
   double R[9], E[9], Rn[9], d[3], ut[3] = {u[3], u[4], u[5]};
 #pragma unroll
   for (int i = 0; i < 9; ++i) R[i] = s.Rwb[i];
   m3_mv(R, ut, d);
-  exp_so3(u, E);
+  exp_so3<kUniform>(u, E);
   m3_mul(R, E, Rn);
   double t[3] = {s.twb[0] + d[0], s.twb[1] + d[1], s.twb[2] + d[2]};
   double Rbw[9], tbw[3], Rcw[9], tcw[3];

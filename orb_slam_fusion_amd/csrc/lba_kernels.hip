@@ -1931,6 +1931,8 @@ __device__ __forceinline__ void load_state(StateD& s, const double* p) {
 // Trial key-frame states: ImuCamPose::Update of VP (g2o_types.cc:192-216) and
 // the additive VV / VG / VA updates from the reduced solve (fixed key frames
 // copied); src: key frame k's current state (33 doubles), dst may be src.
+// Per-lane branches (each lane may hold another key frame): the link
+// kernel's trial states and k_lba_trial's are the same bits.
 __device__ __forceinline__ void lia_trial_state(const LbaArgs& a, int k, const double* src, double* dst) {
   const int h = a.hidx[k];
   if (h < 0) {
@@ -1944,7 +1946,7 @@ __device__ __forceinline__ void lia_trial_state(const LbaArgs& a, int k, const d
   double up[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) up[i] = u[i];
-  pose_update(s, up, calib_of(a), true);
+  pose_update<false>(s, up, calib_of(a), true);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     s.v[i] += u[6 + i];

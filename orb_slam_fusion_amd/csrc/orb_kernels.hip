@@ -805,6 +805,66 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(0);
+    // NMS by group entries (LS > 0), the per-pixel list not needed: lane j
+    // takes entry b0 + j (8 pixels, r * LS + 8 g) and its score-map window --
+    // rows above / at / below, bytes q-1 .. q+8, 3 dwords each (entries are
+    // dword-aligned: LS and 8 g are multiples of 4) -- as u16 pixel pairs
+    // (one v_perm each, as the compass), the 8-neighbour maxima by packed
+    // max, the test s > n by a saturating packed subtract whose bit 15 / 31
+    // (after + 0x7fff) is the flag; keypoints go to the slots in raster order
+    // (entries in order, pixels LSB-first) from a wave scan of the counts.
+    auto nms_entries = [&](int& written) {
+      for (int b0 = 0; b0 < ng; b0 += 64) {
+        const int j = b0 + lane;
+        const uint32_t e = j < ng ? ge[j] : 0u;
+        const int i0 = (int)(e & 0xffffu);
+        const uint32_t m = (e >> 16) & 0xffu;
+        const uint32_t* A = reinterpret_cast<const uint32_t*>(sc + i0);
+        const uint32_t* B = reinterpret_cast<const uint32_t*>(sc + i0 + sp2);
+        const uint32_t* Cr = reinterpret_cast<const uint32_t*>(sc + i0 + 2 * sp2);
+        const uint32_t a0 = A[0], a1 = A[1], a2 = A[2], c0 = Cr[0], c1 = Cr[1], c2 = Cr[2];
+        const uint32_t m0 = B[0], m1 = B[1], m2 = B[2];
+        // pair j (pixels 2j, 2j + 1) at window offset d: bytes 2j + d, 2j + d + 1
+        // of the row, from (w1:w0) for j < 2, else (w2:w1) 4 bytes on
+        auto pr = [&](uint32_t w0, uint32_t w1, uint32_t w2, int jj, int d) {
+          const int o = (jj & 1) * 2 + d;
+          return jj < 2 ? __builtin_amdgcn_perm(w1, w0, psel(o)) : __builtin_amdgcn_perm(w2, w1, psel(o));
+        };
+        uint32_t fb[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const ushort2_t na = max2(max2(as_us2(pr(a0, a1, a2, jj, 0)), as_us2(pr(a0, a1, a2, jj, 1))),
+                                    as_us2(pr(a0, a1, a2, jj, 2)));
+          const ushort2_t nc = max2(max2(as_us2(pr(c0, c1, c2, jj, 0)), as_us2(pr(c0, c1, c2, jj, 1))),
+                                    as_us2(pr(c0, c1, c2, jj, 2)));
+          const ushort2_t nb = max2(as_us2(pr(m0, m1, m2, jj, 0)), as_us2(pr(m0, m1, m2, jj, 2)));
+          const ushort2_t sv2 = as_us2(pr(m0, m1, m2, jj, 1));
+          const ushort2_t d = sub_sat2(sv2, max2(max2(na, nc), nb));  // > 0 iff s > n
+          fb[jj] = __builtin_bit_cast(uint32_t, d + (ushort2_t){0x7fff, 0x7fff});
+        }
+        const uint32_t FA = __builtin_amdgcn_perm(fb[1], fb[0], 0x07050301u) & 0x80808080u;
+        const uint32_t FB = __builtin_amdgcn_perm(fb[3], fb[2], 0x07050301u) & 0x80808080u;
+        uint32_t km = (__builtin_amdgcn_udot4(FA, 0x08040201u, __builtin_amdgcn_udot4(FB, 0x80402010u, 0u, false),
+                                              false) >> 7) & m;
+        const int cnt = __popc(km);
+        const int incl = wave_iscan(cnt);
+        int pos = written + incl - cnt;
+        if (km) {
+          constexpr int LSD = LS ? LS : 1;
+          const int r = i0 / LSD, q0 = i0 - r * LSD;
+          const uint64_t mid = ((uint64_t)m1 << 32) | m0;  // centre bytes 1..8 (byte 8: m2)
+          do {
+            const int k = __builtin_ctz(km);
+            const uint32_t sk = k < 7 ? (uint32_t)(mid >> (8 * (k + 1))) & 0xffu : m2 & 0xffu;
+            if (pos < c.slot_cap)
+              out[pos] = (uint32_t)(xrel0 + q0 + k) | ((uint32_t)(yrel0 + r) << 12) | (sk << 24);
+            ++pos;
+            km &= km - 1;
+          } while (km);
+        }
+        written += __builtin_amdgcn_readlane(incl, 63);
+      }
+    };
 #if ORB_FAST_SV_FULL
     // the whole survivor list, expanded once (raster order: entries in order,
     // pixels LSB-first), then scores and NMS over it
@@ -834,6 +894,9 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     __syncthreads();
     STAMP(1);
     int written = 0;
+    if constexpr (LS != 0) {
+      nms_entries(written);
+    } else {
     for (int jb = 0; jb < ns; jb += 64) {
       const int j = jb + lane;
       bool kp = false;
@@ -855,6 +918,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
           out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
       }
       written += __popcll(km);
+    }
     }
     __syncthreads();
 #else
@@ -897,7 +961,9 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // is kept iff its score beats all 8 neighbours' (0 for non-corners and
     // for the zero border outside the detection area)
     int written = 0;
-    for (int b0 = 0; b0 < ng; b0 += 64) {
+    if constexpr (LS != 0) {
+      nms_entries(written);
+    } else for (int b0 = 0; b0 < ng; b0 += 64) {
       const int ns = expand(b0);
       for (int jb = 0; jb < ns; jb += 64) {
         const int j = jb + lane;
