@@ -39,6 +39,24 @@ using namespace orbgpu;
 
 namespace {
 
+// host phase clocks of run_window (tools/lba_host_bench.cpp builds with
+// LBA_HOST_PHASES); nothing otherwise
+#ifdef LBA_HOST_PHASES
+double g_host_phase_us[16];
+std::chrono::steady_clock::time_point g_host_phase_t;
+#define LBA_HOST_PHASE(k)                                                                    \
+  do {                                                                                       \
+    const auto now_ = std::chrono::steady_clock::now();                                      \
+    if ((k) > 0)                                                                             \
+      g_host_phase_us[k] += std::chrono::duration<double, std::micro>(now_ - g_host_phase_t).count(); \
+    g_host_phase_t = now_;                                                                   \
+  } while (0)
+#else
+#define LBA_HOST_PHASE(k) \
+  do {                    \
+  } while (0)
+#endif
+
 constexpr int kAhead = 2;  // LM steps queued ahead of the device
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -219,6 +237,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   };
   int trace_steps = 0;
 
+  LBA_HOST_PHASE(0);
   // ---- graph layout of this shard, O(edges): free-pose indices, point-major
   // edges (insertion order kept inside a point), per-pose edge lists, pairs
   std::vector<int> hidx(n_kf, -1), free_kf;
@@ -249,29 +268,52 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // the structurally non-zero pose pairs of S: every diagonal block, and (i, j)
   // when some point of the shard is seen by both (the other blocks stay the
   // zeros the per-call clear leaves; a sharded rank's zeros add nothing)
+  LBA_HOST_PHASE(1);
   std::vector<int> pair_list;
-  std::vector<int> pf(std::max(ne, 1));  // free-pose index of each point-major edge (-1: fixed)
+  // point-major order: perm[j] = the caller's index of shard edge j (one
+  // scatter of indices, then sequential gathers), pf[j] its free-pose index
+  std::vector<int> perm(std::max(ne, 1)), pf(std::max(ne, 1));  // pf: -1 = fixed pose
   {
     std::vector<int> fill(cnt.begin(), cnt.end() - 1);
     for (int i = 0; i < n_edges; ++i) {
-      const orbgpu_lba_edge& e = edges[i];
-      if (e.point >= pt_begin && e.point < pt_end) pf[fill[e.point - pt_begin]++] = hidx[e.kf];
+      const int p = edges[i].point;
+      if (p >= pt_begin && p < pt_end) perm[fill[p - pt_begin]++] = i;
     }
-    std::vector<uint8_t> nz((size_t)nf * nf, 0);
-    for (int f = 0; f < nf; ++f) nz[(size_t)f * nf + f] = 1;
-    for (int p = 0; p < np; ++p)
-      for (int u = cnt[p]; u < cnt[p + 1]; ++u)
-        for (int v = u + 1; v < cnt[p + 1]; ++v) {
-          const int fa = pf[u], fb = pf[v];
-          if (fa >= 0 && fb >= 0) nz[(size_t)std::min(fa, fb) * nf + std::max(fa, fb)] = 1;
-        }
-    for (int i = 0; i < nf; ++i)
-      for (int j = i; j < nf; ++j)
-        if (nz[(size_t)i * nf + j]) {
-          pair_list.push_back(i);
-          pair_list.push_back(j);
-        }
+    for (int j = 0; j < ne; ++j) pf[j] = hidx[edges[perm[j]].kf];
+  LBA_HOST_PHASE(2);
+    auto add_pair = [&](int i, int j) {
+      pair_list.push_back(i);
+      pair_list.push_back(j);
+    };
+    if (nf <= 64) {
+      // a point's free poses as one bit mask, OR-ed into each of its poses' rows
+      std::vector<uint64_t> rows(nf);
+      for (int f = 0; f < nf; ++f) rows[f] = 1ull << f;
+      for (int p = 0; p < np; ++p) {
+        uint64_t msk = 0;
+        for (int u = cnt[p]; u < cnt[p + 1]; ++u)
+          if (pf[u] >= 0) msk |= 1ull << pf[u];
+        for (int u = cnt[p]; u < cnt[p + 1]; ++u)
+          if (pf[u] >= 0) rows[pf[u]] |= msk;
+      }
+      for (int i = 0; i < nf; ++i)
+        for (int j = i; j < nf; ++j)
+          if ((rows[i] >> j) & 1) add_pair(i, j);
+    } else {
+      std::vector<uint8_t> nz((size_t)nf * nf, 0);
+      for (int f = 0; f < nf; ++f) nz[(size_t)f * nf + f] = 1;
+      for (int p = 0; p < np; ++p)
+        for (int u = cnt[p]; u < cnt[p + 1]; ++u)
+          for (int v = u + 1; v < cnt[p + 1]; ++v) {
+            const int fa = pf[u], fb = pf[v];
+            if (fa >= 0 && fb >= 0) nz[(size_t)std::min(fa, fb) * nf + std::max(fa, fb)] = 1;
+          }
+      for (int i = 0; i < nf; ++i)
+        for (int j = i; j < nf; ++j)
+          if (nz[(size_t)i * nf + j]) add_pair(i, j);
+    }
   }
+  LBA_HOST_PHASE(3);
   const int n_pairs = (int)pair_list.size() / 2;
   // Schur path: point ranges (k_lba_schur_split), S of them so that a
   // (pair, range) block gets about kSchurSplitEdges of its pose's edges.
@@ -290,7 +332,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::vector<int> pbx(sc_split + 1, np);
   for (int x = 0; x < sc_split; ++x)
     pbx[x] = (int)(std::lower_bound(cnt.begin(), cnt.end() - 1, (int)((long long)x * ne / sc_split)) - cnt.begin());
-  std::vector<int> gidx(ne);  // shard edge -> caller's edge index
+  LBA_HOST_PHASE(4);
+  const std::vector<int>& gidx = perm;  // shard edge -> caller's edge index
   std::vector<int> pose_cnt(nf + 1, 0);
   // IMU links incident to each free key frame (link order)
   std::vector<int> inc(nf + 1, 0), inc_list;
@@ -305,13 +348,14 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     }
   }
 
+  LBA_HOST_PHASE(5);
   // ---- sizes: upload | download | compute
   const size_t KS = (size_t)m.pstride * n_kf, P3 = 3 * (size_t)std::max(np, 1);
   const size_t E = std::max(ne, 1), P = std::max(np, 1), F = std::max(nf, 1);
   const size_t NI = std::max(m.n_imu, 1);
   // blocks of the widest grid that writes a.partials (k_lba_sums with, for
   // kModelImu, its link-assembly blocks)
-  const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + nf + 1 +
+  const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + kSumsQ * (long)nf + 1 +
                     (imu ? ((long)n * n + n + 255) / 256 : 0);
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)1) + E;
@@ -359,8 +403,10 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? 2 * kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
                c_itot = take(2 + NI),  // [0] total, [2 + l] per link
+               c_ppart = take(27 * (size_t)kSumsQ * F),
                c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
                                      sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));
+  LBA_HOST_PHASE(6);
   if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
@@ -374,17 +420,12 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::memcpy(U + u_ctrl, &ctrl0, sizeof(ctrl0));
   std::memset(U + u_cnt, 0, 128);
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
-  {
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int i = 0; i < n_edges; ++i) {
-      const orbgpu_lba_edge& e = edges[i];
-      if (e.point < pt_begin || e.point >= pt_end) continue;
-      const int j = fill[e.point - pt_begin]++;
-      le[j] = LbaEdgeDev{e.point - pt_begin, e.kf, hidx[e.kf], 0, e.u, e.v, e.ur, e.inv_sigma2};
-      gidx[j] = i;
-      if (hidx[e.kf] >= 0) ++pose_cnt[hidx[e.kf] + 1];
-    }
+  for (int j = 0; j < ne; ++j) {  // sequential stores into the pinned image
+    const orbgpu_lba_edge& e = edges[perm[j]];
+    le[j] = LbaEdgeDev{e.point - pt_begin, e.kf, pf[j], 0, e.u, e.v, e.ur, e.inv_sigma2};
+    if (pf[j] >= 0) ++pose_cnt[pf[j] + 1];
   }
+  LBA_HOST_PHASE(7);
   int* I = reinterpret_cast<int*>(U + u_ints);
   int* I_slot = I;  // int4 records first (16-B aligned)
   int* I_hidx = I_slot + 4 * E;
@@ -402,19 +443,24 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
   std::copy(pose_cnt.begin(), pose_cnt.end(), I_pb);
   {
+    // host-side copies only (pf, cnt): nothing is read back from pinned memory
+    std::copy(pf.begin(), pf.begin() + ne, I_ef);
     std::vector<int> fill(pose_cnt.begin(), pose_cnt.end() - 1);
-    for (int j = 0; j < ne; ++j) {
-      I_ef[j] = le[j].f;
-      I_es[j] = -1;
-      if (le[j].f < 0) continue;
-      I_es[j] = fill[le[j].f];
-      int* r = I_slot + 4 * (size_t)fill[le[j].f]++;
-      const int p = le[j].point;
-      r[0] = j;
-      r[1] = p;
-      r[2] = cnt[p];
-      r[3] = cnt[p + 1];
-    }
+    for (int p = 0; p < np; ++p)
+      for (int j = cnt[p]; j < cnt[p + 1]; ++j) {
+        const int f = pf[j];
+        if (f < 0) {
+          I_es[j] = -1;
+          continue;
+        }
+        const int k = fill[f]++;
+        I_es[j] = k;
+        int* r = I_slot + 4 * (size_t)k;
+        r[0] = j;
+        r[1] = p;
+        r[2] = cnt[p];
+        r[3] = cnt[p + 1];
+      }
   }
   for (int k = 0; k < n_pairs; ++k) {
     I_pi[k] = pair_list[2 * k];
@@ -423,21 +469,34 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::copy(free_kf.begin(), free_kf.end(), I_fk);
   std::copy(inc.begin(), inc.end(), I_inc);
   std::copy(inc_list.begin(), inc_list.end(), I_incl);
+  LBA_HOST_PHASE(8);
   int* const SC = reinterpret_cast<int*>(U + u_sc);
   int* const SP = SC + (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1);
   // per free pose, where each point range starts in its (point-ordered) slots
-  for (int f = 0; f < nf && sc_split > 0; ++f) {
-    int k = pose_cnt[f];
-    for (int x = 0; x <= sc_split; ++x) {
-      while (k < pose_cnt[f + 1] && I_slot[4 * (size_t)k + 1] < pbx[x]) ++k;
-      SP[(size_t)f * (sc_split + 1) + x] = x == sc_split ? pose_cnt[f + 1] : k;
+  if (sc_split > 0) {
+    // slots are in point order within a pose: walk the points once, counting
+    // each pose's slots below each range start
+    std::vector<int> below((size_t)nf * (sc_split + 1), 0), seen(nf, 0);
+    int x = 0;
+    for (int p = 0; p <= np; ++p) {
+      while (x <= sc_split && pbx[x] <= p) {  // range x starts at point pbx[x]
+        for (int f = 0; f < nf; ++f) below[(size_t)f * (sc_split + 1) + x] = seen[f];
+        ++x;
+      }
+      if (p == np) break;
+      for (int j = cnt[p]; j < cnt[p + 1]; ++j)
+        if (pf[j] >= 0) ++seen[pf[j]];
     }
+    for (int f = 0; f < nf; ++f)
+      for (int y = 0; y <= sc_split; ++y)
+        SP[(size_t)f * (sc_split + 1) + y] = pose_cnt[f] + (y == sc_split ? seen[f] : below[(size_t)f * (sc_split + 1) + y]);
   }
   if (sc.ok) {
     std::memcpy(SC, sc.chunk.data(), sizeof(int4) * sc.chunk.size());
     std::memcpy(SC + 4 * sc.chunk.size(), sc.tile0.data(), sizeof(int) * sc.tile0.size());
     std::memcpy(SC + 4 * sc.chunk.size() + sc.tile0.size(), sc.order.data(), sizeof(int) * sc.order.size());
   }
+  LBA_HOST_PHASE(9);
   auto* S0 = reinterpret_cast<double*>(U + u_state);
   std::copy(m.state0, m.state0 + KS, S0);
   std::copy(m.state0, m.state0 + KS, S0 + KS);
@@ -449,6 +508,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     std::memcpy(U + u_imu, m.imu, sizeof(LiaImuDev) * m.n_imu);
     std::memcpy(U + u_close, m.close + pt_begin, np);
   }
+  LBA_HOST_PHASE(10);
   const auto t_layout = clk::now();
   if (hipMemcpyAsync(h->arena, U, up, hipMemcpyHostToDevice, st) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
@@ -512,6 +572,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.red = dp(c_red);
   a.scal = dp(c_scal);
   a.partials = dp(c_part);
+  a.pose_part = dp(c_ppart);
   a.counter = reinterpret_cast<unsigned*>(A + u_cnt);
   a.ctrl = reinterpret_cast<LbaCtrl*>(A + u_ctrl);
   a.host = h->host_dev;

@@ -618,70 +618,69 @@ __device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, 
   a.himu[idx] = v;
 }
 
-// ---- buildSystem, vertex side.  Blocks [0, n_free): one free pose each,
-// its edges strided over the threads, a fixed tree per term -> Hpp (6 x 6
-// full), bp and the pose diagonal.  Blocks [n_free, ...): one point per
-// thread summing its edges' Hll / bl in insertion order.  The last block
-// opens the iteration: iniChi, and at iteration 0 computeLambdaInit (tau *
-// max |diag| over pose and point blocks).
+// ---- buildSystem, vertex side.  Blocks [0, kSumsQ n_free): a quarter of
+// one free pose's slots each (slot j of the pose to block j / 256 mod kSumsQ),
+// a fixed tree per term (DPP row sums, then the 16 rows in order) -> a
+// partial of Hpp (lower 21) and bp per (pose, quarter) in a.pose_part.
+// Blocks [kSumsQ n_free, +points): one point per thread summing its edges'
+// Hll / bl in insertion order.  kModelImu: then the link-assembly blocks.
+// The last block adds each pose's quarters in order (Hpp 6 x 6 full, bp,
+// the pose diagonal) and opens the iteration: iniChi, and at iteration 0
+// computeLambdaInit (tau * max |diag| over pose and point blocks).
 __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
-  __shared__ double red[4 * 27];
+  __shared__ double red[16 * 27];
   const LbaCtrl& c = *a.ctrl;
   if (c.done || !c.need_build) return;
   const LinPtr L = lin_of(a, c.state);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_pose_blocks = kSumsQ * a.n_free;
+  const int n_pt_blocks = (max(a.n_pts, 1) + kThreads - 1) / kThreads;
   double hmax = 0;
-  if ((int)blockIdx.x < a.n_free) {
-    const int f = blockIdx.x;
+  if ((int)blockIdx.x < n_pose_blocks) {
+    const int f = blockIdx.x / kSumsQ, q = blockIdx.x - kSumsQ * f;
     double acc[27];
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] = 0;
-    const int j0 = a.pose_begin[f], j1 = a.pose_begin[f + 1];
+    const int j1 = a.pose_begin[f + 1];
     // the pose's slots are contiguous in hpp_e's component rows: every load
-    // of a wave reads 512 consecutive bytes (four slots' terms in flight)
-    for (int jb = j0 + threadIdx.x; jb < j1; jb += 4 * kThreads) {
-      double hv[4][27];
+    // of a wave reads 512 consecutive bytes (two slots' terms in flight)
+    constexpr int kStep = kSumsQ * kThreads;
+    for (int jb = a.pose_begin[f] + q * kThreads + threadIdx.x; jb < j1; jb += 2 * kStep) {
+      double hv[2][27];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int k = 0; k < 27; ++k)
-          hv[u][k] = jb + u * kThreads < j1 ? L.hpp_e[(size_t)k * a.n_slots + jb + u * kThreads] : 0.0;
+          hv[u][k] = jb + u * kStep < j1 ? L.hpp_e[(size_t)k * a.n_slots + jb + u * kStep] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (jb + u * kThreads < j1)
+      for (int u = 0; u < 2; ++u)
+        if (jb + u * kStep < j1)
 #pragma unroll
           for (int k = 0; k < 27; ++k) acc[k] += hv[u][k];
     }
 #pragma unroll
     for (int k = 0; k < 27; ++k) {
       double v = acc[k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == 0) red[27 * wave + k] = v;
+      v += dpp_f64<0x111, 0xf>(v);
+      v += dpp_f64<0x112, 0xf>(v);
+      v += dpp_f64<0x114, 0xf>(v);
+      v += dpp_f64<0x118, 0xf>(v);
+      if ((lane & 15) == 15) red[(wave * 4 + (lane >> 4)) * 27 + k] = v;
     }
     __syncthreads();
     if (threadIdx.x < 27) {
       const int k = threadIdx.x;
-      const double v = ((red[k] + red[27 + k]) + red[54 + k]) + red[81 + k];
-      if (k < 21) {
-        int s = 0, q = k;  // lower-triangle index k -> (s, q)
-        while (q > s) {
-          q -= s + 1;
-          ++s;
-        }
-        a.hpp[36 * (size_t)f + 6 * s + q] = v;
-        a.hpp[36 * (size_t)f + 6 * q + s] = v;
-        if (s == q) a.diag[a.pdim * f + s] = v;
-      } else {
-        a.bp[6 * (size_t)f + (k - 21)] = v;
-      }
+      double v = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += red[r * 27 + k];
+      a.pose_part[27 * (size_t)blockIdx.x + k] = v;
     }
-  } else if ((int)blockIdx.x >= a.n_free + (max(a.n_pts, 1) + kThreads - 1) / kThreads) {
+  } else if ((int)blockIdx.x >= n_pose_blocks + n_pt_blocks) {
     // kModelImu: the links' part of the system (lia_assemble_entry)
-    const long b = (long)blockIdx.x - a.n_free - (max(a.n_pts, 1) + kThreads - 1) / kThreads;
+    const long b = (long)blockIdx.x - n_pose_blocks - n_pt_blocks;
     lia_assemble_entry(a, c.state, b * kThreads + threadIdx.x);
   } else {
-    const int p = (blockIdx.x - a.n_free) * kThreads + threadIdx.x;
+    const int p = (blockIdx.x - n_pose_blocks) * kThreads + threadIdx.x;
     if (p < a.n_pts) {
       double H[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       const int i0 = a.pt_begin[p], i1 = a.pt_begin[p + 1];
@@ -711,6 +710,27 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   }
   if (threadIdx.x == 0) a.partials[blockIdx.x] = hmax;
   if (!last_block(a.counter + 1)) return;
+  // each pose's quarters in order -> Hpp (6 x 6 full), bp, the pose diagonal
+  for (int idx = threadIdx.x; idx < 27 * a.n_free; idx += kThreads) {
+    const int f = idx / 27, k = idx - 27 * f;
+    const double* pp = a.pose_part + 27 * (size_t)kSumsQ * f + k;
+    double v = 0;
+#pragma unroll
+    for (int q = 0; q < kSumsQ; ++q) v += pp[27 * q];
+    if (k < 21) {
+      int s2 = 0, q2 = k;  // lower-triangle index k -> (s2, q2)
+      while (q2 > s2) {
+        q2 -= s2 + 1;
+        ++s2;
+      }
+      a.hpp[36 * (size_t)f + 6 * s2 + q2] = v;
+      a.hpp[36 * (size_t)f + 6 * q2 + s2] = v;
+      if (s2 == q2) a.diag[a.pdim * f + s2] = v;
+    } else {
+      a.bp[6 * (size_t)f + (k - 21)] = v;
+    }
+  }
+  __syncthreads();
   // max is order-independent: every reduction order gives the same value
   double m = 0;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) m = fmax(m, a.partials[b]);
@@ -2466,7 +2486,7 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   }
   // kModelImu: extra blocks assemble the links' part of the system
   const unsigned asm_blocks = imu && a.n_sys > 0 ? blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads) : 0;
-  hipLaunchKernelGGL(k_lba_sums, dim3(a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads) + asm_blocks),
+  hipLaunchKernelGGL(k_lba_sums, dim3(kSumsQ * a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads) + asm_blocks),
                      dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }

@@ -132,6 +132,7 @@ struct LbaArgs {
   double* red;               // [4]: init / trial reduce buffer (chi2, landmark scale, bad, stop)
   double* scal;              // [2]: pose part of computeScale, solve failure
   double* partials;          // block partials (2 per block)
+  double* pose_part;         // [kSumsQ n_free][27] k_lba_sums' per-(pose, quarter) Hpp / bp partials
   unsigned* counter;         // last-block-done tickets (self-resetting), one per stage
   LbaCtrl* ctrl;
   LbaHostWords* host;        // host-mapped
@@ -173,6 +174,7 @@ hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
 // and a copy of the LbaCtrl at ctrl_out
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, void* ctrl_out, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
+constexpr int kSumsQ = 4;                // k_lba_sums blocks per free pose
 constexpr int kSchurSplitMax = 8;        // point ranges of k_lba_schur_split (one per XCD)
 constexpr int kSchurSplitEdges = 128;    // target pose edges per (pair, range) block
 constexpr int kSchurBandMax = 15;       // free poses a Schur chunk spans (6 w + 1 <= 96 rows)
