@@ -616,6 +616,15 @@ __device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, 
     }
   }
   a.himu[idx] = v;
+  // the system takes the links' part directly (the solves stage one array):
+  // every entry here, and the Schur writes add it to the pose pairs' blocks
+  // and the pose rows of b_s / b_p they overwrite per trial
+  if (grad) {
+    a.sys[(size_t)n * n + r] = v;
+    a.sys[(size_t)n * n + n + r] = v;
+  } else {
+    a.sys[idx] = v;
+  }
 }
 
 // ---- buildSystem, vertex side.  Blocks [0, kSumsQ n_free): a quarter of
@@ -759,6 +768,28 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   }
 }
 
+// one Schur entry of pose pair (fi, fj): t < 36 the block entry (s, q) = (t /
+// 6, t % 6) (a diagonal pair: its lower entries, mirrored -- exactly
+// symmetric), else b_s / b_p of row t - 36; sum = the points' part
+__device__ __forceinline__ void schur_write(const LbaArgs& a, int fi, int fj, int t, double sum) {
+  const bool diag = fi == fj;
+  const int n = a.n_sys, P = a.pdim;  // P: the pose block's rows (VP first in a kModelImu key frame)
+  if (t < 36) {
+    const int s = t / 6, q = t - 6 * s;
+    if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
+    const size_t o = (size_t)(P * fi + s) * n + P * fj + q;
+    // kModelImu: + the links' part (symmetric: the link forms are)
+    const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum + (a.himu ? a.himu[o] : 0.0);
+    a.sys[o] = v;
+    a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
+  } else {
+    const int s = t - 36;
+    const double hb = a.himu ? a.himu[(size_t)n * n + P * fi + s] : 0.0;
+    a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum + hb;  // b_s
+    a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s] + hb;   // b_p (computeScale)
+  }
+}
+
 // ---- Schur complement of the points at the trial's lambda: one 512-thread
 // block per free-pose pair (fi <= fj).  Threads stride over pose fi's edges
 // (point order); each finds its point's edges to pose fj and adds
@@ -777,7 +808,6 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
   const double* const hpl = lin_of(a, c.state).hpl;
   const int pr = blockIdx.x;
   const int fi = a.pair_i[pr], fj = a.pair_j[pr];
-  const int n = a.n_sys;
   const bool diag = fi == fj;
   double acc[42];
 #pragma unroll
@@ -851,18 +881,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
     double sum = 0;
 #pragma unroll 8
     for (int r = 0; r < kSchurWaves * 4; ++r) sum += red[r * 42 + t];
-    if (t < 36) {
-      const int s = t / 6, q = t - 6 * s;
-      if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
-      const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
-      const int P = a.pdim;  // the pose block's rows (VP first in a kModelImu key frame)
-      a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
-      a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
-    } else {
-      const int s = t - 36, P = a.pdim;
-      a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
-      a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
-    }
+    schur_write(a, fi, fj, t, sum);
   }
 }
 
@@ -882,21 +901,6 @@ __global__ __launch_bounds__(kSchurThreads) void k_lba_schur(LbaArgs a) {
 constexpr int kSplitThreads = 128;
 constexpr int kSplitWaves = kSplitThreads / 64;
 
-__device__ __forceinline__ void schur_write(const LbaArgs& a, int fi, int fj, int t, double sum) {
-  const bool diag = fi == fj;
-  const int n = a.n_sys, P = a.pdim;  // P: the pose block's rows (VP first in a kModelImu key frame)
-  if (t < 36) {
-    const int s = t / 6, q = t - 6 * s;
-    if (diag && q > s) return;  // diagonal block: lower triangle, mirrored (exactly symmetric)
-    const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
-    a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
-    a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
-  } else {
-    const int s = t - 36;
-    a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
-    a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
-  }
-}
 
 __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
   __shared__ double red[kSplitWaves * 4 * 42];
@@ -1179,16 +1183,10 @@ __global__ __launch_bounds__(64) void k_lba_schur_sum(LbaArgs a) {
     }
     if (past) break;
   }
-  const int n = a.n_sys, P = a.pdim;
   if (!live) return;
-  if (t < 36) {
-    const double v = (diag ? a.hpp[36 * (size_t)fi + 6 * s + q] : 0.0) - sum;
-    a.sys[(size_t)(P * fi + s) * n + P * fj + q] = v;
-    a.sys[(size_t)(P * fj + q) * n + P * fi + s] = v;
-  } else {
-    a.sys[(size_t)n * n + P * fi + s] = a.bp[6 * (size_t)fi + s] - sum;  // b_s
-    a.sys[(size_t)n * n + n + P * fi + s] = a.bp[6 * (size_t)fi + s];   // b_p (computeScale)
-  }
+  // (a diagonal pair's live entries are its upper ones, s <= q: the transposed
+  // lower entry, which schur_write takes, has the same sum)
+  schur_write(a, fi, fj, t < 36 ? (diag ? 6 * q + s : t) : t, sum);
 }
 
 // ---- reduced camera system (S + lambda I) x = b_s: L D L^T by 16 x 16 tiles
@@ -1418,7 +1416,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
       return S + (size_t)(16 * I) * LD + 16 * J;
   };
   const double* src = a.sys;
-  const double* hm = a.himu;  // kModelImu: the IMU links' part of the system (else NULL)
+  const double* hm = nullptr;  // (the links' part is in a.sys already: lia_assemble_entry, schur_write)
   if constexpr (kLds) {
     // S + lambda I (lower tiles) with identity padding (D = 1, L = 0): wave w
     // stages tiles w, w + 8, ... (tile (I, J) of the row-major enumeration),
@@ -1783,7 +1781,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_ldl_stage(LbaArgs a) {
   const int n = a.n_sys, N = a.n_pad, r = blockIdx.x;
   const size_t LD = (size_t)N + 1;
   const double* src = a.sys;
-  const double* hm = a.himu;
+  const double* hm = nullptr;  // (in a.sys already)
   const int cend = 16 * ((r >> 4) + 1);
   for (int cc = threadIdx.x; cc < cend; cc += kThreads) {
     const bool in = r < n && cc < n;
@@ -1912,7 +1910,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_back(LbaArgs a) {
     __syncthreads();
   }
   const double* src = a.sys;
-  const double* hm = a.himu;
+  const double* hm = nullptr;  // (in a.sys already)
   double sc = 0;
   for (int r = t; r < n; r += kSolveThreads) {
     const double xv = y[r];
