@@ -35,7 +35,7 @@ W, H = 752, 480
 PARAMS = (1000, 1.2, 8, 20, 7)
 POSE_OBS = 600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PROFILE_ROUND = "r03"  # profiles/<round>/kernels.json (tools/profile_round.sh)
+PROFILE_ROUND = "r04"  # profiles/<round>/kernels.json (tools/profile_round.sh)
 
 
 def level_sizes(inv_scale):
@@ -132,12 +132,16 @@ def load_profile():
 
 def load_fast_stamps():
     """k_fast_cells phase stamps (tools/stamps.py on the ORB_STAMPS build):
-    the share of cells that ran the minTh fallback pass."""
-    f = REPO / "profiles" / PROFILE_ROUND / "fast_stamps.json"
-    try:
-        return json.loads(f.read_text()) if f.exists() else None
-    except ValueError:
-        return None
+    the share of cells that ran the minTh fallback pass -- from the latest
+    round that recorded them (-> (data, path))."""
+    for r in sorted({PROFILE_ROUND, "r04", "r03", "r02"}, reverse=True):
+        f = REPO / "profiles" / r / "fast_stamps.json"
+        try:
+            if f.exists():
+                return json.loads(f.read_text()), f"profiles/{r}/fast_stamps.json"
+        except ValueError:
+            pass
+    return None, None
 
 
 def main() -> int:
@@ -330,10 +334,10 @@ def main() -> int:
                 row["valu_insts_per_64_images"] = round(p["insts_valu_per_launch"] * 64 /
                                                         prof["images_per_launch"])
         if st == "fast_cells":
-            fs = load_fast_stamps()
+            fs, fsrc = load_fast_stamps()
             if fs:  # minTh fallback cells (stamp counters 10/11, tools/stamps.py)
                 row["fallback_cell_share"] = round(fs["fallback_frac"], 4)
-                row["fallback_source"] = f"profiles/{PROFILE_ROUND}/fast_stamps.json"
+                row["fallback_source"] = fsrc
         kernels[st] = row
     roofline = {
         "bound": "hbm",
