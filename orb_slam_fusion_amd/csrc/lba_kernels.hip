@@ -1694,25 +1694,30 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   __syncthreads();
   LBA_STAMP(5);
   // backward: L^T x = y by tiles from the last (L_KK^-T mat-vec, then the
-  // rows above take the tile's contribution)
-  for (int K = T - 1; K >= 0; --K) {
-    const int k0 = 16 * K;
-    if (t < 16) {
+  // rows above take the tile's contribution) -- by wave 0 alone: a step is
+  // two 16-FMA chains and LDS round trips, and wave-level syncs instead of
+  // two workgroup barriers a step (the same operations in the same order)
+  if (wave == 0) {
+    for (int K = T - 1; K >= 0; --K) {
+      const int k0 = 16 * K;
       double s = 0;
+      if (lane < 16) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * kTileSz + k * kTileLd + t], y[k0 + k], s);
-      __builtin_amdgcn_wave_barrier();
-      y[k0 + t] = s;
-    }
-    __syncthreads();
-    for (int r = t; r < k0; r += kSolveThreads) {
-      double s = 0;
+        for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * kTileSz + k * kTileLd + lane], y[k0 + k], s);
+      }
+      wave_lds_sync();  // every read of y_K before the writes
+      if (lane < 16) y[k0 + lane] = s;
+      wave_lds_sync();
+      for (int r = lane; r < k0; r += 64) {
+        double u = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s = fma(tile(K, r >> 4)[k * TS + (r & 15)], y[k0 + k], s);
-      y[r] -= s;
+        for (int k = 0; k < 16; ++k) u = fma(tile(K, r >> 4)[k * TS + (r & 15)], y[k0 + k], u);
+        y[r] -= u;
+      }
+      wave_lds_sync();
     }
-    __syncthreads();
   }
+  __syncthreads();
   LBA_STAMP(6);
   // x_p and the pose part of computeScale: x . (lambda x + b_p)
   double sc = 0;
@@ -1986,6 +1991,161 @@ __device__ __forceinline__ void lia_trial_state(const LbaArgs& a, int k, const d
   }
 }
 
+// One link by one wave (lane): its data and the two key-frame states staged
+// in LDS (states from the table ts -- k_lba_trial's trial states -- when
+// given, else from the state array st), the error / chi2 and, kBuild, the
+// form and gradient into copy qcopy of imu_q.  Returns the link's chi2 (every
+// lane).
+struct LinkLds {
+  double J[9 * 24];
+  double OJ[9 * 24];
+  double E[9];      // the link's error (inertial_edge_core, lane 0)
+  double Info[81];  // the link's information (x1e-2 when downweighted)
+  LiaImuDev L;      // the link (preintegration)
+  double S[2 * kImuStateStride];
+};
+
+template <bool kBuild>
+__device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, const double* st, const double* ts,
+                                           int qcopy, LinkLds& sh) {
+  {
+    // every load in flight before the first store: the edge chain below
+    // then reads LDS, not one HBM round trip per field it reaches
+    constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
+    static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
+    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
+    const double* sb = ts ? ts : st;
+    uint32_t w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
+    double sv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
+      sv[u] = k < 2 * kImuStateStride ? sb[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&sh.L);
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (lane + 64 * u < 2 * kImuStateStride) sh.S[lane + 64 * u] = sv[u];
+    wave_lds_sync();
+  }
+  const LiaImuDev& E = sh.L;
+  const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
+  for (int k = lane; k < 81; k += 64) sh.Info[k] = E.pi.info[k] * isc;
+  StateD s1, s2;
+  load_state(s1, sh.S);
+  load_state(s2, sh.S + kImuStateStride);
+  double* J = sh.J;
+  if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
+    for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
+    wave_lds_sync();
+    if (lane < 9) {
+      const int i = lane / 3, j = lane % 3;
+      J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
+      J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
+      J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
+      J[(3 + i) * 24 + 12 + j] = -(double)E.pi.JVa[3 * i + j];
+      J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
+    }
+  }
+  inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sh.E);
+  wave_lds_sync();
+  double e[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) e[k] = sh.E[k];
+  // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
+  double part = 0;
+  if (lane < 9) {
+    double t = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) t += sh.Info[lane * 9 + q] * e[q];
+    double el = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
+    part = el * t;
+  }
+  double chi = 0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) chi += readlane_f64(part, q);
+  double rho0 = chi, w = 1.0;
+  if (E.flags & ORBGPU_LIA_ROBUST) huber_rho(chi, sqrt(16.92), rho0, w);
+  double eg[3], ea[3], Og[3], Oa[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    eg[i] = s2.bg[i] - s1.bg[i];
+    ea[i] = s2.ba[i] - s1.ba[i];
+  }
+  double cg = 0, ca = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    Og[i] = E.pi.info_g[3 * i] * eg[0] + E.pi.info_g[3 * i + 1] * eg[1] + E.pi.info_g[3 * i + 2] * eg[2];
+    Oa[i] = E.pi.info_a[3 * i] * ea[0] + E.pi.info_a[3 * i + 1] * ea[1] + E.pi.info_a[3 * i + 2] * ea[2];
+    cg += eg[i] * Og[i];
+    ca += ea[i] * Oa[i];
+  }
+  if (kBuild) {
+    // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
+    for (int k = lane; k < 9 * 24; k += 64) {
+      const int r = k / 24, col = k - 24 * r;
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * J[q * 24 + col];
+      sh.OJ[k] = v;
+    }
+    double We[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * e[q];
+      We[r] = v;
+    }
+    wave_lds_sync();
+    double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * qcopy);
+    for (int k = lane; k < 900; k += 64) {
+      const int p = k / 30, q = k - 30 * p;
+      double v = 0;
+      if (p < 24 && q < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sh.OJ[r * 24 + q];
+      }
+      // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
+      const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
+      if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
+        if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
+      const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
+      if ((p >= 12 && p < 15) || (p >= 27))
+        if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
+      Q[k] = v;
+    }
+    if (lane < 30) {
+      const int p = lane;
+      double g = 0;
+      if (p < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
+      }
+      double og = 0, oa = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        og = p - 9 == i || p - 24 == i ? Og[i] : og;
+        oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
+      }
+      if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
+      if (p >= 24 && p < 27) g -= og;
+      if (p >= 12 && p < 15) g += oa;
+      if (p >= 27) g -= oa;
+      Q[900 + p] = g;
+    }
+  }
+  return (rho0 + cg) + ca;
+}
+
 // ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
 __device__ __forceinline__ void trial_pose(const LbaArgs& a, int s0, int k, double* out) {
   Se3 T = load_pose(a.poses[s0] + 7 * k);
@@ -2052,6 +2212,24 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   }
   const int i = blockIdx.x * kThreads + threadIdx.x;
   double part[3] = {0, 0, 0};  // robust chi2, landmark scale, singular landmark blocks
+  // kModelImu: blocks past the edges' take the IMU links, a wave per link, at
+  // the trial states of the LDS table (the same bits the edges use): each
+  // link's chi2 to imu_tot[2 + l] and, speculatively, its form into the
+  // other copy of imu_q -- in the same launch as the edges, not after them
+  bool link_block = false;
+  if constexpr (M == kModelImu) {
+    __shared__ LinkLds lsh[kThreads / 64];
+    const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
+    if ((int)blockIdx.x >= neb) {
+      const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
+      if (l < a.n_imu) {
+        const double chi = lia_link<true>(a, l, threadIdx.x & 63, tposes, nullptr, s1, lsh[w]);
+        if ((threadIdx.x & 63) == 0) a.imu_tot[2 + l] = chi;
+      }
+      link_block = true;
+    }
+  }
+  if (!link_block) {  // (block-uniform)
   // the points of this block's edges (a contiguous range: edges are point-
   // major), each back-substituted once by one thread into LDS -- not once per
   // edge; the block holding a point's first edge writes it and adds its
@@ -2128,6 +2306,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     // trial is accepted (LinPtr above)
     lin_edge<M>(a, e, i, tposes + a.pstride * e.kf, X, err, lin_of(a, s1));
   }
+  }  // !link_block
   block_sum<3>(part, red);
   if (threadIdx.x == 0)
 #pragma unroll
@@ -2135,8 +2314,12 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   if (!last_block(a.counter + 2)) return;
   double s[3];
   sum_partials<3>(a.partials, gridDim.x, s, red);
-  if (M == kModelImu) s[0] += a.imu_tot[0];  // the IMU links at the trial state (k_lia_imu)
   if (threadIdx.x == 0) {
+    if (M == kModelImu) {  // the IMU links at the trial state (this launch's link waves), in link order
+      double tot = 0;
+      for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
+      s[0] += tot;
+    }
     if (a.n_edgeless > 0) {  // points without edges: (0 + lambda I)^-1
       const double h0[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       double Di[9];
@@ -2227,169 +2410,21 @@ __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* _
 // on the four waves of one workgroup, three in a row: 36 µs per build.)
 constexpr int kImuThreads = 64;
 
-// kBuild with trial = 0: the build's forms at the current state (skipped when
-// the accepted trial already left them); with trial = 1: the trial's errors
-// and chi2 and, speculatively, its forms into the other copy of imu_q (as
-// k_lba_trial does for the visual edges, lin_of).
+// The links at the current state, one 64-thread workgroup per link:
+// kBuild, the build's forms (the first LM step; later builds take the
+// accepted trial's, written by k_lba_trial<kModelImu>'s link waves); else
+// the errors at the initial state (lba_begin), each link's chi2 to
+// imu_tot[2 + l] and the last workgroup's sum in link order to imu_tot[0].
 template <bool kBuild>
-__global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a, int trial) {
+__global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
-  if (c.done || (kBuild && !trial && (!c.need_build || (c.lin_state == c.state && !a.force_lin)))) return;
-  __shared__ double sJ[9 * 24];
-  __shared__ double sOJ[9 * 24];
-  __shared__ double sE[9];       // the link's error (inertial_edge_core, lane 0)
-  __shared__ double sInfo[81];   // the link's information (x1e-2 when downweighted)
-  __shared__ LiaImuDev sL;       // the link (preintegration) and the two key-frame states,
-  __shared__ double sS[2 * kImuStateStride];  // staged in one round trip
+  if (c.done || (kBuild && (!c.need_build || (c.lin_state == c.state && !a.force_lin)))) return;
+  __shared__ LinkLds sh;
   const int lane = threadIdx.x;
-  const int l = blockIdx.x;      // (grid max(n_imu, 1): block 0 alone when there is no link)
-  // a trial of a window k_lba_trial stages (kMaxKfImuLds) forms the two trial
-  // states here from the current ones; larger windows read k_lia_trial_states'
-  const bool own_trial = trial && a.n_kf <= kMaxKfImuLds;
-  const double* st = a.poses[trial && !own_trial ? c.state ^ 1 : c.state];
+  const int l = blockIdx.x;  // (grid max(n_imu, 1): block 0 alone when there is no link)
   double chi_link = 0;
-  if (l < a.n_imu) {
-    {
-      // every load in flight before the first store: the edge chain below
-      // then reads LDS, not one HBM round trip per field it reaches
-      constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
-      static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
-      const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
-      uint32_t w[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
-      double sv[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
-        sv[u] = k < 2 * kImuStateStride ? st[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
-      }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(&sL);
-#pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (lane + 64 * u < 2 * kImuStateStride) sS[lane + 64 * u] = sv[u];
-      wave_lds_sync();
-      if (own_trial) {  // lane 0: kf1, lane 1: kf2, in place
-        if (lane < 2) lia_trial_state(a, lane ? k2 : k1, sS + kImuStateStride * lane, sS + kImuStateStride * lane);
-        wave_lds_sync();
-      }
-    }
-    const LiaImuDev& E = sL;
-    const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
-    for (int k = lane; k < 81; k += 64) sInfo[k] = E.pi.info[k] * isc;
-    StateD s1, s2;
-    load_state(s1, sS);
-    load_state(s2, sS + kImuStateStride);
-    double* J = sJ;
-    if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
-      for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
-      wave_lds_sync();
-      if (lane < 9) {
-        const int i = lane / 3, j = lane % 3;
-        J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
-        J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
-        J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
-        J[(3 + i) * 24 + 12 + j] = -(double)E.pi.JVa[3 * i + j];
-        J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
-      }
-    }
-    inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sE);
-    wave_lds_sync();
-    double e[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) e[k] = sE[k];
-    // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
-    double part = 0;
-    if (lane < 9) {
-      double t = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) t += sInfo[lane * 9 + q] * e[q];
-      double el = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
-      part = el * t;
-    }
-    double chi = 0;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) chi += readlane_f64(part, q);
-    double rho0 = chi, w = 1.0;
-    if (E.flags & ORBGPU_LIA_ROBUST) huber_rho(chi, sqrt(16.92), rho0, w);
-    double eg[3], ea[3], Og[3], Oa[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      eg[i] = s2.bg[i] - s1.bg[i];
-      ea[i] = s2.ba[i] - s1.ba[i];
-    }
-    double cg = 0, ca = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      Og[i] = E.pi.info_g[3 * i] * eg[0] + E.pi.info_g[3 * i + 1] * eg[1] + E.pi.info_g[3 * i + 2] * eg[2];
-      Oa[i] = E.pi.info_a[3 * i] * ea[0] + E.pi.info_a[3 * i + 1] * ea[1] + E.pi.info_a[3 * i + 2] * ea[2];
-      cg += eg[i] * Og[i];
-      ca += ea[i] * Oa[i];
-    }
-    chi_link = (rho0 + cg) + ca;
-    if (kBuild) {
-      // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
-      for (int k = lane; k < 9 * 24; k += 64) {
-        const int r = k / 24, col = k - 24 * r;
-        double v = 0;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) v += (w * sInfo[r * 9 + q]) * J[q * 24 + col];
-        sOJ[k] = v;
-      }
-      double We[9];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        double v = 0;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) v += (w * sInfo[r * 9 + q]) * e[q];
-        We[r] = v;
-      }
-      wave_lds_sync();
-      double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * (trial ? c.state ^ 1 : c.state));
-      for (int k = lane; k < 900; k += 64) {
-        const int p = k / 30, q = k - 30 * p;
-        double v = 0;
-        if (p < 24 && q < 24) {
-#pragma unroll
-          for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sOJ[r * 24 + q];
-        }
-        // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
-        const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
-        if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
-          if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
-        const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
-        if ((p >= 12 && p < 15) || (p >= 27))
-          if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
-        Q[k] = v;
-      }
-      if (lane < 30) {
-        const int p = lane;
-        double g = 0;
-        if (p < 24) {
-#pragma unroll
-          for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
-        }
-        double og = 0, oa = 0;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          og = p - 9 == i || p - 24 == i ? Og[i] : og;
-          oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
-        }
-        if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
-        if (p >= 24 && p < 27) g -= og;
-        if (p >= 12 && p < 15) g += oa;
-        if (p >= 27) g -= oa;
-        Q[900 + p] = g;
-      }
-    }
-  }
-  if (kBuild && !trial) return;
+  if (l < a.n_imu) chi_link = lia_link<kBuild>(a, l, lane, a.poses[c.state], nullptr, c.state, sh);
+  if (kBuild) return;
   if (lane == 0) a.imu_tot[2 + l] = chi_link;
   if (!last_block(a.counter + 3)) return;
   if (threadIdx.x == 0) {
@@ -2463,7 +2498,7 @@ size_t lba_solve_work_doubles(int mode, int n_pad) {
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
-    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a);
     hipLaunchKernelGGL(k_lba_begin<kModelImu>, g, dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_lba_begin<kModelSe3>, g, dim3(kThreads), 0, st, a);
@@ -2480,7 +2515,7 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
       hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
   }
   if (linearize && imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
-    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 0);
+    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a);
   }
   // kModelImu: extra blocks assemble the links' part of the system
   const unsigned asm_blocks = imu && a.n_sys > 0 ? blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads) : 0;
@@ -2535,8 +2570,8 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   if (a.model == kModelImu) {
     if (a.n_kf > kMaxKfImuLds)
       hipLaunchKernelGGL(k_lia_trial_states, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
-    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a, 1);
-    hipLaunchKernelGGL(k_lba_trial<kModelImu>, g, dim3(kThreads), 0, st, a);
+    // the links ride in the trial launch: (n_imu + 3) / 4 more blocks, a wave per link
+    hipLaunchKernelGGL(k_lba_trial<kModelImu>, dim3(g.x + (a.n_imu + 3) / 4), dim3(kThreads), 0, st, a);
   } else {
     if (a.n_kf > kMaxKfLds)
       hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
