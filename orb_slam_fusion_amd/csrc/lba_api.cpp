@@ -402,7 +402,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_work = take(lba_solve_work_doubles(solve_mode, npad)),
                c_xp = take(n + 2), c_red = take(4), c_scal = take(2), c_part = take(3 * (size_t)nblk),
                c_imuq = take(imu ? 2 * kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
-               c_itot = take(2 + NI),  // [0] total, [2 + l] per link
+               c_itot = take(2 + NI),  // [2 + l] per link
                c_ppart = take(27 * (size_t)kSumsQ * F),
                c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
                                      sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));

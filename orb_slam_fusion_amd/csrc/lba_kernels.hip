@@ -23,8 +23,9 @@
 // kModelImu key frame (lba_launch.h): ImuCamPose state, body-frame visual
 // Jacobians (EdgeMono / EdgeStereo, g2o_types.cc:334-415), 15 reduced-system
 // rows per free key frame, and the IMU links (EdgeInertial + EdgeGyroRW +
-// EdgeAccRW, no points) evaluated by one workgroup (k_lia_imu) and added to
-// the camera-side system (lia_assemble_entry, in k_lba_sums) before the solve.
+// EdgeAccRW, no points) evaluated a wave per link (lia_link) by extra blocks
+// of the begin / linearize / trial launches, and added to the camera-side
+// system (lia_assemble_entry, in k_lba_sums) before the solve.
 //
 // Sums inside a launch have a fixed order (per-thread loops in edge order,
 // fixed trees, block partials summed by the last block in block order), so
@@ -452,10 +453,206 @@ __device__ void ctl_decide(const LbaArgs& a, double chi_trial, double scale_l, i
 }
 
 // ---- computeActiveErrors at the initial state ----------------------------
+__device__ __forceinline__ void load_state(StateD& s, const double* p) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    s.Rwb[i] = p[i];
+    s.Rcw[i] = p[12 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    s.twb[i] = p[9 + i];
+    s.tcw[i] = p[21 + i];
+    s.v[i] = p[24 + i];
+    s.bg[i] = p[27 + i];
+    s.ba[i] = p[30 + i];
+  }
+}
+
+// ---- LocalInertialBA's IMU links: the EdgeInertial error (and, building,
+// its Jacobian), every lane of the link's wave computing the same values
+// (inertial_edge_core); the link's robust chi2 (Huber sqrt(16.92) on flagged
+// links, the information x1e-2 on the window's last link) plus EdgeGyroRW /
+// EdgeAccRW.  Building, the link's quadratic form over its 30 dims (kf1 VP
+// VV VG VA | kf2 VP VV VG VA; EdgeInertial's 24 columns are the first 24) and
+// the gradient -J^T W e.  The links ride as extra blocks (a wave per link) in
+// k_lba_begin (chi2 at the initial state), k_lba_linearize (the first build's
+// forms) and k_lba_trial (chi2 and, speculatively, forms at the trial state);
+// each link's chi2 goes to imu_tot[2 + l] and the launch's last block sums
+// them in link order.  (Round 2 ran the links on the four waves of one
+// workgroup, three in a row: 36 us per build; round 3 a workgroup per link
+// in a launch of its own.)
+//
+// One link by one wave (lane): its data and the two key-frame states staged
+// in LDS (states from the table ts -- k_lba_trial's trial states -- when
+// given, else from the state array st), the error / chi2 and, kBuild, the
+// form and gradient into copy qcopy of imu_q.  Returns the link's chi2 (every
+// lane).
+struct LinkLds {
+  double J[9 * 24];
+  double OJ[9 * 24];
+  double E[9];      // the link's error (inertial_edge_core, lane 0)
+  double Info[81];  // the link's information (x1e-2 when downweighted)
+  LiaImuDev L;      // the link (preintegration)
+  double S[2 * kImuStateStride];
+};
+
+template <bool kBuild>
+__device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, const double* st, const double* ts,
+                                           int qcopy, LinkLds& sh) {
+  {
+    // every load in flight before the first store: the edge chain below
+    // then reads LDS, not one HBM round trip per field it reaches
+    constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
+    static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
+    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
+    const double* sb = ts ? ts : st;
+    uint32_t w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
+    double sv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
+      sv[u] = k < 2 * kImuStateStride ? sb[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&sh.L);
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (lane + 64 * u < 2 * kImuStateStride) sh.S[lane + 64 * u] = sv[u];
+    wave_lds_sync();
+  }
+  const LiaImuDev& E = sh.L;
+  const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
+  for (int k = lane; k < 81; k += 64) sh.Info[k] = E.pi.info[k] * isc;
+  StateD s1, s2;
+  load_state(s1, sh.S);
+  load_state(s2, sh.S + kImuStateStride);
+  double* J = sh.J;
+  if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
+    for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
+    wave_lds_sync();
+    if (lane < 9) {
+      const int i = lane / 3, j = lane % 3;
+      J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
+      J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
+      J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
+      J[(3 + i) * 24 + 12 + j] = -(double)E.pi.JVa[3 * i + j];
+      J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
+    }
+  }
+  inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sh.E);
+  wave_lds_sync();
+  double e[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) e[k] = sh.E[k];
+  // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
+  double part = 0;
+  if (lane < 9) {
+    double t = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) t += sh.Info[lane * 9 + q] * e[q];
+    double el = 0;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
+    part = el * t;
+  }
+  double chi = 0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) chi += readlane_f64(part, q);
+  double rho0 = chi, w = 1.0;
+  if (E.flags & ORBGPU_LIA_ROBUST) huber_rho(chi, sqrt(16.92), rho0, w);
+  double eg[3], ea[3], Og[3], Oa[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    eg[i] = s2.bg[i] - s1.bg[i];
+    ea[i] = s2.ba[i] - s1.ba[i];
+  }
+  double cg = 0, ca = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    Og[i] = E.pi.info_g[3 * i] * eg[0] + E.pi.info_g[3 * i + 1] * eg[1] + E.pi.info_g[3 * i + 2] * eg[2];
+    Oa[i] = E.pi.info_a[3 * i] * ea[0] + E.pi.info_a[3 * i + 1] * ea[1] + E.pi.info_a[3 * i + 2] * ea[2];
+    cg += eg[i] * Og[i];
+    ca += ea[i] * Oa[i];
+  }
+  if (kBuild) {
+    // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
+    for (int k = lane; k < 9 * 24; k += 64) {
+      const int r = k / 24, col = k - 24 * r;
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * J[q * 24 + col];
+      sh.OJ[k] = v;
+    }
+    double We[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      double v = 0;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * e[q];
+      We[r] = v;
+    }
+    wave_lds_sync();
+    double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * qcopy);
+    for (int k = lane; k < 900; k += 64) {
+      const int p = k / 30, q = k - 30 * p;
+      double v = 0;
+      if (p < 24 && q < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sh.OJ[r * 24 + q];
+      }
+      // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
+      const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
+      if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
+        if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
+      const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
+      if ((p >= 12 && p < 15) || (p >= 27))
+        if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
+      Q[k] = v;
+    }
+    if (lane < 30) {
+      const int p = lane;
+      double g = 0;
+      if (p < 24) {
+#pragma unroll
+        for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
+      }
+      double og = 0, oa = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        og = p - 9 == i || p - 24 == i ? Og[i] : og;
+        oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
+      }
+      if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
+      if (p >= 24 && p < 27) g -= og;
+      if (p >= 12 && p < 15) g += oa;
+      if (p >= 27) g -= oa;
+      Q[900 + p] = g;
+    }
+  }
+  return (rho0 + cg) + ca;
+}
+
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   __shared__ double red[4];
   const int i = blockIdx.x * kThreads + threadIdx.x;
+  if constexpr (M == kModelImu) {
+    // blocks past the edges' take the IMU links at the initial state, a wave
+    // per link (its chi2 to imu_tot[2 + l]); their edge part below is empty
+    __shared__ LinkLds lsh[kThreads / 64];
+    const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
+    const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
+    if ((int)blockIdx.x >= neb && l < a.n_imu) {
+      const double chi = lia_link<false>(a, l, threadIdx.x & 63, a.poses[0], nullptr, 0, lsh[w]);
+      if ((threadIdx.x & 63) == 0) a.imu_tot[2 + l] = chi;
+    }
+  }
   // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
   // which get no Schur terms) stay zero: clear it once per call
   for (size_t k = i, nz = (size_t)a.n_sys * a.n_sys + 2 * (size_t)a.n_sys; k < nz;
@@ -480,8 +677,12 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   if (!last_block(a.counter + 0)) return;
   double s[1];
   sum_partials<1>(a.partials, gridDim.x, s, red);
-  if (M == kModelImu) s[0] += a.imu_tot[0];  // the IMU links at the initial state (k_lia_imu)
   if (threadIdx.x == 0) {
+    if (M == kModelImu) {  // the IMU links at the initial state (this launch's link waves), in link order
+      double tot = 0;
+      for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
+      s[0] += tot;
+    }
     const int stop = host_stop(a);
     if (a.sharded) {
       a.red[0] = s[0];
@@ -580,6 +781,16 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   const LbaCtrl& c = *a.ctrl;
   // nothing due, or the accepted trial already left this state's terms
   if (c.done || !c.need_build || (c.lin_state == c.state && !a.force_lin)) return;
+  if constexpr (M == kModelImu) {
+    // blocks past the edges' build the IMU links' forms, a wave per link
+    __shared__ LinkLds lsh[kThreads / 64];
+    const int neb = (a.n_edges + kThreads - 1) / kThreads;
+    if ((int)blockIdx.x >= neb) {
+      const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
+      if (l < a.n_imu) lia_link<true>(a, l, threadIdx.x & 63, a.poses[c.state], nullptr, c.state, lsh[w]);
+      return;
+    }
+  }
   const int i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n_edges) return;
   const LbaEdgeDev e = a.edges[i];
@@ -1223,7 +1434,8 @@ __device__ __forceinline__ double rcp_f64(double d) {
   return fma(x, fma(-d, x, 1.0), x);
 }
 
-constexpr int kSolveStageTiles = 7;  // LDS path: n_pad <= 160 -> <= 55 tiles, <= 7 per wave
+constexpr int kSolveStageTiles = 8;  // LDS path: n_pad <= 160 -> <= 55 tiles: tile 0 + <= 8 per wave of 1-7
+static_assert(1 + (kSolveWaves - 1) * kSolveStageTiles >= 55, "LDS solve staging covers T = 10 (the LDS budget's largest)");
 
 // ---- DPP64 row broadcasts for the diagonal tile (lane li of every 16-lane
 // row owns row li): v_mov_b64_dpp / v_fmac_f64_dpp with row_newbcast:N read
@@ -1366,7 +1578,7 @@ __device__ unsigned long long g_lba_stamps[16];
   do {                                                                \
     if (t == 0) {                                                     \
       const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
-      g_lba_stamps[k] += now_ - stamp_last;                           \
+      stamp_acc[k] += now_ - stamp_last;                              \
       stamp_last = now_;                                              \
     }                                                                 \
   } while (0)
@@ -1388,6 +1600,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar loops
 #ifdef LBA_SOLVE_STAMPS
   unsigned long long stamp_last = __builtin_amdgcn_s_memtime();
+  unsigned long long stamp_acc[16] = {};  // registers (constant indices): no memory round trip per stamp
 #endif
   double* S;
   double* Li;
@@ -1418,11 +1631,13 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   const double* src = a.sys;
   const double* hm = nullptr;  // (the links' part is in a.sys already: lia_assemble_entry, schur_write)
   if constexpr (kLds) {
-    // S + lambda I (lower tiles) with identity padding (D = 1, L = 0): wave w
-    // stages tiles w, w + 8, ... (tile (I, J) of the row-major enumeration),
-    // a lane 4 consecutive entries of one tile row; every load of the wave in
-    // flight before the LDS writes, no index divisions
+    // S + lambda I (lower tiles) with identity padding (D = 1, L = 0): wave 0
+    // stages tile 0 alone and factors it while waves 1-7 stage tiles w, w +
+    // 7, ... (tile (I, J) of the row-major enumeration), a lane 4 consecutive
+    // entries of one tile row; every load of the wave in flight before the
+    // LDS writes, no index divisions
     const int ntile = T * (T + 1) / 2;
+    auto tile_q = [&](int u) { return wave == 0 ? (u == 0 ? 0 : ntile) : wave + (kSolveWaves - 1) * u; };
     const int lr = lane >> 2, lc = 4 * (lane & 3);
     double v[kSolveStageTiles][4];
     auto tile_of = [&](int q, int& I, int& J) {
@@ -1433,7 +1648,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     auto stage = [&](auto with_imu) {
 #pragma unroll
       for (int u = 0; u < kSolveStageTiles; ++u) {
-        const int q = wave + kSolveWaves * u;
+        const int q = tile_q(u);
         if (q < ntile) {
           int I, J;
           tile_of(q, I, J);
@@ -1455,7 +1670,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
       stage(std::false_type{});
 #pragma unroll
     for (int u = 0; u < kSolveStageTiles; ++u) {
-      const int q = wave + kSolveWaves * u;
+      const int q = tile_q(u);
       if (q < ntile) {
         int I, J;
         tile_of(q, I, J);
@@ -1488,6 +1703,14 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   for (int r = t; r < N; r += kSolveThreads)
     y[r] = r < n ? src[(size_t)n * n + r] + (hm ? hm[(size_t)n * n + r] : 0.0) : 0.0;
   if (t == 0) bad = 0;
+  if constexpr (kLds) {
+    // diagonal tile 0 from wave 0's own writes (tile 0, y_0) while the other
+    // waves still stage
+    if (wave == 0 && T > 0) {
+      wave_lds_sync();
+      diag_tile_factor(tile(0, 0), TS, y, Li, Dg, y, &bad, lane);
+    }
+  }
   __syncthreads();
   LBA_STAMP(0);
 
@@ -1610,8 +1833,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
 #pragma unroll
     for (int q = 0; q < 7; ++q)
       if (kRowWave[q] == wave) slot = q;
-    if (wave == 0 && T > 0) diag_tile(0);  // (T == 0: every key frame fixed, nothing to factor)
-    __syncthreads();
+    // (diagonal tile 0 was factored during the staging; T == 0: every key
+    // frame fixed, nothing to factor)
     LBA_STAMP(1);
     for (int K = 0; K < T - 1; ++K) {
       if (K > 0) write_back(K - 1);
@@ -1738,6 +1961,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     a.scal[1] = bad;
   }
   LBA_STAMP(7);
+#ifdef LBA_SOLVE_STAMPS
+  if (t == 0)
+    for (int k = 0; k < 16; ++k) g_lba_stamps[k] += stamp_acc[k];
+#endif
 }
 
 // ---- the reduced camera system of a large window (kSolveGrid): the same
@@ -1935,21 +2162,6 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_back(LbaArgs a) {
   }
 }
 
-__device__ __forceinline__ void load_state(StateD& s, const double* p) {
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    s.Rwb[i] = p[i];
-    s.Rcw[i] = p[12 + i];
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    s.twb[i] = p[9 + i];
-    s.tcw[i] = p[21 + i];
-    s.v[i] = p[24 + i];
-    s.bg[i] = p[27 + i];
-    s.ba[i] = p[30 + i];
-  }
-}
 
 // Trial key-frame states: ImuCamPose::Update of VP (g2o_types.cc:192-216) and
 // the additive VV / VG / VA updates from the reduced solve (fixed key frames
@@ -1989,161 +2201,6 @@ __device__ __forceinline__ void lia_trial_state(const LbaArgs& a, int k, const d
     dst[27 + i] = s.bg[i];
     dst[30 + i] = s.ba[i];
   }
-}
-
-// One link by one wave (lane): its data and the two key-frame states staged
-// in LDS (states from the table ts -- k_lba_trial's trial states -- when
-// given, else from the state array st), the error / chi2 and, kBuild, the
-// form and gradient into copy qcopy of imu_q.  Returns the link's chi2 (every
-// lane).
-struct LinkLds {
-  double J[9 * 24];
-  double OJ[9 * 24];
-  double E[9];      // the link's error (inertial_edge_core, lane 0)
-  double Info[81];  // the link's information (x1e-2 when downweighted)
-  LiaImuDev L;      // the link (preintegration)
-  double S[2 * kImuStateStride];
-};
-
-template <bool kBuild>
-__device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, const double* st, const double* ts,
-                                           int qcopy, LinkLds& sh) {
-  {
-    // every load in flight before the first store: the edge chain below
-    // then reads LDS, not one HBM round trip per field it reaches
-    constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
-    static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
-    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
-    const double* sb = ts ? ts : st;
-    uint32_t w[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
-    double sv[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
-      sv[u] = k < 2 * kImuStateStride ? sb[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
-    }
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&sh.L);
-#pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (lane + 64 * u < 2 * kImuStateStride) sh.S[lane + 64 * u] = sv[u];
-    wave_lds_sync();
-  }
-  const LiaImuDev& E = sh.L;
-  const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
-  for (int k = lane; k < 81; k += 64) sh.Info[k] = E.pi.info[k] * isc;
-  StateD s1, s2;
-  load_state(s1, sh.S);
-  load_state(s2, sh.S + kImuStateStride);
-  double* J = sh.J;
-  if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
-    for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
-    wave_lds_sync();
-    if (lane < 9) {
-      const int i = lane / 3, j = lane % 3;
-      J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
-      J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
-      J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
-      J[(3 + i) * 24 + 12 + j] = -(double)E.pi.JVa[3 * i + j];
-      J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
-    }
-  }
-  inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sh.E);
-  wave_lds_sync();
-  double e[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) e[k] = sh.E[k];
-  // chi2 = e^T Omega e, one row per lane, then a fixed-order sum
-  double part = 0;
-  if (lane < 9) {
-    double t = 0;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) t += sh.Info[lane * 9 + q] * e[q];
-    double el = 0;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) el = lane == q ? e[q] : el;
-    part = el * t;
-  }
-  double chi = 0;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) chi += readlane_f64(part, q);
-  double rho0 = chi, w = 1.0;
-  if (E.flags & ORBGPU_LIA_ROBUST) huber_rho(chi, sqrt(16.92), rho0, w);
-  double eg[3], ea[3], Og[3], Oa[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    eg[i] = s2.bg[i] - s1.bg[i];
-    ea[i] = s2.ba[i] - s1.ba[i];
-  }
-  double cg = 0, ca = 0;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    Og[i] = E.pi.info_g[3 * i] * eg[0] + E.pi.info_g[3 * i + 1] * eg[1] + E.pi.info_g[3 * i + 2] * eg[2];
-    Oa[i] = E.pi.info_a[3 * i] * ea[0] + E.pi.info_a[3 * i + 1] * ea[1] + E.pi.info_a[3 * i + 2] * ea[2];
-    cg += eg[i] * Og[i];
-    ca += ea[i] * Oa[i];
-  }
-  if (kBuild) {
-    // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
-    for (int k = lane; k < 9 * 24; k += 64) {
-      const int r = k / 24, col = k - 24 * r;
-      double v = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * J[q * 24 + col];
-      sh.OJ[k] = v;
-    }
-    double We[9];
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      double v = 0;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * e[q];
-      We[r] = v;
-    }
-    wave_lds_sync();
-    double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * qcopy);
-    for (int k = lane; k < 900; k += 64) {
-      const int p = k / 30, q = k - 30 * p;
-      double v = 0;
-      if (p < 24 && q < 24) {
-#pragma unroll
-        for (int r = 0; r < 9; ++r) v += J[r * 24 + p] * sh.OJ[r * 24 + q];
-      }
-      // EdgeGyroRW (VG1 = -I at 9, VG2 = +I at 24), EdgeAccRW (12 / 27)
-      const int pg = p < 15 ? p - 9 : p - 24, qg = q < 15 ? q - 9 : q - 24;
-      if ((p >= 9 && p < 12) || (p >= 24 && p < 27))
-        if ((q >= 9 && q < 12) || (q >= 24 && q < 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_g[3 * pg + qg];
-      const int pa = p < 15 ? p - 12 : p - 27, qa = q < 15 ? q - 12 : q - 27;
-      if ((p >= 12 && p < 15) || (p >= 27))
-        if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
-      Q[k] = v;
-    }
-    if (lane < 30) {
-      const int p = lane;
-      double g = 0;
-      if (p < 24) {
-#pragma unroll
-        for (int r = 0; r < 9; ++r) g -= J[r * 24 + p] * We[r];
-      }
-      double og = 0, oa = 0;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        og = p - 9 == i || p - 24 == i ? Og[i] : og;
-        oa = p - 12 == i || p - 27 == i ? Oa[i] : oa;
-      }
-      if (p >= 9 && p < 12) g += og;  // -J^T Omega e with J = -I / +I
-      if (p >= 24 && p < 27) g -= og;
-      if (p >= 12 && p < 15) g += oa;
-      if (p >= 27) g -= oa;
-      Q[900 + p] = g;
-    }
-  }
-  return (rho0 + cg) + ca;
 }
 
 // ---- the trial poses T' = exp(x_p) T (free keyframes; fixed ones copied)
@@ -2397,43 +2454,6 @@ __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* _
   }
 }
 
-// ---- LocalInertialBA's IMU links ------------------------------------------
-// One 64-thread workgroup (one wave) per link, all links in parallel: the
-// EdgeInertial error (and, building, its Jacobian) at the current or trial
-// state, every lane computing the same values (inertial_edge_core); the
-// link's robust chi2 (Huber sqrt(16.92) on flagged links, the information
-// x1e-2 on the window's last link) plus EdgeGyroRW / EdgeAccRW.  Building, it
-// writes the link's quadratic form over the 30 dims (kf1 VP VV VG VA | kf2 VP
-// VV VG VA; EdgeInertial's 24 columns are the first 24) and the gradient
-// -J^T W e.  Evaluating, each link's chi2 goes to imu_tot[2 + l] and the last
-// workgroup sums them in link order into imu_tot[0].  (Round 2 ran the links
-// on the four waves of one workgroup, three in a row: 36 µs per build.)
-constexpr int kImuThreads = 64;
-
-// The links at the current state, one 64-thread workgroup per link:
-// kBuild, the build's forms (the first LM step; later builds take the
-// accepted trial's, written by k_lba_trial<kModelImu>'s link waves); else
-// the errors at the initial state (lba_begin), each link's chi2 to
-// imu_tot[2 + l] and the last workgroup's sum in link order to imu_tot[0].
-template <bool kBuild>
-__global__ __launch_bounds__(kImuThreads) void k_lia_imu(LbaArgs a) {
-  const LbaCtrl& c = *a.ctrl;
-  if (c.done || (kBuild && (!c.need_build || (c.lin_state == c.state && !a.force_lin)))) return;
-  __shared__ LinkLds sh;
-  const int lane = threadIdx.x;
-  const int l = blockIdx.x;  // (grid max(n_imu, 1): block 0 alone when there is no link)
-  double chi_link = 0;
-  if (l < a.n_imu) chi_link = lia_link<kBuild>(a, l, lane, a.poses[c.state], nullptr, c.state, sh);
-  if (kBuild) return;
-  if (lane == 0) a.imu_tot[2 + l] = chi_link;
-  if (!last_block(a.counter + 3)) return;
-  if (threadIdx.x == 0) {
-    double tot = 0;
-    for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
-    a.imu_tot[0] = tot;
-  }
-}
-
 // windows with more key frames than k_lba_trial<kModelImu> stages in LDS
 // (kMaxKfImuLds): the trial states to the state buffer first, a thread per
 // key frame
@@ -2498,8 +2518,8 @@ size_t lba_solve_work_doubles(int mode, int n_pad) {
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
-    hipLaunchKernelGGL(k_lia_imu<false>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a);
-    hipLaunchKernelGGL(k_lba_begin<kModelImu>, g, dim3(kThreads), 0, st, a);
+    // the links ride in the launch: (n_imu + 3) / 4 more blocks, a wave per link
+    hipLaunchKernelGGL(k_lba_begin<kModelImu>, dim3(g.x + (a.n_imu + 3) / 4), dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_lba_begin<kModelSe3>, g, dim3(kThreads), 0, st, a);
   }
@@ -2508,14 +2528,14 @@ hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
 
 hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   const bool imu = a.model == kModelImu;
-  if (linearize && a.n_edges > 0) {
+  // (before k_lba_sums, which closes the build: need_build = 0) kModelImu:
+  // the links' forms ride in the launch, (n_imu + 3) / 4 more blocks
+  const unsigned lin_blocks = blocks(a.n_edges, kThreads) + (imu && a.n_sys > 0 ? (a.n_imu + 3) / 4 : 0);
+  if (linearize && lin_blocks > 0) {
     if (imu)
-      hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(lin_blocks), dim3(kThreads), 0, st, a);
     else
-      hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(blocks(a.n_edges, kThreads)), dim3(kThreads), 0, st, a);
-  }
-  if (linearize && imu && a.n_sys > 0) {  // before k_lba_sums, which closes the build (need_build = 0)
-    hipLaunchKernelGGL(k_lia_imu<true>, dim3(a.n_imu > 0 ? a.n_imu : 1), dim3(kImuThreads), 0, st, a);
+      hipLaunchKernelGGL(k_lba_linearize<kModelSe3>, dim3(lin_blocks), dim3(kThreads), 0, st, a);
   }
   // kModelImu: extra blocks assemble the links' part of the system
   const unsigned asm_blocks = imu && a.n_sys > 0 ? blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads) : 0;

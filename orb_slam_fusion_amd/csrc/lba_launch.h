@@ -150,7 +150,7 @@ struct LbaArgs {
   double* imu_q;             // 2 x [n_imu * kImuPairQ] (one copy per LM state) per link: form over
                              //   (kf1 dims, kf2 dims) + gradient
   double* himu;              // [n_sys^2 + n_sys] the links' part of the camera system | gradient
-  double* imu_tot;           // [1] robust chi2 of the links at the last evaluation
+  double* imu_tot;           // [2 + n_imu]: per link (from 2) robust chi2 at the last evaluation
 };
 
 // Every launcher dispatches on a.model.  kModelImu adds, per stage: the IMU
