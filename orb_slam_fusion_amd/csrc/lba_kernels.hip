@@ -644,12 +644,14 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   const int i = blockIdx.x * kThreads + threadIdx.x;
   if constexpr (M == kModelImu) {
     // blocks past the edges' take the IMU links at the initial state, a wave
-    // per link (its chi2 to imu_tot[2 + l]); their edge part below is empty
+    // per link: its chi2 to imu_tot[2 + l] and its form into copy 0 of imu_q
+    // -- the first build's (state 0), so that build has no link work left
+    // (k_lba_linearize takes the links only when every build relinearises)
     __shared__ LinkLds lsh[kThreads / 64];
     const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
     const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
     if ((int)blockIdx.x >= neb && l < a.n_imu) {
-      const double chi = lia_link<false>(a, l, threadIdx.x & 63, a.poses[0], nullptr, 0, lsh[w]);
+      const double chi = lia_link<true>(a, l, threadIdx.x & 63, a.poses[0], nullptr, 0, lsh[w]);
       if ((threadIdx.x & 63) == 0) a.imu_tot[2 + l] = chi;
     }
   }
@@ -782,7 +784,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   // nothing due, or the accepted trial already left this state's terms
   if (c.done || !c.need_build || (c.lin_state == c.state && !a.force_lin)) return;
   if constexpr (M == kModelImu) {
-    // blocks past the edges' build the IMU links' forms, a wave per link
+    // blocks past the edges' build the IMU links' forms, a wave per link (launched
+    // only when every build relinearises; else k_lba_begin / k_lba_trial wrote them)
     __shared__ LinkLds lsh[kThreads / 64];
     const int neb = (a.n_edges + kThreads - 1) / kThreads;
     if ((int)blockIdx.x >= neb) {
@@ -2529,8 +2532,11 @@ hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
 hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   const bool imu = a.model == kModelImu;
   // (before k_lba_sums, which closes the build: need_build = 0) kModelImu:
-  // the links' forms ride in the launch, (n_imu + 3) / 4 more blocks
-  const unsigned lin_blocks = blocks(a.n_edges, kThreads) + (imu && a.n_sys > 0 ? (a.n_imu + 3) / 4 : 0);
+  // the first build's link forms come from k_lba_begin and every later
+  // build's from the accepted trial; only when every build relinearises
+  // (force_lin) do the links ride in this launch, (n_imu + 3) / 4 more blocks
+  const unsigned lin_blocks =
+      blocks(a.n_edges, kThreads) + (imu && a.force_lin && a.n_sys > 0 ? (a.n_imu + 3) / 4 : 0);
   if (linearize && lin_blocks > 0) {
     if (imu)
       hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(lin_blocks), dim3(kThreads), 0, st, a);
