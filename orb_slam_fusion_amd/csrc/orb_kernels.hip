@@ -1521,17 +1521,8 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   if (gidx >= n_img * kps) return;  // wave-uniform
   const int img = gidx / kps;
   const int slot = gidx - img * kps;
-  // the slot's level: every level's first slot loaded at once (one scalar
-  // round trip, not one per level step)
   int l = 0;
-  {
-    const int nl = P->levels;
-    int off[kMaxLevels];
-#pragma unroll
-    for (int k = 1; k < kMaxLevels; ++k) off[k] = P->lev[k].out_off;
-#pragma unroll
-    for (int k = 1; k < kMaxLevels; ++k) l += (k < nl && slot >= off[k]) ? 1 : 0;
-  }
+  while (l + 1 < P->levels && slot >= P->lev[l + 1].out_off) ++l;
   const LevelGeom& g = P->lev[l];
   const int cnt = __builtin_amdgcn_readfirstlane(oct_count[img * P->levels + l]);
   const uint32_t kp = __builtin_amdgcn_readfirstlane(oct_out[(size_t)img * kps + slot]);
@@ -1547,8 +1538,6 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   const int rx0 = (cx - 15) & ~3, bx0 = (cx - 18) & ~3;
   const uint8_t* rsrc = img0 + (size_t)(cy - 15) * sp + rx0;
   const uint8_t* bsrc = blur + (size_t)img * P->blur_bytes + g.blur_off + (size_t)(cy - 18) * g.pitch + bx0;
-  uint4 icw[kIcSlots / 64];
-  float4 pat[4];
   {
     constexpr int kRs = 5, kBs = 7;  // steps
     const int rr = min(lane / 9, 6), rq = lane - (lane / 9) * 9;      // lanes 63: duplicate of 62
@@ -1560,12 +1549,6 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
 #pragma unroll
     for (int k = 0; k < kBs; ++k)
       vb[k] = *reinterpret_cast<const uint32_t*>(bsrc + (uint32_t)(min(br + 6 * k, kBlurH - 1) * g.pitch + 4 * bq));
-    // the IC_Angle table entries and the BRIEF pattern (constant tables,
-    // independent of the patch) in flight with the patch loads
-#pragma unroll
-    for (int k = 0; k < kIcSlots / 64; ++k) icw[k] = *reinterpret_cast<const uint4*>(c_ic.e[(cx - 15) & 3][64 * k + lane]);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) pat[w] = c_pattern_f[64 * w + lane];
     uint32_t* rd = reinterpret_cast<uint32_t*>(raw + rr * kRawW + 4 * rq);
     uint32_t* bd = reinterpret_cast<uint32_t*>(blp + br * kBlurW + 4 * bq);
 #pragma unroll
@@ -1582,10 +1565,11 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   // IC_Angle (see c_ic)
   int m10, m01;
   {
+    const uint32_t(*tab)[4] = c_ic.e[(cx - 15) & 3];
     uint32_t A = 0, B = 0, S = 0;
 #pragma unroll
     for (int k = 0; k < kIcSlots / 64; ++k) {
-      const uint4 w = icw[k];
+      const uint4 w = *reinterpret_cast<const uint4*>(tab[64 * k + lane]);
       const uint32_t val = *reinterpret_cast<const uint32_t*>(raw + w.w);
       A = __builtin_amdgcn_udot4(val, w.x, A, false);
       B = __builtin_amdgcn_udot4(val, w.y, B, false);
@@ -1606,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   uint64_t words[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
-    const float4 pt = pat[w];
+    const float4 pt = c_pattern_f[64 * w + lane];
     const f32x2 X = {pt.x, pt.y}, Y = {pt.z, pt.w};
     // the reference's fma(x, b, y * a) and fma(x, a, -(y * b)) for both points
     // as packed FP32 (v_pk_mul_f32 / v_pk_fma_f32, each lane IEEE-exact);
