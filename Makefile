@@ -43,6 +43,14 @@ $(LIB)/liborbgpu_varB.so: $(VARB_OBJS)
 
 varB: $(LIB)/liborbgpu_varB.so
 
+# ad-hoc A/B variant of the extractor kernels (orb_kernels.hip compiled with
+# DEFS, every other object shared): make var NAME=pf4 DEFS=-DORB_BLUR_PF=4
+var: $(GPU_OBJS)
+	@mkdir -p $(OBJDIR)/var_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(OBJDIR)/var_$(NAME)/orb_kernels.hip.o $(CSRC)/orb_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $(LIB)/liborbgpu_$(NAME).so $(OBJDIR)/var_$(NAME)/orb_kernels.hip.o \
+	  $(filter-out $(OBJDIR)/orb_kernels.hip.o,$(GPU_OBJS))
+
 $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 	@mkdir -p $(LIB)
 	$(CXX) -std=c++17 -O2 -fPIC -shared -o $@ $<
@@ -71,4 +79,4 @@ stamps:
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
 
-.PHONY: varB all oracle clean stamps
+.PHONY: varB var all oracle clean stamps

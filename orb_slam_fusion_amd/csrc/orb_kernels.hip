@@ -423,6 +423,9 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
   }
 }
 
+#ifndef ORB_BLUR_PF
+#define ORB_BLUR_PF 8
+#endif
 __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, 
   // Streamed down the strip: the 3 dword loads of source row r + kPf are
   // issued while row r is filtered horizontally, and output row r - 6 leaves
   // as soon as its 7 rows exist, so only a 7-row window of sums is live.
-  constexpr int kPf = 8;  // rows of loads in flight
+  constexpr int kPf = ORB_BLUR_PF;  // rows of loads in flight
   const bool edge = __builtin_amdgcn_ballot_w64((int)base != x - 4) != 0;
   uint32_t lo_sel[3] = {0, 0, 0}, hi_sel[3] = {0, 0, 0};
   if (edge) blur_window_sel(x, g.w, (int)base, lo_sel, hi_sel);
