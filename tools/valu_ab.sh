@@ -1,16 +1,17 @@
-# SQ instruction counts of the extractor kernels for two library builds
-# (ORBGPU_LIB): base (liborbgpu_base.so) vs current, same frames
+# SQ instruction counts of the extractor kernels for library builds
+# (ORBGPU_LIB; LIBS overrides the list): base / varB / current, same frames
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/valu_ab; rm -rf $O; mkdir -p $O
-for L in liborbgpu_base liborbgpu_varB liborbgpu; do
+LIBS=${LIBS:-liborbgpu_base liborbgpu_varB liborbgpu}
+for L in $LIBS; do
   [ -f orb_slam_fusion_amd/lib/$L.so ] || continue
   timeout -s KILL 120 env ORBGPU_LIB=orb_slam_fusion_amd/lib/$L.so rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --kernel-trace -d $O/$L -o p --output-format csv -- python3 tools/prof_stages.py --frames 32 --iters 5 --mode ext > $O/$L.log 2>&1 || { echo "pmc failed"; tail -3 $O/$L.log; exit 1; }
 done
-python3 - "$O" <<'PY'
+python3 - "$O" $LIBS <<'PY'
 import csv, glob, sys, collections
-for L in ("liborbgpu_base", "liborbgpu_varB", "liborbgpu"):
+for L in sys.argv[2:]:
     fs = glob.glob(f"{sys.argv[1]}/{L}/**/*counter_collection.csv", recursive=True)
     if not fs:
         continue
