@@ -187,12 +187,6 @@ __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t
 
 // buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
 constexpr int kBufRsrcWord3 = 0x00020000;
-// resize staging fast path: source rows of a tile window, 8 per step (A/B
-// switch: ORB_RESIZE_STAGE_FAST=0 keeps the general index path)
-#ifndef ORB_RESIZE_STAGE_FAST
-#define ORB_RESIZE_STAGE_FAST 1
-#endif
-constexpr int kRsRowSteps = (kResizeTileH * 3 / 2 + 3 + 7) / 8;  // scale <= 1.5
 
 // One output tile (tyx) of level l of image img by 256 threads (tid) with an
 // LDS slice of PlanHeader::rs_lds bytes; every thread of the workgroup passes
@@ -227,32 +221,8 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
   // 16-byte chunks when rows are 16-aligned and no chunk straddles the end of a
   // source row: chunks wholly past it are skipped (their LDS bytes only meet
   // the zero weight of the single-tap columns, sx + 1 = sw)
-  const bool al16 = ((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && (c1 < sp || (sw & 15) == 0);
-  const int nq16 = (c1 < sp ? ncol : min(ncol, sw - c0)) >> 4;
-  if (ORB_RESIZE_STAGE_FAST && al16 && nq16 <= 32 && nrow <= 8 * kRsRowSteps) {
-    // a window of <= 32 chunks a row (every scale up to ~1.5 at this tile
-    // width): lane t copies chunk t % 32 of rows t / 32 + 8 u -- no index
-    // divisions, two VALU a chunk (the window's first row is the scalar
-    // offset)
-    const int q = tid & 31, r0 = tid >> 5;
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(S + c0), (short)0, (int)0xffffffff, kBufRsrcWord3);
-    uint8_t* const ld0 = lds + __mul24(r0, ncol) + 16 * q;
-    const bool qv = q < nq16;
-    uint4 v[kRsRowSteps];
-#pragma unroll
-    for (int u = 0; u < kRsRowSteps; ++u) {
-      // rows past the window re-read its last row (in bounds, not stored)
-      const uint32_t rl = (uint32_t)min(r0 + 8 * u, nrow - 1);
-      const auto w = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(__umul24(rl, (uint32_t)sp) + 16u * q),
-                                                           rr0 * sp, 0);
-      v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-#pragma unroll
-    for (int u = 0; u < kRsRowSteps; ++u)
-      if (qv && r0 + 8 * u < nrow) *reinterpret_cast<uint4*>(ld0 + 8 * u * ncol) = v[u];
-  } else if (al16) {
-    const int nq = nq16, total = nrow * nq;
+  if (((((uintptr_t)S) | (uintptr_t)sp) & 15) == 0 && (c1 < sp || (sw & 15) == 0)) {
+    const int nq = (c1 < sp ? ncol : min(ncol, sw - c0)) >> 4, total = nrow * nq;
     const uint32_t mg = ((1u << 19) + nq - 1) / nq;
     // raw buffer loads on the window's first column: one 32-bit VGPR offset
     // per chunk, no 64-bit address arithmetic
