@@ -74,10 +74,29 @@ struct orbgpu_lba_ctx {
   size_t staging_cap = 0;
   LbaHostWords* host = nullptr;  // pinned, mapped, coherent
   LbaHostWords* host_dev = nullptr;
+  char* res = nullptr;  // pinned, mapped, coherent: a one-rank call's results (LbaArgs::res_*)
+  char* res_dev = nullptr;
+  size_t res_cap = 0;
+  uint32_t calls = 0;
   ~orbgpu_lba_ctx() {
     if (arena) (void)hipFree(arena);
     if (staging) (void)hipHostFree(staging);
     if (host) (void)hipHostFree(host);
+    if (res) (void)hipHostFree(res);
+  }
+  bool reserve_results(size_t bytes) {
+    if (bytes <= res_cap) return true;
+    if (res) (void)hipHostFree(res);
+    res = res_dev = nullptr;
+    res_cap = 0;
+    void* dp = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&res), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&dp, res, 0) != hipSuccess)
+      return false;
+    res_dev = static_cast<char*>(dp);
+    res_cap = bytes;
+    return true;
   }
   bool reserve(size_t dev_bytes, size_t host_bytes) {
     if (dev_bytes > arena_cap) {
@@ -407,7 +426,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
                                      sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));
   LBA_HOST_PHASE(6);
-  if (!h->reserve(cz, std::max(up, dn))) return ORBGPU_ERR_NOMEM;
+  if (!h->reserve(cz, std::max(up, dn)) || (!reduce && !h->reserve_results(dn))) return ORBGPU_ERR_NOMEM;
 
   // ---- fill the upload image in pinned memory
   char* U = h->staging;
@@ -417,6 +436,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   ctrl0.max_iters = iterations;
   ctrl0.need_build = 1;
   ctrl0.lin_state = -1;
+  ctrl0.call = (int)(++h->calls & 0x7fffffffu);
   std::memcpy(U + u_ctrl, &ctrl0, sizeof(ctrl0));
   std::memset(U + u_cnt, 0, 128);
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
@@ -576,6 +596,12 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.counter = reinterpret_cast<unsigned*>(A + u_cnt);
   a.ctrl = reinterpret_cast<LbaCtrl*>(A + u_ctrl);
   a.host = h->host_dev;
+  a.early_out = reduce ? 0 : 1;
+  if (!reduce) {  // the results' layout is the download block's (d_*)
+    a.res_ctrl = reinterpret_cast<uint32_t*>(h->res_dev);
+    a.res_out = reinterpret_cast<double*>(h->res_dev + d_out);
+    a.res_outlier = reinterpret_cast<uint8_t*>(h->res_dev + d_outlier);
+  }
   a.model = m.model;
   a.pdim = m.pdim;
   a.pstride = m.pstride;
@@ -597,13 +623,19 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   hw->stop = (stop_flag && *stop_flag) ? 1u : 0u;
   if (lba_begin(a, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
 
+  // one-rank: whether a step was queued behind the one that ended the LM
+  // (its k_lba_sums then writes the results to host memory)
+  bool step_after_end = false;
   if (!reduce) {
     // ---- the device runs the LM loop; keep kAhead steps queued
     const int max_steps = iterations * 10;  // every iteration ends within 10 trials
     int issued = 0;
     while (issued < max_steps) {
       const unsigned long long p = hw->progress;
-      if (p >> 32) break;
+      if (p >> 32) {
+        step_after_end = issued > (int)(p & 0xffffffffu);
+        break;
+      }
       if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
         if (lba_step(a, st, issued == 0 || a.force_lin) != hipSuccess) return ORBGPU_ERR_DEVICE;
@@ -682,17 +714,36 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     }
   }
 
-  // ---- outliers, final state, one copy back
+  // ---- outliers, final state
   const auto t_loop = clk::now();
-  char* D = A + d_begin;
-  if (lba_classify(a, reinterpret_cast<uint8_t*>(D + d_outlier), reinterpret_cast<double*>(D + d_out), D, st) !=
-          hipSuccess ||
-      hipMemcpyAsync(h->staging, D, dn, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
-  std::memcpy(&wo.ctrl, h->staging, sizeof(LbaCtrl));
-  const auto* out = reinterpret_cast<const double*>(h->staging + d_out);
-  const auto* lo = reinterpret_cast<const uint8_t*>(h->staging + d_outlier);
+  const char* R = nullptr;
+  if (!reduce) {
+    // one rank: the results arrive in host memory, written by the step queued
+    // behind the LM's end or else by one launch now; the host returns as soon
+    // as they are complete (the queued no-op kernels drain on the stream)
+    if (!step_after_end && lba_classify_to_host(a, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    const uint32_t want = (uint32_t)ctrl0.call;
+    for (unsigned spin = 0; __atomic_load_n(&hw->results, __ATOMIC_ACQUIRE) != want; ++spin) {
+      if ((spin & 63u) == 63u) {  // a failed or drained stream without the results
+        const hipError_t q = hipStreamQuery(st);
+        if (q != hipSuccess && q != hipErrorNotReady) return ORBGPU_ERR_DEVICE;
+        if (q == hipSuccess && __atomic_load_n(&hw->results, __ATOMIC_ACQUIRE) != want) return ORBGPU_ERR_DEVICE;
+      }
+      std::this_thread::yield();
+    }
+    R = h->res;
+  } else {
+    char* D = A + d_begin;
+    if (lba_classify(a, reinterpret_cast<uint8_t*>(D + d_outlier), reinterpret_cast<double*>(D + d_out), D, st) !=
+            hipSuccess ||
+        hipMemcpyAsync(h->staging, D, dn, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return ORBGPU_ERR_DEVICE;
+    R = h->staging;
+  }
+  std::memcpy(&wo.ctrl, R, sizeof(LbaCtrl));
+  const auto* out = reinterpret_cast<const double*>(R + d_out);
+  const auto* lo = reinterpret_cast<const uint8_t*>(R + d_outlier);
   wo.n_out = 0;
   for (int j = 0; j < ne; ++j) {
     outlier[gidx[j]] = lo[j];

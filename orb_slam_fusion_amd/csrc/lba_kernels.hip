@@ -841,6 +841,62 @@ __device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, 
   }
 }
 
+template <int M>
+__device__ __forceinline__ void classify_elem(const LbaArgs& a, int s, int i, uint8_t* __restrict__ outlier,
+                                              double* __restrict__ out, uint32_t* __restrict__ ctrl_out) {
+  // the final LM state for the host's one copy back
+  if (i < (int)(sizeof(LbaCtrl) / 4)) ctrl_out[i] = reinterpret_cast<const uint32_t*>(a.ctrl)[i];
+  if (i < a.pstride * a.n_kf) out[i] = a.poses[s][i];
+  if (i < 3 * a.n_pts) out[(size_t)a.pstride * a.n_kf + i] = a.pts[s][i];
+  if (i >= a.n_edges) return;
+  const LbaEdgeDev e = a.edges[i];
+  const double* x = a.pts[s] + 3 * e.point;
+  const double X[3] = {x[0], x[1], x[2]};
+  double tmp[3];
+  const bool depth = vis_error<M>(a, e, a.poses[s] + a.pstride * e.kf, X, tmp);
+  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
+  const double chi = lba_chi2(e, ev);
+  if constexpr (M == kModelSe3) {
+    outlier[i] = (chi > (e.ur < 0.f ? 5.991 : 7.815) || !depth) ? 1 : 0;
+  } else {
+    constexpr float chi2Mono2 = 5.991f, chi2Stereo2 = 7.815f;
+    bool bad;
+    if (e.ur < 0.f) {
+      const bool close = a.close[e.point] != 0;
+      bad = (chi > chi2Mono2 && !close) || (chi > 1.5f * chi2Mono2 && close) || !depth;
+    } else {
+      bad = chi > chi2Stereo2;
+    }
+    outlier[i] = bad ? 1 : 0;
+  }
+}
+
+__device__ __forceinline__ int classify_items(const LbaArgs& a) {
+  return max(max(a.n_edges, a.pstride * a.n_kf), max(3 * a.n_pts, (int)(sizeof(LbaCtrl) / 4)));
+}
+
+// The results straight into host-mapped memory (a.res_*), grid-stride over
+// any grid; every block releases its stores at system scope before its
+// ticket, and the last block publishes the call's number
+// (LbaHostWords::results) and marks the call classified.  Run by every
+// block of k_lba_sums once the LM is done (the step queued behind the one
+// that ended it), or by k_lba_classify_host when no step follows.
+template <int M>
+__device__ void classify_to_host(const LbaArgs& a) {
+  const LbaCtrl& c = *a.ctrl;
+  const int n = classify_items(a);
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads)
+    classify_elem<M>(a, c.state, i, a.res_outlier, a.res_out, a.res_ctrl);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+  if (!last_block(a.counter + 3)) return;
+  if (threadIdx.x == 0) {
+    a.ctrl->classified = 1;  // later no-op steps' sums skip it (stream-ordered)
+    __hip_atomic_store(&a.host->results, (uint32_t)c.call, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ---- buildSystem, vertex side.  Blocks [0, kSumsQ n_free): a quarter of
 // one free pose's slots each (slot j of the pose to block j / 256 mod kSumsQ),
 // a fixed tree per term (DPP row sums, then the 16 rows in order) -> a
@@ -850,10 +906,15 @@ __device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, 
 // The last block adds each pose's quarters in order (Hpp 6 x 6 full, bp,
 // the pose diagonal) and opens the iteration: iniChi, and at iteration 0
 // computeLambdaInit (tau * max |diag| over pose and point blocks).
+template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   __shared__ double red[16 * 27];
   const LbaCtrl& c = *a.ctrl;
-  if (c.done || !c.need_build) return;
+  if (c.done) {  // the first kernel of a step queued behind the LM's end: the results
+    if (a.early_out && !c.classified) classify_to_host<M>(a);
+    return;
+  }
+  if (!c.need_build) return;
   const LinPtr L = lin_of(a, c.state);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n_pose_blocks = kSumsQ * a.n_free;
@@ -2428,33 +2489,14 @@ template <int M>
 __global__ __launch_bounds__(kThreads) void k_lba_classify(LbaArgs a, uint8_t* __restrict__ outlier,
                                                            double* __restrict__ out,
                                                            uint32_t* __restrict__ ctrl_out) {
-  const int s = a.ctrl->state;
   const int i = blockIdx.x * kThreads + threadIdx.x;
-  // the final LM state for the host's one copy back
-  if (i < (int)(sizeof(LbaCtrl) / 4)) ctrl_out[i] = reinterpret_cast<const uint32_t*>(a.ctrl)[i];
-  if (i < a.pstride * a.n_kf) out[i] = a.poses[s][i];
-  if (i < 3 * a.n_pts) out[(size_t)a.pstride * a.n_kf + i] = a.pts[s][i];
-  if (i >= a.n_edges) return;
-  const LbaEdgeDev e = a.edges[i];
-  const double* x = a.pts[s] + 3 * e.point;
-  const double X[3] = {x[0], x[1], x[2]};
-  double tmp[3];
-  const bool depth = vis_error<M>(a, e, a.poses[s] + a.pstride * e.kf, X, tmp);
-  const double ev[3] = {a.err[3 * i], a.err[3 * i + 1], a.err[3 * i + 2]};
-  const double chi = lba_chi2(e, ev);
-  if constexpr (M == kModelSe3) {
-    outlier[i] = (chi > (e.ur < 0.f ? 5.991 : 7.815) || !depth) ? 1 : 0;
-  } else {
-    constexpr float chi2Mono2 = 5.991f, chi2Stereo2 = 7.815f;
-    bool bad;
-    if (e.ur < 0.f) {
-      const bool close = a.close[e.point] != 0;
-      bad = (chi > chi2Mono2 && !close) || (chi > 1.5f * chi2Mono2 && close) || !depth;
-    } else {
-      bad = chi > chi2Stereo2;
-    }
-    outlier[i] = bad ? 1 : 0;
-  }
+  if (i < classify_items(a)) classify_elem<M>(a, a.ctrl->state, i, outlier, out, ctrl_out);
+}
+
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lba_classify_host(LbaArgs a) {
+  if (a.ctrl->classified) return;
+  classify_to_host<M>(a);
 }
 
 // windows with more key frames than k_lba_trial<kModelImu> stages in LDS
@@ -2545,8 +2587,11 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   }
   // kModelImu: extra blocks assemble the links' part of the system
   const unsigned asm_blocks = imu && a.n_sys > 0 ? blocks((long)a.n_sys * a.n_sys + a.n_sys, kThreads) : 0;
-  hipLaunchKernelGGL(k_lba_sums, dim3(kSumsQ * a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads) + asm_blocks),
-                     dim3(kThreads), 0, st, a);
+  const dim3 sg(kSumsQ * a.n_free + blocks(a.n_pts > 0 ? a.n_pts : 1, kThreads) + asm_blocks);
+  if (imu)
+    hipLaunchKernelGGL(k_lba_sums<kModelImu>, sg, dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_lba_sums<kModelSe3>, sg, dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2615,6 +2660,17 @@ hipError_t lba_step(const LbaArgs& a, hipStream_t st, bool linearize) {
 
 hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st) {
   hipLaunchKernelGGL(k_lba_ctl, dim3(1), dim3(64), 0, st, a, mode);
+  return hipGetLastError();
+}
+
+hipError_t lba_classify_to_host(const LbaArgs& a, hipStream_t st) {
+  long n = a.n_edges;
+  if ((long)a.pstride * a.n_kf > n) n = (long)a.pstride * a.n_kf;
+  if (3L * a.n_pts > n) n = 3L * a.n_pts;
+  if (a.model == kModelImu)
+    hipLaunchKernelGGL(k_lba_classify_host<kModelImu>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_lba_classify_host<kModelSe3>, dim3(blocks(n > 0 ? n : 1, kThreads)), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -56,6 +56,8 @@ struct LbaCtrl {
   int it, q, nbad, need_build, done, state, iters_done, trials, max_iters, stopped;
   int lin_state;   // the state whose per-edge terms (lin_of) are current; -1: none
   int lambda_due;  // sharded: the first build's lambda init waits for the all-reduce (k_lba_ctl)
+  int call;        // the call's sequence number (LbaHostWords::results)
+  int classified;  // the outliers and the final state are in the host-mapped results
 };
 
 // The reduced-camera-system factorisation (lba_kernels.hip): the packed
@@ -71,8 +73,8 @@ static_assert(sizeof(LbaCtrl) % 4 == 0 && sizeof(LbaCtrl) <= 128, "LbaCtrl: copi
 // host-mapped progress word: (done << 32) | trials completed
 struct LbaHostWords {
   unsigned long long progress;
-  uint32_t stop;  // mirror of the caller's *pbStopFlag, read by the device
-  uint32_t pad;
+  uint32_t stop;     // mirror of the caller's *pbStopFlag, read by the device
+  uint32_t results;  // LbaCtrl::call once that call's results are complete in host memory
 };
 
 struct LbaArgs {
@@ -136,6 +138,13 @@ struct LbaArgs {
   unsigned* counter;         // last-block-done tickets (self-resetting), one per stage
   LbaCtrl* ctrl;
   LbaHostWords* host;        // host-mapped
+  // one-rank calls: the outliers, the final state and the LbaCtrl go straight
+  // to host-mapped memory, written by the first kernel of the step queued
+  // after the one that ends the LM (k_lba_sums) or by k_lba_classify
+  int early_out;
+  uint8_t* res_outlier;      // [n_edges]
+  double* res_out;           // [pstride n_kf | 3 n_pts]
+  uint32_t* res_ctrl;        // LbaCtrl copy
   // ---- key-frame model (LocalInertialBA: kModelImu)
   int model;                 // LbaModel
   int pdim;                  // reduced-system rows per free key frame (6 / 15)
@@ -171,8 +180,10 @@ hipError_t lba_schur(const LbaArgs& a, hipStream_t st);
 hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st);
 hipError_t lba_ctl(const LbaArgs& a, int mode, hipStream_t st);
 // outliers + the final state: out = [poses 7 n_kf | pts 3 n_pts] (doubles),
-// and a copy of the LbaCtrl at ctrl_out
+// and a copy of the LbaCtrl at ctrl_out; to_host: into a.res_* (host-mapped)
+// unless already there, then LbaHostWords::results = the call
 hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, void* ctrl_out, hipStream_t st);
+hipError_t lba_classify_to_host(const LbaArgs& a, hipStream_t st);
 size_t lba_solve_lds_bytes(int n_pad);
 constexpr int kSumsQ = 4;                // k_lba_sums blocks per free pose
 constexpr int kSchurSplitMax = 8;        // point ranges of k_lba_schur_split (one per XCD)

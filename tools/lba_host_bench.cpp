@@ -19,6 +19,10 @@ hipError_t lba_schur(const LbaArgs&, hipStream_t) { return hipSuccess; }
 hipError_t lba_solve_trial(const LbaArgs&, hipStream_t) { return hipSuccess; }
 hipError_t lba_ctl(const LbaArgs&, int, hipStream_t) { return hipSuccess; }
 hipError_t lba_classify(const LbaArgs&, uint8_t*, double*, void*, hipStream_t) { return hipSuccess; }
+hipError_t lba_classify_to_host(const LbaArgs& a, hipStream_t) {  // the results flag, as the device would
+  a.host->results = (uint32_t)reinterpret_cast<const LbaCtrl*>(a.ctrl)->call;
+  return hipSuccess;
+}
 size_t lba_solve_lds_bytes(int) { return 0; }
 int lba_solve_mode(int) { return 0; }
 bool lba_solve_mode_fits(int, int) { return true; }
@@ -32,8 +36,12 @@ hipError_t hipHostFree(void* p) { std::free(p); return hipSuccess; }
 hipError_t hipMalloc(void** p, size_t n) { *p = std::malloc(n); return hipSuccess; }
 hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { *p = std::calloc(1, n); return hipSuccess; }
 hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int) { *d = h; return hipSuccess; }
-hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipSuccess; }
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+  std::memcpy(d, s, n < 128 ? n : 128);  // the LbaCtrl at the image's head only (the call number)
+  return hipSuccess;
+}
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
 hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) { *s = nullptr; return hipSuccess; }
 hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
 }
