@@ -141,6 +141,28 @@ def test_lba_all_fixed_and_empty(gpu_available):
     assert np.allclose(got["poses"], p.poses_init)
 
 
+def test_lba_zero_iterations_and_repeat(gpu_available):
+    """iterations = 0: no LM step is queued, so one classify launch writes the
+    results to host memory (the other calls get them from the k_lba_sums of
+    the step queued behind the LM's end); then calls of different sizes on
+    one context, each against the oracle (a call must never return an
+    earlier call's results)."""
+    lba = LocalBundleAdjuster()
+    p = synth.lba_problem(seed=9, n_kf=6, n_pts=120, obs_per_pt=3, n_fixed=1)
+    got = lba.optimize(p, iterations=0)
+    ref = oracle.lba(p, iters=0)
+    assert got["stats"][2] == 0 and got["stats"][3] == 0
+    assert np.allclose(got["poses_d"], p.poses_init)
+    check_flags(got["outlier"], ref, np.where(p.edges["ur"] < 0, 5.991, 7.815))
+    for seed, n_kf, n_pts in ((10, 8, 300), (11, 5, 60), (10, 8, 300)):
+        q = synth.lba_problem(seed=seed, n_kf=n_kf, n_pts=n_pts, obs_per_pt=3, n_fixed=1)
+        g = lba.optimize(q)
+        r = oracle.lba(q)
+        assert g["stats"][3] == r["stats"][3]
+        assert np.allclose(g["pts"], r["pts"], rtol=1e-5, atol=1e-5)
+        check_flags(g["outlier"], r, np.where(q.edges["ur"] < 0, 5.991, 7.815))
+
+
 def test_lba_stop_flag(gpu_available):
     import ctypes
 

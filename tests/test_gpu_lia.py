@@ -134,3 +134,19 @@ def test_lia_trial_states_past_lds_table(gpu_available):
                            consecutive=True)
     assert len(pb.kfs) > 128
     _compare(pb)
+
+
+def test_lia_zero_iterations(gpu_available):
+    """iterations = 0: the results come from the one classify launch (no LM
+    step is queued); states unchanged, flags and err as the oracle's."""
+    pb = synth.lia_problem(6, n_opt=5, n_fixed_cov=3, n_pts=150, max_obs=4)
+    got = LocalBundleAdjuster().optimize_inertial(pb, iterations=0)
+    ref = oracle.lia(pb, iterations=0)
+    assert got["stats"][2] == 0 and got["stats"][3] == 0
+    assert abs(got["stats"][0] - ref["stats"][0]) <= 1e-8 * ref["stats"][0]
+    assert np.array_equal(got["kfs"], np.ascontiguousarray(pb.kfs, got["kfs"].dtype))
+    mono = pb.edges["ur"] < 0
+    close = pb.close[pb.edges["point"]] != 0
+    thr = np.where(mono, np.where(close, float(np.float32(1.5) * np.float32(5.991)), float(np.float32(5.991))),
+                   float(np.float32(7.815)))
+    check_flags(got["outlier"], ref, thr)
