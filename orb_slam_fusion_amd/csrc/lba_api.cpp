@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -289,6 +290,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // zeros the per-call clear leaves; a sharded rank's zeros add nothing)
   LBA_HOST_PHASE(1);
   std::vector<int> pair_list;
+  std::vector<int> pose_cnt(nf + 1, 0);  // free-pose edges per pose (then its CSR)
   // point-major order: perm[j] = the caller's index of shard edge j (one
   // scatter of indices, then sequential gathers), pf[j] its free-pose index
   std::vector<int> perm(std::max(ne, 1)), pf(std::max(ne, 1));  // pf: -1 = fixed pose
@@ -298,23 +300,32 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       const int p = edges[i].point;
       if (p >= pt_begin && p < pt_end) perm[fill[p - pt_begin]++] = i;
     }
-    for (int j = 0; j < ne; ++j) pf[j] = hidx[edges[perm[j]].kf];
   LBA_HOST_PHASE(2);
     auto add_pair = [&](int i, int j) {
       pair_list.push_back(i);
       pair_list.push_back(j);
     };
-    if (nf <= 64) {
-      // a point's free poses as one bit mask, OR-ed into each of its poses' rows
-      std::vector<uint64_t> rows(nf);
-      for (int f = 0; f < nf; ++f) rows[f] = 1ull << f;
-      for (int p = 0; p < np; ++p) {
-        uint64_t msk = 0;
-        for (int u = cnt[p]; u < cnt[p + 1]; ++u)
-          if (pf[u] >= 0) msk |= 1ull << pf[u];
+    // one walk in point order: each edge's free-pose index, the per-pose edge
+    // counts and (nf <= 64) a point's free poses as one bit mask, OR-ed into
+    // each of its poses' rows
+    const bool masks = nf <= 64;
+    std::vector<uint64_t> rows(masks ? nf : 0);
+    for (int f = 0; f < (int)rows.size(); ++f) rows[f] = 1ull << f;
+    for (int p = 0; p < np; ++p) {
+      uint64_t msk = 0;
+      for (int u = cnt[p]; u < cnt[p + 1]; ++u) {
+        const int f = hidx[edges[perm[u]].kf];
+        pf[u] = f;
+        if (f >= 0) {
+          ++pose_cnt[f + 1];
+          msk |= 1ull << (f & 63);
+        }
+      }
+      if (masks)
         for (int u = cnt[p]; u < cnt[p + 1]; ++u)
           if (pf[u] >= 0) rows[pf[u]] |= msk;
-      }
+    }
+    if (masks) {
       for (int i = 0; i < nf; ++i)
         for (int j = i; j < nf; ++j)
           if ((rows[i] >> j) & 1) add_pair(i, j);
@@ -337,8 +348,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // Schur path: point ranges (k_lba_schur_split), S of them so that a
   // (pair, range) block gets about kSchurSplitEdges of its pose's edges.
   // ORBGPU_SCHUR=pair|band|split picks a path for A/B runs (tools/).
-  int n_free_edges = 0;
-  for (int u = 0; u < ne; ++u) n_free_edges += pf[u] >= 0;
+  const int n_free_edges = std::accumulate(pose_cnt.begin(), pose_cnt.end(), 0);
   int sc_split = nf > 0 ? (n_free_edges + nf * kSchurSplitEdges - 1) / (nf * kSchurSplitEdges) : 0;
   sc_split = std::min(std::max(sc_split, 1), kSchurSplitMax);
   SchurChunks sc;
@@ -353,7 +363,6 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     pbx[x] = (int)(std::lower_bound(cnt.begin(), cnt.end() - 1, (int)((long long)x * ne / sc_split)) - cnt.begin());
   LBA_HOST_PHASE(4);
   const std::vector<int>& gidx = perm;  // shard edge -> caller's edge index
-  std::vector<int> pose_cnt(nf + 1, 0);
   // IMU links incident to each free key frame (link order)
   std::vector<int> inc(nf + 1, 0), inc_list;
   if (imu) {
@@ -440,11 +449,6 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::memcpy(U + u_ctrl, &ctrl0, sizeof(ctrl0));
   std::memset(U + u_cnt, 0, 128);
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
-  for (int j = 0; j < ne; ++j) {  // sequential stores into the pinned image
-    const orbgpu_lba_edge& e = edges[perm[j]];
-    le[j] = LbaEdgeDev{e.point - pt_begin, e.kf, pf[j], 0, e.u, e.v, e.ur, e.inv_sigma2};
-    if (pf[j] >= 0) ++pose_cnt[pf[j] + 1];
-  }
   LBA_HOST_PHASE(7);
   int* I = reinterpret_cast<int*>(U + u_ints);
   int* I_slot = I;  // int4 records first (16-B aligned)
@@ -462,13 +466,29 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::copy(cnt.begin(), cnt.end(), I_pt);
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
   std::copy(pose_cnt.begin(), pose_cnt.end(), I_pb);
+  // one walk in point order (host-side arrays only: nothing is read back from
+  // pinned memory): the edge image, each edge's free pose and pose slot, the
+  // slot records, and (k_lba_schur_split) per free pose the slot where each
+  // point range starts (slots are in point order within a pose)
+  int* const SC = reinterpret_cast<int*>(U + u_sc);
+  int* const SP = SC + (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1);
   {
-    // host-side copies only (pf, cnt): nothing is read back from pinned memory
-    std::copy(pf.begin(), pf.begin() + ne, I_ef);
     std::vector<int> fill(pose_cnt.begin(), pose_cnt.end() - 1);
-    for (int p = 0; p < np; ++p)
+    int x = 0;
+    const int S1 = sc_split + 1;
+    auto range_starts = [&](int p) {  // range x starts at point pbx[x]
+      while (x <= sc_split && pbx[x] <= p) {
+        for (int f = 0; f < nf; ++f) SP[(size_t)f * S1 + x] = fill[f];
+        ++x;
+      }
+    };
+    for (int p = 0; p < np; ++p) {
+      if (sc_split > 0) range_starts(p);
       for (int j = cnt[p]; j < cnt[p + 1]; ++j) {
+        const orbgpu_lba_edge& e = edges[perm[j]];
         const int f = pf[j];
+        le[j] = LbaEdgeDev{p, e.kf, f, 0, e.u, e.v, e.ur, e.inv_sigma2};
+        I_ef[j] = f;
         if (f < 0) {
           I_es[j] = -1;
           continue;
@@ -481,6 +501,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
         r[2] = cnt[p];
         r[3] = cnt[p + 1];
       }
+    }
+    if (sc_split > 0) range_starts(np);
   }
   for (int k = 0; k < n_pairs; ++k) {
     I_pi[k] = pair_list[2 * k];
@@ -490,27 +512,6 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::copy(inc.begin(), inc.end(), I_inc);
   std::copy(inc_list.begin(), inc_list.end(), I_incl);
   LBA_HOST_PHASE(8);
-  int* const SC = reinterpret_cast<int*>(U + u_sc);
-  int* const SP = SC + (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1);
-  // per free pose, where each point range starts in its (point-ordered) slots
-  if (sc_split > 0) {
-    // slots are in point order within a pose: walk the points once, counting
-    // each pose's slots below each range start
-    std::vector<int> below((size_t)nf * (sc_split + 1), 0), seen(nf, 0);
-    int x = 0;
-    for (int p = 0; p <= np; ++p) {
-      while (x <= sc_split && pbx[x] <= p) {  // range x starts at point pbx[x]
-        for (int f = 0; f < nf; ++f) below[(size_t)f * (sc_split + 1) + x] = seen[f];
-        ++x;
-      }
-      if (p == np) break;
-      for (int j = cnt[p]; j < cnt[p + 1]; ++j)
-        if (pf[j] >= 0) ++seen[pf[j]];
-    }
-    for (int f = 0; f < nf; ++f)
-      for (int y = 0; y <= sc_split; ++y)
-        SP[(size_t)f * (sc_split + 1) + y] = pose_cnt[f] + (y == sc_split ? seen[f] : below[(size_t)f * (sc_split + 1) + y]);
-  }
   if (sc.ok) {
     std::memcpy(SC, sc.chunk.data(), sizeof(int4) * sc.chunk.size());
     std::memcpy(SC + 4 * sc.chunk.size(), sc.tile0.data(), sizeof(int) * sc.tile0.size());
