@@ -401,6 +401,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   up = align_up(up + sizeof(int) * n_ints, 256);
   const size_t u_sc = up;
   up = align_up(up + sizeof(int) * n_sc, 256);
+  const size_t u_pcnt = up;  // per-pair tickets of k_lba_schur_split (zero)
+  up = align_up(up + sizeof(unsigned) * (size_t)std::max(n_pairs, 1), 256);
   const size_t u_state = up;
   up = align_up(up + sizeof(double) * (2 * KS + 2 * P3), 256);
   const size_t u_imu = up;
@@ -448,6 +450,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   ctrl0.call = (int)(++h->calls & 0x7fffffffu);
   std::memcpy(U + u_ctrl, &ctrl0, sizeof(ctrl0));
   std::memset(U + u_cnt, 0, 128);
+  std::memset(U + u_pcnt, 0, sizeof(unsigned) * (size_t)std::max(n_pairs, 1));
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
   LBA_HOST_PHASE(7);
   int* I = reinterpret_cast<int*>(U + u_ints);
@@ -550,6 +553,14 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // trial's terms (same values; tests/test_gpu_lba.py compares the two)
   a.force_lin = std::getenv("ORBGPU_LBA_RELINEARIZE") != nullptr;
   a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
+  a.pair_cnt = reinterpret_cast<unsigned*>(A + u_pcnt);
+  // each pair's ranges folded by its last block (ORBGPU_SCHUR_FOLD=launch: by
+  // k_lba_schur_fold, for A/B runs)
+  static const bool fold_launch = [] {
+    const char* e = std::getenv("ORBGPU_SCHUR_FOLD");
+    return e && std::strcmp(e, "launch") == 0;
+  }();
+  a.sc_fold_inline = fold_launch ? 0 : 1;
   if (sc_split > 1) a.sc_part = dp(c_scp);
   if (sc.ok) {
     const int* dS = reinterpret_cast<const int*>(A + u_sc);

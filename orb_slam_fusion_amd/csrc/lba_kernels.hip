@@ -1260,15 +1260,44 @@ __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
     if ((lane & 15) == 15) red[(wave * 4 + (lane >> 4)) * 42 + k] = v;
   }
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t >= (diag ? 42 : 36)) return;
+  const int t = threadIdx.x, nk = diag ? 42 : 36;
   double sum = 0;
+  if (t < nk) {
 #pragma unroll
-  for (int r = 0; r < kSplitWaves * 4; ++r) sum += red[r * 42 + t];
-  if (S == 1)
-    schur_write(a, fi, fj, t, sum);
-  else
-    a.sc_part[42 * (size_t)blockIdx.x + t] = sum;
+    for (int r = 0; r < kSplitWaves * 4; ++r) sum += red[r * 42 + t];
+  }
+  if (S == 1) {
+    if (t < nk) schur_write(a, fi, fj, t, sum);
+    return;
+  }
+  if (t < nk) a.sc_part[42 * (size_t)blockIdx.x + t] = sum;
+  if (!a.sc_fold_inline) return;  // k_lba_schur_fold adds the ranges
+  // the pair's last block to finish (a ticket per pair, self-resetting) adds
+  // its S range partials in range order -- k_lba_schur_fold's sum, without
+  // the launch
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned tk = __hip_atomic_fetch_add(a.pair_cnt + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == (unsigned)(S - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(a.pair_cnt + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last || t >= nk) return;
+  const double* part = a.sc_part + 42 * (size_t)pr * S + t;
+  double v[kSchurSplitMax];
+#pragma unroll
+  for (int y = 0; y < kSchurSplitMax; ++y) v[y] = y < S ? part[42 * y] : 0.0;
+  double tot = 0;
+#pragma unroll
+  for (int y = 0; y < kSchurSplitMax; ++y)
+    if (y < S) tot += v[y];
+  schur_write(a, fi, fj, t, tot);
 }
 
 // each pair's S range partials added in range order, then written as above
@@ -2599,7 +2628,8 @@ hipError_t lba_schur(const LbaArgs& a, hipStream_t st) {
   if (a.n_pairs <= 0) return hipSuccess;
   if (a.sc_split > 0) {
     hipLaunchKernelGGL(k_lba_schur_split, dim3(a.n_pairs * a.sc_split), dim3(kSplitThreads), 0, st, a);
-    if (a.sc_split > 1) hipLaunchKernelGGL(k_lba_schur_fold, dim3(a.n_pairs), dim3(64), 0, st, a);
+    if (a.sc_split > 1 && !a.sc_fold_inline)
+      hipLaunchKernelGGL(k_lba_schur_fold, dim3(a.n_pairs), dim3(64), 0, st, a);
   } else if (a.n_chunks > 0) {
     if (lds_optin(reinterpret_cast<const void*>(&k_lba_schur_band), kSchurChunkLds) != hipSuccess)
       return hipErrorInvalidValue;

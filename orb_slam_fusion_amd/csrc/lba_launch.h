@@ -108,6 +108,8 @@ struct LbaArgs {
   int force_lin;             // 1: every build re-linearises (ORBGPU_LBA_RELINEARIZE; tests compare)
   int sc_split;
   const int* pose_split;  // [n_free * (sc_split + 1)]
+  int sc_fold_inline;     // 1: each pair's last range block folds the ranges (else k_lba_schur_fold)
+  unsigned* pair_cnt;     // [n_pairs] per-pair tickets (self-resetting; zero in every upload)
   int n_chunks;
   const int* sc_order;  // [points with a free edge] shard point index, chunk order
   const int4* sc_chunk;  // [n_chunks] {first in sc_order, points, b0, w}
