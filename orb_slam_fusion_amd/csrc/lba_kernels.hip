@@ -1015,10 +1015,15 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
     }
   }
   __syncthreads();
-  // max is order-independent: every reduction order gives the same value
+  // the maxima only feed computeLambdaInit (the first build): later builds
+  // skip their loads.  max is order-independent: every reduction order gives
+  // the same value
+  const bool first = c.it == 0;
   double m = 0;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) m = fmax(m, a.partials[b]);
-  for (int k = threadIdx.x; k < a.n_sys; k += kThreads) m = fmax(m, fabs(a.diag[k]));
+  if (first) {
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) m = fmax(m, a.partials[b]);
+    for (int k = threadIdx.x; k < a.n_sys; k += kThreads) m = fmax(m, fabs(a.diag[k]));
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
   __syncthreads();
@@ -1031,8 +1036,9 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
       // this shard's point maximum; the host max-reduces it and sum-reduces
       // the pose diagonal, then k_lba_ctl(kCtlLambda) finishes lambda init
       double hm = 0;
-      for (int b = a.n_free; b < (int)gridDim.x; ++b) hm = fmax(hm, a.partials[b]);
-      a.diag[a.n_sys] = hm;
+      if (first)
+        for (int b = a.n_free; b < (int)gridDim.x; ++b) hm = fmax(hm, a.partials[b]);
+      a.diag[a.n_sys] = hm;  // (reduced, and read, only at the first build)
       cw.lambda_due = cw.it == 0 ? 1 : 0;
     } else if (cw.it == 0) {
       ctl_lambda(a, mx);
