@@ -452,6 +452,10 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   std::memset(U + u_cnt, 0, 128);
   std::memset(U + u_pcnt, 0, sizeof(unsigned) * (size_t)std::max(n_pairs, 1));
   auto* le = reinterpret_cast<LbaEdgeDev*>(U + u_edges);
+  for (int j = 0; j < ne; ++j) {  // one sequential store stream into the pinned image
+    const orbgpu_lba_edge& e = edges[perm[j]];
+    le[j] = LbaEdgeDev{e.point - pt_begin, e.kf, pf[j], 0, e.u, e.v, e.ur, e.inv_sigma2};
+  }
   LBA_HOST_PHASE(7);
   int* I = reinterpret_cast<int*>(U + u_ints);
   int* I_slot = I;  // int4 records first (16-B aligned)
@@ -470,9 +474,13 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
   std::copy(pose_cnt.begin(), pose_cnt.end(), I_pb);
   // one walk in point order (host-side arrays only: nothing is read back from
-  // pinned memory): the edge image, each edge's free pose and pose slot, the
-  // slot records, and (k_lba_schur_split) per free pose the slot where each
-  // point range starts (slots are in point order within a pose)
+  // pinned memory): each edge's pose slot, the slot records and
+  // (k_lba_schur_split) per free pose the slot where each point range starts
+  // (slots are in point order within a pose).  The edge image and the free-
+  // pose indices go in sequential passes of their own: interleaving them here
+  // measured slower (layout 87 -> 113 µs), the pinned image taking several
+  // store streams at once
+  std::copy(pf.begin(), pf.begin() + ne, I_ef);
   int* const SC = reinterpret_cast<int*>(U + u_sc);
   int* const SP = SC + (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1);
   {
@@ -488,10 +496,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     for (int p = 0; p < np; ++p) {
       if (sc_split > 0) range_starts(p);
       for (int j = cnt[p]; j < cnt[p + 1]; ++j) {
-        const orbgpu_lba_edge& e = edges[perm[j]];
         const int f = pf[j];
-        le[j] = LbaEdgeDev{p, e.kf, f, 0, e.u, e.v, e.ur, e.inv_sigma2};
-        I_ef[j] = f;
         if (f < 0) {
           I_es[j] = -1;
           continue;
@@ -554,13 +559,15 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.force_lin = std::getenv("ORBGPU_LBA_RELINEARIZE") != nullptr;
   a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
   a.pair_cnt = reinterpret_cast<unsigned*>(A + u_pcnt);
-  // each pair's ranges folded by its last block (ORBGPU_SCHUR_FOLD=launch: by
-  // k_lba_schur_fold, for A/B runs)
-  static const bool fold_launch = [] {
+  // each pair's ranges folded by k_lba_schur_fold; ORBGPU_SCHUR_FOLD=inline:
+  // by the pair's last range block instead (a per-pair ticket: measured
+  // slower, 17.9 µs against 8.7 + 4.8 at C4 -- every block's agent-scope
+  // release costs more than the launch it saves)
+  static const bool fold_inline = [] {
     const char* e = std::getenv("ORBGPU_SCHUR_FOLD");
-    return e && std::strcmp(e, "launch") == 0;
+    return e && std::strcmp(e, "inline") == 0;
   }();
-  a.sc_fold_inline = fold_launch ? 0 : 1;
+  a.sc_fold_inline = fold_inline ? 1 : 0;
   if (sc_split > 1) a.sc_part = dp(c_scp);
   if (sc.ok) {
     const int* dS = reinterpret_cast<const int*>(A + u_sc);
