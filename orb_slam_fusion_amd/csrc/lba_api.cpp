@@ -384,7 +384,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // blocks of the widest grid that writes a.partials (k_lba_sums with, for
   // kModelImu, its link-assembly blocks)
   const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + kSumsQ * (long)nf + 1 +
-                    (imu ? ((long)n * n + n + 255) / 256 + (m.n_imu + 3) / 4 : 0);  // (+ the trial's link blocks)
+                    (imu ? ((long)n * n + n + 255) / 256 + m.n_imu : 0);  // (+ the trial's link blocks)
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)1) + E;
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order

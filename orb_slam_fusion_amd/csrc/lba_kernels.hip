@@ -23,7 +23,7 @@
 // kModelImu key frame (lba_launch.h): ImuCamPose state, body-frame visual
 // Jacobians (EdgeMono / EdgeStereo, g2o_types.cc:334-415), 15 reduced-system
 // rows per free key frame, and the IMU links (EdgeInertial + EdgeGyroRW +
-// EdgeAccRW, no points) evaluated a wave per link (lia_link) by extra blocks
+// EdgeAccRW, no points) evaluated a block per link (lia_link) by extra blocks
 // of the begin / linearize / trial launches, and added to the camera-side
 // system (lia_assemble_entry, in k_lba_sums) before the solve.
 //
@@ -475,7 +475,7 @@ __device__ __forceinline__ void load_state(StateD& s, const double* p) {
 // links, the information x1e-2 on the window's last link) plus EdgeGyroRW /
 // EdgeAccRW.  Building, the link's quadratic form over its 30 dims (kf1 VP
 // VV VG VA | kf2 VP VV VG VA; EdgeInertial's 24 columns are the first 24) and
-// the gradient -J^T W e.  The links ride as extra blocks (a wave per link) in
+// the gradient -J^T W e.  The links ride as extra blocks (a block per link) in
 // k_lba_begin (chi2 at the initial state), k_lba_linearize (the first build's
 // forms) and k_lba_trial (chi2 and, speculatively, forms at the trial state);
 // each link's chi2 goes to imu_tot[2 + l] and the launch's last block sums
@@ -483,11 +483,13 @@ __device__ __forceinline__ void load_state(StateD& s, const double* p) {
 // workgroup, three in a row: 36 us per build; round 3 a workgroup per link
 // in a launch of its own.)
 //
-// One link by one wave (lane): its data and the two key-frame states staged
-// in LDS (states from the table ts -- k_lba_trial's trial states -- when
-// given, else from the state array st), the error / chi2 and, kBuild, the
-// form and gradient into copy qcopy of imu_q.  Returns the link's chi2 (every
-// lane).
+// One link by one 256-thread block (tid; every thread must call): its data
+// and the two key-frame states staged in LDS (states from the table ts --
+// k_lba_trial's trial states -- when given, else from the state array st);
+// every wave runs the error chain (the same values), so the chi2 needs no
+// exchange, and the form's 216 + 900 entries are spread over the block.
+// kBuild: the form and gradient into copy qcopy of imu_q.  Returns the link's
+// chi2 (every thread).
 struct LinkLds {
   double J[9 * 24];
   double OJ[9 * 24];
@@ -498,46 +500,44 @@ struct LinkLds {
 };
 
 template <bool kBuild>
-__device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, const double* st, const double* ts,
+__device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int tid, const double* st, const double* ts,
                                            int qcopy, LinkLds& sh) {
+  constexpr int NT = kThreads;  // the link's block
+  const int lane = tid & 63;
   {
     // every load in flight before the first store: the edge chain below
     // then reads LDS, not one HBM round trip per field it reaches
-    constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + 63) / 64;
+    constexpr int kW = (int)(sizeof(LiaImuDev) / 4), kU = (kW + NT - 1) / NT;
     static_assert(sizeof(LiaImuDev) % 8 == 0, "LiaImuDev staging");
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.imu + l);
     const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
     const double* sb = ts ? ts : st;
     uint32_t w[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) w[u] = lane + 64 * u < kW ? src[lane + 64 * u] : 0u;
-    double sv[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = lane + 64 * u, which = k >= kImuStateStride ? 1 : 0;
-      sv[u] = k < 2 * kImuStateStride ? sb[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
-    }
+    for (int u = 0; u < kU; ++u) w[u] = tid + NT * u < kW ? src[tid + NT * u] : 0u;
+    const int k = tid, which = k >= kImuStateStride ? 1 : 0;
+    const double sv =
+        k < 2 * kImuStateStride ? sb[kImuStateStride * (which ? k2 : k1) + k - which * kImuStateStride] : 0.0;
+    static_assert(2 * kImuStateStride <= NT, "one state double a thread");
     uint32_t* dst = reinterpret_cast<uint32_t*>(&sh.L);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
-      if (lane + 64 * u < kW) dst[lane + 64 * u] = w[u];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (lane + 64 * u < 2 * kImuStateStride) sh.S[lane + 64 * u] = sv[u];
-    wave_lds_sync();
+      if (tid + NT * u < kW) dst[tid + NT * u] = w[u];
+    if (k < 2 * kImuStateStride) sh.S[k] = sv;
+    __syncthreads();
   }
   const LiaImuDev& E = sh.L;
   const double isc = (E.flags & ORBGPU_LIA_DOWNWEIGHT) ? 1e-2 : 1.0;  // information() * 1e-2
-  for (int k = lane; k < 81; k += 64) sh.Info[k] = E.pi.info[k] * isc;
+  for (int k = tid; k < 81; k += NT) sh.Info[k] = E.pi.info[k] * isc;
   StateD s1, s2;
   load_state(s1, sh.S);
   load_state(s2, sh.S + kImuStateStride);
   double* J = sh.J;
   if (kBuild) {  // the constant blocks and the zeros (inertial_edge_core writes the rest)
-    for (int k = lane; k < 9 * 24; k += 64) J[k] = 0;
-    wave_lds_sync();
-    if (lane < 9) {
-      const int i = lane / 3, j = lane % 3;
+    for (int k = tid; k < 9 * 24; k += NT) J[k] = 0;
+    __syncthreads();
+    if (tid < 9) {
+      const int i = tid / 3, j = tid % 3;
       J[(6 + i) * 24 + 3 + j] = i == j ? -1.0 : 0.0;
       J[(3 + i) * 24 + 9 + j] = -(double)E.pi.JVg[3 * i + j];
       J[(6 + i) * 24 + 9 + j] = -(double)E.pi.JPg[3 * i + j];
@@ -545,8 +545,9 @@ __device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, co
       J[(6 + i) * 24 + 12 + j] = -(double)E.pi.JPa[3 * i + j];
     }
   }
-  inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, lane, J, sh.E);
-  wave_lds_sync();
+  // every wave runs the chain (the same values); thread 0 stores J's blocks and e
+  inertial_edge_core(s1, s2, E.pi, (double)E.pi.dT, tid, J, sh.E);
+  __syncthreads();
   double e[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) e[k] = sh.E[k];
@@ -582,7 +583,7 @@ __device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, co
   }
   if (kBuild) {
     // W = w Omega; OJ = W J (9 x 24) into LDS, We = W e in registers
-    for (int k = lane; k < 9 * 24; k += 64) {
+    for (int k = tid; k < 9 * 24; k += NT) {
       const int r = k / 24, col = k - 24 * r;
       double v = 0;
 #pragma unroll
@@ -597,9 +598,9 @@ __device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, co
       for (int q = 0; q < 9; ++q) v += (w * sh.Info[r * 9 + q]) * e[q];
       We[r] = v;
     }
-    wave_lds_sync();
+    __syncthreads();
     double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * qcopy);
-    for (int k = lane; k < 900; k += 64) {
+    for (int k = tid; k < 900; k += NT) {
       const int p = k / 30, q = k - 30 * p;
       double v = 0;
       if (p < 24 && q < 24) {
@@ -615,8 +616,8 @@ __device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int lane, co
         if ((q >= 12 && q < 15) || (q >= 27)) v += ((p < 15) == (q < 15) ? 1.0 : -1.0) * E.pi.info_a[3 * pa + qa];
       Q[k] = v;
     }
-    if (lane < 30) {
-      const int p = lane;
+    if (tid < 30) {
+      const int p = tid;
       double g = 0;
       if (p < 24) {
 #pragma unroll
@@ -647,12 +648,12 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
     // per link: its chi2 to imu_tot[2 + l] and its form into copy 0 of imu_q
     // -- the first build's (state 0), so that build has no link work left
     // (k_lba_linearize takes the links only when every build relinearises)
-    __shared__ LinkLds lsh[kThreads / 64];
+    __shared__ LinkLds lsh;
     const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
-    const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
-    if ((int)blockIdx.x >= neb && l < a.n_imu) {
-      const double chi = lia_link<true>(a, l, threadIdx.x & 63, a.poses[0], nullptr, 0, lsh[w]);
-      if ((threadIdx.x & 63) == 0) a.imu_tot[2 + l] = chi;
+    const int l = (int)blockIdx.x - neb;
+    if (l >= 0 && l < a.n_imu) {  // (block-uniform)
+      const double chi = lia_link<true>(a, l, threadIdx.x, a.poses[0], nullptr, 0, lsh);
+      if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
     }
   }
   // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
@@ -784,13 +785,13 @@ __global__ __launch_bounds__(kThreads) void k_lba_linearize(LbaArgs a) {
   // nothing due, or the accepted trial already left this state's terms
   if (c.done || !c.need_build || (c.lin_state == c.state && !a.force_lin)) return;
   if constexpr (M == kModelImu) {
-    // blocks past the edges' build the IMU links' forms, a wave per link (launched
+    // blocks past the edges' build the IMU links' forms, a block per link (launched
     // only when every build relinearises; else k_lba_begin / k_lba_trial wrote them)
-    __shared__ LinkLds lsh[kThreads / 64];
+    __shared__ LinkLds lsh;
     const int neb = (a.n_edges + kThreads - 1) / kThreads;
     if ((int)blockIdx.x >= neb) {
-      const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
-      if (l < a.n_imu) lia_link<true>(a, l, threadIdx.x & 63, a.poses[c.state], nullptr, c.state, lsh[w]);
+      const int l = (int)blockIdx.x - neb;
+      if (l < a.n_imu) lia_link<true>(a, l, threadIdx.x, a.poses[c.state], nullptr, c.state, lsh);
       return;
     }
   }
@@ -2368,19 +2369,19 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   }
   const int i = blockIdx.x * kThreads + threadIdx.x;
   double part[3] = {0, 0, 0};  // robust chi2, landmark scale, singular landmark blocks
-  // kModelImu: blocks past the edges' take the IMU links, a wave per link, at
-  // the trial states of the LDS table (the same bits the edges use): each
+  // kModelImu: blocks past the edges' take the IMU links, a block per link,
+  // at the trial states of the LDS table (the same bits the edges use): each
   // link's chi2 to imu_tot[2 + l] and, speculatively, its form into the
   // other copy of imu_q -- in the same launch as the edges, not after them
   bool link_block = false;
   if constexpr (M == kModelImu) {
-    __shared__ LinkLds lsh[kThreads / 64];
+    __shared__ LinkLds lsh;
     const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
     if ((int)blockIdx.x >= neb) {
-      const int w = threadIdx.x >> 6, l = 4 * ((int)blockIdx.x - neb) + w;
-      if (l < a.n_imu) {
-        const double chi = lia_link<true>(a, l, threadIdx.x & 63, tposes, nullptr, s1, lsh[w]);
-        if ((threadIdx.x & 63) == 0) a.imu_tot[2 + l] = chi;
+      const int l = (int)blockIdx.x - neb;
+      if (l < a.n_imu) {  // (block-uniform)
+        const double chi = lia_link<true>(a, l, threadIdx.x, tposes, nullptr, s1, lsh);
+        if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
       }
       link_block = true;
     }
@@ -2598,8 +2599,8 @@ size_t lba_solve_work_doubles(int mode, int n_pad) {
 hipError_t lba_begin(const LbaArgs& a, hipStream_t st) {
   const dim3 g(blocks(a.n_edges > 0 ? a.n_edges : 1, kThreads));
   if (a.model == kModelImu) {
-    // the links ride in the launch: (n_imu + 3) / 4 more blocks, a wave per link
-    hipLaunchKernelGGL(k_lba_begin<kModelImu>, dim3(g.x + (a.n_imu + 3) / 4), dim3(kThreads), 0, st, a);
+    // the links ride in the launch: n_imu more blocks, a block per link
+    hipLaunchKernelGGL(k_lba_begin<kModelImu>, dim3(g.x + a.n_imu), dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_lba_begin<kModelSe3>, g, dim3(kThreads), 0, st, a);
   }
@@ -2611,9 +2612,9 @@ hipError_t lba_build(const LbaArgs& a, hipStream_t st, bool linearize) {
   // (before k_lba_sums, which closes the build: need_build = 0) kModelImu:
   // the first build's link forms come from k_lba_begin and every later
   // build's from the accepted trial; only when every build relinearises
-  // (force_lin) do the links ride in this launch, (n_imu + 3) / 4 more blocks
+  // (force_lin) do the links ride in this launch, n_imu more blocks
   const unsigned lin_blocks =
-      blocks(a.n_edges, kThreads) + (imu && a.force_lin && a.n_sys > 0 ? (a.n_imu + 3) / 4 : 0);
+      blocks(a.n_edges, kThreads) + (imu && a.force_lin && a.n_sys > 0 ? a.n_imu : 0);
   if (linearize && lin_blocks > 0) {
     if (imu)
       hipLaunchKernelGGL(k_lba_linearize<kModelImu>, dim3(lin_blocks), dim3(kThreads), 0, st, a);
@@ -2677,8 +2678,8 @@ hipError_t lba_solve_trial(const LbaArgs& a, hipStream_t st) {
   if (a.model == kModelImu) {
     if (a.n_kf > kMaxKfImuLds)
       hipLaunchKernelGGL(k_lia_trial_states, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
-    // the links ride in the trial launch: (n_imu + 3) / 4 more blocks, a wave per link
-    hipLaunchKernelGGL(k_lba_trial<kModelImu>, dim3(g.x + (a.n_imu + 3) / 4), dim3(kThreads), 0, st, a);
+    // the links ride in the trial launch: n_imu more blocks, a block per link
+    hipLaunchKernelGGL(k_lba_trial<kModelImu>, dim3(g.x + a.n_imu), dim3(kThreads), 0, st, a);
   } else {
     if (a.n_kf > kMaxKfLds)
       hipLaunchKernelGGL(k_lba_trial_poses, dim3(blocks(a.n_kf, kThreads)), dim3(kThreads), 0, st, a);
