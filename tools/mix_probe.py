@@ -2,7 +2,7 @@
 to price each part's share of the concurrent mix on one GPU.
 
     python tools/mix_probe.py [--pose on|off] [--groups 1|2] [--pipes 2]
-                              [--frames 2560] [--steps 6]
+                              [--pose-chunk N] [--frames 2560] [--steps 6]
 
 Prints {"frames_per_s": ..., ...}.  --pose off drops the PoseOptimization
 launches (extraction alone); --groups sets the pose kernel's trial groups
@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--frames", type=int, default=2560)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--pose-chunk", type=int, default=0, help="pose problems per launch (0: the whole group)")
     a = ap.parse_args()
     import torch
 
@@ -66,7 +67,10 @@ def main():
             f0 = g * Bg
             sl = slice(f0, f0 + Bg)
             if a.pose == "on":
-                opt.batch(cam, d_pin[sl], d_obs[sl], d_nobs[sl], d_pout[sl], d_out[sl], d_inl[sl], stream=s_pose)
+                ck = a.pose_chunk or Bg
+                for c0 in range(f0, f0 + Bg, ck):
+                    cs = slice(c0, c0 + ck)
+                    opt.batch(cam, d_pin[cs], d_obs[cs], d_nobs[cs], d_pout[cs], d_out[cs], d_inl[cs], stream=s_pose)
             for k, e in enumerate(pipes):
                 isl = slice(2 * (f0 + Bp * k), 2 * (f0 + Bp * (k + 1)))
                 e.extract_batch(d_imgs[isl], d_kps[isl], d_desc[isl], d_n[isl], d_mono[isl], stream=0)
@@ -79,6 +83,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(json.dumps({"frames_per_s": round(B * a.steps / el, 1), "pose": a.pose, "groups": a.groups,
+                      "pose_chunk": a.pose_chunk,
                       "pipes": P, "frames": B, "steps": a.steps}))
 
 
