@@ -423,10 +423,20 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
   }
 }
 
+// A/B switch: k_blur and k_octree held to 64 VGPRs (8 waves a SIMD), for
+// the co-residency of the concurrent pipelines' kernels
+#ifndef ORB_OCC8
+#define ORB_OCC8 0
+#endif
+#if ORB_OCC8
+#define ORB_WPE8 __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define ORB_WPE8
+#endif
 #ifndef ORB_BLUR_PF
 #define ORB_BLUR_PF 6  // (call L: 6 / 4 / 8 rows -> 68 / 62 / 73 VGPRs, 131.4k / 131.3k / 131.0k frames/s)
 #endif
-__global__ __launch_bounds__(256) void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
+__global__ __launch_bounds__(256) ORB_WPE8 void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
   constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
@@ -1114,7 +1124,7 @@ struct OctLds {
   int* knl;                          //                        node position
 };
 
-__global__ __launch_bounds__(kOctThreads) void k_octree(
+__global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
     const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
     const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
     uint32_t* __restrict__ dense, int* __restrict__ knode, uint32_t* __restrict__ oct_out,
