@@ -1688,19 +1688,6 @@ __device__ unsigned long long g_lba_stamps[16];
   } while (0)
 #endif
 
-// sum_k<16 A(k) b[k] as four interleaved 4-term FMA chains added
-// ((c0 + c1) + (c2 + c3)): a dependent v_fma_f64 costs ~14.5 cycles against
-// ~6 issued back to back, so the back substitution's 16-term dots take a
-// quarter of the chain.  One fixed order for every solve path (the LDS /
-// block / grid solves give the same x_p).
-template <class F>
-__device__ __forceinline__ double dot16(F A, const double* b) {
-  double c[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < 16; ++k) c[k & 3] = fma(A(k), b[k], c[k & 3]);
-  return (c[0] + c[1]) + (c[2] + c[3]);
-}
-
 template <bool kLds>
 __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
   extern __shared__ double smem[];
@@ -2037,13 +2024,18 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_solve(LbaArgs a) {
     for (int K = T - 1; K >= 0; --K) {
       const int k0 = 16 * K;
       double s = 0;
-      if (lane < 16) s = dot16([&](int k) { return Li[(size_t)K * kTileSz + k * kTileLd + lane]; }, y + k0);
+      if (lane < 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) s = fma(Li[(size_t)K * kTileSz + k * kTileLd + lane], y[k0 + k], s);
+      }
       wave_lds_sync();  // every read of y_K before the writes
       if (lane < 16) y[k0 + lane] = s;
       wave_lds_sync();
       for (int r = lane; r < k0; r += 64) {
-        const double* const tk = tile(K, r >> 4) + (r & 15);
-        y[r] -= dot16([&](int k) { return tk[k * TS]; }, y + k0);
+        double u = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) u = fma(tile(K, r >> 4)[k * TS + (r & 15)], y[k0 + k], u);
+        y[r] -= u;
       }
       wave_lds_sync();
     }
@@ -2233,13 +2225,20 @@ __global__ __launch_bounds__(kSolveThreads) void k_lba_ldl_back(LbaArgs a) {
   for (int K = T - 1; K >= 0; --K) {
     const int k0 = 16 * K;
     if (t < 16) {
-      const double s = dot16([&](int k) { return h.Li[(size_t)K * kTileSz + k * kTileLd + t]; }, y + k0);
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s = fma(h.Li[(size_t)K * kTileSz + k * kTileLd + t], y[k0 + k], s);
       __builtin_amdgcn_wave_barrier();
       y[k0 + t] = s;
     }
     __syncthreads();
     const double* const rowK = h.S + (size_t)k0 * LD;
-    for (int r = t; r < k0; r += kSolveThreads) y[r] -= dot16([&](int k) { return rowK[k * LD + r]; }, y + k0);
+    for (int r = t; r < k0; r += kSolveThreads) {
+      double s = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s = fma(rowK[k * LD + r], y[k0 + k], s);
+      y[r] -= s;
+    }
     __syncthreads();
   }
   const double* src = a.sys;
