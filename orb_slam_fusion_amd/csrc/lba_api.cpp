@@ -363,7 +363,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     pbx[x] = (int)(std::lower_bound(cnt.begin(), cnt.end() - 1, (int)((long long)x * ne / sc_split)) - cnt.begin());
   LBA_HOST_PHASE(4);
   const std::vector<int>& gidx = perm;  // shard edge -> caller's edge index
-  // IMU links incident to each free key frame (link order)
+  // IMU links incident to each free key frame (link order), one record each:
+  // {link, the key frame's side (0: kf1), the other key frame's free index
+  // (-1: fixed), its side}
   std::vector<int> inc(nf + 1, 0), inc_list;
   if (imu) {
     std::vector<std::vector<int>> lists(nf);
@@ -372,7 +374,10 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
         if (hidx[k] >= 0) lists[hidx[k]].push_back(l);
     for (int f = 0; f < nf; ++f) {
       inc[f + 1] = inc[f] + (int)lists[f].size();
-      inc_list.insert(inc_list.end(), lists[f].begin(), lists[f].end());
+      for (int l : lists[f]) {
+        const int sr = hidx[m.imu[l].kf1] == f ? 0 : 1;
+        inc_list.insert(inc_list.end(), {l, sr, hidx[sr ? m.imu[l].kf1 : m.imu[l].kf2], 1 - sr});
+      }
     }
   }
 
@@ -386,7 +391,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + kSumsQ * (long)nf + 1 +
                     (imu ? ((long)n * n + n + 255) / 256 + m.n_imu : 0);  // (+ the trial's link blocks)
   const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
-                        F + (nf + 1) + std::max(inc_list.size(), (size_t)1) + E;
+                        F + (nf + 1) + std::max(inc_list.size(), (size_t)4) + E;
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order
   const size_t n_sc = (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1) +
                       (size_t)nf * (sc_split + 1);
@@ -459,7 +464,8 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   LBA_HOST_PHASE(7);
   int* I = reinterpret_cast<int*>(U + u_ints);
   int* I_slot = I;  // int4 records first (16-B aligned)
-  int* I_hidx = I_slot + 4 * E;
+  int* I_incl = I_slot + 4 * E;  // int4 link records
+  int* I_hidx = I_incl + std::max(inc_list.size(), (size_t)4);
   int* I_pt = I_hidx + n_kf;
   int* I_pb = I_pt + (np + 1);
   int* I_ef = I_pb + (nf + 1);
@@ -467,8 +473,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   int* I_pj = I_pi + std::max(n_pairs, 1);
   int* I_fk = I_pj + std::max(n_pairs, 1);
   int* I_inc = I_fk + F;
-  int* I_incl = I_inc + (nf + 1);
-  int* I_es = I_incl + std::max(inc_list.size(), (size_t)1);
+  int* I_es = I_inc + (nf + 1);
   std::copy(hidx.begin(), hidx.end(), I_hidx);
   std::copy(cnt.begin(), cnt.end(), I_pt);
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
@@ -631,7 +636,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     a.imu = reinterpret_cast<const LiaImuDev*>(A + u_imu);
     a.free_kf = dI + (I_fk - I);
     a.imu_inc = dI + (I_inc - I);
-    a.imu_inc_list = dI + (I_incl - I);
+    a.imu_inc_rec = reinterpret_cast<const int4*>(dI + (I_incl - I));
     a.imu_q = dp(c_imuq);
     a.himu = dp(c_himu);
     a.imu_tot = dp(c_itot);

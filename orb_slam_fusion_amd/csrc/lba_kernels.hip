@@ -816,18 +816,15 @@ __device__ __forceinline__ void lia_assemble_entry(const LbaArgs& a, int state, 
   const int cc = grad ? 0 : (int)(idx - (long)r * n);
   const int fr = r / kImuDim, dr = r - kImuDim * fr;
   const int fc = cc / kImuDim, dc = cc - kImuDim * fc;
-  const int kr = a.free_kf[fr], kc = a.free_kf[fc];
   double v = 0;
   for (int j = a.imu_inc[fr]; j < a.imu_inc[fr + 1]; ++j) {
-    const int l = a.imu_inc_list[j];
-    const int k1 = a.imu[l].kf1, k2 = a.imu[l].kf2;
-    const int sr = k1 == kr ? 0 : 1;
-    const double* Q = a.imu_q + (size_t)kImuPairQ * (l + (size_t)a.n_imu * state);
+    const int4 rec = a.imu_inc_rec[j];  // {link, fr's side, the other's free index, its side}
+    const double* Q = a.imu_q + (size_t)kImuPairQ * (rec.x + (size_t)a.n_imu * state);
     if (grad) {
-      v += Q[900 + kImuDim * sr + dr];
+      v += Q[900 + kImuDim * rec.y + dr];
     } else {
-      const int sc = k1 == kc ? 0 : (k2 == kc ? 1 : -1);
-      if (sc >= 0) v += Q[(kImuDim * sr + dr) * 30 + kImuDim * sc + dc];
+      const int sc = fc == fr ? rec.y : (rec.z == fc ? rec.w : -1);
+      if (sc >= 0) v += Q[(kImuDim * rec.y + dr) * 30 + kImuDim * sc + dc];
     }
   }
   a.himu[idx] = v;

@@ -157,7 +157,7 @@ struct LbaArgs {
   const LiaImuDev* imu;      // [n_imu]
   const int* free_kf;        // [n_free] key frame of each free index
   const int* imu_inc;        // [n_free + 1] CSR of the links incident to a free key frame,
-  const int* imu_inc_list;   //   link ids ascending
+  const int4* imu_inc_rec;   //   link order: {link, its side, the other's free index (-1 fixed), side}
   double* imu_q;             // 2 x [n_imu * kImuPairQ] (one copy per LM state) per link: form over
                              //   (kf1 dims, kf2 dims) + gradient
   double* himu;              // [n_sys^2 + n_sys] the links' part of the camera system | gradient
