@@ -29,12 +29,18 @@ def harness(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("shuffle", [False, True])
-def test_lba_host_path_under_asan(harness, shuffle):
+@pytest.mark.parametrize("shuffle,lia", [(False, False), (True, False), (False, True)])
+def test_lba_host_path_under_asan(harness, shuffle, lia):
+    """lia: then the LocalInertialBA layout on the same graph (link records,
+    zero iterations: the explicit results launch)."""
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
     if shuffle:
         env["SHUFFLE"] = "1"
+    if lia:
+        env["LIA"] = "1"
     r = subprocess.run([str(harness), "3"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["edges"] == 18000
+    lines = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert lines[0]["edges"] == 18000
+    if lia:
+        assert lines[1]["lia_status"] == 0

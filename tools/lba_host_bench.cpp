@@ -94,6 +94,40 @@ int main(int argc, char** argv) {
               tot / reps);
   for (int k = 1; k <= 10; ++k) std::printf("%s%.1f", k > 1 ? ", " : "", g_host_phase_us[k] / reps);
   std::printf("]}\n");
+  if (std::getenv("LIA")) {
+    // the LocalInertialBA layout on the same graph: 12 free key frames with
+    // IMU, 8 fixed, a link between consecutive key frames (the last flagged
+    // robust + downweighted), iterations = 0 (the explicit results launch)
+    std::vector<orbgpu_imu_state> ks(n_kf);
+    for (auto& k : ks) {
+      std::memset(&k, 0, sizeof(k));
+      k.Rwb[0] = k.Rwb[4] = k.Rwb[8] = 1.f;
+      k.Rcw[0] = k.Rcw[4] = k.Rcw[8] = 1.f;
+    }
+    std::vector<uint8_t> lfixed(n_kf, 0), has_imu(n_kf, 1), close(n_pts, 0);
+    for (int k = 12; k < n_kf; ++k) lfixed[k] = 1;
+    std::vector<orbgpu_lia_imu_edge> links;
+    for (int k = 1; k < 13; ++k) {
+      orbgpu_lia_imu_edge l;
+      std::memset(&l, 0, sizeof(l));
+      l.kf1 = k;
+      l.kf2 = k - 1;
+      l.flags = k == 12 ? (ORBGPU_LIA_ROBUST | ORBGPU_LIA_DOWNWEIGHT) : 0;
+      l.preint.dT = 0.2f;
+      links.push_back(l);
+    }
+    orbgpu_imu_calib cal;
+    std::memset(&cal, 0, sizeof(cal));
+    std::vector<orbgpu_imu_state> ko(n_kf);
+    std::vector<double> kd(21 * n_kf);
+    double ls[7];
+    const orbgpu_status r = orbgpu_lia_optimize(h, &cal, n_kf, ks.data(), lfixed.data(), has_imu.data(), n_pts,
+                                                pts.data(), close.data(), (int)edges.size(), edges.data(),
+                                                (int)links.size(), links.data(), 0, 1e-2, ko.data(), kd.data(),
+                                                xo.data(), out.data(), ls);
+    std::printf("{\"lia_status\": %d}\n", (int)r);
+    if (r != ORBGPU_OK) return 2;
+  }
   orbgpu_lba_ctx_destroy(h);
   return 0;
 }
