@@ -662,7 +662,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
       }
       if (stop_flag) hw->stop = *stop_flag ? 1u : 0u;
       if (issued - (int)(p & 0xffffffffu) < kAhead) {
-        if (lba_step(a, st, issued == 0 || a.force_lin) != hipSuccess) return ORBGPU_ERR_DEVICE;
+        if (lba_step(a, st, a.force_lin) != hipSuccess) return ORBGPU_ERR_DEVICE;  // (state 0: k_lba_begin)
         ++issued;
         trace_steps = issued;
       } else {

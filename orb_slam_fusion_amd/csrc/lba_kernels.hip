@@ -393,7 +393,7 @@ __device__ void ctl_init(const LbaArgs& a, double chi, int stop) {
   c.iters_done = 0;
   c.trials = 0;
   c.need_build = 1;
-  c.lin_state = -1;
+  c.lin_state = 0;  // k_lba_begin wrote state 0's per-edge terms
   c.stopped = stop;
   // SparseOptimizer::optimize: for (i < iterations && !terminate() ...)
   c.done = (c.max_iters <= 0 || stop) ? 1 : 0;
@@ -639,63 +639,6 @@ __device__ __forceinline__ double lia_link(const LbaArgs& a, int l, int tid, con
   return (rho0 + cg) + ca;
 }
 
-template <int M>
-__global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
-  __shared__ double red[4];
-  const int i = blockIdx.x * kThreads + threadIdx.x;
-  if constexpr (M == kModelImu) {
-    // blocks past the edges' take the IMU links at the initial state, a wave
-    // per link: its chi2 to imu_tot[2 + l] and its form into copy 0 of imu_q
-    // -- the first build's (state 0), so that build has no link work left
-    // (k_lba_linearize takes the links only when every build relinearises)
-    __shared__ LinkLds lsh;
-    const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
-    const int l = (int)blockIdx.x - neb;
-    if (l >= 0 && l < a.n_imu) {  // (block-uniform)
-      const double chi = lia_link<true>(a, l, threadIdx.x, a.poses[0], nullptr, 0, lsh);
-      if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
-    }
-  }
-  // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
-  // which get no Schur terms) stay zero: clear it once per call
-  for (size_t k = i, nz = (size_t)a.n_sys * a.n_sys + 2 * (size_t)a.n_sys; k < nz;
-       k += (size_t)gridDim.x * kThreads)
-    a.sys[k] = 0.0;
-  double r0 = 0;
-  if (i < a.n_edges) {
-    const LbaEdgeDev e = a.edges[i];
-    const double* x = a.pts[0] + 3 * e.point;
-    const double X[3] = {x[0], x[1], x[2]};
-    double err[3];
-    vis_error<M>(a, e, a.poses[0] + a.pstride * e.kf, X, err);
-    a.err[3 * i] = err[0];
-    a.err[3 * i + 1] = err[1];
-    a.err[3 * i + 2] = err[2];
-    double w;
-    huber_rho(lba_chi2(e, err), lba_delta(e), r0, w);
-  }
-  double v[1] = {r0};
-  block_sum<1>(v, red);
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = v[0];
-  if (!last_block(a.counter + 0)) return;
-  double s[1];
-  sum_partials<1>(a.partials, gridDim.x, s, red);
-  if (threadIdx.x == 0) {
-    if (M == kModelImu) {  // the IMU links at the initial state (this launch's link waves), in link order
-      double tot = 0;
-      for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
-      s[0] += tot;
-    }
-    const int stop = host_stop(a);
-    if (a.sharded) {
-      a.red[0] = s[0];
-      a.red[1] = stop;
-    } else {
-      ctl_init(a, s[0], stop);
-    }
-  }
-}
-
 // ---- buildSystem, edge side: Jacobians at the current state and each
 // edge's terms of Hll / bl (point), Hpl and Hpp / bp (free pose)
 // (base_binary_edge.hpp:56-119 with the robust weight of base_edge.h:91-97).
@@ -777,6 +720,69 @@ __device__ __forceinline__ void lin_edge(const LbaArgs& a, const LbaEdgeDev& e, 
   double* hplo = L.hpl + 18 * (size_t)i;
 #pragma unroll
   for (int k = 0; k < 18; ++k) hplo[k] = hpl[k];
+}
+
+// computeActiveErrors at the initial state, the robust chi2 and the LM's
+// start (ctl_init), the first build's per-edge terms, the system cleared;
+// kModelImu: the links' chi2 and forms
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
+  __shared__ double red[4];
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if constexpr (M == kModelImu) {
+    // blocks past the edges' take the IMU links at the initial state, a wave
+    // per link: its chi2 to imu_tot[2 + l] and its form into copy 0 of imu_q
+    // -- the first build's (state 0), so that build has no link work left
+    // (k_lba_linearize takes the links only when every build relinearises)
+    __shared__ LinkLds lsh;
+    const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
+    const int l = (int)blockIdx.x - neb;
+    if (l >= 0 && l < a.n_imu) {  // (block-uniform)
+      const double chi = lia_link<true>(a, l, threadIdx.x, a.poses[0], nullptr, 0, lsh);
+      if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
+    }
+  }
+  // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
+  // which get no Schur terms) stay zero: clear it once per call
+  for (size_t k = i, nz = (size_t)a.n_sys * a.n_sys + 2 * (size_t)a.n_sys; k < nz;
+       k += (size_t)gridDim.x * kThreads)
+    a.sys[k] = 0.0;
+  double r0 = 0;
+  if (i < a.n_edges) {
+    const LbaEdgeDev e = a.edges[i];
+    const double* x = a.pts[0] + 3 * e.point;
+    const double X[3] = {x[0], x[1], x[2]};
+    double err[3];
+    vis_error<M>(a, e, a.poses[0] + a.pstride * e.kf, X, err);
+    a.err[3 * i] = err[0];
+    a.err[3 * i + 1] = err[1];
+    a.err[3 * i + 2] = err[2];
+    double w;
+    huber_rho(lba_chi2(e, err), lba_delta(e), r0, w);
+    // the first build's per-edge terms (state 0, these errors: what
+    // k_lba_linearize would compute), so no step needs a linearize launch
+    lin_edge<M>(a, e, i, a.poses[0] + a.pstride * e.kf, X, err, lin_of(a, 0));
+  }
+  double v[1] = {r0};
+  block_sum<1>(v, red);
+  if (threadIdx.x == 0) a.partials[blockIdx.x] = v[0];
+  if (!last_block(a.counter + 0)) return;
+  double s[1];
+  sum_partials<1>(a.partials, gridDim.x, s, red);
+  if (threadIdx.x == 0) {
+    if (M == kModelImu) {  // the IMU links at the initial state (this launch's link waves), in link order
+      double tot = 0;
+      for (int k = 0; k < a.n_imu; ++k) tot += a.imu_tot[2 + k];
+      s[0] += tot;
+    }
+    const int stop = host_stop(a);
+    if (a.sharded) {
+      a.red[0] = s[0];
+      a.red[1] = stop;
+    } else {
+      ctl_init(a, s[0], stop);
+    }
+  }
 }
 
 template <int M>
