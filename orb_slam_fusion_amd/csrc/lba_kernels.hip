@@ -998,30 +998,13 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   }
   if (threadIdx.x == 0) a.partials[blockIdx.x] = hmax;
   if (!last_block(a.counter + 1)) return;
-  // each pose's quarters in order -> Hpp (6 x 6 full), bp, the pose
-  // diagonal; four entries a thread with every load in flight before the
-  // first sum (the loop's stores would otherwise hold each round's loads)
-  constexpr int kQU = 4;
-  for (int base = 0; base < 27 * a.n_free; base += kQU * kThreads) {
-  double qv[kQU][kSumsQ];
-#pragma unroll
-  for (int u = 0; u < kQU; ++u) {
-    const int idx = base + u * kThreads + threadIdx.x;
-    if (idx < 27 * a.n_free) {
-      const int f = idx / 27, k = idx - 27 * f;
-      const double* pp = a.pose_part + 27 * (size_t)kSumsQ * f + k;
-#pragma unroll
-      for (int q = 0; q < kSumsQ; ++q) qv[u][q] = pp[27 * q];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kQU; ++u) {
-    const int idx = base + u * kThreads + threadIdx.x;
-    if (idx >= 27 * a.n_free) continue;
+  // each pose's quarters in order -> Hpp (6 x 6 full), bp, the pose diagonal
+  for (int idx = threadIdx.x; idx < 27 * a.n_free; idx += kThreads) {
     const int f = idx / 27, k = idx - 27 * f;
+    const double* pp = a.pose_part + 27 * (size_t)kSumsQ * f + k;
     double v = 0;
 #pragma unroll
-    for (int q = 0; q < kSumsQ; ++q) v += qv[u][q];
+    for (int q = 0; q < kSumsQ; ++q) v += pp[27 * q];
     if (k < 21) {
       int s2 = 0, q2 = k;  // lower-triangle index k -> (s2, q2)
       while (q2 > s2) {
@@ -1034,7 +1017,6 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
     } else {
       a.bp[6 * (size_t)f + (k - 21)] = v;
     }
-  }
   }
   __syncthreads();
   // the maxima only feed computeLambdaInit (the first build): later builds
