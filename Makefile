@@ -43,6 +43,20 @@ $(LIB)/liborbgpu_varB.so: $(VARB_OBJS)
 
 varB: $(LIB)/liborbgpu_varB.so
 
+# debug variant: every wave-uniform branch (uniform_dev.h) checks that all
+# active lanes agree; orbgpu_debug_uniform_violations() reports the count
+# (tests/conftest.py asserts zero after each test when this library is loaded:
+# ORBGPU_LIB=orb_slam_fusion_amd/lib/liborbgpu_checkuniform.so pytest -m gpu)
+$(OBJDIR)/cu/%.o: $(CSRC)/% $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)/cu
+	$(HIPCC) $(HIPFLAGS) -DORBGPU_CHECK_UNIFORM=1 -c -o $@ $<
+
+CU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/cu/%.o,$(GPU_SRCS))
+$(LIB)/liborbgpu_checkuniform.so: $(CU_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
+
+checkuniform: $(LIB)/liborbgpu_checkuniform.so
+
 # ad-hoc A/B variant of the extractor kernels (orb_kernels.hip compiled with
 # DEFS, every other object shared): make var NAME=pf4 DEFS=-DORB_BLUR_PF=4
 var: $(GPU_OBJS)
@@ -79,4 +93,4 @@ stamps:
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
 
-.PHONY: varB var all oracle clean stamps
+.PHONY: varB var all oracle clean stamps checkuniform

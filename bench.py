@@ -178,7 +178,7 @@ def main() -> int:
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the synthetic-sequence (C5 layout) side line")
     ap.add_argument("--no-lba-sharded", action="store_true",
-                    help="skip the 2-rank point-sharded LBA side line")
+                    help="skip the 4-rank point-sharded LBA side line")
     args = ap.parse_args()
 
     import torch

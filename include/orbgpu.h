@@ -69,6 +69,25 @@ int orbgpu_extractor_levels(const orbgpu_extractor* h);
 #define ORBGPU_RESIZE_SCALAR 1
 orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode);
 
+/* Where DistributeOctTree's node list lives (orb_extractor.cc:542-742; the
+ * reference's std::list has no bound, and neither does its per-level budget,
+ * :432-444).  ORBGPU_OCTREE_NODES_AUTO (default): in LDS whenever the plan's
+ * node capacity fits a workgroup's 160 KB, else in HBM -- every num_features
+ * the reference accepts, e.g. OrbExtractor(5 * nFeatures, ...) at
+ * tracking.cc:202-204,811-813.  ORBGPU_OCTREE_NODES_HBM: always in HBM (same
+ * results; the test switch for the large-plan path).  Re-plans the handle. */
+#define ORBGPU_OCTREE_NODES_AUTO 0
+#define ORBGPU_OCTREE_NODES_HBM 1
+orbgpu_status orbgpu_extractor_set_octree_nodes(orbgpu_extractor* h, int mode);
+
+/* Host-only plan probe (no device call): whether (params, width x height) is
+ * a geometry the extractor accepts (ORBGPU_OK) -- every one whose pyramid
+ * levels hold the FAST grid (orb_extractor.cc:748-760: a level narrower than
+ * 2 * 16 + 35 px divides by a zero cell count in the reference) -- with the
+ * per-image keypoint slots and whether the octree nodes go to HBM. */
+orbgpu_status orbgpu_extractor_plan(const orbgpu_orb_params* params, int width, int height,
+                                    int* kp_slots, int* octree_hbm);
+
 /* Upper bound on keypoints one image can produce at the given geometry. */
 int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height);
 

@@ -113,12 +113,15 @@ class OracleExtractor:
         img = np.ascontiguousarray(img, np.uint8)
         h, w = img.shape
         cap = 8192
-        kps = np.zeros(cap, KEYPOINT_DTYPE)
-        desc = np.zeros((cap, 32), np.uint8)
-        n = ctypes.c_int()
-        mono = lib().orc_extract(self._h, _p(img), w, h, w, int(lapping[0]), int(lapping[1]),
-                                 _p(kps), _p(desc), cap, ctypes.byref(n))
-        assert n.value <= cap
+        while True:  # n is reported even when it exceeds cap: run again with room for it
+            kps = np.zeros(cap, KEYPOINT_DTYPE)
+            desc = np.zeros((cap, 32), np.uint8)
+            n = ctypes.c_int()
+            mono = lib().orc_extract(self._h, _p(img), w, h, w, int(lapping[0]), int(lapping[1]),
+                                     _p(kps), _p(desc), cap, ctypes.byref(n))
+            if n.value <= cap:
+                break
+            cap = n.value
         return mono, kps[: n.value].copy(), desc[: n.value].copy()
 
     def params(self):

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_bow_assemble(BowLaunch a) {
   int pos = block_excl_scan(cnt, tmp, &n_words);
   uint32_t* bw = a.bow_words + o;
   double* bwt = a.bow_weights + o;
-  double wsum[16];  // per <= 16 (m <= 4096)
+  double wsum[32];  // per <= 32 (m <= kBowMaxFeatures = 8192)
   int nh = 0;
   for (int i = b; i < e; ++i) {
     if (!head(i)) continue;

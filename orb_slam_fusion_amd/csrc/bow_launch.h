@@ -7,7 +7,7 @@
 
 namespace orbgpu {
 
-constexpr int kBowMaxFeatures = 4096;  // per frame (LDS sort of the assembly)
+constexpr int kBowMaxFeatures = 8192;  // per frame (LDS sort of the assembly: 16 B a feature, 128 KB)
 
 struct VocabDev {
   const uint8_t* desc;       // [n_nodes][32]

@@ -7,6 +7,7 @@
 // (fp64 solver TUs, parity by tolerance).
 #pragma once
 #include "f64_math_dev.h"
+#include "uniform_dev.h"
 #include <hip/hip_runtime.h>
 
 #include "../../include/orbgpu.h"
@@ -97,7 +98,7 @@ __device__ __forceinline__ void exp_so3(const double* w, double* R) {
   m3_hat(w, W);
   m3_mul(W, W, WW);
   double s, c;
-  auto uni = [](bool b) { return kUniform ? __builtin_amdgcn_readfirstlane(b ? 1 : 0) != 0 : b; };
+  auto uni = [](bool b) { return kUniform ? uniform_branch(b ? 1 : 0) != 0 : b; };
   if (uni(d < 1e-5)) {
     s = 1.0;
     c = 0.5;
@@ -124,10 +125,10 @@ __device__ __forceinline__ void log_so3(const double* R, double* w) {
   w[1] = (R[2] - R[6]) / 2;
   w[2] = (R[3] - R[1]) / 2;
   const double ct = (t - 1.0) * 0.5;
-  if (__builtin_amdgcn_readfirstlane(ct > 1 || ct < -1 ? 1 : 0)) return;
+  if (uniform_branch(ct > 1 || ct < -1 ? 1 : 0)) return;
   const double th = acos(ct);
   const double s = sin(th);
-  if (__builtin_amdgcn_readfirstlane(fabs(s) < 1e-5 ? 1 : 0)) return;
+  if (uniform_branch(fabs(s) < 1e-5 ? 1 : 0)) return;
   const double f = div_by(th, recip_f64(s));  // |s| >= 1e-5 here
   w[0] *= f;
   w[1] *= f;
@@ -141,12 +142,12 @@ __device__ __forceinline__ void right_j(const double* v, double* J) {
   const double d = sqrt(d2);
 #pragma unroll
   for (int i = 0; i < 9; ++i) J[i] = i % 4 == 0 ? 1.0 : 0.0;
-  if (__builtin_amdgcn_readfirstlane(d < 1e-5 ? 1 : 0)) return;
+  if (uniform_branch(d < 1e-5 ? 1 : 0)) return;
   double W[9], WW[9];
   m3_hat(v, W);
   m3_mul(W, W, WW);
   double a, b;
-  if (__builtin_amdgcn_readfirstlane(d2 < kSeriesD2 ? 1 : 0)) {
+  if (uniform_branch(d2 < kSeriesD2 ? 1 : 0)) {
     // the coefficients' Taylor series in d^2 (truncation < 1e-20 below 0.05)
     if (kInv) {  // 1/d^2 - (1 + cos d) / (2 d sin d)
       a = 0.5;
@@ -181,7 +182,7 @@ __device__ __forceinline__ void delta_rotation(const orbgpu_imu_preint& p, const
   for (int i = 0; i < 3; ++i) w[i] = p.JRg[3 * i] * dbg[0] + p.JRg[3 * i + 1] * dbg[1] + p.JRg[3 * i + 2] * dbg[2];
   const float th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   float imag, real;
-  if (__builtin_amdgcn_readfirstlane(th2 < 1e-5f * 1e-5f ? 1 : 0)) {
+  if (uniform_branch(th2 < 1e-5f * 1e-5f ? 1 : 0)) {
     const float po4 = th2 * th2;
     imag = 0.5f - (float)(1.0 / 48.0) * th2 + (float)(1.0 / 3840.0) * po4;
     real = 1.f - (float)(1.0 / 8.0) * th2 + (float)(1.0 / 384.0) * po4;

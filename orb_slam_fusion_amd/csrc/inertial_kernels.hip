@@ -1144,3 +1144,5 @@ extern "C" int orbgpu_debug_inertial_stamps(unsigned long long* out, int n) {
   return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_in_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+ORBGPU_UNIFORM_READER(inertial)

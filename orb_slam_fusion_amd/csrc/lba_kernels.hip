@@ -1493,7 +1493,7 @@ __global__ __launch_bounds__(64) void k_lba_schur_sum(LbaArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) sum += v[u];
-      if (__builtin_amdgcn_readfirstlane(past ? 1 : 0)) break;
+      if (uniform_branch(past ? 1 : 0)) break;
     }
     if (past) break;
   }
@@ -2728,3 +2728,5 @@ hipError_t lba_classify(const LbaArgs& a, uint8_t* outlier, double* out, void* c
 }
 
 }  // namespace orbgpu
+
+ORBGPU_UNIFORM_READER(lba)

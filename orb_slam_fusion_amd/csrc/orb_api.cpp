@@ -46,6 +46,7 @@ struct orbgpu_extractor {
   HostPlan plan;
   int plan_w = -1, plan_h = -1;
   int resize_rounding = ORBGPU_RESIZE_SSE;
+  int octree_nodes = ORBGPU_OCTREE_NODES_AUTO;
   PlanHeader* d_plan = nullptr;
   Cell* d_cells = nullptr;
   int* d_rs = nullptr;
@@ -56,6 +57,8 @@ struct orbgpu_extractor {
   uint8_t *d_pyr = nullptr, *d_blur = nullptr;
   uint32_t *d_slots = nullptr, *d_dense = nullptr, *d_oct_out = nullptr;
   int *d_cell_count = nullptr, *d_knode = nullptr, *d_oct_count = nullptr;
+  uint8_t* d_oct_nodes = nullptr;  // octree node arrays of HBM-node plans (per (image, level) block)
+  size_t ws_nodes = 0;
   float* d_angle = nullptr;
   uint64_t* d_desc = nullptr;
   int* d_err = nullptr;
@@ -149,7 +152,7 @@ orbgpu_status ensure_plan(orbgpu_extractor* h, int w, int ht) {
   drop_graphs(h);
   std::string why;
   HostPlan p;
-  if (!make_plan(h->params, w, ht, p, why, h->resize_rounding)) return ORBGPU_ERR_INVALID;
+  if (!make_plan(h->params, w, ht, p, why, h->resize_rounding, h->octree_nodes)) return ORBGPU_ERR_INVALID;
   if (p.cells.size() > h->cells_cap) {
     dfree(h->d_cells);
     if (dalloc(&h->d_cells, p.cells.size()) != hipSuccess) return ORBGPU_ERR_NOMEM;
@@ -207,6 +210,14 @@ orbgpu_status ensure_workspace(orbgpu_extractor* h, int n) {
     if (dalloc(&h->d_cell_count, cells)) return ORBGPU_ERR_NOMEM;
     h->ws_cells = cells;
   }
+  if (P.oct_hbm_nodes) {
+    const size_t nodes = (size_t)n * P.levels * oct_node_bytes(P.node_cap);
+    if (nodes > h->ws_nodes) {
+      dfree(h->d_oct_nodes);
+      if (dalloc(&h->d_oct_nodes, nodes)) return ORBGPU_ERR_NOMEM;
+      h->ws_nodes = nodes;
+    }
+  }
   if (kp > h->ws_kp) {
     dfree(h->d_oct_out);
     dfree(h->d_angle);
@@ -253,6 +264,7 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   a.angle = h->d_angle;
   a.desc = h->d_desc;
   a.octree_lds = octree_lds_bytes(h->plan.hdr);
+  a.oct_nodes = h->plan.hdr.oct_hbm_nodes ? h->d_oct_nodes : nullptr;
   a.lap0 = lap ? lap[0] : 0;
   a.lap1 = lap ? lap[1] : 0;
   a.kps_out = kps;
@@ -323,6 +335,7 @@ static bool same_launch(const ExtractLaunch& x, const ExtractLaunch& y) {
          x.slots == y.slots && x.cell_count == y.cell_count && x.dense == y.dense &&
          x.knode == y.knode && x.oct_out == y.oct_out && x.oct_count == y.oct_count &&
          x.angle == y.angle && x.desc == y.desc && x.octree_lds == y.octree_lds &&
+         x.oct_nodes == y.oct_nodes &&
          x.lap0 == y.lap0 && x.lap1 == y.lap1 && x.kps_out == y.kps_out &&
          x.desc_out == y.desc_out && x.cap == y.cap && x.n_out == y.n_out &&
          x.mono_out == y.mono_out && x.err == y.err && x.n_cu == y.n_cu && x.events == y.events &&
@@ -433,6 +446,7 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_cell_count);
   dfree(h->d_oct_out);
   dfree(h->d_oct_count);
+  dfree(h->d_oct_nodes);
   dfree(h->d_angle);
   dfree(h->d_desc);
   dfree(h->d_err);
@@ -476,6 +490,28 @@ orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode
   const int w = h->plan_w, ht = h->plan_h;
   h->plan_w = h->plan_h = -1;  // re-plan (and retire captured graphs) with the new column split
   return ensure_plan(h, w, ht);
+}
+
+orbgpu_status orbgpu_extractor_set_octree_nodes(orbgpu_extractor* h, int mode) {
+  if (!h || (mode != ORBGPU_OCTREE_NODES_AUTO && mode != ORBGPU_OCTREE_NODES_HBM)) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (h->stream && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (mode == h->octree_nodes) return ORBGPU_OK;
+  h->octree_nodes = mode;
+  const int w = h->plan_w, ht = h->plan_h;
+  h->plan_w = h->plan_h = -1;  // re-plan; ensure_workspace sizes the node range on the next call
+  return ensure_plan(h, w, ht);
+}
+
+orbgpu_status orbgpu_extractor_plan(const orbgpu_orb_params* params, int width, int height,
+                                    int* kp_slots, int* octree_hbm) {
+  if (!params) return ORBGPU_ERR_INVALID;
+  HostPlan p;
+  std::string why;
+  if (!make_plan(*params, width, height, p, why)) return ORBGPU_ERR_INVALID;
+  if (kp_slots) *kp_slots = p.hdr.kp_slots;
+  if (octree_hbm) *octree_hbm = p.hdr.oct_hbm_nodes;
+  return ORBGPU_OK;
 }
 
 int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height) {
@@ -671,7 +707,7 @@ orbgpu_status orbgpu_stereo_match_batch(orbgpu_extractor* h, int n_frames, const
                                         float bf, float mb, float* d_uright, float* d_depth,
                                         void* hip_stream) {
   if (!h || n_frames <= 0 || !d_imgs || !d_kps || !d_descs || !d_n || !d_uright || !d_depth ||
-      cap_per_image <= 0 || cap_per_image > 4096 || !(mb > 0.0f))
+      cap_per_image <= 0 || cap_per_image > 65535 || !(mb > 0.0f))  // u16 row lists
     return ORBGPU_ERR_INVALID;
   if (h->plan_w < 0 || h->ws_images < 2 * n_frames) return ORBGPU_ERR_INVALID;  // no batch yet
   if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;

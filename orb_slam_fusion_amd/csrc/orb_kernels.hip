@@ -1102,7 +1102,7 @@ __device__ __forceinline__ void run_add(int* cnt, int key) {
   if (head && key >= 0) {
     const uint64_t after = lane == 63 ? 0ull : (heads >> (lane + 1));
     const int len = after ? __builtin_ctzll(after) + 1 : 64 - lane;
-    atomicAdd(&cnt[key], len);
+    __hip_atomic_fetch_add(&cnt[key], len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -1124,11 +1124,20 @@ struct OctLds {
   int* knl;                          //                        node position
 };
 
+// kHbm: the node arrays (oct_node_bytes(NC) per block) live in a per-block
+// HBM range instead of LDS -- plans whose node capacity does not fit the
+// 160 KB (num_features of several thousand: the reference's
+// OrbExtractor(5 * nFeatures, ...), tracking.cc:202-204).  Same code, same
+// order; the counters' atomics are workgroup-scoped (the block's waves share
+// one CU and its L1, so the barriers order them like LDS).  Only the scan
+// scratch, the block scalars and the first kcap candidates stay in LDS.
+template <bool kHbm>
 __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
     const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
     const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
     uint32_t* __restrict__ dense, int* __restrict__ knode, uint32_t* __restrict__ oct_out,
-    int* __restrict__ oct_count, int* __restrict__ err, int n_img, int kcap) {
+    int* __restrict__ oct_count, int* __restrict__ err, int n_img, int kcap,
+    uint8_t* __restrict__ node_ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
   const int L = P->levels;
   // level-major block order: the (largest) level-0 blocks are dispatched first
@@ -1140,7 +1149,8 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
 
   OctLds s;
   {
-    unsigned long long* p64 = reinterpret_cast<unsigned long long*>(lds_raw);
+    uint8_t* nodes = kHbm ? node_ws + (size_t)blockIdx.x * oct_node_bytes(NC) : lds_raw;
+    unsigned long long* p64 = reinterpret_cast<unsigned long long*>(nodes);
     s.best = p64;
     int* p = reinterpret_cast<int*>(p64 + NC);
     int** fields[] = {&s.x0, &s.y0, &s.x1, &s.y1, &s.cnt, &s.nx0, &s.ny0, &s.nx1, &s.ny1,
@@ -1153,6 +1163,7 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
     p += 4 * NC;
     s.cpos = p;
     p += 4 * NC;
+    if (kHbm) p = reinterpret_cast<int*>(lds_raw);
     s.scan_tmp = p;
     p += kOctThreads + 1;
     s.scal = p;
@@ -1445,7 +1456,7 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
   for (int k = t; k < K; k += kOctThreads) {
     const unsigned long long v =
         ((unsigned long long)(KD(k) >> 24) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)k);
-    atomicMax(&s.best[KN(k)], v);
+    __hip_atomic_fetch_max(&s.best[KN(k)], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   const int n_out = min(S, g.out_cap);
@@ -1646,7 +1657,8 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
                                                   int* __restrict__ n_out, int* __restrict__ mono_out,
                                                   int* __restrict__ err) {
   __shared__ int lvl_base[kMaxLevels + 1];
-  __shared__ int flags[4096];
+  constexpr int kChunk = 4096;  // keypoints partitioned per block scan (any n: chunks carry the count)
+  __shared__ int flags[kChunk];
   __shared__ int scan_tmp[kOctThreads + 1];
   const int img = blockIdx.x, t = threadIdx.x, L = P->levels;
   if (t == 0) {
@@ -1659,7 +1671,7 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
   }
   __syncthreads();
   const int n = lvl_base[L];
-  if (n > 4096 || n > cap) {
+  if (n > cap) {
     if (t == 0) {
       n_out[img] = n;
       mono_out[img] = -1;
@@ -1684,38 +1696,45 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
       y *= P->lev[l].scale;
     }
   };
-  for (int gi = t; gi < n; gi += 256) {
-    float x, y;
-    int l, slot;
-    xy_of(gi, x, y, l, slot);
-    flags[gi] = (x >= (float)lap0 && x <= (float)lap1) ? 1 : 0;  // stereo
-  }
-  __syncthreads();
-  const int n_stereo = block_scan(flags, n, scan_tmp);
-  for (int gi = t; gi < n; gi += 256) {
-    float x, y;
-    int l, slot;
-    xy_of(gi, x, y, l, slot);
-    const bool st = (x >= (float)lap0 && x <= (float)lap1);
-    const int before_st = flags[gi];
-    const int dst = st ? n - 1 - before_st : gi - before_st;
-    const size_t so = (size_t)img * P->kp_slots + slot;
-    const uint32_t kp = oct_out[so];
-    KeyPointOut o;
-    o.x = x;
-    o.y = y;
-    o.size = P->lev[l].patch_size;
-    o.angle = angle_in[so];
-    o.response = (float)(kp >> 24);
-    o.octave = l;
-    o.class_id = -1;
-    kps[(size_t)img * cap + dst] = o;
-    const uint64_t* d = desc_in + so * 4;
-    uint64_t* od = descs + ((size_t)img * cap + dst) * 4;
-    od[0] = d[0];
-    od[1] = d[1];
-    od[2] = d[2];
-    od[3] = d[3];
+  int n_stereo = 0;  // stereo keypoints before the current chunk
+  for (int c0 = 0; c0 < n; c0 += kChunk) {
+    const int cn = min(kChunk, n - c0);
+    for (int i = t; i < cn; i += 256) {
+      float x, y;
+      int l, slot;
+      xy_of(c0 + i, x, y, l, slot);
+      flags[i] = (x >= (float)lap0 && x <= (float)lap1) ? 1 : 0;  // stereo
+    }
+    __syncthreads();
+    const int chunk_stereo = block_scan(flags, cn, scan_tmp);
+    for (int i = t; i < cn; i += 256) {
+      const int gi = c0 + i;
+      float x, y;
+      int l, slot;
+      xy_of(gi, x, y, l, slot);
+      const bool st = (x >= (float)lap0 && x <= (float)lap1);
+      const int before_st = n_stereo + flags[i];
+      const int dst = st ? n - 1 - before_st : gi - before_st;
+      const size_t so = (size_t)img * P->kp_slots + slot;
+      const uint32_t kp = oct_out[so];
+      KeyPointOut o;
+      o.x = x;
+      o.y = y;
+      o.size = P->lev[l].patch_size;
+      o.angle = angle_in[so];
+      o.response = (float)(kp >> 24);
+      o.octave = l;
+      o.class_id = -1;
+      kps[(size_t)img * cap + dst] = o;
+      const uint64_t* d = desc_in + so * 4;
+      uint64_t* od = descs + ((size_t)img * cap + dst) * 4;
+      od[0] = d[0];
+      od[1] = d[1];
+      od[2] = d[2];
+      od[3] = d[3];
+    }
+    n_stereo += chunk_stereo;
+    __syncthreads();  // flags are the next chunk's
   }
   if (t == 0) {
     n_out[img] = n;
@@ -1764,10 +1783,10 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   hipLaunchKernelGGL(fast, dim3(n * H.n_cells), dim3(64), H.max_roi_lds, st, a.plan,
                      a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count);
   mark(3);
-  hipLaunchKernelGGL(k_octree, dim3(n * H.levels), dim3(kOctThreads), a.octree_lds, st, a.plan,
-                     a.cells,
-                     (const uint32_t*)a.slots, (const int*)a.cell_count, a.dense, a.knode,
-                     a.oct_out, a.oct_count, a.err, n, kOctreeLdsCand);
+  hipLaunchKernelGGL(H.oct_hbm_nodes ? k_octree<true> : k_octree<false>, dim3(n * H.levels),
+                     dim3(kOctThreads), a.octree_lds, st, a.plan, a.cells, (const uint32_t*)a.slots,
+                     (const int*)a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, a.err, n,
+                     H.oct_kcap, a.oct_nodes);
   mark(4);
   const long waves = (long)n * H.kp_slots;
   hipLaunchKernelGGL(k_describe, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a.plan, src,
@@ -1787,8 +1806,10 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
 // shrink each other's limit); sizes up to 64 KB need no opt-in.
 hipError_t set_lds_limits(size_t octree_bytes, size_t resize_bytes) {
   if (octree_bytes > 64 * 1024) {
-    const hipError_t e = lds_optin((const void*)k_octree, (int)octree_bytes);
-    if (e != hipSuccess) return e;
+    for (const void* k : {(const void*)k_octree<false>, (const void*)k_octree<true>}) {
+      const hipError_t e = lds_optin(k, (int)octree_bytes);
+      if (e != hipSuccess) return e;
+    }
   }
   if (resize_bytes > 64 * 1024) {
     const hipError_t e = lds_optin((const void*)k_resize, (int)resize_bytes);

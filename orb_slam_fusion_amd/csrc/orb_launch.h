@@ -28,6 +28,7 @@ struct ExtractLaunch {
   float* angle;
   uint64_t* desc;
   size_t octree_lds;
+  uint8_t* oct_nodes;  // HBM node arrays (plans with oct_hbm_nodes), else null
   int lap0, lap1;
   void* kps_out;   // orbgpu_keypoint[n_images][cap]
   void* desc_out;  // uint8_t[n_images][cap][32]

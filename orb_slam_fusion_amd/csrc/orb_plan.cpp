@@ -47,7 +47,7 @@ void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::ve
 }
 
 bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::string& why,
-               int resize_rounding) {
+               int resize_rounding, int octree_nodes) {
   const int L = p.num_levels;
   if (L < 1 || L > kMaxLevels) return why = "num_levels out of range", false;
   if (!(p.scale_factor > 1.0f)) return why = "scale_factor must be > 1", false;
@@ -236,8 +236,24 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   P.rs_lds = (rs_lds + 15) & ~15;
   if (P.rs_lds > 160 * 1024) return why = "scale factor too large for the resize tile", false;
   if (P.max_roi_lds > 64 * 1024) return why = "FAST cell too large", false;
-  if (P.kp_slots > 4096) return why = "too many keypoints per image for the assembly kernel", false;
-  if (octree_lds_bytes(P) > 160 * 1024) return why = "num_features too large for the octree LDS", false;
+  // octree storage: the node arrays and kOctreeLdsCand candidates in LDS;
+  // fewer candidates in LDS (the rest in HBM, as beyond kOctreeLdsCand) when
+  // the nodes leave less room; the node arrays in HBM (k_octree<true>) when
+  // they alone do not fit -- any num_features the reference accepts
+  // (orb_extractor.cc:432-444 bounds no level's budget).
+  {
+    const size_t fixed = octree_fixed_lds_bytes(), nodes = oct_node_bytes(P.node_cap);
+    if (octree_nodes != ORBGPU_OCTREE_NODES_HBM && nodes + fixed + (size_t)kOctreeLdsCand * 8 <= kOctreeLdsMax) {
+      P.oct_hbm_nodes = 0;
+      P.oct_kcap = kOctreeLdsCand;
+    } else if (octree_nodes != ORBGPU_OCTREE_NODES_HBM && nodes + fixed + 64 * 8 <= kOctreeLdsMax) {
+      P.oct_hbm_nodes = 0;
+      P.oct_kcap = (int)((kOctreeLdsMax - nodes - fixed) / 8) & ~63;
+    } else {
+      P.oct_hbm_nodes = 1;
+      P.oct_kcap = kOctreeLdsCand;
+    }
+  }
   return true;
 }
 
@@ -267,9 +283,13 @@ int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch) {
   return ((pitch * rows + 15) & ~15) + ((pitch * (dh + 2) + 15) & ~15) + sv + 4 * ng + 16 + 16;
 }
 
+// k_octree's LDS besides the nodes: the scan scratch (256 + 1 ints) and 16
+// block scalars.
+size_t octree_fixed_lds_bytes() { return (256 + 1) * 4 + 16 * 4; }
+
 size_t octree_lds_bytes(const PlanHeader& P) {
-  const size_t nc = P.node_cap;
-  return nc * 8 + nc * 17 * 4 + nc * 8 * 4 + (256 + 1) * 4 + 16 * 4 + (size_t)kOctreeLdsCand * 8;
+  const size_t cand = (size_t)P.oct_kcap * 8;
+  return (P.oct_hbm_nodes ? 0 : oct_node_bytes(P.node_cap)) + octree_fixed_lds_bytes() + cand;
 }
 
 }  // namespace orbgpu

@@ -3,7 +3,9 @@
 // from the image size (orb_extractor.cc:407-465, 744-849, 1093-1117) is
 // computed once per (params, width, height) and lives in one device buffer.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
+#include <hip/hip_runtime.h>
 
 namespace orbgpu {
 
@@ -58,7 +60,9 @@ struct PlanHeader {
   int blur_bytes;   // per image, all levels
   int slots;        // per image candidate slots
   int kp_slots;     // per image octree-output slots
-  int node_cap;     // LDS node capacity used by the octree kernel
+  int node_cap;     // node capacity of the octree kernel (per (image, level) block)
+  int oct_kcap;     // octree candidates held in LDS (the rest in HBM)
+  int oct_hbm_nodes;  // 1: the node arrays live in HBM (k_octree<true>), 0: in LDS
   int blur_tiles;   // per image
   int max_roi;      // largest cell ROI (bytes)
   int max_roi_lds;  // LDS bytes of one FAST cell (staged ROI + score map + lists)
@@ -72,5 +76,10 @@ constexpr int kBlurTileW = 256, kBlurTileH = 128;   // 64 threads x 4 cols, 4 wa
 constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 4 waves x 8 rows, 64 lanes x 4 px
 constexpr int kLevelAlign = 16;
 constexpr int kOctreeLdsCand = 2048;  // octree candidates per (image, level) kept in LDS (rest in HBM)
+constexpr int kOctreeLdsMax = 160 * 1024;  // LDS of one gfx950 workgroup
+
+// Bytes of the octree's node arrays for node capacity nc: the 64-bit best
+// response, 17 per-node ints and 8 per-node child ints (k_octree's carve).
+__host__ __device__ constexpr size_t oct_node_bytes(int nc) { return (size_t)nc * (8 + 17 * 4 + 8 * 4); }
 
 }  // namespace orbgpu

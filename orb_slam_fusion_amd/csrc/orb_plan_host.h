@@ -20,9 +20,12 @@ void scale_tables(const orbgpu_orb_params& p, std::vector<float>& scale, std::ve
                   std::vector<float>& s2, std::vector<float>& inv_s2,
                   std::vector<int>& feats_per_level);
 // resize_rounding: ORBGPU_RESIZE_SSE / ORBGPU_RESIZE_SCALAR (include/orbgpu.h)
+// octree_nodes: ORBGPU_OCTREE_NODES_AUTO (LDS whenever the node arrays fit) or
+// ORBGPU_OCTREE_NODES_HBM (always HBM: the test path for the large plans)
 bool make_plan(const orbgpu_orb_params& p, int width, int height, HostPlan& out, std::string& why,
-               int resize_rounding = 0);
+               int resize_rounding = 0, int octree_nodes = 0);
 size_t octree_lds_bytes(const PlanHeader& P);
+size_t octree_fixed_lds_bytes();
 int fast_cell_lds_bytes(int cols, int rows);
 int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch);
 

@@ -842,3 +842,15 @@ extern "C" int orbgpu_debug_pose_stamps(unsigned long long* out, int n) {
   return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_pose_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+ORBGPU_UNIFORM_READER(pose)
+#if ORBGPU_CHECK_UNIFORM
+extern "C" unsigned orbgpu_uniform_violations_inertial(void);
+extern "C" unsigned orbgpu_uniform_violations_lba(void);
+// Debug builds only (make checkuniform): wave-uniform branch violations
+// since the last call, summed over the kernel translation units (uniform_dev.h).
+extern "C" unsigned orbgpu_debug_uniform_violations(void) {
+  return orbgpu_uniform_violations_pose() + orbgpu_uniform_violations_inertial() +
+         orbgpu_uniform_violations_lba();
+}
+#endif

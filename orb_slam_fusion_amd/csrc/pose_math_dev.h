@@ -7,6 +7,7 @@
 //   RobustKernelHuber::robustify    core/robust_kernel_impl.cpp:72-85
 #pragma once
 #include "f64_math_dev.h"
+#include "uniform_dev.h"
 #include <hip/hip_runtime.h>
 
 namespace orbgpu {
@@ -91,7 +92,7 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   double R[3][3], V[3][3];
   // all lanes evaluate the same exp: wave-uniform branches (scalar, no exec masking)
   const int small = theta < 0.00001 ? 1 : 0;
-  if (kUniform ? __builtin_amdgcn_readfirstlane(small) : small) {
+  if (kUniform ? uniform_branch(small) : small) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -105,7 +106,7 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
     const double t2 = w0 * w0 + w1 * w1 + w2 * w2;
     const int series = t2 < 0.0625 ? 1 : 0;
     double a, b, d;
-    if (kUniform ? __builtin_amdgcn_readfirstlane(series) : series) {
+    if (kUniform ? uniform_branch(series) : series) {
       // 1/(2k+1)!, 1/(2k+2)!, 1/(2k+3)! with alternating signs, k = 0..7
       a = fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, fma(t2, -7.6471637318198164759e-13,
           1.6059043836821614599e-10), -2.5052108385441718775e-08), 2.7557319223985890653e-06),
@@ -136,7 +137,7 @@ __device__ __forceinline__ Se3 se3_exp(const double u[6]) {
   // Eigen quaternionbase_assign_impl, the three pivot cases written out
   double t = R[0][0] + R[1][1] + R[2][2];
   const int qc = t > 0 ? 0 : R[2][2] > (R[1][1] > R[0][0] ? R[1][1] : R[0][0]) ? 1 : R[1][1] > R[0][0] ? 2 : 3;
-  const int qcase = kUniform ? __builtin_amdgcn_readfirstlane(qc) : qc;
+  const int qcase = kUniform ? uniform_branch(qc) : qc;
   if (qcase == 0) {
     t = sqrt_f64(t + 1.0);  // the chosen pivot's argument is >= 1
     e.qw = 0.5 * t;
@@ -222,7 +223,7 @@ __device__ __forceinline__ bool ldlt6_solve(double (&A)[6][6], const double (&b)
       }
     // every lane holds the same matrix: make the pivot wave-uniform so the
     // swap below is a scalar branch, not exec-masked divergent code
-    p = __builtin_amdgcn_readfirstlane(p);
+    p = uniform_branch(p);
     perm[k] = p;
 #pragma unroll
     for (int pp = 0; pp < 6; ++pp)

@@ -93,6 +93,13 @@ class OrbExtractor:
         check(lib().orbgpu_extractor_set_resize_rounding(self._h, int(mode)),
               "orbgpu_extractor_set_resize_rounding")
 
+    def set_octree_nodes(self, mode: int) -> None:
+        """Where DistributeOctTree's node list lives: ORBGPU_OCTREE_NODES_AUTO
+        (0: LDS when it fits the workgroup, else HBM) or ORBGPU_OCTREE_NODES_HBM
+        (1: always HBM; same results)."""
+        check(lib().orbgpu_extractor_set_octree_nodes(self._h, int(mode)),
+              "orbgpu_extractor_set_octree_nodes")
+
     def max_keypoints(self, width: int, height: int) -> int:
         return int(lib().orbgpu_extractor_max_keypoints(self._h, width, height))
 

@@ -157,3 +157,46 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(OSError, match="no CPU fallback"):
         _lib.lib()
+
+
+def _plan(params, w, h):
+    so = _lib.lib()
+    slots, hbm = ctypes.c_int(-1), ctypes.c_int(-1)
+    st = so.orbgpu_extractor_plan(ctypes.byref(_lib.OrbParams(*params)), w, h,
+                                  ctypes.byref(slots), ctypes.byref(hbm))
+    return st, slots.value, hbm.value
+
+
+@pytest.mark.parametrize("size", [(752, 480), (1241, 376), (640, 480), (1024, 768)])
+def test_plan_accepts_every_reference_extractor(size):
+    """no (num_features, scale <= 2, levels <= 16) the
+    reference constructs is refused -- including OrbExtractor(5 * nFeatures,
+    ...) (tracking.cc:202-204,811-813) and budgets far past any LDS.  Only
+    geometries whose smallest level cannot hold the FAST grid are skipped
+    (the reference divides by a zero cell count there, orb_extractor.cc:748-760)."""
+    w, h = size
+    for nf in (1, 100, 1000, 1200, 2000, 5000, 6000, 10000, 20000, 60000):
+        for sf in (1.1, 1.2, 1.5, 2.0):
+            for L in (1, 4, 8, 12, 16):
+                if min(w, h) / sf ** (L - 1) < 80:
+                    continue  # the smallest level would not hold the grid
+                st, slots, hbm = _plan((nf, sf, L, 20, 7), w, h)
+                assert st == _lib.ORBGPU_OK, (nf, sf, L, size)
+                assert slots >= nf, (nf, sf, L, size, slots)
+                assert hbm in (0, 1)
+
+
+def test_plan_octree_storage_policy():
+    """The octree's node arrays stay in LDS up to the reference's 5x
+    extractor at EuRoC / KITTI sizes and go to HBM only beyond it."""
+    assert _plan((1000, 1.2, 8, 20, 7), 752, 480)[2] == 0
+    assert _plan((5000, 1.2, 8, 20, 7), 752, 480)[2] == 0
+    assert _plan((6000, 1.2, 8, 20, 7), 1241, 376)[2] == 0
+    st, slots, hbm = _plan((20000, 1.2, 8, 20, 7), 1241, 376)
+    assert st == _lib.ORBGPU_OK and hbm == 1 and slots >= 20000
+
+
+def test_plan_refuses_degenerate_geometry():
+    assert _plan((1000, 1.2, 8, 20, 7), 60, 60)[0] == _lib.ORBGPU_ERR_INVALID
+    assert _plan((1000, 1.0, 8, 20, 7), 752, 480)[0] == _lib.ORBGPU_ERR_INVALID
+    assert _lib.lib().orbgpu_extractor_plan(None, 752, 480, None, None) == _lib.ORBGPU_ERR_INVALID

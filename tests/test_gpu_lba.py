@@ -277,14 +277,15 @@ def test_lba_stop_flag_mid_run(gpu_available):
     assert any(0 < t < full["stats"][3] for t in seen), (seen, full["stats"][3])
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("ordered", [False, True])
-def test_lba_two_ranks_one_gpu(gpu_available, tmp_path, ordered):
-    """The point-sharded C4 window on two ranks (fresh child processes, both on
-    cuda:0), partial reduced camera systems / chi2 / LM scale summed through
+def test_lba_ranks_one_gpu(gpu_available, tmp_path, ordered, world):
+    """The point-sharded C4 window on 2 and 4 ranks (fresh child processes, all
+    on cuda:0), partial reduced camera systems / chi2 / LM scale summed through
     lba.dist_reduce over gloo (optimizer.cc:1359-1360, block_solver.hpp:383-460
     split by points): the same LM path and state as the one-rank GPU run.
     ordered: the stream-ordered form (lba.dist_enqueue; gloo stages through
-    the host), which must issue the same collective sequence on both ranks."""
+    the host), which must issue the same collective sequence on every rank."""
     import os
     import socket
     import subprocess
@@ -295,24 +296,25 @@ def test_lba_two_ranks_one_gpu(gpu_available, tmp_path, ordered):
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     worker = REPO / "tools" / "lba_shard_worker.py"
-    procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), str(tmp_path), "0",
-                               "1" if ordered else "0"], env=env) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, str(worker), str(r), str(world), str(port), str(tmp_path),
+                               "0", "1" if ordered else "0"], env=env) for r in range(world)]
     for pr in procs:
         assert pr.wait(timeout=100) == 0
-    r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
+    r = [np.load(tmp_path / f"r{k}.npz") for k in range(world)]
     p = synth.lba_problem()
     single = LocalBundleAdjuster().optimize(p)
     cut = r[0]["cut"]
-    assert (r[0]["poses_d"] == r[1]["poses_d"]).all()  # every rank solves the same system
-    for k in range(2):
+    assert len(cut) == world + 1
+    for k in range(world):
+        assert (r[k]["poses_d"] == r[0]["poses_d"]).all()  # every rank solves the same system
         assert (r[k]["stats"][1:5] == r[0]["stats"][1:5]).all()
     assert r[0]["stats"][2] == single["stats"][2] and r[0]["stats"][3] == single["stats"][3]
     assert abs(r[0]["stats"][1] - single["stats"][1]) <= 1e-9 * single["stats"][1]
     assert np.allclose(r[0]["poses_d"], single["poses_d"], rtol=1e-9, atol=1e-12)
-    pts = np.concatenate([r[0]["pts"][cut[0]:cut[1]], r[1]["pts"][cut[1]:cut[2]]])
+    pts = np.concatenate([r[k]["pts"][cut[k]:cut[k + 1]] for k in range(world)])
     assert np.allclose(pts, single["pts"], rtol=1e-6, atol=1e-6)
-    owner = (p.edges["point"] >= cut[1]).astype(int)
-    outl = np.where(owner == 0, r[0]["outlier"], r[1]["outlier"])
+    owner = np.searchsorted(cut[1:], p.edges["point"], side="right")  # rank owning each edge's point
+    outl = np.choose(owner, [r[k]["outlier"] for k in range(world)])
     assert (outl == single["outlier"]).all()
 
 

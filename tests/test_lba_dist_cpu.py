@@ -1,4 +1,4 @@
-"""World-size-2 gloo test of the point-sharded LocalBundleAdjustment layout
+"""World-size-2 and -4 gloo test of the point-sharded LocalBundleAdjustment layout
 (SURVEY §8e): each rank runs the oracle on its half of the points, the
 partial reduced camera system / chi2 / LM scale are completed by the
 product's all-reduce hook (orb_slam_fusion_amd.lba.dist_reduce, gloo on host
@@ -10,6 +10,7 @@ import sys
 from pathlib import Path
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 REPO = Path(__file__).resolve().parents[1]
@@ -41,15 +42,15 @@ def _worker(rank, world, port, out_dir):
     dist.init(world, rank)
     p = _problem()
     n = len(p.pts_init)
-    cut = [0, n // 2 + 7, n]  # uneven shards on purpose
+    cut = [0] + [k * n // world + 7 for k in range(1, world)] + [n]  # uneven shards on purpose
     r = oracle.lba(p, pt_range=(cut[rank], cut[rank + 1]), reduce=dist_reduce())
     np.savez(Path(out_dir) / f"r{rank}.npz", poses=r["poses"], pts=r["pts"], outlier=r["outlier"],
              stats=r["stats"], cut=np.array(cut))
     dist.finalize()
 
 
-def test_gloo_world2_lba_shards(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_lba_shards(tmp_path, world):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     r = [np.load(tmp_path / f"r{k}.npz") for k in range(world)]
     sys.path.insert(0, str(REPO / "oracle"))
@@ -59,12 +60,13 @@ def test_gloo_world2_lba_shards(tmp_path):
     p = _problem()
     single = oracle.lba(p)
     cut = r[0]["cut"]
-    assert (r[0]["poses"] == r[1]["poses"]).all()  # every rank solves the same system
+    for k in range(world):
+        assert (r[k]["poses"] == r[0]["poses"]).all()  # every rank solves the same system
+        assert r[k]["stats"][1] == r[0]["stats"][1]  # global chi2
     assert np.allclose(r[0]["poses"], single["poses"], rtol=1e-9, atol=1e-12)
-    pts = np.concatenate([r[0]["pts"][cut[0]:cut[1]], r[1]["pts"][cut[1]:cut[2]]])
+    pts = np.concatenate([r[k]["pts"][cut[k]:cut[k + 1]] for k in range(world)])
     assert np.allclose(pts, single["pts"], rtol=1e-9, atol=1e-12)
-    owner = (p.edges["point"] >= cut[1]).astype(int)
-    outl = np.where(owner == 0, r[0]["outlier"], r[1]["outlier"])
+    owner = np.searchsorted(cut[1:], p.edges["point"], side="right")
+    outl = np.choose(owner, [r[k]["outlier"] for k in range(world)])
     assert (outl == single["outlier"]).all()
-    assert r[0]["stats"][1] == r[1]["stats"][1]  # global chi2
     assert abs(r[0]["stats"][1] - single["stats"][1]) <= 1e-9 * single["stats"][1]

@@ -118,8 +118,8 @@ def measure_lia(calls: int = 10, cpu_calls: int = 3, b_large: bool = False) -> d
     return out
 
 
-def measure_sharded(calls: int = 10) -> dict:
-    """The C4 window point-sharded over 2 ranks on ONE GPU (two fresh child
+def measure_sharded(calls: int = 10, world: int = 4) -> dict:
+    """The C4 window point-sharded over `world` ranks on ONE GPU (fresh child
     processes, gloo all-reduce of the device buffers through lba.dist_reduce):
     a capability line (the exchange's cost with both ranks sharing the GPU),
     not a multi-GPU scaling figure."""
@@ -139,24 +139,25 @@ def measure_sharded(calls: int = 10) -> dict:
         port = s.getsockname()[1]
         s.close()
         with tempfile.TemporaryDirectory() as tmp:
-            procs = [subprocess.Popen([sys.executable, str(worker), str(r), "2", str(port), tmp,
+            procs = [subprocess.Popen([sys.executable, str(worker), str(r), str(world), str(port), tmp,
                                        str(calls), "1" if ordered else "0"], env=env,
-                                      stdout=sys.stderr) for r in range(2)]
+                                      stdout=sys.stderr) for r in range(world)]
             # (gloo's connection messages go to stderr: bench.py's stdout is its one JSON line)
             if any(p.wait(timeout=300) != 0 for p in procs):
                 return None
-            return [dict(np.load(Path(tmp) / f"r{k}.npz")) for k in range(2)]
+            return [dict(np.load(Path(tmp) / f"r{k}.npz")) for k in range(world)]
 
     r = run(False)
     if r is None:
         return {"error": "worker failed"}
     ro = run(True)
-    out = {"workload": "C4 LocalBundleAdjustment point-sharded over 2 ranks on 1 GPU "
+    out = {"workload": f"C4 LocalBundleAdjustment point-sharded over {world} ranks on 1 GPU "
                        "(gloo all-reduce of S, b, chi2, scale per LM trial)",
            "ms_per_call": round(float(max(x["ms_per_call"] for x in r)), 3),
            "lm_iterations": int(r[0]["stats"][2]), "lm_trials": int(r[0]["stats"][3]),
            "chi2": float(r[0]["stats"][1]),
-           "ranks_identical_poses": bool((r[0]["poses_d"] == r[1]["poses_d"]).all()),
+           "ranks": world,
+           "ranks_identical_poses": bool(all((x["poses_d"] == r[0]["poses_d"]).all() for x in r)),
            "scaling": "unmeasured (both ranks on one GPU)"}
     if ro is not None:  # the stream-ordered form (reductions enqueued on the library stream)
         out["ordered"] = {
