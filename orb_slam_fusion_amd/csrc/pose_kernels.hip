@@ -853,4 +853,23 @@ extern "C" unsigned orbgpu_debug_uniform_violations(void) {
   return orbgpu_uniform_violations_pose() + orbgpu_uniform_violations_inertial() +
          orbgpu_uniform_violations_lba();
 }
+
+// Positive control of the checker: se3_exp<true> on a wave whose lanes do NOT
+// agree (lane 0 takes the theta < 1e-5 branch, the rest the series) must be
+// counted.  Returns the violations it raised (cleared), or ~0u on an error.
+namespace orbgpu {
+__global__ void k_uniform_selftest(double* out) {
+  const int lane = threadIdx.x & 63;
+  const double u[6] = {2e-3 * lane, 0, 0, 0, 0, 0};
+  out[threadIdx.x] = se3_exp<true>(u).qw;
+}
+}  // namespace orbgpu
+extern "C" unsigned orbgpu_debug_uniform_selftest(void) {
+  double* d = nullptr;
+  if (orbgpu_debug_uniform_violations() != 0 || hipMalloc(&d, 64 * sizeof(double)) != hipSuccess) return ~0u;
+  hipLaunchKernelGGL(orbgpu::k_uniform_selftest, dim3(1), dim3(64), 0, nullptr, d);
+  const unsigned v = hipDeviceSynchronize() == hipSuccess ? orbgpu_uniform_violations_pose() : ~0u;
+  (void)hipFree(d);
+  return v;
+}
 #endif

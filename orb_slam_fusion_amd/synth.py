@@ -199,13 +199,16 @@ class LiaProblem:
 def lia_problem(seed: int = LIA_SEED, n_opt: int = 10, n_fixed_cov: int = 10, n_pts: int = 2000,
                 max_obs: int = 8, outlier_frac: float = 0.05, stereo_frac: float = 0.5,
                 b_large: bool = False, rec_init: bool = False, perturb: float = 1.0,
-                no_imu: tuple = (), max_depth: float = 40.0, consecutive: bool = False) -> LiaProblem:
+                no_imu: tuple = (), max_depth: float = 40.0, consecutive: bool = False,
+                kf_rot_scale: tuple = ()) -> LiaProblem:
     """no_imu: window indices of key frames without IMU data (`!pKFi->bImu`:
     VertexPose only, optimizer.cc:2466-2484) -- the temporal links touching
     them are left out, as :2503 skips them.  max_depth: farthest visible
     depth.  consecutive: a point's observers are max_obs consecutive key
     frames of those that see it (a banded window) instead of a random
-    subset."""
+    subset.  kf_rot_scale: per free key frame (window order), a multiplier of
+    its initial rotation error only (LM updates of very different sizes within
+    one trial)."""
     rng = np.random.default_rng(seed)
     c = lia_calib()
     fx, fy, cx, cy, bf = LIA_CAM
@@ -235,7 +238,8 @@ def lia_problem(seed: int = LIA_SEED, n_opt: int = 10, n_fixed_cov: int = 10, n_
         if fixed[i]:
             kfs[i] = kfs_true[i]
         else:
-            kfs[i] = lia_state(c, R_true[k] @ _exp_so3(rng.normal(0, 3e-3 * s, 3)),
+            rs = kf_rot_scale[i] if i < len(kf_rot_scale) else 1.0
+            kfs[i] = lia_state(c, R_true[k] @ _exp_so3(rng.normal(0, 3e-3 * s, 3) * rs),
                                t_true[k] + rng.normal(0, 2e-2 * s, 3),
                                v_true[k] + rng.normal(0, 2e-2 * s, 3),
                                bg_true[k] + rng.normal(0, 1e-3 * s, 3),

@@ -162,3 +162,21 @@ def test_capacity_and_mode_checks(gpu_available):
     assert so.orbgpu_pose_inertial(opt._h, 1, *args, None, p(case["obs"]), 5, 0, p(res),
                                    p(out)) == _lib.ORBGPU_OK
     opt.close()
+
+
+@pytest.mark.parametrize("seed", [40, 41])
+def test_rotation_updates_cross_exp_branches(gpu_available, seed):
+    """an IMU prediction off by ~0.1 rad, so the LM's
+    rotation updates run through every ExpSO3 / right-Jacobian branch (closed
+    form at d >= 0.05, the d^2 < 0.0025 series, the d < 1e-5 identity) on the
+    way to convergence -- the wave-uniform branches of imu_math_dev.h, which
+    the checked build (make checkuniform) verifies lane by lane."""
+    case = ic.make_case(seed, mode=0, n_obs=300, perturb=25.0)
+    ref, ref_out = oracle.pose_inertial(case)
+    ret, res, out = _gpu(case)
+    assert ret == int(ref["n_good"]) and ret > 200
+    _check(res, out, ref, ref_out)
+    R0 = case["cur"]["Rwb"].reshape(3, 3).astype(float)
+    M = res["Rwb_d"].reshape(3, 3) @ R0.T
+    corr = np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2
+    assert corr > 0.05  # the first update alone takes the closed form

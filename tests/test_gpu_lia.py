@@ -150,3 +150,19 @@ def test_lia_zero_iterations(gpu_available):
     thr = np.where(mono, np.where(close, float(np.float32(1.5) * np.float32(5.991)), float(np.float32(5.991))),
                    float(np.float32(7.815)))
     check_flags(got["outlier"], ref, thr)
+
+
+def test_lia_update_sizes_straddle_exp_branches(gpu_available):
+    """free key frames whose initial rotation errors differ
+    by four orders of magnitude, interleaved, so one trial's per-key-frame
+    updates (one key frame per lane) straddle ExpSO3's d = 1e-5 and
+    d^2 = 0.0025 branch points within a wave -- the case the round-3
+    wave-uniform ExpSO3 got wrong."""
+    scales = (1e-3, 25.0, 1.0) * 3 + (1e-3,)
+    pb = synth.lia_problem(19, n_opt=10, n_fixed_cov=4, n_pts=1200, kf_rot_scale=scales)
+    got, _ = _compare(pb)
+    corr = []
+    for k in range(10):
+        M = got["kfs21"][k, :9].reshape(3, 3) @ pb.kfs["Rwb"][k].reshape(3, 3).astype(float).T
+        corr.append(np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2)
+    assert max(corr) > 0.1 and min(corr) < 1e-3, corr

@@ -133,3 +133,19 @@ def test_pose_context_reuse_graph_replay(gpu_available):
         assert inl == inl_ref, (seed, n)
         assert np.array_equal(fr.outlier, out_ref)
         assert np.max(np.abs(fr.pose - p_ref)) <= TOL_F
+
+
+def test_uniform_branch_checker_catches_divergence(gpu_available):
+    """Positive control of the checked build (make checkuniform): a wave whose
+    lanes disagree at a wave-uniform branch is counted.  Runs only when
+    ORBGPU_LIB names that build."""
+    import ctypes
+    import os
+
+    if "checkuniform" not in os.environ.get("ORBGPU_LIB", ""):
+        pytest.skip("checked build not loaded")
+    from orb_slam_fusion_amd._lib import lib
+
+    fn = lib().orbgpu_debug_uniform_selftest
+    fn.restype = ctypes.c_uint
+    assert fn() == 1  # one wave, one violating branch (the small-angle test)
