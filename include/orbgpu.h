@@ -69,6 +69,15 @@ int orbgpu_extractor_levels(const orbgpu_extractor* h);
 #define ORBGPU_RESIZE_SCALAR 1
 orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode);
 
+/* How the pyramid's resize chain is launched (same bytes either way):
+ * ORBGPU_PYRAMID_PER_LEVEL (default) one launch per level over the whole
+ * device; ORBGPU_PYRAMID_FUSED one launch, a workgroup per image walking the
+ * levels (k_pyramid; slower at every measured batch, kept for A/B).  The
+ * environment variable ORBGPU_RESIZE=fused sets the default at creation. */
+#define ORBGPU_PYRAMID_PER_LEVEL 0
+#define ORBGPU_PYRAMID_FUSED 1
+orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode);
+
 /* Where DistributeOctTree's node list lives (orb_extractor.cc:542-742; the
  * reference's std::list has no bound, and neither does its per-level budget,
  * :432-444).  ORBGPU_OCTREE_NODES_AUTO (default): in LDS whenever the plan's
@@ -282,6 +291,27 @@ orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered);
 #define ORBGPU_LBA_SOLVER_BLOCK 1
 #define ORBGPU_LBA_SOLVER_GRID 2
 orbgpu_status orbgpu_lba_ctx_set_solver(orbgpu_lba_ctx* c, int solver);
+
+/* The Schur complement's path (identical results within rounding; for A/B
+ * runs and tests): SPLIT (default) by point range, PAIR by pose pair, BAND by
+ * point band (falls back to PAIR when a point spans more than 15 free key
+ * frames).  The environment variable ORBGPU_SCHUR=split|pair|band sets the
+ * default once, when the context is created. */
+#define ORBGPU_LBA_SCHUR_SPLIT 0
+#define ORBGPU_LBA_SCHUR_PAIR 1
+#define ORBGPU_LBA_SCHUR_BAND 2
+orbgpu_status orbgpu_lba_ctx_set_schur(orbgpu_lba_ctx* c, int mode);
+
+/* on != 0: every LM build re-linearises at the accepted state instead of
+ * taking the accepted trial's per-edge terms (bit-identical; a test switch).
+ * Default: whether ORBGPU_LBA_RELINEARIZE is set when the context is created. */
+orbgpu_status orbgpu_lba_ctx_set_relinearize(orbgpu_lba_ctx* c, int on);
+
+/* Device-memory budget of the context (bytes; 0 = none, the default).  A
+ * window whose arena would exceed it returns ORBGPU_ERR_NOMEM before any
+ * device work, the context stays usable -- the caller's hook for a per-window
+ * memory bound (the drop-ins throw on NOMEM). */
+orbgpu_status orbgpu_lba_ctx_set_memory_limit(orbgpu_lba_ctx* c, size_t bytes);
 
 /* Window size: the reduced camera system (6 rows per free key frame) is
  * factorised packed in LDS by one workgroup up to 160 rows, from HBM by one

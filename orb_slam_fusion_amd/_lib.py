@@ -28,6 +28,13 @@ ORBGPU_LBA_SOLVER_LDS = 0
 ORBGPU_LBA_SOLVER_BLOCK = 1
 ORBGPU_LBA_SOLVER_GRID = 2
 ORBGPU_RESIZE_SCALAR = 1
+ORBGPU_LBA_SCHUR_SPLIT = 0
+ORBGPU_LBA_SCHUR_PAIR = 1
+ORBGPU_LBA_SCHUR_BAND = 2
+ORBGPU_OCTREE_NODES_AUTO = 0
+ORBGPU_OCTREE_NODES_HBM = 1
+ORBGPU_PYRAMID_PER_LEVEL = 0
+ORBGPU_PYRAMID_FUSED = 1
 
 STATUS_NAMES = {
     ORBGPU_OK: "OK",
@@ -171,6 +178,7 @@ SIGNATURES = {
     "orbgpu_extractor_max_keypoints": (_I, [_P, _I, _I]),
     "orbgpu_extractor_set_resize_rounding": (_I, [_P, _I]),
     "orbgpu_extractor_set_octree_nodes": (_I, [_P, _I]),
+    "orbgpu_extractor_set_pyramid_launch": (_I, [_P, _I]),
     "orbgpu_extractor_plan": (_I, [_P, _I, _I, _P, _P]),
     "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "orbgpu_extractor_pyramid_level": (_I, [_P, _I, ctypes.POINTER(_P), _P, _P, _P]),
@@ -263,6 +271,9 @@ SIGNATURES = {
     "orbgpu_lba_ctx_create": (_I, [_I, ctypes.POINTER(_P)]),
     "orbgpu_lba_ctx_set_reduce_ordered": (_I, [_P, _I]),
     "orbgpu_lba_ctx_set_solver": (_I, [_P, _I]),
+    "orbgpu_lba_ctx_set_schur": (_I, [_P, _I]),
+    "orbgpu_lba_ctx_set_relinearize": (_I, [_P, _I]),
+    "orbgpu_lba_ctx_set_memory_limit": (_I, [_P, ctypes.c_size_t]),
     "orbgpu_lba_ctx_destroy": (None, [_P]),
     "orbgpu_lba_optimize": (
         _I,

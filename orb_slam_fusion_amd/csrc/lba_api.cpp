@@ -68,6 +68,9 @@ struct orbgpu_lba_ctx {
   int device = 0;
   int reduce_ordered = 0;  // orbgpu_lba_ctx_set_reduce_ordered
   int solver = ORBGPU_LBA_SOLVER_AUTO;  // orbgpu_lba_ctx_set_solver
+  int schur = ORBGPU_LBA_SCHUR_SPLIT;   // orbgpu_lba_ctx_set_schur (default: ORBGPU_SCHUR at creation)
+  int relinearize = 0;                  // orbgpu_lba_ctx_set_relinearize (default: ORBGPU_LBA_RELINEARIZE)
+  size_t mem_limit = 0;                 // orbgpu_lba_ctx_set_memory_limit (0: none)
   hipStream_t stream = nullptr;
   char* arena = nullptr;  // device
   size_t arena_cap = 0;
@@ -85,8 +88,13 @@ struct orbgpu_lba_ctx {
     if (host) (void)hipHostFree(host);
     if (res) (void)hipHostFree(res);
   }
+  // The previous call may have left no-op LM steps queued on `stream` that
+  // still read the arena and write the results block: they drain before either
+  // buffer is replaced (explicitly -- not by relying on hipFree's implicit
+  // synchronisation).
   bool reserve_results(size_t bytes) {
     if (bytes <= res_cap) return true;
+    if (hipStreamSynchronize(stream) != hipSuccess) return false;
     if (res) (void)hipHostFree(res);
     res = res_dev = nullptr;
     res_cap = 0;
@@ -100,6 +108,9 @@ struct orbgpu_lba_ctx {
     return true;
   }
   bool reserve(size_t dev_bytes, size_t host_bytes) {
+    if (mem_limit && dev_bytes > mem_limit) return false;  // ORBGPU_ERR_NOMEM, nothing touched
+    if ((dev_bytes > arena_cap || host_bytes > staging_cap) && hipStreamSynchronize(stream) != hipSuccess)
+      return false;
     if (dev_bytes > arena_cap) {
       if (arena) (void)hipFree(arena);
       arena = nullptr;
@@ -127,6 +138,13 @@ orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out) {
   auto* c = new (std::nothrow) orbgpu_lba_ctx();
   if (!c) return ORBGPU_ERR_NOMEM;
   c->device = device;
+  // A/B defaults for tools (read once here, never per call): ORBGPU_SCHUR =
+  // split | pair | band, ORBGPU_LBA_RELINEARIZE set -> re-linearise every build
+  if (const char* e = std::getenv("ORBGPU_SCHUR"))
+    c->schur = std::strcmp(e, "pair") == 0 ? ORBGPU_LBA_SCHUR_PAIR
+               : std::strcmp(e, "band") == 0 ? ORBGPU_LBA_SCHUR_BAND
+                                             : ORBGPU_LBA_SCHUR_SPLIT;
+  c->relinearize = std::getenv("ORBGPU_LBA_RELINEARIZE") != nullptr ? 1 : 0;
   void* hw = nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(&hw, sizeof(LbaHostWords), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -148,6 +166,24 @@ orbgpu_status orbgpu_lba_ctx_create(int device, orbgpu_lba_ctx** out) {
 orbgpu_status orbgpu_lba_ctx_set_reduce_ordered(orbgpu_lba_ctx* c, int ordered) {
   if (!c) return ORBGPU_ERR_INVALID;
   c->reduce_ordered = ordered ? 1 : 0;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_lba_ctx_set_schur(orbgpu_lba_ctx* c, int mode) {
+  if (!c || mode < ORBGPU_LBA_SCHUR_SPLIT || mode > ORBGPU_LBA_SCHUR_BAND) return ORBGPU_ERR_INVALID;
+  c->schur = mode;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_lba_ctx_set_memory_limit(orbgpu_lba_ctx* c, size_t bytes) {
+  if (!c) return ORBGPU_ERR_INVALID;
+  c->mem_limit = bytes;
+  return ORBGPU_OK;
+}
+
+orbgpu_status orbgpu_lba_ctx_set_relinearize(orbgpu_lba_ctx* c, int on) {
+  if (!c) return ORBGPU_ERR_INVALID;
+  c->relinearize = on ? 1 : 0;
   return ORBGPU_OK;
 }
 
@@ -347,15 +383,13 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   const int n_pairs = (int)pair_list.size() / 2;
   // Schur path: point ranges (k_lba_schur_split), S of them so that a
   // (pair, range) block gets about kSchurSplitEdges of its pose's edges.
-  // ORBGPU_SCHUR=pair|band|split picks a path for A/B runs (tools/).
+  // orbgpu_lba_ctx_set_schur picks a path for A/B runs and tests.
   const int n_free_edges = std::accumulate(pose_cnt.begin(), pose_cnt.end(), 0);
   int sc_split = nf > 0 ? (n_free_edges + nf * kSchurSplitEdges - 1) / (nf * kSchurSplitEdges) : 0;
   sc_split = std::min(std::max(sc_split, 1), kSchurSplitMax);
   SchurChunks sc;
-  if (const char* e = std::getenv("ORBGPU_SCHUR")) {
-    if (std::strcmp(e, "split") != 0) sc_split = 0;
-    if (std::strcmp(e, "band") == 0) build_schur_chunks(np, nf, cnt, pf, sc);
-  }
+  if (h->schur != ORBGPU_LBA_SCHUR_SPLIT) sc_split = 0;
+  if (h->schur == ORBGPU_LBA_SCHUR_BAND) build_schur_chunks(np, nf, cnt, pf, sc);
   if (nf == 0 || n_pairs == 0) sc_split = 0;
   // range x = points [pbx[x], pbx[x + 1]), cut at about x ne / S edges
   std::vector<int> pbx(sc_split + 1, np);
@@ -561,7 +595,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.sc_split = sc_split;
   // the build re-linearises every iteration instead of taking the accepted
   // trial's terms (same values; tests/test_gpu_lba.py compares the two)
-  a.force_lin = std::getenv("ORBGPU_LBA_RELINEARIZE") != nullptr;
+  a.force_lin = h->relinearize;
   a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
   a.pair_cnt = reinterpret_cast<unsigned*>(A + u_pcnt);
   // each pair's ranges folded by k_lba_schur_fold; ORBGPU_SCHUR_FOLD=inline:

@@ -1026,7 +1026,10 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
   double m = 0;
   if (first) {
     for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) m = fmax(m, a.partials[b]);
-    for (int k = threadIdx.x; k < a.n_sys; k += kThreads) m = fmax(m, fabs(a.diag[k]));
+    // pose rows only: the inertial model (pdim 15) writes a.diag for rows
+    // 0..5 of a key frame (its lambda is the caller's, lambda_init > 0)
+    for (int k = threadIdx.x; k < a.n_sys; k += kThreads)
+      if (k % a.pdim < 6) m = fmax(m, fabs(a.diag[k]));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
@@ -2512,7 +2515,8 @@ __global__ void k_lba_ctl(LbaArgs a, int mode) {
     if (!c.lambda_due) return;
     c.lambda_due = 0;
     double m = a.diag[a.n_sys];
-    for (int k = 0; k < a.n_sys; ++k) m = fmax(m, fabs(a.diag[k]));
+    for (int k = 0; k < a.n_sys; ++k)
+      if (k % a.pdim < 6) m = fmax(m, fabs(a.diag[k]));  // pose rows (see k_lba_sums)
     ctl_lambda(a, m);
     return;
   }

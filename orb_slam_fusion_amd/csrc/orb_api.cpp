@@ -47,6 +47,7 @@ struct orbgpu_extractor {
   int plan_w = -1, plan_h = -1;
   int resize_rounding = ORBGPU_RESIZE_SSE;
   int octree_nodes = ORBGPU_OCTREE_NODES_AUTO;
+  int pyramid_launch = ORBGPU_PYRAMID_PER_LEVEL;  // orbgpu_extractor_set_pyramid_launch
   PlanHeader* d_plan = nullptr;
   Cell* d_cells = nullptr;
   int* d_rs = nullptr;
@@ -240,13 +241,10 @@ ExtractLaunch make_launch(orbgpu_extractor* h, const uint8_t* imgs, size_t pitch
   a.plan = h->d_plan;
   a.n_cu = h->n_cu;
   // the resize chain per level (default), or as one launch (k_pyramid, a
-  // workgroup per image) with ORBGPU_RESIZE=fused -- bit-identical, slower
-  // at every batch size measured
-  {
-    const char* e = std::getenv("ORBGPU_RESIZE");
-    const bool fused = e && std::strcmp(e, "fused") == 0;
-    a.pyramid_groups = fused ? pyramid_groups_for((size_t)h->plan.hdr.rs_lds) : 0;
-  }
+  // workgroup per image) -- bit-identical, slower at every batch size
+  // measured
+  a.pyramid_groups =
+      h->pyramid_launch == ORBGPU_PYRAMID_FUSED ? pyramid_groups_for((size_t)h->plan.hdr.rs_lds) : 0;
   a.cells = h->d_cells;
   a.rs_tab = h->d_rs;
   a.imgs = imgs;
@@ -408,6 +406,8 @@ orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int devic
   if (!h) return ORBGPU_ERR_NOMEM;
   h->params = *params;
   h->device = device;
+  if (const char* e = std::getenv("ORBGPU_RESIZE"))  // A/B default for tools, read once
+    if (std::strcmp(e, "fused") == 0) h->pyramid_launch = ORBGPU_PYRAMID_FUSED;
   h->max_w = max_width;
   h->max_h = max_height;
   h->max_images = max_images;
@@ -501,6 +501,14 @@ orbgpu_status orbgpu_extractor_set_octree_nodes(orbgpu_extractor* h, int mode) {
   const int w = h->plan_w, ht = h->plan_h;
   h->plan_w = h->plan_h = -1;  // re-plan; ensure_workspace sizes the node range on the next call
   return ensure_plan(h, w, ht);
+}
+
+orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode) {
+  if (!h || (mode != ORBGPU_PYRAMID_PER_LEVEL && mode != ORBGPU_PYRAMID_FUSED)) return ORBGPU_ERR_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (h->stream && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  h->pyramid_launch = mode;  // the next launch differs from a captured one: no stale graph replays
+  return ORBGPU_OK;
 }
 
 orbgpu_status orbgpu_extractor_plan(const orbgpu_orb_params* params, int width, int height,

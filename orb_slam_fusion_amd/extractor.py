@@ -93,6 +93,12 @@ class OrbExtractor:
         check(lib().orbgpu_extractor_set_resize_rounding(self._h, int(mode)),
               "orbgpu_extractor_set_resize_rounding")
 
+    def set_pyramid_launch(self, mode: int) -> None:
+        """ORBGPU_PYRAMID_PER_LEVEL (0, default: a launch per level) or
+        ORBGPU_PYRAMID_FUSED (1: one k_pyramid launch, a workgroup per image)."""
+        check(lib().orbgpu_extractor_set_pyramid_launch(self._h, int(mode)),
+              "orbgpu_extractor_set_pyramid_launch")
+
     def set_octree_nodes(self, mode: int) -> None:
         """Where DistributeOctTree's node list lives: ORBGPU_OCTREE_NODES_AUTO
         (0: LDS when it fits the workgroup, else HBM) or ORBGPU_OCTREE_NODES_HBM

@@ -105,6 +105,21 @@ class LocalBundleAdjuster:
         default): A/B timing and the path-equivalence tests."""
         check(lib().orbgpu_lba_ctx_set_solver(self._h, int(solver)), "orbgpu_lba_ctx_set_solver")
 
+    def set_schur(self, mode: int) -> None:
+        """The Schur complement's path (_lib.ORBGPU_LBA_SCHUR_*: SPLIT by
+        point range, the default; PAIR; BAND)."""
+        check(lib().orbgpu_lba_ctx_set_schur(self._h, int(mode)), "orbgpu_lba_ctx_set_schur")
+
+    def set_relinearize(self, on: bool) -> None:
+        """Re-linearise every LM build instead of taking the accepted trial's
+        terms (bit-identical; the test of that identity)."""
+        check(lib().orbgpu_lba_ctx_set_relinearize(self._h, 1 if on else 0), "orbgpu_lba_ctx_set_relinearize")
+
+    def set_memory_limit(self, nbytes: int) -> None:
+        """Device-memory budget of the context (0 = none): a window over it
+        raises ORBGPU_ERR_NOMEM before any device work."""
+        check(lib().orbgpu_lba_ctx_set_memory_limit(self._h, int(nbytes)), "orbgpu_lba_ctx_set_memory_limit")
+
     def optimize(self, problem, iterations: int = 10, pt_range=None, group=None,
                  stop_flag: Optional[ctypes.c_uint8] = None, lambda_init: float = 0.0,
                  ordered: bool = False) -> dict:

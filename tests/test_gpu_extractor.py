@@ -52,9 +52,11 @@ def _diagnose(ex, orc, L):
     return "; ".join(lines) or "stages equal"
 
 
-def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False):
+def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False, fused=False):
     h, w = img.shape
     ex = OrbExtractor(*params, max_width=w, max_height=h)
+    if fused:
+        ex.set_pyramid_launch(1)  # ORBGPU_PYRAMID_FUSED
     if rounding is not None:
         ex.set_resize_rounding(rounding)
     if octree_hbm:
@@ -66,7 +68,7 @@ def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False):
         with oracle.resize_rounding(rounding):  # the oracle's levels follow the same split
             m_ref, k_ref, d_ref = orc.extract(img, lapping)
     m, k, d = ex(img, None, lapping)
-    ctx = f"{w}x{h} params={params} lapping={lapping} rounding={rounding} octree_hbm={octree_hbm}"
+    ctx = f"{w}x{h} params={params} lapping={lapping} rounding={rounding} octree_hbm={octree_hbm} fused={fused}"
     # the reference blurs only levels that kept keypoints (orb_extractor.cc
     # operator(): `if (nkeypointsLevel == 0) continue;`), the GPU every level
     ref_levels = set(k_ref["octave"].tolist())
@@ -171,12 +173,14 @@ def test_getters_match_oracle(gpu_available):
     assert ex.GetLevels() == 8
 
 
-def test_batch_matches_single(gpu_available):
+def _batch_matches_single(fused):
     import torch
 
     B = 6
     imgs = np.stack([synth.stereo_frame(i // 2)[i % 2] for i in range(B)])
     ex = OrbExtractor(*C2, max_images=B)
+    if fused:
+        ex.set_pyramid_launch(1)
     cap = ex.max_keypoints(752, 480)
     d_imgs = torch.from_numpy(imgs).cuda()
     kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
@@ -193,6 +197,10 @@ def test_batch_matches_single(gpu_available):
         assert n_h[i] == len(k_ref) and mono_h[i] == m_ref
         assert kps_h[i, : n_h[i]].tobytes() == k_ref.tobytes(), f"image {i} keypoints"
         assert desc_h[i, : n_h[i]].tobytes() == d_ref.tobytes(), f"image {i} descriptors"
+
+
+def test_batch_matches_single(gpu_available):
+    _batch_matches_single(False)
 
 
 def test_repeat_calls_deterministic(gpu_available):
@@ -255,32 +263,30 @@ def test_handles_with_different_plans_coexist(gpu_available):
 
 
 @pytest.mark.parametrize("case", ["c2", "euroc", "odd", "scale2", "scale15", "rounding1"])
-def test_fused_pyramid_bit_exact(gpu_available, monkeypatch, case):
+def test_fused_pyramid_bit_exact(gpu_available, case):
     """The resize chain as ONE launch (k_pyramid: a workgroup per image whose
     tile groups walk the levels, the same tile code as the per-level
-    launches; opt-in by ORBGPU_RESIZE=fused) gives the same bytes."""
-    monkeypatch.setenv("ORBGPU_RESIZE", "fused")
+    launches; opt-in by orbgpu_extractor_set_pyramid_launch) gives the same bytes."""
     if case == "c2":
-        assert _compare(C2, synth.stereo_frame(0)[0]) > 900
+        assert _compare(C2, synth.stereo_frame(0)[0], fused=True) > 900
     elif case == "euroc":
-        assert _compare(EUROC, synth.stereo_frame(10)[1]) > 1100
+        assert _compare(EUROC, synth.stereo_frame(10)[1], fused=True) > 1100
     elif case == "odd":
         full, _ = synth.stereo_frame(20, w=641, h=397)
-        _compare((1000, 1.2, 8, 20, 7), full)
+        _compare((1000, 1.2, 8, 20, 7), full, fused=True)
     elif case == "scale2":  # a wide resize window: fewer tile groups fit a workgroup's LDS
         full, _ = synth.stereo_frame(21, w=1024, h=768)
-        _compare((1000, 2.0, 4, 20, 7), full)
+        _compare((1000, 2.0, 4, 20, 7), full, fused=True)
     elif case == "scale15":
         full, _ = synth.stereo_frame(21, w=1024, h=768)
-        _compare((1000, 1.5, 6, 20, 7), full)
+        _compare((1000, 1.5, 6, 20, 7), full, fused=True)
     else:
-        assert _compare(C2, synth.stereo_frame(4)[0], rounding=1) > 900
+        assert _compare(C2, synth.stereo_frame(4)[0], rounding=1, fused=True) > 900
 
 
-def test_fused_pyramid_batch(gpu_available, monkeypatch):
+def test_fused_pyramid_batch(gpu_available):
     """A batch through the one-launch pyramid equals the oracle image by image."""
-    monkeypatch.setenv("ORBGPU_RESIZE", "fused")
-    test_batch_matches_single(gpu_available)
+    _batch_matches_single(True)
 
 
 # --- every extractor the reference constructs (VERDICT r4 item 2) ---------

@@ -44,9 +44,9 @@ def check_flags(got_out, ref, thr):
     assert exempt.size <= MAX_EXEMPT, exempt.tolist()
 
 
-def _compare(p, iters=10, tol=1e-6, lambda_init=0.0):
+def _compare(p, iters=10, tol=1e-6, lambda_init=0.0, adj=None):
     ref = oracle.lba(p, iters=iters, lambda_init=lambda_init)
-    got = LocalBundleAdjuster().optimize(p, iterations=iters, lambda_init=lambda_init)
+    got = (adj or LocalBundleAdjuster()).optimize(p, iterations=iters, lambda_init=lambda_init)
     assert got["stats"][2] == ref["stats"][2]  # LM iterations
     assert got["stats"][3] == ref["stats"][3]  # trials
     assert abs(got["stats"][1] - ref["stats"][1]) <= tol * ref["stats"][1]
@@ -323,24 +323,47 @@ def _same(a, b):
         assert np.array_equal(a[k], b[k]), k
 
 
-def test_lba_trial_terms_equal_relinearised(gpu_available, monkeypatch):
+def test_lba_trial_terms_equal_relinearised(gpu_available):
     """An accepted trial leaves its state's per-edge terms for the next build
     (lin_of / LbaCtrl::lin_state); re-linearising every build instead
-    (ORBGPU_LBA_RELINEARIZE) computes the same values: bit-identical runs."""
+    (orbgpu_lba_ctx_set_relinearize) computes the same values: bit-identical runs."""
     p = synth.lba_problem(seed=31, n_kf=12, n_pts=900, obs_per_pt=5, n_fixed=2, outlier_pct=5)
     spec = LocalBundleAdjuster().optimize(p)
-    monkeypatch.setenv("ORBGPU_LBA_RELINEARIZE", "1")
-    relin = LocalBundleAdjuster().optimize(p)
+    adj = LocalBundleAdjuster()
+    adj.set_relinearize(True)
+    relin = adj.optimize(p)
     _same(spec, relin)
     assert spec["stats"][3] >= 3  # several accepted trials
 
 
 @pytest.mark.parametrize("mode", ["split", "pair", "band"])
-def test_lba_schur_paths(gpu_available, monkeypatch, mode):
+def test_lba_schur_paths(gpu_available, mode):
     """The Schur complement by point range (default), by pose pair and by
-    point band (ORBGPU_SCHUR; band falls back to pairs when a point spans more
-    than 15 free key frames) each match the oracle and repeat bit for bit."""
-    monkeypatch.setenv("ORBGPU_SCHUR", mode)
+    point band (orbgpu_lba_ctx_set_schur; band falls back to pairs when a
+    point spans more than 15 free key frames) each match the oracle and repeat
+    bit for bit."""
+    from orb_slam_fusion_amd import _lib
+
+    m = {"split": _lib.ORBGPU_LBA_SCHUR_SPLIT, "pair": _lib.ORBGPU_LBA_SCHUR_PAIR,
+         "band": _lib.ORBGPU_LBA_SCHUR_BAND}[mode]
     p = synth.lba_problem(seed=32)
-    got, _ = _compare(p)
-    _same(got, LocalBundleAdjuster().optimize(p))
+    adj = LocalBundleAdjuster()
+    adj.set_schur(m)
+    got, _ = _compare(p, adj=adj)
+    _same(got, adj.optimize(p))
+
+
+def test_lba_memory_limit_nomem(gpu_available):
+    """a window past the context's device-memory budget returns
+    ORBGPU_ERR_NOMEM before any device work, and the context stays usable
+    (the same window then matches a fresh context bit for bit)."""
+    from orb_slam_fusion_amd._lib import ORBGPU_ERR_NOMEM, OrbGpuError
+
+    p = synth.lba_problem(seed=7, n_kf=8, n_pts=400, obs_per_pt=4, n_fixed=2)
+    adj = LocalBundleAdjuster()
+    adj.set_memory_limit(4096)
+    with pytest.raises(OrbGpuError) as e:
+        adj.optimize(p)
+    assert e.value.status == ORBGPU_ERR_NOMEM
+    adj.set_memory_limit(0)
+    _same(adj.optimize(p), LocalBundleAdjuster().optimize(p))

@@ -114,14 +114,15 @@ def test_lia_then_lba_on_one_context(gpu_available):
     assert np.array_equal(b1["poses_d"], b2["poses_d"])
 
 
-def test_lia_trial_terms_equal_relinearised(gpu_available, monkeypatch):
+def test_lia_trial_terms_equal_relinearised(gpu_available):
     """The accepted trial's visual terms and IMU link forms (written while the
     trial is evaluated) equal a fresh linearisation at the accepted state
-    (ORBGPU_LBA_RELINEARIZE): bit-identical runs."""
+    (orbgpu_lba_ctx_set_relinearize): bit-identical runs."""
     pb = synth.lia_problem()
     spec = LocalBundleAdjuster().optimize_inertial(pb)
-    monkeypatch.setenv("ORBGPU_LBA_RELINEARIZE", "1")
-    relin = LocalBundleAdjuster().optimize_inertial(pb)
+    adj = LocalBundleAdjuster()
+    adj.set_relinearize(True)
+    relin = adj.optimize_inertial(pb)
     for k in ("stats", "kfs21", "pts", "outlier"):
         assert np.array_equal(spec[k], relin[k]), k
 
