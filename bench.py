@@ -159,6 +159,9 @@ def main() -> int:
     ap.add_argument("--pipes", type=int, default=2,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
                          "each launch group split evenly between them)")
+    ap.add_argument("--phase-stage", type=int, default=1,
+                    help="pipeline k+1 starts each launch group when pipeline k has finished this "
+                         "stage of it (0 pyramid .. 5 assembly; -1: no offset)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lba", action="store_true", help="skip the LocalBundleAdjustment side line")
@@ -237,6 +240,16 @@ def main() -> int:
     # independent).
     s_pose = torch.cuda.Stream(dev, priority=-1)  # high-priority pool: its own HW queue
     pose_ev = []
+    # pipeline k + 1 runs each group part-way behind pipeline k (--phase-stage):
+    # its VALU-bound stages then overlap the other's latency-bound ones
+    s_pipe = [torch.cuda.Stream(dev) for _ in pipes]
+    ph_ev = []
+    if args.phase_stage >= 0:
+        for k in range(P - 1):
+            ev = torch.cuda.Event()
+            ev.record(s_pipe[k])  # creates the event
+            pipes[k].set_stage_event(args.phase_stage, ev)
+            ph_ev.append(ev)
 
     def step(timed: bool):
         for g in range(G):
@@ -253,9 +266,11 @@ def main() -> int:
             if timed:
                 e1.record(s_pose)
                 pose_ev.append((e0, e1))
-            for k, e in enumerate(pipes):  # stream=0: the handle's own HIP stream
+            for k, e in enumerate(pipes):
                 isl = slice(2 * (f0 + Bp * k), 2 * (f0 + Bp * (k + 1)))
-                e.extract_batch(d_imgs[isl], d_kps[isl], d_desc[isl], d_n[isl], d_mono[isl], stream=0)
+                if k > 0 and ph_ev:
+                    s_pipe[k].wait_event(ph_ev[k - 1])
+                e.extract_batch(d_imgs[isl], d_kps[isl], d_desc[isl], d_n[isl], d_mono[isl], stream=s_pipe[k])
 
     for _ in range(args.warmup):
         step(False)

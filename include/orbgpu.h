@@ -69,6 +69,15 @@ int orbgpu_extractor_levels(const orbgpu_extractor* h);
 #define ORBGPU_RESIZE_SCALAR 1
 orbgpu_status orbgpu_extractor_set_resize_rounding(orbgpu_extractor* h, int mode);
 
+/* Stage signal for pipelining batch extractions across streams: every later
+ * orbgpu_extract_batch on this handle records `hip_event` (a hipEvent_t the
+ * caller owns) on its stream right after `stage` -- 0 pyramid, 1 blur,
+ * 2 FAST, 3 octree, 4 describe, 5 assembly -- so another stream can start
+ * its own batch when this one is part-way (NULL: no signal).  bench.py
+ * offsets its two extractor pipelines this way: one's VALU-bound stages
+ * (pyramid, blur, FAST) then run beside the other's latency-bound ones. */
+orbgpu_status orbgpu_extractor_set_stage_event(orbgpu_extractor* h, int stage, void* hip_event);
+
 /* How the pyramid's resize chain is launched (same bytes either way):
  * ORBGPU_PYRAMID_PER_LEVEL (default) one launch per level over the whole
  * device; ORBGPU_PYRAMID_FUSED one launch, a workgroup per image walking the

@@ -179,6 +179,7 @@ SIGNATURES = {
     "orbgpu_extractor_set_resize_rounding": (_I, [_P, _I]),
     "orbgpu_extractor_set_octree_nodes": (_I, [_P, _I]),
     "orbgpu_extractor_set_pyramid_launch": (_I, [_P, _I]),
+    "orbgpu_extractor_set_stage_event": (_I, [_P, _I, _P]),
     "orbgpu_extractor_plan": (_I, [_P, _I, _I, _P, _P]),
     "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
     "orbgpu_extractor_pyramid_level": (_I, [_P, _I, ctypes.POINTER(_P), _P, _P, _P]),

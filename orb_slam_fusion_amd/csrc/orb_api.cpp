@@ -48,6 +48,8 @@ struct orbgpu_extractor {
   int resize_rounding = ORBGPU_RESIZE_SSE;
   int octree_nodes = ORBGPU_OCTREE_NODES_AUTO;
   int pyramid_launch = ORBGPU_PYRAMID_PER_LEVEL;  // orbgpu_extractor_set_pyramid_launch
+  hipEvent_t stage_event = nullptr;  // orbgpu_extractor_set_stage_event (batch launches)
+  int stage_event_at = -1;
   PlanHeader* d_plan = nullptr;
   Cell* d_cells = nullptr;
   int* d_rs = nullptr;
@@ -337,6 +339,7 @@ static bool same_launch(const ExtractLaunch& x, const ExtractLaunch& y) {
          x.lap0 == y.lap0 && x.lap1 == y.lap1 && x.kps_out == y.kps_out &&
          x.desc_out == y.desc_out && x.cap == y.cap && x.n_out == y.n_out &&
          x.mono_out == y.mono_out && x.err == y.err && x.n_cu == y.n_cu && x.events == y.events &&
+         x.stage_event == y.stage_event && x.stage_event_at == y.stage_event_at &&
          x.pyramid_groups == y.pyramid_groups;
 }
 
@@ -503,6 +506,13 @@ orbgpu_status orbgpu_extractor_set_octree_nodes(orbgpu_extractor* h, int mode) {
   return ensure_plan(h, w, ht);
 }
 
+orbgpu_status orbgpu_extractor_set_stage_event(orbgpu_extractor* h, int stage, void* hip_event) {
+  if (!h || (hip_event && (stage < 0 || stage >= kStages))) return ORBGPU_ERR_INVALID;
+  h->stage_event = static_cast<hipEvent_t>(hip_event);
+  h->stage_event_at = hip_event ? stage : -1;
+  return ORBGPU_OK;
+}
+
 orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode) {
   if (!h || (mode != ORBGPU_PYRAMID_PER_LEVEL && mode != ORBGPU_PYRAMID_FUSED)) return ORBGPU_ERR_INVALID;
   if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
@@ -632,6 +642,8 @@ orbgpu_status orbgpu_extract_batch(orbgpu_extractor* h, const uint8_t* d_imgs, i
   ExtractLaunch a = make_launch(h, d_imgs, image_pitch, stride, n_images, lap, d_kps, d_descs,
                                 cap_per_image, d_n, d_mono);
   if (h->prof_used < h->prof_slots) a.events = &h->prof_events[(size_t)h->prof_used++ * (kStages + 1)];
+  a.stage_event = h->stage_event;
+  a.stage_event_at = h->stage_event_at;
   if (launch_extract(a, s) != hipSuccess) return ORBGPU_ERR_DEVICE;
   h->host_pyr_valid = false;
   h->last_w = 0;  // the host pyramid getter serves the host-buffer path only

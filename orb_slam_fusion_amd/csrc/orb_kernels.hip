@@ -1484,7 +1484,8 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kRawW = 36, kRawH = 31;   // 31x31 patch + dword alignment slack
 constexpr int kBlurW = 40, kBlurH = 37;  // 37x37 (|sample offset| <= 18) + slack
-constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave
+constexpr int kDescLds = kRawW * kRawH + kBlurW * kBlurH;  // per wave (the round-4 kernel)
+[[maybe_unused]] constexpr int kDescLdsUsed = kDescLds;
 
 
 // IC_Angle by v_dot4_u32_u8 over the staged 31-row patch: item t = (row
@@ -1522,6 +1523,172 @@ constexpr IcTab make_ic_tab() {
 }
 __constant__ IcTab c_ic = make_ic_tab();
 
+#ifndef ORB_DESC_KPW
+#define ORB_DESC_KPW 1  // keypoints per k_describe wave: 1 (default) or 4 (A/B: 16 lanes each)
+#endif
+#if ORB_DESC_KPW == 4
+// Four keypoints per wave, 16 lanes each (lane 16 g + j: keypoint g).  The
+// per-keypoint scalar work -- the moment reductions, fastAtan2, the glibc
+// sinf / cosf port (≈100 VALU a keypoint, every lane computing the same
+// value in a one-keypoint wave) -- now serves four keypoints per
+// instruction.  A wave takes 4 consecutive output slots of ONE (image,
+// level) (PlanHeader::kp_quads, LevelGeom::quad_off), so the level planes are
+// wave-uniform: both patches are staged by raw buffer loads whose row step is
+// the SGPR offset (2 rows x 8 dwords per step, the 9th / 9th-10th dword
+// columns in their own steps) -- no per-load address VALU -- 42 dword loads a
+// lane in flight.  IC_Angle: item i = j + 16 k of the same c_ic table (row
+// i / 9, dword i % 9), a 16-lane rotate-add reduction (row_ror 8, 4, 2, 1).
+// BRIEF: lane j computes tests 16 j .. 16 j + 15 of its keypoint -- the
+// reference's fmaf offsets and cvRound as the round-4 kernel -- and shifts
+// each t0 < t1 (the sign of t0 - t1) into its u16 by one v_alignbit, then
+// stores descriptor bytes 2 j, 2 j + 1.  Dead slots of a live wave replay
+// the level's last live keypoint and store nothing.
+constexpr int kRawRows = 32, kBlurRows = 38;  // one spare row each: 2-row load steps
+#ifndef ORB_DESC_REUSE
+#define ORB_DESC_REUSE 1  // the blurred patch overwrites the raw one after IC_Angle
+#endif
+#ifndef ORB_DESC_WG
+#define ORB_DESC_WG 1  // waves per k_describe workgroup
+#endif
+constexpr int kDescSlice = ORB_DESC_REUSE ? (kBlurW * kBlurRows + 15) & ~15
+                                          : (kRawW * kRawRows + kBlurW * kBlurRows + 15) & ~15;
+constexpr int kDescWaveLds = 4 * kDescSlice;
+
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {  // sum over the lane's 16-lane row
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x122, 0xf, 0xf, false);  // row_ror:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x121, 0xf, 0xf, false);  // row_ror:1
+  return v;
+}
+
+__global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
+                                                 const uint8_t* __restrict__ pyr,
+                                                 const uint8_t* __restrict__ blur,
+                                                 const uint32_t* __restrict__ oct_out,
+                                                 const int* __restrict__ oct_count,
+                                                 float* __restrict__ angle_out,
+                                                 uint64_t* __restrict__ desc_out, int n_img) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_wg[ORB_DESC_WG * kDescWaveLds];
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int wave = ORB_DESC_WG > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  uint8_t* lds_all = lds_wg + wave * kDescWaveLds;
+  const int nq = P->kp_quads;
+  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * ORB_DESC_WG + wave;
+  if (gidx >= n_img * nq) return;  // wave-uniform
+  const int img = gidx / nq, q = gidx - img * nq;
+  int l = 0;
+  while (l + 1 < P->levels && q >= P->lev[l + 1].quad_off) ++l;
+  const LevelGeom& gl = P->lev[l];
+  const int cnt = __builtin_amdgcn_readfirstlane(oct_count[img * P->levels + l]);
+  const int s0 = 4 * (q - gl.quad_off);
+  if (s0 >= cnt) return;  // wave-uniform: no live slot
+  const bool live = s0 + g < cnt;
+  const int slot = gl.out_off + min(s0 + g, cnt - 1);
+  const uint32_t kp = oct_out[(size_t)img * P->kp_slots + slot];
+  const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
+  uint8_t* raw = lds_all + g * kDescSlice;
+  uint8_t* blp = ORB_DESC_REUSE ? raw : raw + kRawW * kRawRows;
+
+  // ---- both patches: rows 2k + (j >> 3), dword j & 7 (SGPR row step), then
+  // the raw 9th dword (rows j, j + 16) and the blurred 9th / 10th (rows
+  // (j >> 1) + 8 m, dword 8 + (j & 1))
+  int sp;
+  const uint8_t* rbase = level_plane(P, src, pyr, img, l, sp);
+  const uint8_t* bbase = blur + (size_t)img * P->blur_bytes + gl.blur_off;
+  const int bp = gl.pitch;
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(rbase), (short)0,
+                                                                      (int)0xffffffff, kBufRsrcWord3);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bbase), (short)0,
+                                                                      (int)0xffffffff, kBufRsrcWord3);
+  const int rx0 = (cx - 15) & ~3, bx0 = (cx - 18) & ~3;
+  const int rq = j & 7, rh = j >> 3;
+  const int vr = (cy - 15 + rh) * sp + rx0 + 4 * rq;
+  const int vb = (cy - 18 + rh) * bp + bx0 + 4 * rq;
+  const int vr8 = (cy - 15 + j) * sp + rx0 + 32;
+  const int vb8 = (cy - 18 + (j >> 1)) * bp + bx0 + 32 + 4 * (j & 1);
+  uint32_t r_main[16], r_c8[2], b_main[19], b_c8[5];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r_main[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, vr, 2 * k * sp, 0);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) r_c8[m] = __builtin_amdgcn_raw_buffer_load_b32(rr, vr8, 16 * m * sp, 0);
+#pragma unroll
+  for (int k = 0; k < 19; ++k) b_main[k] = __builtin_amdgcn_raw_buffer_load_b32(br, vb, 2 * k * bp, 0);
+  const bool b8_last = (j >> 1) + 32 < kBlurRows;  // rows 38, 39 do not exist
+#pragma unroll
+  for (int m = 0; m < 5; ++m)
+    b_c8[m] = (m < 4 || b8_last) ? __builtin_amdgcn_raw_buffer_load_b32(br, vb8, 8 * m * bp, 0) : 0u;
+  {
+    uint32_t* d = reinterpret_cast<uint32_t*>(raw + rh * kRawW + 4 * rq);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k * 2 * kRawW / 4] = r_main[k];
+    uint32_t* d8 = reinterpret_cast<uint32_t*>(raw + j * kRawW + 32);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) d8[m * 16 * kRawW / 4] = r_c8[m];
+  }
+  auto stage_blurred = [&]() {
+    uint32_t* e = reinterpret_cast<uint32_t*>(blp + rh * kBlurW + 4 * rq);
+#pragma unroll
+    for (int k = 0; k < 19; ++k) e[k * 2 * kBlurW / 4] = b_main[k];
+    uint32_t* e8 = reinterpret_cast<uint32_t*>(blp + (j >> 1) * kBlurW + 32 + 4 * (j & 1));
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+      if (m < 4 || b8_last) e8[m * 8 * kBlurW / 4] = b_c8[m];
+  };
+  if (!ORB_DESC_REUSE) stage_blurred();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // ---- IC_Angle (see c_ic): items j + 16 k, k < 18 (288 >= 279; the rest zero)
+  int m10, m01;
+  {
+    const uint32_t(*tab)[4] = c_ic.e[(cx - 15) & 3];
+    uint32_t A = 0, B = 0, S = 0;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      const uint4 w = *reinterpret_cast<const uint4*>(tab[16 * k + j]);
+      const uint32_t val = *reinterpret_cast<const uint32_t*>(raw + w.w);
+      A = __builtin_amdgcn_udot4(val, w.x, A, false);
+      B = __builtin_amdgcn_udot4(val, w.y, B, false);
+      S = __builtin_amdgcn_udot4(val, w.z, S, false);
+    }
+    const int s = (int)row_sum16(S);
+    m10 = (int)row_sum16(A) - 15 * s;
+    m01 = (int)row_sum16(B) - 15 * s;
+  }
+  if (ORB_DESC_REUSE) {  // the raw patch's reads are done (in order within the wave)
+    stage_blurred();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  const float angle = dev_fast_atan2((float)m01, (float)m10);
+  const float ang = angle * (float)(3.14159265358979323846 / 180.0);
+  const float a = dev_cosf(ang), b = dev_sinf(ang);
+
+  // ---- steered BRIEF: tests 16 j + 15 .. 16 j, each t0 < t1 shifted in
+  const uint8_t* ctr = blp + 18 * kBlurW + (cx - bx0);
+  const uint8_t* ctr_m = ctr - (uint32_t)(0x400000u * kBlurW + 0x4B400000u);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    const float4 pt = c_pattern_f[16 * j + i];
+    const f32x2 X = {pt.x, pt.y}, Y = {pt.z, pt.w};
+    constexpr float kMagic = 12582912.0f;  // cvRound as in the round-4 kernel (below)
+    const f32x2 R = __builtin_elementwise_fma(X, (f32x2){b, b}, Y * (f32x2){a, a}) + (f32x2){kMagic, kMagic};
+    const f32x2 Q = __builtin_elementwise_fma(X, (f32x2){a, a}, Y * (f32x2){-b, -b}) + (f32x2){kMagic, kMagic};
+    const int t0 = ctr_m[__umul24(__float_as_uint(R.x), (uint32_t)kBlurW) + __float_as_uint(Q.x)];
+    const int t1 = ctr_m[__umul24(__float_as_uint(R.y), (uint32_t)kBlurW) + __float_as_uint(Q.y)];
+    acc = __builtin_amdgcn_alignbit(acc, (uint32_t)(t0 - t1), 31);  // (acc << 1) | (t0 < t1)
+  }
+  if (live) {
+    const size_t o = (size_t)img * P->kp_slots + slot;
+    reinterpret_cast<uint16_t*>(desc_out + o * 4)[j] = (uint16_t)acc;
+    if (j == 0) angle_out[o] = angle;
+  }
+}
+#else
 // One wave per octree output slot (measured against a persistent, software-
 // pipelined variant: the extra registers halved residency and lost, 201 vs
 // 167 us).  The slot's count and keypoint are loaded together; dead slots
@@ -1635,6 +1802,8 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
   if (lane < 4) desc_out[o * 4 + lane] = words[lane];
   if (lane == 0) angle_out[o] = angle;
 }
+
+#endif  // ORB_DESC_KPW
 
 // --------------------------------------------------------------------------
 // k_assemble: operator() tail (orb_extractor.cc:1033-1090) for one image:
@@ -1758,6 +1927,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   const int n = a.n_images;
   auto mark = [&](int i) {
     if (a.events) (void)hipEventRecord(a.events[i], st);
+    if (a.stage_event && i == a.stage_event_at + 1) (void)hipEventRecord(a.stage_event, st);
   };
   mark(0);
   if (a.pyramid_groups > 0) {  // one launch: a workgroup per image (k_pyramid)
@@ -1788,8 +1958,13 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                      (const int*)a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, a.err, n,
                      H.oct_kcap, a.oct_nodes);
   mark(4);
+#if ORB_DESC_KPW == 4
+  hipLaunchKernelGGL(k_describe, dim3((unsigned)(((long)n * H.kp_quads + ORB_DESC_WG - 1) / ORB_DESC_WG)),
+                     dim3(64 * ORB_DESC_WG), 0, st, a.plan, src,
+#else
   const long waves = (long)n * H.kp_slots;
   hipLaunchKernelGGL(k_describe, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a.plan, src,
+#endif
                      (const uint8_t*)a.pyr, (const uint8_t*)a.blur, (const uint32_t*)a.oct_out,
                      (const int*)a.oct_count, a.angle, a.desc, n);
   mark(5);

@@ -39,6 +39,8 @@ struct ExtractLaunch {
   int n_cu;            // compute units of the device (persistent grids)
   int pyramid_groups;  // > 0: the resize chain as one k_pyramid launch, this many tile groups a workgroup
   hipEvent_t* events;  // optional: kStages + 1 events recorded around the stages
+  hipEvent_t stage_event;  // optional: recorded right after stage stage_event_at (orbgpu_extractor_set_stage_event)
+  int stage_event_at;
 };
 
 // Stage boundaries recorded when ExtractLaunch::events is set.

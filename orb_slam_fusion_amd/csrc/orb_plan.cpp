@@ -77,7 +77,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
 
   out.cells.clear();
   out.rs_tab.clear();
-  int pyr = 0, blur = 0, slots = 0, kps = 0, tiles = 0, max_roi = 0, node_cap = 64, rs_lds = 0;
+  int pyr = 0, blur = 0, slots = 0, kps = 0, quads = 0, tiles = 0, max_roi = 0, node_cap = 64, rs_lds = 0;
   int max_roi_lds = 0, need_pitch = 0;
   for (int l = 0; l < L; ++l) {
     LevelGeom& g = P.lev[l];
@@ -212,6 +212,8 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
     g.out_off = kps;
     g.out_cap = std::max(g.budget + 3, 4 * g.n_roots);
     kps += g.out_cap;
+    g.quad_off = quads;
+    quads += (g.out_cap + 3) / 4;
     node_cap = std::max({node_cap, g.out_cap, g.cell_end - g.cell_begin, g.n_roots});
   }
   P.n_cells = (int)out.cells.size();
@@ -219,6 +221,7 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
   P.blur_bytes = (blur + 255) & ~255;
   P.slots = slots;
   P.kp_slots = kps;
+  P.kp_quads = quads;
   P.node_cap = (node_cap + 63) & ~63;
   P.blur_tiles = tiles;
   P.max_roi = (max_roi + 15) & ~15;

@@ -40,6 +40,7 @@ struct LevelGeom {
   int rel_w, rel_h;  // max_x - min_x, max_y - min_y
   int out_off;       // first output slot of this level in an image's keypoint block
   int out_cap;       // node-count bound: max(budget + 3, 4 * n_roots)
+  int quad_off;      // first k_describe wave (4 output slots each) of this level in an image
   // blur tiling (kBlurTileW x kBlurTileH outputs per 256-thread block)
   int blur_tile_begin, tiles_x, tiles_y;
 };
@@ -60,6 +61,7 @@ struct PlanHeader {
   int blur_bytes;   // per image, all levels
   int slots;        // per image candidate slots
   int kp_slots;     // per image octree-output slots
+  int kp_quads;     // per image k_describe waves: sum over levels of ceil(out_cap / 4)
   int node_cap;     // node capacity of the octree kernel (per (image, level) block)
   int oct_kcap;     // octree candidates held in LDS (the rest in HBM)
   int oct_hbm_nodes;  // 1: the node arrays live in HBM (k_octree<true>), 0: in LDS

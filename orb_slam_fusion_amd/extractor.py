@@ -93,6 +93,15 @@ class OrbExtractor:
         check(lib().orbgpu_extractor_set_resize_rounding(self._h, int(mode)),
               "orbgpu_extractor_set_resize_rounding")
 
+    def set_stage_event(self, stage: int, event) -> None:
+        """Record ``event`` (a torch.cuda.Event, already created by one record,
+        or a raw hipEvent_t; None clears) after ``stage`` (0 pyramid .. 5
+        assembly) of every later extract_batch: the signal another stream
+        waits on to run its batch part-way behind this one."""
+        raw = None if event is None else int(getattr(event, "cuda_event", event))
+        check(lib().orbgpu_extractor_set_stage_event(self._h, int(stage), ctypes.c_void_p(raw)),
+              "orbgpu_extractor_set_stage_event")
+
     def set_pyramid_launch(self, mode: int) -> None:
         """ORBGPU_PYRAMID_PER_LEVEL (0, default: a launch per level) or
         ORBGPU_PYRAMID_FUSED (1: one k_pyramid launch, a workgroup per image)."""
