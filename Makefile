@@ -57,13 +57,14 @@ $(LIB)/liborbgpu_checkuniform.so: $(CU_OBJS)
 
 checkuniform: $(LIB)/liborbgpu_checkuniform.so
 
-# ad-hoc A/B variant of the extractor kernels (orb_kernels.hip compiled with
-# DEFS, every other object shared): make var NAME=pf4 DEFS=-DORB_BLUR_PF=4
+# ad-hoc A/B variant of the extractor (orb_kernels.hip and orb_plan.cpp
+# compiled with DEFS, every other object shared): make var NAME=pf4 DEFS=-DORB_BLUR_PF=4
 var: $(GPU_OBJS)
 	@mkdir -p $(OBJDIR)/var_$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(OBJDIR)/var_$(NAME)/orb_kernels.hip.o $(CSRC)/orb_kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c -o $(OBJDIR)/var_$(NAME)/orb_plan.cpp.o $(CSRC)/orb_plan.cpp
 	$(HIPCC) $(HIPFLAGS) -shared -o $(LIB)/liborbgpu_$(NAME).so $(OBJDIR)/var_$(NAME)/orb_kernels.hip.o \
-	  $(filter-out $(OBJDIR)/orb_kernels.hip.o,$(GPU_OBJS))
+	  $(OBJDIR)/var_$(NAME)/orb_plan.cpp.o $(filter-out $(OBJDIR)/orb_kernels.hip.o $(OBJDIR)/orb_plan.cpp.o,$(GPU_OBJS))
 
 $(LIB)/liborbsynth.so: $(CSRC)/synth.cpp
 	@mkdir -p $(LIB)

@@ -156,7 +156,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=256,
                     help="stereo frames per launch group (tools/sweep_batch.sh: 256 fills the "
                          "device's tail-latency gaps best, DESIGN §5)")
-    ap.add_argument("--pipes", type=int, default=2,
+    ap.add_argument("--pipes", type=int, default=4,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
                          "each launch group split evenly between them)")
     ap.add_argument("--phase-stage", type=int, default=1,

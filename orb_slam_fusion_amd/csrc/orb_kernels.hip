@@ -433,27 +433,23 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
 #else
 #define ORB_WPE8
 #endif
+// the tail-strip path must not raise k_blur's register count above the
+// strip path's 68 (7 waves a SIMD)
+#if ORB_OCC8
+#define ORB_BLUR_WPE
+#else
+#define ORB_BLUR_WPE __attribute__((amdgpu_waves_per_eu(7, 8)))
+#endif
 #ifndef ORB_BLUR_PF
 #define ORB_BLUR_PF 6  // (call L: 6 / 4 / 8 rows -> 68 / 62 / 73 VGPRs, 131.4k / 131.3k / 131.0k frames/s)
 #endif
-__global__ __launch_bounds__(256) ORB_WPE8 void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
-                                              const uint8_t* __restrict__ pyr,
-                                              uint8_t* __restrict__ blur) {
-  constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
-  const int img = wid / P->blur_tiles;
-  int t = wid - img * P->blur_tiles;
-  int l = 0;
-  while (l + 1 < P->levels && t >= P->lev[l + 1].blur_tile_begin) ++l;
-  const LevelGeom& g = P->lev[l];
-  t -= g.blur_tile_begin;
-  const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
-  const int x = tx * kBlurTileW + 4 * (threadIdx.x & 63);
-  // wave-uniform row origin: row addressing and row bounds stay scalar
-  const int ys = ty * kBlurTileH + R * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (x >= g.w || ys >= g.h) return;
-  int sp;
-  const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
+// One wave's blur strip: every lane owns columns x..x+3 of R output rows from
+// ys (kTail: ys per lane -- the strips of a tail wave -- else wave-uniform).
+template <bool kTail>
+__device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, const LevelGeom& g,
+                                           const uint8_t* S, int sp, uint8_t* __restrict__ dst,
+                                           int x, int ys) {
+  constexpr int R = kBlurTileH / 4;  // output rows per thread
   const uint32_t base = (uint32_t)min(max(x - 4, 0), g.w - 12);
   // Streamed down the strip: the 3 dword loads of source row r + kPf are
   // issued while row r is filtered horizontally, and output row r - 6 leaves
@@ -467,11 +463,14 @@ __global__ __launch_bounds__(256) ORB_WPE8 void k_blur(const PlanHeader* __restr
   // opaque to alias analysis and would make them reloaded every row
   const int gh = g.h, pitch = g.pitch;
   // raw buffer accesses: the lane's column is the VGPR offset, the row the
-  // SGPR offset, so no per-row 64-bit address arithmetic on the VALU
+  // SGPR offset (kTail: the row is per lane, in the VGPR offset), so no
+  // per-row 64-bit address arithmetic on the VALU
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(S), (short)0, (int)0xffffffff, kBufRsrcWord3);
   auto load_row = [&](int r) {
-    const auto w = __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base, reflect101(ys - 3 + r, gh) * sp, 0);
+    const int ro = reflect101(ys - 3 + r, gh) * sp;
+    const auto w = kTail ? __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base + ro, 0, 0)
+                         : __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base, ro, 0);
 #pragma unroll
     for (int k = 0; k < 3; ++k) d[r][k] = w[k];
   };
@@ -487,8 +486,8 @@ __global__ __launch_bounds__(256) ORB_WPE8 void k_blur(const PlanHeader* __restr
   const ushort2_t k01 = as_us2(18u | (34u << 16)), k23 = as_us2(48u | (56u << 16));
   const ushort2_t k45 = as_us2(48u | (34u << 16)), k6 = as_us2(18u);
   // columns past w land in the row's pitch padding (pitch is a multiple of 16)
-  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-      blur + (size_t)img * P->blur_bytes + g.blur_off, (short)0, (int)0xffffffff, kBufRsrcWord3);
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)0xffffffff,
+                                                                       kBufRsrcWord3);
   uint32_t hw[R + 6][4];
   uint32_t pr[R + 5][4];  // pr[r] = hw[r] | hw[r+1] << 16
 #pragma unroll
@@ -525,11 +524,47 @@ __global__ __launch_bounds__(256) ORB_WPE8 void k_blur(const PlanHeader* __restr
           a = __builtin_amdgcn_udot2(as_us2(pr[o + 4][j]), k45, a, false);
           v[j] = __builtin_amdgcn_udot2(as_us2(hw[o + 6][j]), k6, a, false);
         }
-        __builtin_amdgcn_raw_buffer_store_b32(
-            __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu),
-            drs, x, (ys + o) * pitch, 0);
+        const uint32_t packed =
+            __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
+        if (kTail)
+          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x + (ys + o) * pitch, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x, (ys + o) * pitch, 0);
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(256) ORB_WPE8 ORB_BLUR_WPE void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
+                                              const uint8_t* __restrict__ pyr,
+                                              uint8_t* __restrict__ blur) {
+  constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = wid / P->blur_tiles;
+  int t = wid - img * P->blur_tiles;
+  int l = 0;
+  while (l + 1 < P->levels && t >= P->lev[l + 1].blur_tile_begin) ++l;
+  const LevelGeom& g = P->lev[l];
+  t -= g.blur_tile_begin;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sp;
+  const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
+  uint8_t* dst = blur + (size_t)img * P->blur_bytes + g.blur_off;
+  const int nfull = g.tiles_x * g.tiles_y;
+  if (t < nfull) {
+    const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
+    const int x = tx * kBlurTileW + 4 * lane;
+    // wave-uniform row origin: row addressing and row bounds stay scalar
+    const int ys = ty * kBlurTileH + R * wave;
+    if (x >= g.w || ys >= g.h) return;
+    blur_strip<false>(P, g, S, sp, dst, x, ys);
+  } else {
+    // tail wave: tail_s strips of tail_nl lanes, strip s at rows ys0 + 32 s
+    const int tw = 4 * (t - nfull) + wave;
+    const int s = lane / g.tail_nl, c = lane - s * g.tail_nl;
+    const int x = g.tiles_x * kBlurTileW + 4 * c, ys = (tw * g.tail_s + s) * R;
+    if (s >= g.tail_s || x >= g.w || ys >= g.h) return;
+    blur_strip<true>(P, g, S, sp, dst, x, ys);
   }
 }
 

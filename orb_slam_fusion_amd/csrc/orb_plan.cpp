@@ -94,9 +94,24 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
     g.blur_off = blur;
     blur += g.pitch * g.h;
     g.blur_tile_begin = tiles;
-    g.tiles_x = (g.w + kBlurTileW - 1) / kBlurTileW;
     g.tiles_y = (g.h + kBlurTileH - 1) / kBlurTileH;
-    tiles += g.tiles_x * g.tiles_y;
+    {
+      const int fx = g.w / kBlurTileW, tw = g.w - fx * kBlurTileW, nl = (tw + 3) / 4;
+#ifndef ORB_BLUR_TAIL
+#define ORB_BLUR_TAIL 1  // A/B build switch: 0 = every tail is one more tile column
+#endif
+      if (ORB_BLUR_TAIL && tw > 0 && nl <= 32) {  // >= 2 strips a wave: a strip path
+        g.tiles_x = fx;
+        g.tail_nl = nl;
+        g.tail_s = 64 / nl;
+        const int waves = (g.h + 32 * g.tail_s - 1) / (32 * g.tail_s);
+        g.tail_blocks = (waves + 3) / 4;
+      } else {
+        g.tiles_x = fx + (tw > 0);
+        g.tail_nl = g.tail_s = g.tail_blocks = 0;
+      }
+    }
+    tiles += g.tiles_x * g.tiles_y + g.tail_blocks;
 
     // resize taps for level l from level l-1 (cv::resize INTER_LINEAR)
     if (l > 0) {

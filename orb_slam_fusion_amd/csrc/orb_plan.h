@@ -41,8 +41,13 @@ struct LevelGeom {
   int out_off;       // first output slot of this level in an image's keypoint block
   int out_cap;       // node-count bound: max(budget + 3, 4 * n_roots)
   int quad_off;      // first k_describe wave (4 output slots each) of this level in an image
-  // blur tiling (kBlurTileW x kBlurTileH outputs per 256-thread block)
+  // blur tiling (kBlurTileW x kBlurTileH outputs per 256-thread block): tiles_x
+  // x tiles_y full-width tiles, then the tail columns [tiles_x * 256, w) when
+  // they need at most 32 lanes: packed as tail_s strips of tail_nl lanes x 32
+  // rows per wave (tail_blocks blocks of 4 such waves); a wider tail is one
+  // more tile column (tail_blocks = 0)
   int blur_tile_begin, tiles_x, tiles_y;
+  int tail_nl, tail_s, tail_blocks;
 };
 
 struct Cell {
