@@ -159,7 +159,7 @@ def main() -> int:
     ap.add_argument("--pipes", type=int, default=4,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
                          "each launch group split evenly between them)")
-    ap.add_argument("--phase-stage", type=int, default=1,
+    ap.add_argument("--phase-stage", type=int, default=2,
                     help="pipeline k+1 starts each launch group when pipeline k has finished this "
                          "stage of it (0 pyramid .. 5 assembly; -1: no offset)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

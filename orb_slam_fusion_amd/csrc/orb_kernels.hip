@@ -188,36 +188,11 @@ __device__ __forceinline__ void rs_horiz(const RsRow& r, int off, const uint32_t
 // buffer resource word 3 for raw (stride 0, untyped dword) accesses on gfx9
 constexpr int kBufRsrcWord3 = 0x00020000;
 
-// One output tile (tyx) of level l of image img by 256 threads (tid) with an
-// LDS slice of PlanHeader::rs_lds bytes; every thread of the workgroup passes
-// its one barrier.  live = false: the group takes part in the barrier and
-// writes nothing (k_pyramid's spare groups).
-__device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
-                                            const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
-                                            int tyx, uint8_t* __restrict__ lds, int tid, bool live) {
-  constexpr int RW = kResizeTileH / 4;  // output rows per wave
-  const LevelGeom& g = P->lev[l];
-  const int sw = P->lev[l - 1].w;
-  const int x0 = (tyx % g.rs_tiles_x) * kResizeTileW, y0 = (tyx / g.rs_tiles_x) * kResizeTileH;
-  const int xl = min(x0 + kResizeTileW, g.w) - 1, yl = min(y0 + kResizeTileH, g.h) - 1;
-  const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
-  const int2* yt = reinterpret_cast<const int2*>(rs_tab + g.rs_y);
-  const int c0 = xt[x0].x & ~15;
-  const int c1 = min(xt[xl].x + 1, sw - 1) | 15;
-  const int rr0 = yt[y0].x & 0xffff, rr1 = yt[yl].x >> 16;
-  const int ncol = c1 - c0 + 1, nrow = rr1 - rr0 + 1;  // ncol: multiple of 16
-  int sp;
-  const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
-
-  // taps, fetched up front (before any store, so no wait ever queues behind one)
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int x = x0 + 4 * lane;
-  const int ys = y0 + RW * wave;  // wave-uniform first output row
-  int2 xa[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) xa[k] = xt[min(x + k, g.w - 1)];
-  const int2 tl = yt[min(ys + (lane & (RW - 1)), yl)];
-
+// Stages source rows [rr0, rr0 + nrow) x columns [c0, c1] (ncol = c1 - c0 + 1,
+// a multiple of 16) of a level plane into LDS (row pitch ncol), 256 threads.
+__device__ __forceinline__ void rs_stage(const uint8_t* S, int sp, int sw, int c0, int c1, int rr0, int nrow,
+                                         uint8_t* __restrict__ lds, int tid) {
+  const int ncol = c1 - c0 + 1;
   // 16-byte chunks when rows are 16-aligned and no chunk straddles the end of a
   // source row: chunks wholly past it are skipped (their LDS bytes only meet
   // the zero weight of the single-tap columns, sx + 1 = sw)
@@ -251,6 +226,40 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
       lds[i] = S[(size_t)(rr0 + r) * sp + min(c0 + c, sw - 1)];
     }
   }
+
+}
+
+// One output tile (tyx) of level l of image img by 256 threads (tid) with an
+// LDS slice of PlanHeader::rs_lds bytes; every thread of the workgroup passes
+// its one barrier.  live = false: the group takes part in the barrier and
+// writes nothing (k_pyramid's spare groups).
+__device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
+                                            const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
+                                            int tyx, uint8_t* __restrict__ lds, int tid, bool live) {
+  constexpr int RW = kResizeTileH / 4;  // output rows per wave
+  const LevelGeom& g = P->lev[l];
+  const int sw = P->lev[l - 1].w;
+  const int x0 = (tyx % g.rs_tiles_x) * kResizeTileW, y0 = (tyx / g.rs_tiles_x) * kResizeTileH;
+  const int xl = min(x0 + kResizeTileW, g.w) - 1, yl = min(y0 + kResizeTileH, g.h) - 1;
+  const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
+  const int2* yt = reinterpret_cast<const int2*>(rs_tab + g.rs_y);
+  const int c0 = xt[x0].x & ~15;
+  const int c1 = min(xt[xl].x + 1, sw - 1) | 15;
+  const int rr0 = yt[y0].x & 0xffff, rr1 = yt[yl].x >> 16;
+  const int ncol = c1 - c0 + 1, nrow = rr1 - rr0 + 1;  // ncol: multiple of 16
+  int sp;
+  const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
+
+  // taps, fetched up front (before any store, so no wait ever queues behind one)
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int x = x0 + 4 * lane;
+  const int ys = y0 + RW * wave;  // wave-uniform first output row
+  int2 xa[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xa[k] = xt[min(x + k, g.w - 1)];
+  const int2 tl = yt[min(ys + (lane & (RW - 1)), yl)];
+
+  rs_stage(S, sp, sw, c0, c1, rr0, nrow, lds, tid);
 
   // per-lane column taps -> byte selectors relative to the lane's LDS window
   int sx[4], sx1[4];
@@ -345,6 +354,79 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
   }
 }
 
+// The narrow right-hand tail of level l (columns [rs_tail_x0, w): at most
+// kRsTailGroups groups of 4) for output rows [64 tb, 64 tb + 64): in the tile
+// layout those columns would leave most lanes of their waves idle.  Here lane
+// = output row, the 4 waves share the 64 rows and take the column groups
+// round robin; a group's taps are wave-uniform (scalar), every lane runs the
+// horizontal pass on its own two source rows (no reuse across output rows)
+// and the same vertical rounding as resize_tile: the same bytes.  One barrier
+// (after staging), as resize_tile.
+__device__ __forceinline__ void resize_tail(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
+                                            const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
+                                            int tb, uint8_t* __restrict__ lds, int tid) {
+  const LevelGeom& g = P->lev[l];
+  const int sw = P->lev[l - 1].w;
+  const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
+  const int2* yt = reinterpret_cast<const int2*>(rs_tab + g.rs_y);
+  const int x0 = g.rs_tail_x0, y0 = 64 * tb, yl = min(y0 + 63, g.h - 1);
+  const int c0 = xt[x0].x & ~15;
+  const int c1 = min(xt[g.w - 1].x + 1, sw - 1) | 15;
+  const int rr0 = yt[y0].x & 0xffff, rr1 = yt[yl].x >> 16;
+  const int ncol = c1 - c0 + 1, nrow = rr1 - rr0 + 1;
+  int sp;
+  const uint8_t* S = level_plane(P, src, pyr, img, l - 1, sp);
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int y = y0 + lane;
+  const int2 ty = yt[min(y, yl)];
+  rs_stage(S, sp, sw, c0, c1, rr0, nrow, lds, tid);
+  __syncthreads();
+  const uint8_t* rowA = lds + ((ty.x & 0xffff) - rr0) * ncol;
+  const uint8_t* rowB = lds + ((int)((uint32_t)ty.x >> 16) - rr0) * ncol;
+  const uint32_t b0 = (uint32_t)ty.y & 0xffffu, b1 = (uint32_t)ty.y >> 16;
+  const uint32_t s0 = b0 << 12, s1 = b1 << 12;
+  uint8_t* D = pyr + (size_t)img * P->pyr_bytes + g.pyr_off + (size_t)min(y, yl) * g.pitch;
+  const int ng = (g.w - x0 + 3) >> 2;
+  for (int q = wave; q < ng; q += 4) {  // wave-uniform
+    const int x = x0 + 4 * q;
+    int sx[4], sx1[4], bi[4];
+    uint32_t aw[4], tail_k = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int2 xa = xt[min(x + k, g.w - 1)];
+      sx[k] = xa.x - c0;
+      sx1[k] = min(xa.x + 1, c1) - c0;
+      aw[k] = (uint32_t)xa.y;
+      bi[k] = sx[k] | (sx1[k] << 16);
+      if (min(x + k, g.w - 1) >= g.vec8_end) tail_k |= 1u << k;
+    }
+    const int lo = min(min(sx[0], sx[1]), min(sx[2], sx[3]));
+    const int hi = max(max(sx1[0], sx1[1]), max(sx1[2], sx1[3]));
+    const int base4 = lo & ~3, off = lo & 3;
+    uint32_t sel[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      sel[k] = (uint32_t)(sx[k] - lo) | 0x0c00u | ((uint32_t)(sx1[k] - lo) << 16) | 0x0c000000u;
+    const bool bytewise = hi - lo > 7;
+    uint32_t hA[4], qA[4], hB[4], qB[4];
+    rs_horiz(rs_load(rowA, base4, bi, bytewise), off, sel, aw, bytewise, hA, qA);
+    rs_horiz(rs_load(rowB, base4, bi, bytewise), off, sel, aw, bytewise, hB, qB);
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2;
+    if (tail_k) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (tail_k & (1u << k)) v[k] = ((hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22) << 2;
+    }
+    const ushort2_t p01 = as_us2(v[0] | (v[1] << 16)) >> (ushort2_t){2, 2};
+    const ushort2_t p23 = as_us2(v[2] | (v[3] << 16)) >> (ushort2_t){2, 2};
+    if (y <= yl)
+      *reinterpret_cast<uint32_t*>(D + x) =
+          __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
+  }
+}
+
 // k_resize: one tile per workgroup, one launch per level (tiles of all the
 // batch's images).
 __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P,
@@ -352,11 +434,14 @@ __global__ __launch_bounds__(256) void k_resize(const PlanHeader* __restrict__ P
                                                 uint8_t* __restrict__ pyr, int l) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const LevelGeom& g = P->lev[l];
-  const int nb = gridDim.x * gridDim.y * gridDim.z;
-  const int wid = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nb);
-  const int img = wid / (g.rs_tiles_x * g.rs_tiles_y);
-  const int tyx = wid - img * (g.rs_tiles_x * g.rs_tiles_y);
-  resize_tile(P, rs_tab, src, pyr, l, img, tyx, lds, threadIdx.x, true);
+  const int nt = g.rs_tiles_x * g.rs_tiles_y, per = nt + g.rs_tail_blocks;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = wid / per;
+  const int t = wid - img * per;
+  if (t < nt)
+    resize_tile(P, rs_tab, src, pyr, l, img, t, lds, threadIdx.x, true);
+  else
+    resize_tail(P, rs_tab, src, pyr, l, img, t - nt, lds, threadIdx.x);
 }
 
 // k_pyramid: the whole chain (levels 1 .. L-1) of one image per workgroup of
@@ -378,10 +463,13 @@ __global__ __launch_bounds__(1024) void k_pyramid(const PlanHeader* __restrict__
   uint8_t* const my = lds + grp * rs_lds;
   for (int l = 1; l < P->levels; ++l) {
     const LevelGeom& g = P->lev[l];
-    const int nt = g.rs_tiles_x * g.rs_tiles_y;
+    const int nm = g.rs_tiles_x * g.rs_tiles_y, nt = nm + g.rs_tail_blocks;
     for (int t0 = 0; t0 < nt; t0 += G) {
       const int tile = t0 + grp;
-      resize_tile(P, rs_tab, src, pyr, l, img, tile < nt ? tile : 0, my, tid, tile < nt);
+      if (tile >= nm && tile < nt)  // group-uniform; one barrier either way
+        resize_tail(P, rs_tab, src, pyr, l, img, tile - nm, my, tid);
+      else
+        resize_tile(P, rs_tab, src, pyr, l, img, tile < nt ? tile : 0, my, tid, tile < nt);
       __syncthreads();  // the slice is restaged by the group's next tile; the level is complete
     }
   }
@@ -1971,8 +2059,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   } else {
     for (int l = 1; l < H.levels; ++l) {
       const LevelGeom& g = H.lev[l];
-      dim3 grid(g.rs_tiles_x, g.rs_tiles_y, n);
-      hipLaunchKernelGGL(k_resize, grid, dim3(256), H.rs_lds, st, a.plan, a.rs_tab, src, a.pyr, l);
+      const unsigned blocks = (unsigned)(g.rs_tiles_x * g.rs_tiles_y + g.rs_tail_blocks) * (unsigned)n;
+      hipLaunchKernelGGL(k_resize, dim3(blocks), dim3(256), H.rs_lds, st, a.plan, a.rs_tab, src, a.pyr, l);
     }
   }
   mark(1);

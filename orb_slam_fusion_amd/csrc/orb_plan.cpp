@@ -146,6 +146,20 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
       // largest source window of a kResizeTileW x kResizeTileH output tile
       g.rs_tiles_x = (g.w + kResizeTileW - 1) / kResizeTileW;
       g.rs_tiles_y = (g.h + kResizeTileH - 1) / kResizeTileH;
+      // a narrow right-hand tail goes to resize_tail (lane = output row)
+      g.rs_tail_x0 = 0;
+      g.rs_tail_blocks = 0;
+      {
+#ifndef ORB_RS_TAIL
+#define ORB_RS_TAIL 1  // A/B build switch: 0 = the tiles cover every column
+#endif
+        const int fx = g.w / kResizeTileW, ng = (g.w - fx * kResizeTileW + 3) / 4;
+        if (ORB_RS_TAIL && ng > 0 && ng <= kRsTailGroups) {
+          g.rs_tiles_x = fx;
+          g.rs_tail_x0 = fx * kResizeTileW;
+          g.rs_tail_blocks = (g.h + 63) / 64;
+        }
+      }
       g.rs_src_cols = 0;
       g.rs_src_rows = 0;
       const int* tab = out.rs_tab.data();
@@ -159,6 +173,17 @@ bool make_plan(const orbgpu_orb_params& p, int W, int H, HostPlan& out, std::str
         const int ya = ty * kResizeTileH, yb = std::min(ya + kResizeTileH, g.h) - 1;
         const int r0 = tab[g.rs_y + 2 * ya] & 0xffff, r1 = tab[g.rs_y + 2 * yb] >> 16;
         g.rs_src_rows = std::max(g.rs_src_rows, r1 - r0 + 1);
+      }
+      if (g.rs_tail_blocks) {  // resize_tail's windows: the tail columns x 64 output rows
+        const int c0 = tab[g.rs_x + 2 * g.rs_tail_x0] & ~15;
+        const int c1 = std::min(tab[g.rs_x + 2 * (g.w - 1)] + 1, s.w - 1) | 15;
+        for (int b = 0; b < g.rs_tail_blocks; ++b) {
+          const int ya = 64 * b, yb = std::min(ya + 63, g.h - 1);
+          const int r0 = tab[g.rs_y + 2 * ya] & 0xffff, r1 = tab[g.rs_y + 2 * yb] >> 16;
+          const int nq = (c1 - c0 + 1) / 16;
+          if ((long long)(r1 - r0 + 1) * nq * nq >= (1 << 19)) return why = "scale factor too large for the resize tail", false;
+          rs_lds = std::max(rs_lds, (c1 - c0 + 1) * (r1 - r0 + 1) + 16);
+        }
       }
       rs_lds = std::max(rs_lds, g.rs_src_cols * g.rs_src_rows + 16);  // + k_resize's 3-dword overreach
       // k_resize splits a staging index i < rows x nq by the multiply-shift

@@ -27,6 +27,8 @@ struct LevelGeom {
   int xmax;          // first dst column whose right neighbour is out of range
   int rs_tiles_x, rs_tiles_y;  // resize tiles (kResizeTileW x kResizeTileH outputs)
   int rs_src_cols, rs_src_rows;  // largest source window of a tile (LDS staging)
+  int rs_tail_x0;      // first column of the tail path (resize_tail), when rs_tail_blocks > 0
+  int rs_tail_blocks;  // 64-row blocks of the tail path (0: the tiles cover every column)
   int vec16_end;     // VResizeLinearVec_32s8u: 16-lane blocks end here
   int vec8_end;      //                          8-lane blocks end here
   // FAST grid (:748-825)
@@ -81,6 +83,7 @@ struct PlanHeader {
 
 constexpr int kBlurTileW = 256, kBlurTileH = 128;   // 64 threads x 4 cols, 4 waves x 32 rows
 constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 4 waves x 8 rows, 64 lanes x 4 px
+constexpr int kRsTailGroups = 48;  // widest tail (4-column groups) taken by resize_tail
 constexpr int kLevelAlign = 16;
 constexpr int kOctreeLdsCand = 2048;  // octree candidates per (image, level) kept in LDS (rest in HBM)
 constexpr int kOctreeLdsMax = 160 * 1024;  // LDS of one gfx950 workgroup
