@@ -1659,23 +1659,27 @@ __constant__ IcTab c_ic = make_ic_tab();
 // wave-uniform: both patches are staged by raw buffer loads whose row step is
 // the SGPR offset (2 rows x 8 dwords per step, the 9th / 9th-10th dword
 // columns in their own steps) -- no per-load address VALU -- 42 dword loads a
-// lane in flight.  IC_Angle: item i = j + 16 k of the same c_ic table (row
-// i / 9, dword i % 9), a 16-lane rotate-add reduction (row_ror 8, 4, 2, 1).
-// BRIEF: lane j computes tests 16 j .. 16 j + 15 of its keypoint -- the
-// reference's fmaf offsets and cvRound as the round-4 kernel -- and shifts
-// each t0 < t1 (the sign of t0 - t1) into its u16 by one v_alignbit, then
-// stores descriptor bytes 2 j, 2 j + 1.  Dead slots of a live wave replay
-// the level's last live keypoint and store nothing.
+// lane in flight.  The IC_Angle weights (W_u, W_1 per item; W_v = row x W_1,
+// the item's LDS offset 4 i) and the BRIEF pattern live in the workgroup's
+// LDS (filled once per 4-wave block): the constant-table round trips to the
+// L1/L2 that made the first version of this kernel wait were most of its time.
+// IC_Angle: item i = j + 16 k (row i / 9, dword i % 9), a 16-lane rotate-add
+// reduction (row_ror 8, 4, 2, 1).  BRIEF: lane j computes tests 16 j .. 16 j +
+// 15 of its keypoint -- the reference's fmaf offsets and cvRound as the
+// one-keypoint kernel -- and shifts each t0 < t1 (the sign of t0 - t1) into
+// its u16 by one v_alignbit, then stores descriptor bytes 2 j, 2 j + 1.
+// Dead slots of a live wave replay the level's last live keypoint and store
+// nothing.
 constexpr int kRawRows = 32, kBlurRows = 38;  // one spare row each: 2-row load steps
-#ifndef ORB_DESC_REUSE
-#define ORB_DESC_REUSE 1  // the blurred patch overwrites the raw one after IC_Angle
-#endif
 #ifndef ORB_DESC_WG
-#define ORB_DESC_WG 1  // waves per k_describe workgroup
+#define ORB_DESC_WG 4  // waves per k_describe workgroup (they share the tables)
 #endif
-constexpr int kDescSlice = ORB_DESC_REUSE ? (kBlurW * kBlurRows + 15) & ~15
-                                          : (kRawW * kRawRows + kBlurW * kBlurRows + 15) & ~15;
+constexpr int kDescSlice = (kBlurW * kBlurRows + 15) & ~15;  // the blurred patch reuses the raw one's bytes
 constexpr int kDescWaveLds = 4 * kDescSlice;
+constexpr int kIcItems4 = 288;                  // 18 x 16 items (279 live)
+constexpr int kDescPatLds = 256 * 16;           // BRIEF pattern, float4 per test
+constexpr int kDescIcLds = 4 * kIcItems4 * 8;   // IC weights (W_u, W_1) per alignment o
+constexpr int kDescTabLds = kDescPatLds + kDescIcLds;
 
 __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {  // sum over the lane's 16-lane row
   v += __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8
@@ -1692,10 +1696,22 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
                                                  const int* __restrict__ oct_count,
                                                  float* __restrict__ angle_out,
                                                  uint64_t* __restrict__ desc_out, int n_img) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_wg[ORB_DESC_WG * kDescWaveLds];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_wg[kDescTabLds + ORB_DESC_WG * kDescWaveLds];
+  // ---- the block's tables (every wave takes part: the barrier comes first)
+  {
+    const int t = threadIdx.x;
+    for (int i = t; i < 256; i += 64 * ORB_DESC_WG)
+      reinterpret_cast<float4*>(lds_wg)[i] = c_pattern_f[i];
+    for (int i = t; i < 4 * kIcItems4; i += 64 * ORB_DESC_WG) {
+      const int o = i / kIcItems4, it = i - o * kIcItems4;
+      reinterpret_cast<uint2*>(lds_wg + kDescPatLds)[i] = make_uint2(c_ic.e[o][it][0], c_ic.e[o][it][2]);
+    }
+  }
+  __syncthreads();
+  const float4* pat = reinterpret_cast<const float4*>(lds_wg);
   const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
   const int wave = ORB_DESC_WG > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  uint8_t* lds_all = lds_wg + wave * kDescWaveLds;
+  uint8_t* lds_all = lds_wg + kDescTabLds + wave * kDescWaveLds;
   const int nq = P->kp_quads;
   const int gidx = xcd_remap(blockIdx.x, gridDim.x) * ORB_DESC_WG + wave;
   if (gidx >= n_img * nq) return;  // wave-uniform
@@ -1711,7 +1727,7 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
   const uint32_t kp = oct_out[(size_t)img * P->kp_slots + slot];
   const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
   uint8_t* raw = lds_all + g * kDescSlice;
-  uint8_t* blp = ORB_DESC_REUSE ? raw : raw + kRawW * kRawRows;
+  uint8_t* blp = raw;
 
   // ---- both patches: rows 2k + (j >> 3), dword j & 7 (SGPR row step), then
   // the raw 9th dword (rows j, j + 16) and the blurred 9th / 10th (rows
@@ -1749,7 +1765,33 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
 #pragma unroll
     for (int m = 0; m < 2; ++m) d8[m * 16 * kRawW / 4] = r_c8[m];
   }
-  auto stage_blurred = [&]() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // ---- IC_Angle: items j + 16 k, k < 18 (288 >= 279; the rest zero).  Raw
+  // rows are 9 dwords, so item i sits at byte 4 i
+  int m10, m01;
+  {
+    const uint2* tab = reinterpret_cast<const uint2*>(lds_wg + kDescPatLds) + ((cx - 15) & 3) * kIcItems4;
+    uint32_t A = 0, B = 0, S = 0;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+      const int i = 16 * k + j;
+      const uint2 w = tab[i];
+      const uint32_t val = *reinterpret_cast<const uint32_t*>(raw + 4 * i);
+      // the item's row sum s (<= 1020) weighted by its row i / 9 (exact
+      // below 4369) is its part of B: every in-circle byte of a row has v + 15 = row
+      const uint32_t si = __builtin_amdgcn_udot4(val, w.y, 0u, false);
+      A = __builtin_amdgcn_udot4(val, w.x, A, false);
+      B = __umul24((uint32_t)i * 7282u >> 16, si) + B;
+      S += si;
+    }
+    const int s = (int)row_sum16(S);
+    m10 = (int)row_sum16(A) - 15 * s;
+    m01 = (int)row_sum16(B) - 15 * s;
+  }
+  {  // the raw patch's reads are done (in order within the wave): the blurred one takes its bytes
     uint32_t* e = reinterpret_cast<uint32_t*>(blp + rh * kBlurW + 4 * rq);
 #pragma unroll
     for (int k = 0; k < 19; ++k) e[k * 2 * kBlurW / 4] = b_main[k];
@@ -1757,35 +1799,10 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
 #pragma unroll
     for (int m = 0; m < 5; ++m)
       if (m < 4 || b8_last) e8[m * 8 * kBlurW / 4] = b_c8[m];
-  };
-  if (!ORB_DESC_REUSE) stage_blurred();
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  // ---- IC_Angle (see c_ic): items j + 16 k, k < 18 (288 >= 279; the rest zero)
-  int m10, m01;
-  {
-    const uint32_t(*tab)[4] = c_ic.e[(cx - 15) & 3];
-    uint32_t A = 0, B = 0, S = 0;
-#pragma unroll
-    for (int k = 0; k < 18; ++k) {
-      const uint4 w = *reinterpret_cast<const uint4*>(tab[16 * k + j]);
-      const uint32_t val = *reinterpret_cast<const uint32_t*>(raw + w.w);
-      A = __builtin_amdgcn_udot4(val, w.x, A, false);
-      B = __builtin_amdgcn_udot4(val, w.y, B, false);
-      S = __builtin_amdgcn_udot4(val, w.z, S, false);
-    }
-    const int s = (int)row_sum16(S);
-    m10 = (int)row_sum16(A) - 15 * s;
-    m01 = (int)row_sum16(B) - 15 * s;
-  }
-  if (ORB_DESC_REUSE) {  // the raw patch's reads are done (in order within the wave)
-    stage_blurred();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
   const float angle = dev_fast_atan2((float)m01, (float)m10);
   const float ang = angle * (float)(3.14159265358979323846 / 180.0);
   const float a = dev_cosf(ang), b = dev_sinf(ang);
@@ -1796,9 +1813,9 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 15; i >= 0; --i) {
-    const float4 pt = c_pattern_f[16 * j + i];
+    const float4 pt = pat[16 * j + i];
     const f32x2 X = {pt.x, pt.y}, Y = {pt.z, pt.w};
-    constexpr float kMagic = 12582912.0f;  // cvRound as in the round-4 kernel (below)
+    constexpr float kMagic = 12582912.0f;  // cvRound as in the one-keypoint kernel (below)
     const f32x2 R = __builtin_elementwise_fma(X, (f32x2){b, b}, Y * (f32x2){a, a}) + (f32x2){kMagic, kMagic};
     const f32x2 Q = __builtin_elementwise_fma(X, (f32x2){a, a}, Y * (f32x2){-b, -b}) + (f32x2){kMagic, kMagic};
     const int t0 = ctr_m[__umul24(__float_as_uint(R.x), (uint32_t)kBlurW) + __float_as_uint(Q.x)];

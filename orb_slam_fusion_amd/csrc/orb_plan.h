@@ -85,7 +85,10 @@ constexpr int kBlurTileW = 256, kBlurTileH = 128;   // 64 threads x 4 cols, 4 wa
 constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 4 waves x 8 rows, 64 lanes x 4 px
 constexpr int kRsTailGroups = 48;  // widest tail (4-column groups) taken by resize_tail
 constexpr int kLevelAlign = 16;
-constexpr int kOctreeLdsCand = 2048;  // octree candidates per (image, level) kept in LDS (rest in HBM)
+#ifndef ORB_OCT_KCAP
+#define ORB_OCT_KCAP 1024  // (A/B: 2048 -> 0.114 ms, 1024 -> 0.099 ms per 256 images: more blocks a CU)
+#endif
+constexpr int kOctreeLdsCand = ORB_OCT_KCAP;  // octree candidates per (image, level) kept in LDS (rest in HBM)
 constexpr int kOctreeLdsMax = 160 * 1024;  // LDS of one gfx950 workgroup
 
 // Bytes of the octree's node arrays for node capacity nc: the 64-bit best
