@@ -86,7 +86,7 @@ constexpr int kResizeTileW = 256, kResizeTileH = 32;  // 4 waves x 8 rows, 64 la
 constexpr int kRsTailGroups = 48;  // widest tail (4-column groups) taken by resize_tail
 constexpr int kLevelAlign = 16;
 #ifndef ORB_OCT_KCAP
-#define ORB_OCT_KCAP 1024  // (A/B: 2048 -> 0.114 ms, 1024 -> 0.099 ms per 256 images: more blocks a CU)
+#define ORB_OCT_KCAP 2048  // A/B: 1024 -> 0.099 ms per 256 images isolated (0.114), bench flat, single-image latency worse
 #endif
 constexpr int kOctreeLdsCand = ORB_OCT_KCAP;  // octree candidates per (image, level) kept in LDS (rest in HBM)
 constexpr int kOctreeLdsMax = 160 * 1024;  // LDS of one gfx950 workgroup
