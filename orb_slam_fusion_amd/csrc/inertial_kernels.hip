@@ -683,6 +683,60 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
   if (sum_here && t < 27) vis_sum(sh, t);
 }
 
+// In-place LDL^T of the 15 x 15 symmetric A (lower triangle, stride kLd) on
+// one wave, natural pivot order: D on the diagonal, L below it.  Lane-owned
+// entries (k = lane + 64 u); one wave_sync per half step.  Returns whether
+// every pivot was > 0 (A positive definite).
+__device__ __forceinline__ bool ldlt15(double* A, int lane) {
+  bool pd = true;
+#pragma unroll 1
+  for (int j = 0; j < 15; ++j) {
+    const double d = A[j * kLd + j];
+    pd = pd && d > 0.0;
+    const double inv = d != 0.0 ? 1.0 / d : 0.0;
+    double nv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u, i = k / 15, c = k - 15 * (k / 15);
+      nv[u] = k < 225 && i > j && c > j && c <= i ? A[i * kLd + c] - A[i * kLd + j] * A[c * kLd + j] * inv : 0.0;
+    }
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = lane + 64 * u, i = k / 15, c = k - 15 * (k / 15);
+      if (k < 225 && i > j && c > j && c <= i) A[i * kLd + c] = nv[u];
+    }
+    if (lane > j && lane < 15) A[lane * kLd + j] *= inv;
+    wave_sync();
+  }
+  return pd;
+}
+
+// X = A^-1 (15 x 15, row stride 16) from the LDL^T factors in A: column c of
+// L^-1 by forward substitution (lane c, in place in X: a lane reads only the
+// entries it wrote), D^-1, then L^-T.  Loops kept rolled: this runs once per
+// call and must not add registers to the kernel's Gauss-Newton loop.
+__device__ __forceinline__ void ldlt15_inverse(const double* A, double* X, int lane) {
+  if (lane < 15) {
+    const int c = lane;
+#pragma unroll 1
+    for (int i = 0; i < 15; ++i) {
+      double v = i == c ? 1.0 : 0.0;
+#pragma unroll 1
+      for (int k = 0; k < i; ++k) v -= A[i * kLd + k] * X[k * 16 + c];
+      X[i * 16 + c] = v;
+    }
+#pragma unroll 1
+    for (int i = 14; i >= 0; --i) {
+      double v = X[i * 16 + c] / A[i * kLd + i];
+#pragma unroll 1
+      for (int k = i + 1; k < 15; ++k) v -= A[k * kLd + i] * X[k * 16 + c];
+      X[i * 16 + c] = v;
+    }
+  }
+  wave_sync();
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     CalibD cal, const orbgpu_imu_state* __restrict__ g_cur, const orbgpu_imu_state* __restrict__ g_prev,
@@ -924,11 +978,35 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
       sh.HM[i * kLd + j] = s;
     }
     __syncthreads();
-    // Marginalize(H, 0, 14): pinv of the previous-frame block (wave 0,
-    // parallel cyclic Jacobi on a 16 x 16 padding), then the Schur complement
+    // Marginalize(H, 0, 14): pinv of the previous-frame block, then the Schur
+    // complement.  The pseudo-inverse drops eigenvalues at or below 1e-6; when
+    // H_pp - tau I is positive definite (an LDL^T with every pivot > 0, tau =
+    // max(2e-6, 1e-12 max|diag|): larger than the cut plus the factorisation's
+    // rounding) none is dropped and pinv = H_pp^-1, taken from the LDL^T of
+    // H_pp (fast path, a few thousand cycles).  Otherwise the parallel cyclic
+    // Jacobi below (wave 0, on a 16 x 16 padding) with the cut.
     if (wave == 0) {
       double* A = sh.H;   // 16 x 16 working copy (stride kLd)
       double* V = sh.V;   // 16 x 16 eigenvectors (stride 16)
+      double dmax = 0;
+      for (int i = 0; i < 15; ++i) dmax = fmax(dmax, fabs(sh.HM[i * kLd + i]));
+      const double tau = fmax(2e-6, 1e-12 * dmax);
+      for (int k = lane; k < 225; k += 64) {
+        const int i = k / 15, j = k - 15 * (k / 15);
+        A[i * kLd + j] = sh.HM[i * kLd + j] - (i == j ? tau : 0.0);
+      }
+      wave_sync();
+      const bool fast = ldlt15(A, lane);
+      if (fast) {
+        for (int k = lane; k < 225; k += 64) {
+          const int i = k / 15, j = k - 15 * (k / 15);
+          A[i * kLd + j] = sh.HM[i * kLd + j];
+        }
+        wave_sync();
+        (void)ldlt15(A, lane);
+        ldlt15_inverse(A, sh.pinv, lane);
+      }
+      if (!fast) {
       for (int k = lane; k < 256; k += 64) {
         const int i = k >> 4, j = k & 15;
         A[i * kLd + j] = (i < 15 && j < 15) ? sh.HM[i * kLd + j] : 0.0;
@@ -1023,6 +1101,7 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
         }
         sh.pinv[i * 16 + j] = s;
       }
+      }  // !fast
     }
     __syncthreads();
     // T = Hcb pinv (into sh.H rows), then H15 = Hcc - T Hbc

@@ -180,3 +180,20 @@ def test_rotation_updates_cross_exp_branches(gpu_available, seed):
     M = res["Rwb_d"].reshape(3, 3) @ R0.T
     corr = np.linalg.norm([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]]) / 2
     assert corr > 0.05  # the first update alone takes the closed form
+
+
+def test_marginalize_rank_deficient_previous_block(gpu_available):
+    """Marginalize's pseudo-inverse drops eigenvalues <= 1e-6 of the
+    previous-frame block (optimizer.cc Marginalize).  The kernel inverts that
+    block by LDL^T when it is clearly positive definite and takes the cyclic
+    Jacobi path with the cut otherwise: no prior information and no bias
+    random walks leave the block rank-deficient (rank 9 of 15), so this case
+    runs the Jacobi path; the other LastFrame cases run the LDL^T path."""
+    case = ic.make_case(50, mode=0, n_obs=300)
+    case["prior"]["H"] = 0.0
+    case["preint"]["info_g"] = 0.0
+    case["preint"]["info_a"] = 0.0
+    ref, ref_out = oracle.pose_inertial(case)
+    ret, res, out = _gpu(case)
+    assert ret == int(ref["n_good"])
+    _check(res, out, ref, ref_out)
