@@ -9,16 +9,16 @@
 #   * rocprofv3 --kernel-trace --stats of the bench command itself;
 #   * kernels.json (tools/pmc_kernels.py): what bench.py's roofline reads;
 #   * bench.json: the bench line without the profiler.
-#   ROUND=r02 bash tools/profile_round.sh
+#   ROUND=r05 bash tools/profile_round.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=${ROUND:-r02}
 O=gpurun_out/prof_$R
 rm -rf "$O"; mkdir -p "$O"
-# the bench's launch size: 128 stereo frames = 256 images a launch (the
-# resize chain then runs as one k_pyramid launch, as in the bench)
-FR=${FRAMES:-128}
+# the bench's launch size: 64 stereo frames = 128 images a launch (four
+# pipelines of a 256-frame group, bench.py's default)
+FR=${FRAMES:-64}
 WL="tools/prof_stages.py --frames $FR --iters 5 --mode both"
 SQ="SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
 for c in FETCH_SIZE WRITE_SIZE; do
@@ -33,7 +33,7 @@ timeout -k 10 120 rocprofv3 --pmc $SQ --kernel-trace -d $O/calib -o calib --outp
 echo "sq passes ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/bench_prof -o bench \
   -- python3 bench.py --no-cpu-baseline --no-lba --no-lia --no-stereo --no-match --no-bow --no-inertial \
-     --no-track --no-latency --no-c5 --no-lba-sharded > $O/bench_under_rocprof.json 2> $O/bench_prof.err \
+     --no-track --no-latency --no-latency-inertial --no-c5 --no-lba-sharded > $O/bench_under_rocprof.json 2> $O/bench_prof.err \
   || { echo "rocprof bench failed"; tail -5 $O/bench_prof.err; exit 1; }
 f=$(find $O/bench_prof -name '*kernel_stats.csv' | head -n1)
 cp "$f" $O/bench_kernel_stats.csv
