@@ -22,7 +22,9 @@ def _same(a, b):
     (5, 4, 5, 0, 2, False, 500),
     (6, 3, 2, 2, 1, False, 600),
     (6, 3, 3, 3, 2, True, 600),
-    (20, 2, 0, 0, 1, False, 4096),  # capacity, 20 children (two 16-lane passes)
+    (20, 2, 0, 0, 1, False, 4096),  # 20 children (two 16-lane passes)
+    (10, 3, 0, 0, 2, False, 6000),  # a 5 x nFeatures frame (tracking.cc:202-204): past 4096 features
+    (10, 3, 1, 0, 1, False, 8192),  # capacity (kBowMaxFeatures)
     (3, 2, 0, 0, 1, False, 0),
 ])
 def test_transform_parity(gpu_available, tmp_path, k, L, scoring, weighting, levelsup, trail, n):

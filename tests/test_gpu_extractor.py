@@ -333,6 +333,14 @@ def test_octree_nodes_hbm_by_plan(gpu_available):
     assert _compare(params, img) > 8000
 
 
+def test_octree_reduced_candidate_cache(gpu_available):
+    """6400 features: the octree's node arrays (1408 nodes) still fit LDS but
+    leave room for only 1280 of the 2048 cached candidates (the rest in HBM,
+    orb_plan.cpp's middle storage policy), bit-exact."""
+    left, _ = synth.stereo_frame(12)
+    assert _compare((6400, 1.2, 8, 20, 7), left) > 4096
+
+
 def test_batch_5x_features(gpu_available):
     """The device batch path at 5000 features: per-image outputs past 4096
     slots, equal to the oracle image by image."""
