@@ -15,7 +15,7 @@ GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
 GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
 
-all: $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial oracle
+all: $(LIB)/liborbgpu.so $(LIB)/liborbgpu_checkuniform.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial oracle
 
 OBJDIR   := build/obj
 GPU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(GPU_SRCS))
