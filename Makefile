@@ -13,7 +13,7 @@ GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels
             $(CSRC)/inertial_kernels.hip $(CSRC)/inertial_api.cpp \
             $(CSRC)/orb_plan.cpp $(CSRC)/orb_api.cpp $(CSRC)/pose_api.cpp $(CSRC)/lba_api.cpp \
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
-GPU_HDRS := $(wildcard $(CSRC)/*.h) $(CSRC)/pattern31.inc include/orbgpu.h
+GPU_HDRS := $(wildcard $(CSRC)/*.h) $(wildcard $(CSRC)/*.inc) include/orbgpu.h
 
 all: $(LIB)/liborbgpu.so $(LIB)/liborbgpu_checkuniform.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial oracle
 

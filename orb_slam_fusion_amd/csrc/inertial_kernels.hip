@@ -31,14 +31,14 @@
 
 #ifdef ORB_STAMPS
 namespace orbgpu {
-extern __device__ unsigned long long g_in_stamps[64 * 16];
+extern __device__ unsigned long long g_in_stamps[64 * 32];
 }
 // IMU-edge sub-phases (thread 0): slot i += time since the previous mark
 #define IMU_EDGE_MARK(i)                                                                   \
   do {                                                                                     \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                          \
     if (threadIdx.x == 0 && blockIdx.x < 64) {                                             \
-      atomicAdd(&orbgpu::g_in_stamps[blockIdx.x * 16 + (i)], now_ - ie_prev_); \
+      atomicAdd(&orbgpu::g_in_stamps[blockIdx.x * 32 + (i)], now_ - ie_prev_); \
     }                                                                                      \
     ie_prev_ = now_;                                                                       \
   } while (0)
@@ -52,7 +52,7 @@ namespace orbgpu {
 // Profiling build only (make stamps): per-phase s_memtime totals of thread 0
 // (wave 0 runs the serial IMU / solve work), flushed once per workgroup.
 #ifdef ORB_STAMPS
-__device__ unsigned long long g_in_stamps[64 * 16];
+__device__ unsigned long long g_in_stamps[64 * 32];
 #define ISTAMP_INIT                      \
   unsigned long long ist_acc_[16] = {};  \
   unsigned long long ist_prev_ = __builtin_amdgcn_s_memtime()
@@ -66,14 +66,14 @@ __device__ unsigned long long g_in_stamps[64 * 16];
   do {                                                                                      \
     if (threadIdx.x == 0)                                                                   \
       for (int i_ = 0; i_ < 16; ++i_)                                                       \
-        if (ist_acc_[i_]) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + i_], ist_acc_[i_]); \
+        if (ist_acc_[i_]) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 32 + i_], ist_acc_[i_]); \
   } while (0)
 #define ISTAMP_ADD_ITER (ist_acc_[8] += 1)
 // a sub-phase of thread 0 (wave 0) straight into slot i
 #define ISTAMP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define ISTAMP_SUB(i, a, b) \
   do {                      \
-    if (threadIdx.x == 0) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + (i)], (b) - (a)); \
+    if (threadIdx.x == 0) atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 32 + (i)], (b) - (a)); \
   } while (0)
 #else
 #define ISTAMP_T(v) (void)0
@@ -675,9 +675,11 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
 #ifdef ORB_STAMPS
   if (t == 64 * kVisWave0) {
     const unsigned long long vt2 = __builtin_amdgcn_s_memtime();
-    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + 10], vt1 - vt0);
-    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 16 + 11], vt2 - vt1);
+    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 32 + 10], vt1 - vt0);
+    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 32 + 11], vt2 - vt1);
   }
+  if (lane == 0)  // each wave's time in the sweep (slots 16 + wave)
+    atomicAdd(&g_in_stamps[(blockIdx.x & 63) * 32 + 16 + wave], __builtin_amdgcn_s_memtime() - vt0);
 #endif
   __syncthreads();
   if (sum_here && t < 27) vis_sum(sh, t);
@@ -1211,15 +1213,15 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
 
 #ifdef ORB_STAMPS
 extern "C" int orbgpu_debug_inertial_stamps(unsigned long long* out, int n) {
-  if (n > 16) n = 16;
-  static unsigned long long buf[64 * 16];
+  if (n > 32) n = 32;
+  static unsigned long long buf[64 * 32];
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(orbgpu::g_in_stamps), sizeof(buf)) != hipSuccess) return -1;
   for (int i = 0; i < n; ++i) {
     out[i] = 0;
-    for (int c = 0; c < 64; ++c) out[i] += buf[c * 16 + i];
+    for (int c = 0; c < 64; ++c) out[i] += buf[c * 32 + i];
   }
-  static const unsigned long long z[64 * 16] = {};
+  static const unsigned long long z[64 * 32] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_in_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -10,6 +10,7 @@ problem, plus a parity spot check (flags and return value equal, states to
     python tools/bench_inertial.py [--problems 64] [--calls 20] [--mode 0]
 """
 import argparse
+import hashlib
 import json
 import sys
 import time
@@ -80,7 +81,9 @@ def _measure(P, calls, mode, cpu_problems, latency_calls):
                        "Gauss-Newton iterations + marginalisation, inputs resident in HBM",
            "gpu_ms_per_batch": round(gpu_ms, 4),
            "gpu_problems_per_s": round(P / gpu_ms * 1e3, 1),
-           "inliers_per_problem": round(float(res["n_inliers"].mean()), 1)}
+           "inliers_per_problem": round(float(res["n_inliers"].mean()), 1),
+           # bit-identity across library builds (tools/inert_ab.sh)
+           "result_sha": hashlib.sha1(res.tobytes() + outs.tobytes()).hexdigest()[:16]}
     # one problem at a time through the host ABI (the tracking thread's view)
     one = PoseInertialOptimizer(max_obs=N_OBS)
     c0 = cases[0]

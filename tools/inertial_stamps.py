@@ -22,15 +22,15 @@ def main(mode: int):
     from orb_slam_fusion_amd._lib import library_path
 
     lib = ctypes.CDLL(str(library_path()))
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     P, calls = 64, 5
     bi.measure(P, 1, mode, cpu_problems=0, latency_calls=1)  # warm up (and clear below)
     torch.cuda.synchronize()
-    lib.orbgpu_debug_inertial_stamps(buf, 16)
+    lib.orbgpu_debug_inertial_stamps(buf, 32)
     # latency_calls=0 / cpu_problems=0: only the batch launches (3 warm-up + calls)
     bi.measure(P, calls, mode, cpu_problems=0, latency_calls=0)
     torch.cuda.synchronize()
-    assert lib.orbgpu_debug_inertial_stamps(buf, 16) == 0
+    assert lib.orbgpu_debug_inertial_stamps(buf, 32) == 0
     v = list(buf)
     runs = P * (calls + 3)
     names = {6: "imu_edges (wave 0)", 0: "visual sweep wait + reduce", 1: "assemble",
@@ -41,7 +41,9 @@ def main(mode: int):
     tot = sum(v[i] for i in names)
     print(json.dumps({"ticks_per_problem": tot / runs, "iterations_per_problem": v[8] / runs,
                       "ticks_per_phase_per_problem": {names[i]: round(v[i] / runs) for i in names},
-                      "sub_phases_per_problem": {sub[i]: round(v[i] / runs) for i in sub}}))
+                      "sub_phases_per_problem": {sub[i]: round(v[i] / runs) for i in sub},
+                      # every vis_sweep (the LM steps' and the final Hessian's)
+                      "sweep_ticks_per_wave_per_problem": [round(v[16 + w] / runs) for w in range(8)]}))
 
 
 if __name__ == "__main__":
