@@ -16,9 +16,9 @@ export TMPDIR=/tmp
 R=${ROUND:-r02}
 O=gpurun_out/prof_$R
 rm -rf "$O"; mkdir -p "$O"
-# the bench's launch size: 64 stereo frames = 128 images a launch (four
-# pipelines of a 256-frame group, bench.py's default)
-FR=${FRAMES:-64}
+# the bench's launch size: 384 stereo frames = 768 images a launch (four
+# pipelines of a 1536-frame group, bench.py's default)
+FR=${FRAMES:-384}
 WL="tools/prof_stages.py --frames $FR --iters 5 --mode both"
 SQ="SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
 for c in FETCH_SIZE WRITE_SIZE; do
