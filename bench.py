@@ -279,7 +279,8 @@ def main() -> int:
     for e in pipes:
         e.check()
 
-    ex.profile(args.steps * G)
+    for e in pipes:  # stage events on every pipeline: the stage times average over all four
+        e.profile(args.steps * G)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -291,7 +292,12 @@ def main() -> int:
     for e in pipes:
         e.check()
 
-    calls, stage_ms = ex.profile_read()
+    calls, stage_ms = 0, {}
+    for e in pipes:
+        c, ms = e.profile_read()
+        calls += c
+        for k, v in ms.items():
+            stage_ms[k] = stage_ms.get(k, 0.0) + v
     pose_ms = sum(a.elapsed_time(b) for a, b in pose_ev) / max(len(pose_ev), 1)
     n_kp = d_n.cpu().numpy()
     inl = d_inl.cpu().numpy()
