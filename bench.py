@@ -352,6 +352,14 @@ def main() -> int:
             for key in ("valu_busy", "rocprof_avg_ms_per_launch", "bound"):
                 if p.get(key) is not None:
                     row[key] = p[key]
+            # the same launch alone on the device (the PMC pass of tools/prof_stages.py,
+            # kernels serialised): in the mix each kernel shares the CUs with the other
+            # pipelines' and the pose stream's, so its duration there is not its speed
+            iso = p.get("pmc_pass_ms_per_launch")
+            if iso and prof.get("images_per_launch") == imgs_per_launch:
+                row["isolated_ms_per_launch"] = iso
+                if b:
+                    row["isolated_frac"] = round(b / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             if p.get("insts_valu_per_launch") is not None and prof.get("images_per_launch"):
                 row["valu_insts_per_64_images"] = round(p["insts_valu_per_launch"] * 64 /
                                                         prof["images_per_launch"])
@@ -375,6 +383,11 @@ def main() -> int:
         "kernels": kernels,
         "valu_busy_definition": "kernel SQ_INSTS_VALU per ns / the same counter per ns of a "
                                 "VALU-saturating kernel (tools/valu_calib.hip), same box",
+        "kernel_durations": f"avg_ms_per_launch: HIP events between the stages of all {P} "
+                            "pipelines' launches in the timed mix, where every kernel runs beside "
+                            "the other pipelines' and the pose stream's (its duration there is its "
+                            "share of the device, not its speed); isolated_ms_per_launch: the same "
+                            "launch size alone (PMC pass, profiles/" + PROFILE_ROUND + "/kernels.json)",
     }
     result = {
         "metric": METRIC,
