@@ -543,7 +543,14 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
   // issued while row r is filtered horizontally, and output row r - 6 leaves
   // as soon as its 7 rows exist, so only a 7-row window of sums is live.
   constexpr int kPf = ORB_BLUR_PF;  // rows of loads in flight
-  const bool edge = __builtin_amdgcn_ballot_w64((int)base != x - 4) != 0;
+  // edge: some lane's window is clamped at the right border (or the level is
+  // narrower than a wave's span) -- every lane rebuilds its window by
+  // per-lane selectors; edgeL: the only clamped lane is x = 0, whose window
+  // -4..7 reflects to bytes (4 3 2 1)(0 1 2 3)(4 5 6 7) of its load: one
+  // perm and two selects per row instead of three perms and three ors
+  const bool edge = __builtin_amdgcn_ballot_w64((int)base != x - 4 && x != 0) != 0;
+  const bool edgeL = !edge && __builtin_amdgcn_ballot_w64(x == 0) != 0;
+  const bool isL = x == 0;
   uint32_t lo_sel[3] = {0, 0, 0}, hi_sel[3] = {0, 0, 0};
   if (edge) blur_window_sel(x, g.w, (int)base, lo_sel, hi_sel);
   uint32_t d[R + 6][3];
@@ -588,6 +595,11 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
         v[k] = __builtin_amdgcn_perm(d[r][1], d[r][0], lo_sel[k]) | __builtin_amdgcn_perm(d[r][2], d[r][2], hi_sel[k]);
 #pragma unroll
       for (int k = 0; k < 3; ++k) d[r][k] = v[k];
+    } else if (edgeL) {
+      const uint32_t d0 = d[r][0], d1 = d[r][1];
+      d[r][0] = __builtin_amdgcn_perm(d1, d0, isL ? 0x01020304u : 0x03020100u);
+      d[r][1] = isL ? d0 : d1;
+      d[r][2] = isL ? d1 : d[r][2];
     }
     const uint32_t lo[4] = {__builtin_amdgcn_alignbyte(d[r][1], d[r][0], 1),
                             __builtin_amdgcn_alignbyte(d[r][1], d[r][0], 2),
