@@ -303,13 +303,14 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
   auto out_row = [&](int y, const uint32_t (&hA)[4], const uint32_t (&qA)[4], const uint32_t (&hB)[4],
                      const uint32_t (&qB)[4], uint32_t b0, uint32_t b1) {
     uint32_t v[4];  // 4x the output byte (< 2^12); the >> 2 is done packed below
+    // (tail columns: h < 255 * 2^11 and b < 2^11, so 24-bit multiplies are exact)
     const uint32_t s0 = b0 << 12, s1 = b1 << 12;
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = mulhi24(qA[k], s0) + mulhi24(qB[k], s1) + 2;
     if (any_tail) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (tail_k & (1u << k)) v[k] = ((hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22) << 2;
+        if (tail_k & (1u << k)) v[k] = ((__umul24(hA[k], b0) + __umul24(hB[k], b1) + (1u << 21)) >> 22) << 2;
     }
     // two columns per 16-bit half: one packed shift per pair, one byte perm
     const ushort2_t p01 = as_us2(v[0] | (v[1] << 16)) >> (ushort2_t){2, 2};
@@ -417,7 +418,7 @@ __device__ __forceinline__ void resize_tail(const PlanHeader* __restrict__ P, co
     if (tail_k) {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (tail_k & (1u << k)) v[k] = ((hA[k] * b0 + hB[k] * b1 + (1u << 21)) >> 22) << 2;
+        if (tail_k & (1u << k)) v[k] = ((__umul24(hA[k], b0) + __umul24(hB[k], b1) + (1u << 21)) >> 22) << 2;
     }
     const ushort2_t p01 = as_us2(v[0] | (v[1] << 16)) >> (ushort2_t){2, 2};
     const ushort2_t p23 = as_us2(v[2] | (v[3] << 16)) >> (ushort2_t){2, 2};
@@ -563,7 +564,10 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(S), (short)0, (int)0xffffffff, kBufRsrcWord3);
   auto load_row = [&](int r) {
-    const int ro = reflect101(ys - 3 + r, gh) * sp;
+    // (kTail: the row is per lane -- a 24-bit multiply, full rate; else
+    // wave-uniform, on the scalar unit)
+    const int ro = kTail ? (int)__umul24((uint32_t)reflect101(ys - 3 + r, gh), (uint32_t)sp)
+                         : reflect101(ys - 3 + r, gh) * sp;
     const auto w = kTail ? __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base + ro, 0, 0)
                          : __builtin_amdgcn_raw_buffer_load_b96(srs, (int)base, ro, 0);
 #pragma unroll
@@ -627,7 +631,7 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
         const uint32_t packed =
             __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
         if (kTail)
-          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x + (ys + o) * pitch, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x + (int)__umul24((uint32_t)(ys + o), (uint32_t)pitch), 0, 0);
         else
           __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x, (ys + o) * pitch, 0);
       }
@@ -721,15 +725,21 @@ __device__ __forceinline__ _Float16 fast_arc_max(const uint8_t* p, int ls) {
   half2_t x[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) x[k] = ring_diff((uint32_t)p[cx[k] + cy[k] * ls], vb);
-  half2_t m3[16], a[16];
+  // The arcs starting at 2i and 2i + 1 share the core x[2i+1 .. 2i+8]:
+  // max(min(core, x[2i]), min(core, x[2i+9])) = min(core, max(x[2i], x[2i+9])),
+  // and core_i = min(pm_i .. pm_i+3) over the pair minima pm_j = min(x[2j+1],
+  // x[2j+2]): 8 + 8 + 8 + 8 ops for the 8 core terms (min / max select their
+  // inputs, so the result is the 16-arc form's, bit for bit), then their max
+  half2_t pm[8], q[8], r[8];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) m3[k] = hmin3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
+  for (int j = 0; j < 8; ++j)
+    pm[j] = __builtin_elementwise_minimum(x[2 * j + 1], x[(2 * j + 2) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; ++k) a[k] = hmin3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
-  half2_t b = hmax3(a[0], a[1], a[2]);
+  for (int i = 0; i < 8; ++i) q[i] = hmin3(pm[i], pm[(i + 1) & 7], pm[(i + 2) & 7]);
 #pragma unroll
-  for (int k = 3; k < 15; k += 2) b = hmax3(b, a[k], a[k + 1]);
-  b = __builtin_elementwise_maximum(b, a[15]);
+  for (int i = 0; i < 8; ++i)
+    r[i] = hmin3(q[i], pm[(i + 3) & 7], __builtin_elementwise_maximum(x[2 * i], x[(2 * i + 9) & 15]));
+  half2_t b = hmax3(hmax3(r[0], r[1], r[2]), hmax3(r[3], r[4], r[5]), __builtin_elementwise_maximum(r[6], r[7]));
   return __builtin_fmaxf16(b.x, b.y);
 }
 
@@ -844,7 +854,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
           v[u] = *reinterpret_cast<const uint32_t*>(Sa + (__umul24(rr[u], (uint32_t)sp) + q4));
 #pragma unroll
         for (int u = 0; u < kFastPf; ++u)
-          *reinterpret_cast<uint32_t*>(roi + ((LS ? rr[u] * (uint32_t)LS : __umul24(rr[u], (uint32_t)ls)) + q4)) = v[u];
+          *reinterpret_cast<uint32_t*>(roi + (__umul24(rr[u], (uint32_t)(LS ? LS : ls)) + q4)) = v[u];
       }
     } else {
       for (int i = lane; i < c.rows * ndw; i += 64) {
@@ -972,23 +982,26 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         const uint32_t* Cr = reinterpret_cast<const uint32_t*>(sc + i0 + 2 * sp2);
         const uint32_t a0 = A[0], a1 = A[1], a2 = A[2], c0 = Cr[0], c1 = Cr[1], c2 = Cr[2];
         const uint32_t m0 = B[0], m1 = B[1], m2 = B[2];
-        // pair j (pixels 2j, 2j + 1) at window offset d: bytes 2j + d, 2j + d + 1
-        // of the row, from (w1:w0) for j < 2, else (w2:w1) 4 bytes on
+        // pair j (pixels 2j, 2j + 1) at window offset d: row bytes b = 2j + d,
+        // b + 1, from (w1:w0) for b < 4, else (w2:w1) at b - 4 -- one form per
+        // byte offset, so the 12 uses of a row are 9 distinct perms (CSE)
         auto pr = [&](uint32_t w0, uint32_t w1, uint32_t w2, int jj, int d) {
-          const int o = (jj & 1) * 2 + d;
-          return jj < 2 ? __builtin_amdgcn_perm(w1, w0, psel(o)) : __builtin_amdgcn_perm(w2, w1, psel(o));
+          const int b = 2 * jj + d;
+          return b < 4 ? __builtin_amdgcn_perm(w1, w0, psel(b)) : __builtin_amdgcn_perm(w2, w1, psel(b - 4));
         };
+        // the u16 scores (0..255) read as f16 are the denormals s * 2^-24, so
+        // packed f16 maximum3 and subtract are exact on them: the 8-neighbour
+        // maximum n is three v_pk_maximum3_f16 and a maximum, and n - s has
+        // its sign bit (15 / 31) set iff s > n (s == n gives +0)
+        auto h2 = [](uint32_t v) { return __builtin_bit_cast(half2_t, v); };
         uint32_t fb[4];
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const ushort2_t na = max2(max2(as_us2(pr(a0, a1, a2, jj, 0)), as_us2(pr(a0, a1, a2, jj, 1))),
-                                    as_us2(pr(a0, a1, a2, jj, 2)));
-          const ushort2_t nc = max2(max2(as_us2(pr(c0, c1, c2, jj, 0)), as_us2(pr(c0, c1, c2, jj, 1))),
-                                    as_us2(pr(c0, c1, c2, jj, 2)));
-          const ushort2_t nb = max2(as_us2(pr(m0, m1, m2, jj, 0)), as_us2(pr(m0, m1, m2, jj, 2)));
-          const ushort2_t sv2 = as_us2(pr(m0, m1, m2, jj, 1));
-          const ushort2_t d = sub_sat2(sv2, max2(max2(na, nc), nb));  // > 0 iff s > n
-          fb[jj] = __builtin_bit_cast(uint32_t, d + (ushort2_t){0x7fff, 0x7fff});
+          const half2_t na = hmax3(h2(pr(a0, a1, a2, jj, 0)), h2(pr(a0, a1, a2, jj, 1)), h2(pr(a0, a1, a2, jj, 2)));
+          const half2_t nc = hmax3(h2(pr(c0, c1, c2, jj, 0)), h2(pr(c0, c1, c2, jj, 1)), h2(pr(c0, c1, c2, jj, 2)));
+          const half2_t n = hmax3(na, nc, __builtin_elementwise_maximum(h2(pr(m0, m1, m2, jj, 0)),
+                                                                          h2(pr(m0, m1, m2, jj, 2))));
+          fb[jj] = __builtin_bit_cast(uint32_t, n - h2(pr(m0, m1, m2, jj, 1)));
         }
         const uint32_t FA = __builtin_amdgcn_perm(fb[1], fb[0], 0x07050301u) & 0x80808080u;
         const uint32_t FB = __builtin_amdgcn_perm(fb[3], fb[2], 0x07050301u) & 0x80808080u;
