@@ -836,14 +836,31 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   {
     const uint8_t* Sa = S - lead;  // rows stay dword-aligned iff sp is; else unaligned loads
     const int ndw = (lead + c.cols + 3) >> 2;
-    if (ndw <= 16) {
+    const uint32_t q4 = 4u * (uint32_t)min(lane & 15, ndw - 1), r0 = (uint32_t)lane >> 4;
+    if (LS != 0 && ndw <= 16 && c.rows <= 4 * kFastPf && c.y0 + 4 * kFastPf <= P->lev[c.level].h) {
+      // The whole ROI in one step of 4 * kFastPf rows from its top row, none
+      // clamped: rows past the ROI (at most 4 kFastPf - rows) are still inside
+      // the level plane (the condition) and land in this wave's LDS past the
+      // ROI -- the score map, cleared below, and the survivor lists, written
+      // later; 4 kFastPf * LS bytes is well inside fast_cell_lds_bytes.  The
+      // row steps are scalar buffer offsets and LDS immediates: two VALU for
+      // the 12 loads and stores instead of four each.
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(Sa), (short)0,
+                                                                          (int)0xffffffff, kBufRsrcWord3);
+      const int voff = (int)(__umul24(r0, (uint32_t)sp) + q4);
+      uint32_t v[kFastPf];
+#pragma unroll
+      for (int u = 0; u < kFastPf; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 4 * u * sp, 0);
+      uint8_t* d = roi + (__umul24(r0, (uint32_t)(LS ? LS : 1)) + q4);
+#pragma unroll
+      for (int u = 0; u < kFastPf; ++u) *reinterpret_cast<uint32_t*>(d + 4 * u * LS) = v[u];
+    } else if (ndw <= 16) {
       // 16 lanes per ROI row, 4 rows per step: lane (q, r0) copies dword q of
       // rows r0, r0 + 4, ... -- a uniform stride, kFastPf loads in flight.
       // Lanes past the ROI width or height are clamped onto its last dword /
       // row: they copy the same dword to the same LDS address as the lane
       // that owns it, so the stores need no predicate; 32-bit offsets from
       // the wave-uniform row base keep the loads on the scalar base.
-      const uint32_t q4 = 4u * (uint32_t)min(lane & 15, ndw - 1), r0 = (uint32_t)lane >> 4;
       const uint32_t rlast = (uint32_t)c.rows - 1u;
       for (int k0 = 0; 4 * k0 < c.rows; k0 += kFastPf) {
         uint32_t v[kFastPf], rr[kFastPf];
@@ -864,7 +881,8 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       }
     }
   }
-  for (int i = lane; i < ((nsc + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
+  // (16-byte stores: the score map's region is rounded up to 16 bytes)
+  for (int i = lane; i < ((nsc + 15) >> 4); i += 64) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   STAMP(6);
   STAMP_ADD(13, 1);
@@ -872,7 +890,10 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   const uint8_t* base = roi + 3 * ls + lead + 3;  // detection pixel (0, 0)
   const uint64_t lt = (1ull << lane) - 1ull;
   const int gpr = (dw + 7) >> 3;  // 8-pixel groups per detection row
-  const int g_r0 = lane / gpr, g_q0 = lane - (lane / gpr) * gpr;
+  // lane / gpr as a 24-bit multiply by the scalar ceil(2^16 / gpr): exact for
+  // lane < 64, gpr <= 16 (dw < 128), no VALU division sequence
+  const uint32_t g_m = (65535u + (uint32_t)gpr) / (uint32_t)gpr;
+  const int g_r0 = (int)(__umul24((uint32_t)lane, g_m) >> 16), g_q0 = lane - __mul24(g_r0, gpr);
   const int g_dr = 64 / gpr, g_dq = 64 - g_dr * gpr;
   const int tail = dw - 8 * (gpr - 1);  // valid pixels of a row's last group (1..8)
 
