@@ -37,6 +37,7 @@ PARAMS = (1000, 1.2, 8, 20, 7)
 POSE_OBS = 600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROFILE_ROUND = "r05"  # profiles/<round>/kernels.json (tools/profile_round.sh)
+SIDE_BATCH = 256  # frames / problems per call of the side lines (stereo, match, BoW, inertial, track)
 
 
 def level_sizes(inv_scale):
@@ -441,28 +442,28 @@ def main() -> int:
         sys.path.insert(0, str(REPO / "tools"))
         from bench_stereo import measure as measure_stereo  # noqa: E402
 
-        result["stereo"] = measure_stereo(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["stereo"] = measure_stereo(frames=SIDE_BATCH, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_match:
         # SURVEY §8(f) rank 2, beside the headline metric (not part of it):
         # SearchByProjection(CurrentFrame, LastFrame) on resident frame outputs
         sys.path.insert(0, str(REPO / "tools"))
         from bench_match import measure as measure_match  # noqa: E402
 
-        result["match"] = measure_match(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["match"] = measure_match(frames=SIDE_BATCH, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_bow:
         # SURVEY §8(f) rank 4, beside the headline metric (not part of it):
         # DBoW2 transform (Frame::ComputeBoW) on resident extractor descriptors
         sys.path.insert(0, str(REPO / "tools"))
         from bench_bow import measure as measure_bow  # noqa: E402
 
-        result["bow"] = measure_bow(frames=Bg, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["bow"] = measure_bow(frames=SIDE_BATCH, calls=20, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_inertial:
         # PoseInertialOptimizationLastFrame (stereo-inertial
         # tracking after IMU initialisation), a batch resident in HBM
         sys.path.insert(0, str(REPO / "tools"))
         from bench_inertial import measure as measure_inertial  # noqa: E402
 
-        result["inertial"] = measure_inertial(problems=Bg, calls=20, mode=0,
+        result["inertial"] = measure_inertial(problems=SIDE_BATCH, calls=20, mode=0,
                                               cpu_problems=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_track:
         # config C3's path on synthetic data: extract + stereo + SearchByProjection
@@ -470,7 +471,7 @@ def main() -> int:
         sys.path.insert(0, str(REPO / "tools"))
         from bench_track import measure as measure_track  # noqa: E402
 
-        result["track"] = measure_track(frames=Bg, calls=10, cpu_frames=0 if args.no_cpu_baseline else 4)
+        result["track"] = measure_track(frames=SIDE_BATCH, calls=10, cpu_frames=0 if args.no_cpu_baseline else 4)
     if rank == 0 and world == 1 and not args.no_latency:
         # north_star's per-frame target: one stereo frame at a time through the
         # host ABI (2-thread extraction + PoseOptimization) vs the CPU oracle
