@@ -3,12 +3,11 @@
 PoseOptimization (600 observations) per frame on MI355X.
 
 A step = B distinct synthetic stereo frames per GPU (default 7680, all
-resident in HBM before the timed region), in launch groups of 1536 frames:
-3072 images through the gfx950 extractor (orbgpu_extract_batch, four
-pipelines of 768 images, each its own HIP stream, each a stage behind the
-previous one) and 1536 pose-only problems through the gfx950
-PoseOptimization (orbgpu_pose_opt_batch) on a concurrent high-priority
-stream.  Frames shard across ranks (contiguous
+resident in HBM before the timed region), as one launch group: 15360
+images through the gfx950 extractor (orbgpu_extract_batch, four pipelines of
+3840 images, each its own HIP stream, each a stage behind the previous one)
+and 7680 pose-only problems through the gfx950 PoseOptimization
+(orbgpu_pose_opt_batch) on a concurrent high-priority stream.  Frames shard across ranks (contiguous
 blocks of B frame ids per rank, orb_slam_fusion_amd/dist.py): no
 data-path collective, weak scaling; the max over ranks of the timed region is
 the job time.  Prints one JSON line on rank 0 (contract in the task README).
@@ -123,7 +122,9 @@ def load_profile():
     """Per-kernel evidence committed under profiles/<round>/ by
     tools/profile_round.sh: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, separate
     passes) and calibrated VALU-busy per extractor-stage launch."""
-    f = REPO / "profiles" / PROFILE_ROUND / "kernels.json"
+    # (BENCH_KERNELS_JSON: the kernels.json tools/profile_round.sh has just
+    # written, so its bench line and its profile come from the same run)
+    f = Path(os.environ.get("BENCH_KERNELS_JSON", REPO / "profiles" / PROFILE_ROUND / "kernels.json"))
     if not f.exists():
         return None
     try:
@@ -155,9 +156,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=7680,
                     help="stereo frames per GPU per step (all distinct, resident in HBM)")
-    ap.add_argument("--batch", type=int, default=1536,
-                    help="stereo frames per launch group (DESIGN §11: 1536 with four pipelines "
-                         "measured best in the tools/ab_bench.sh sweep)")
+    ap.add_argument("--batch", type=int, default=7680,
+                    help="stereo frames per launch group (DESIGN §11: one group of the step's 7680 "
+                         "frames over four pipelines measured best in the tools/ab_bench.sh sweep)")
     ap.add_argument("--pipes", type=int, default=4,
                     help="extractor pipelines per GPU (each its own handle + HIP stream, "
                          "each launch group split evenly between them)")

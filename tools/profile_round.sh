@@ -16,9 +16,9 @@ export TMPDIR=/tmp
 R=${ROUND:-r02}
 O=gpurun_out/prof_$R
 rm -rf "$O"; mkdir -p "$O"
-# the bench's launch size: 384 stereo frames = 768 images a launch (four
-# pipelines of a 1536-frame group, bench.py's default)
-FR=${FRAMES:-384}
+# the bench's launch size: 1920 stereo frames = 3840 images a launch (four
+# pipelines of the 7680-frame group, bench.py's default)
+FR=${FRAMES:-1920}
 WL="tools/prof_stages.py --frames $FR --iters 5 --mode both"
 SQ="SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
 for c in FETCH_SIZE WRITE_SIZE; do
@@ -42,7 +42,7 @@ python3 tools/pmc_kernels.py --traffic $O/traffic --sq $O/sq --calib $O/calib \
   || { echo "summary failed"; tail -5 $O/kernels.log; exit 1; }
 echo "kernels.json ok"
 if [ "${RUN_BENCH:-1}" = "1" ]; then
-  timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err \
+  BENCH_KERNELS_JSON=$O/kernels.json timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err \
     || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
   tail -c 600 $O/bench.json
 fi
