@@ -750,6 +750,14 @@ __device__ __forceinline__ ushort2_t compass2(ushort2_t v, ushort2_t u, ushort2_
   const ushort2_t hi = min2(max2(u, d), max2(l, r));
   return max2(sub_sat2(v, lo), sub_sat2(hi, v));
 }
+// Measurement-only build switch (wrong keypoints): ORB_FAST_SKIP bit 0 skips
+// the NMS, bit 1 the scores, bit 2 the survivor expansion and scores, bit 3
+// the compass loop, and the
+// minTh pass never runs -- the VALU of a phase is the difference
+// (tools/valu_ab.sh over `make var` builds)
+#ifndef ORB_FAST_SKIP
+#define ORB_FAST_SKIP 0
+#endif
 // A/B build switch (make varB): the survivor list expanded once and held
 // whole (LDS 2 bytes a detection pixel) instead of per 64 group entries
 #ifndef ORB_FAST_SV_FULL
@@ -775,6 +783,7 @@ __device__ __forceinline__ int wave_iscan(int v) {
 
 constexpr int kFastPf = 12;  // ROI dwords in flight per lane (one round trip up to 768)
 constexpr int kFastSvChunk = 512;  // survivors of 64 group entries (the list is expanded per 64 entries)
+constexpr int kFastSvCarry = 64;   // + the survivors carried from the previous chunk (< 64)
 
 // LS > 0: the plan's LDS row pitch for every cell (PlanHeader::fast_pitch:
 // the smallest of 48..64 that holds each cell's ROI row and score-map row;
@@ -818,7 +827,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   uint8_t* sc = lds + ((ls * c.rows + 15) & ~15);
   uint16_t* sv = reinterpret_cast<uint16_t*>(sc + ((nsc + 15) & ~15));
   uint32_t* ge = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv) +
-                                             (ORB_FAST_SV_FULL ? ((2 * nd + 15) & ~15) : 2 * kFastSvChunk));
+                                             (ORB_FAST_SV_FULL ? ((2 * nd + 15) & ~15) : 2 * (kFastSvChunk + kFastSvCarry)));
   auto sci = [&](int i) {
     if constexpr (LS != 0) return i + LS + 1;
     return ((i >> QB) + 1) * sp2 + (i & QM) + 1;
@@ -922,7 +931,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     const ushort2_t thv = {(unsigned short)(0x7fff - th), (unsigned short)(0x7fff - th)};
     const _Float16 thp1 = __builtin_bit_cast(_Float16, (uint16_t)(th + 1));  // (th + 1) * 2^-24, exact
     auto bal = [](bool b) { return __builtin_amdgcn_ballot_w64(b); };
-    for (int r = g_r0, g = g_q0;;) {
+    for (int r = g_r0, g = g_q0; !(ORB_FAST_SKIP & 8);) {
       const uint64_t mrv = bal(r < dh);  // lanes whose group row is valid
       if (mrv == 0) break;
       const uint32_t cr = (uint32_t)(min(r, dh - 1) + 3);
@@ -1107,7 +1116,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // survivors, 64 group entries at a time: lane j expands entry b0 + j into
     // sv[] from the wave's inclusive scan of the entries' popcounts (raster
     // order: entries in order, pixels LSB-first), at most kFastSvChunk
-    auto expand = [&](int b0) -> int {
+    auto expand = [&](int b0, int at) -> int {  // appends at sv[at]
       const int j = b0 + lane;
       const uint32_t e = j < ng ? ge[j] : 0u;
       const int i0 = (int)(e & 0xffffu);
@@ -1115,7 +1124,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       uint32_t m = LS ? (e >> 16) & 0xffu : (e >> 16) & (((i0 >> 3) & ((1 << (QB - 3)) - 1)) == gpr - 1 ? tail_mask : 0xffu);
       const int cnt = __popc(m);
       const int incl = wave_iscan(cnt);
-      int pos = incl - cnt;
+      int pos = at + incl - cnt;
       while (m) {
         sv[pos++] = (uint16_t)(i0 + __builtin_ctz(m));
         m &= m - 1;
@@ -1123,20 +1132,29 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       __syncthreads();
       return __builtin_amdgcn_readlane(incl, 63);
     };
-    // scores of every survivor into the map
-    for (int b0 = 0; b0 < ng; b0 += 64) {
-      const int ns = expand(b0);
+    // scores of every survivor into the map: a chunk's survivors are scored
+    // 64 at a time and the last partial wave's (< 64) carried to the front
+    // of sv for the next chunk -- full waves except once per cell, not once
+    // per chunk (the scores are independent of their order)
+    auto score = [&](int i) {
+      // S = max(m - 1, 0) is a corner's score iff m >= th + 1 (then m > 0
+      // and its bit pattern is the integer m)
+      const _Float16 m = fast_arc_max(base + px(i), ls);
+      const uint16_t bits = __builtin_bit_cast(uint16_t, m);
+      sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
+    };
+    int pend = 0;  // survivors carried at sv[0, pend)
+    for (int b0 = 0; b0 < ng && !(ORB_FAST_SKIP & 4); b0 += 64) {
+      const int ns = expand(b0, pend);
       *n_sv += ns;
-      for (int j = lane; j < ns; j += 64) {
-        const int i = sv[j];
-        // S = max(m - 1, 0) is a corner's score iff m >= th + 1 (then m > 0
-        // and its bit pattern is the integer m)
-        const _Float16 m = fast_arc_max(base + px(i), ls);
-        const uint16_t bits = __builtin_bit_cast(uint16_t, m);
-        sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
-      }
+      const int tot = pend + ns, full = tot & ~63;
+      for (int j = lane; j < full && !(ORB_FAST_SKIP & 2); j += 64) score(sv[j]);
+      pend = tot - full;
+      if (full > 0 && lane < pend) sv[lane] = sv[full + lane];  // (disjoint: full >= 64 > pend)
       __syncthreads();  // sv is rewritten by the next chunk
     }
+    if (lane < pend && !(ORB_FAST_SKIP & 2)) score(sv[lane]);
+    __syncthreads();
     STAMP(1);
     // NMS over the survivors again (re-expanded: the list is never held
     // whole), keypoints straight to the cell's slots in raster order: a corner
@@ -1144,9 +1162,9 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // for the zero border outside the detection area)
     int written = 0;
     if constexpr (LS != 0) {
-      nms_entries(written);
+      if (!(ORB_FAST_SKIP & 1)) nms_entries(written);
     } else for (int b0 = 0; b0 < ng; b0 += 64) {
-      const int ns = expand(b0);
+      const int ns = expand(b0, 0);
       for (int jb = 0; jb < ns; jb += 64) {
         const int j = jb + lane;
         bool kp = false;
@@ -1179,7 +1197,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   int ns = 0;
   int written = pass(P->ini_th, &ns);
   STAMP_ADD(12, ns);
-  if (written == 0) {
+  if (written == 0 && !ORB_FAST_SKIP) {
     STAMP_ADD(10, 1);
     for (int i = lane; i < ((nsc + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
     __syncthreads();

@@ -312,7 +312,7 @@ int fast_cell_lds_bytes(int cols, int rows) {
   const int dw = std::max(cols - 6, 0), dh = std::max(rows - 6, 0);
   const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
   const int nsc = std::max(cols - 4, 0) * std::max(rows - 4, 0);
-  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * 512;  // u16 survivors (kFastSvChunk)
+  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * (512 + 64);  // u16 survivors (kFastSvChunk + kFastSvCarry)
   return ((ls * rows + 15) & ~15) + ((nsc + 15) & ~15) + sv + 4 * ng + 16;
 }
 
@@ -322,7 +322,7 @@ int fast_cell_lds_bytes(int cols, int rows) {
 int fast_cell_lds_bytes_pitch(int cols, int rows, int pitch) {
   const int dw = std::max(cols - 6, 0), dh = std::max(rows - 6, 0);
   const int nd = dw * dh, ng = ((dw + 7) >> 3) * dh;
-  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * 512;
+  const int sv = ORB_FAST_SV_FULL ? (2 * nd + 15) & ~15 : 2 * (512 + 64);
   return ((pitch * rows + 15) & ~15) + ((pitch * (dh + 2) + 15) & ~15) + sv + 4 * ng + 16 + 16;
 }
 
