@@ -136,6 +136,17 @@ def test_odd_sizes(gpu_available, size):
     _compare((1000, 1.2, L, 20, 7), full)
 
 
+@pytest.mark.parametrize("size", [(400, 101), (101, 101), (752, 136)])
+def test_tall_and_wide_cells(gpu_available, size):
+    """Cells up to 69 px (one or two cells across a level: ceil(span / n) with
+    n = span // 35): ROIs of 75 rows take k_fast_cells' clamped multi-step
+    ROI load, 75 columns its per-cell-pitch instance; the 752 x 136 levels mix
+    one-step and clamped ROIs (orb_extractor.cc:783-801 cell geometry)."""
+    w, h = size
+    full, _ = synth.stereo_frame(21, w=w, h=h)
+    _compare((300, 1.2, 2, 20, 7), full)
+
+
 @pytest.mark.parametrize("params", [(1000, 1.6, 5, 20, 7), (1000, 1.5, 6, 20, 7), (1000, 2.0, 4, 20, 7)])
 def test_large_scale_factors(gpu_available, params):
     # coarser pyramids: wider resize tap spans, fewer and smaller levels
