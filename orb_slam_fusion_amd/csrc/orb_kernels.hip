@@ -1002,9 +1002,26 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
     // (after + 0x7fff) is the flag; keypoints go to the slots in raster order
     // (entries in order, pixels LSB-first) from a wave scan of the counts.
     auto nms_entries = [&](int& written) {
+      // only entries holding a corner (a non-zero score among their 8 centre
+      // bytes) can keep a keypoint: compact them first, in place (a write
+      // index never passes its read index), so the NMS runs on about half
+      // the waves (≈ 0.36 corners a survivor, profiles/r05/fast_survivors.json)
+      int nce = 0;
       for (int b0 = 0; b0 < ng; b0 += 64) {
         const int j = b0 + lane;
         const uint32_t e = j < ng ? ge[j] : 0u;
+        const uint32_t* B = reinterpret_cast<const uint32_t*>(sc + (e & 0xffffu) + sp2);
+        const bool has = j < ng && ((B[0] >> 8) | B[1] | (B[2] & 0xffu)) != 0u;
+        const uint64_t mg = __builtin_amdgcn_ballot_w64(has);
+        if (has) ge[mbcnt64(mg, (uint32_t)nce)] = e;
+        nce += __popcll(mg);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int b0 = 0; b0 < nce; b0 += 64) {
+        const int j = b0 + lane;
+        const uint32_t e = j < nce ? ge[j] : 0u;
         const int i0 = (int)(e & 0xffffu);
         const uint32_t m = (e >> 16) & 0xffu;
         const uint32_t* A = reinterpret_cast<const uint32_t*>(sc + i0);
