@@ -639,18 +639,25 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
   }
 }
 
-__global__ __launch_bounds__(256) ORB_WPE8 ORB_BLUR_WPE void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
+// waves per k_blur workgroup (A/B: 1 = every strip its own workgroup; the
+// strips never synchronise)
+#ifndef ORB_BLUR_WAVES
+#define ORB_BLUR_WAVES 4
+#endif
+__global__ __launch_bounds__(64 * ORB_BLUR_WAVES) ORB_WPE8 ORB_BLUR_WPE void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
   constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int wid = ORB_BLUR_WAVES == 4 ? bid : bid >> 2;  // the 4-wave tile
   const int img = wid / P->blur_tiles;
   int t = wid - img * P->blur_tiles;
   int l = 0;
   while (l + 1 < P->levels && t >= P->lev[l + 1].blur_tile_begin) ++l;
   const LevelGeom& g = P->lev[l];
   t -= g.blur_tile_begin;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int wave = ORB_BLUR_WAVES == 4 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (bid & 3);
   int sp;
   const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
   uint8_t* dst = blur + (size_t)img * P->blur_bytes + g.blur_off;
@@ -1916,7 +1923,10 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
 // leave before any patch load (their oct_out entries are stale).  Slot, level
 // and keypoint are wave-uniform (scalar unit); the patches are staged as
 // fixed row x dword grids so LDS stores take immediate offsets.
-__global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
+#ifndef ORB_DESC_WAVES
+#define ORB_DESC_WAVES 4  // waves (one keypoint each) per k_describe workgroup
+#endif
+__global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
                                                   const uint8_t* __restrict__ pyr,
                                                   const uint8_t* __restrict__ blur,
                                                   const uint32_t* __restrict__ oct_out,
@@ -1924,12 +1934,12 @@ __global__ __launch_bounds__(256) void k_describe(const PlanHeader* __restrict__
                                                   float* __restrict__ angle_out,
                                                   uint64_t* __restrict__ desc_out, int n_img) {
   constexpr int kSlice = (kDescLds + 15) & ~15;
-  __shared__ __attribute__((aligned(16))) uint8_t lds_all[4 * kSlice];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[ORB_DESC_WAVES * kSlice];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* raw = lds_all + wave * kSlice;
   uint8_t* blp = raw + kRawW * kRawH;
   const int kps = P->kp_slots;
-  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * ORB_DESC_WAVES + wave;
   if (gidx >= n_img * kps) return;  // wave-uniform
   const int img = gidx / kps;
   const int slot = gidx - img * kps;
@@ -2162,7 +2172,7 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
     }
   }
   mark(1);
-  hipLaunchKernelGGL(k_blur, dim3(n * H.blur_tiles), dim3(256), 0, st, a.plan, src,
+  hipLaunchKernelGGL(k_blur, dim3(n * H.blur_tiles * (4 / ORB_BLUR_WAVES)), dim3(64 * ORB_BLUR_WAVES), 0, st, a.plan, src,
                      (const uint8_t*)a.pyr, a.blur);
   mark(2);
   auto fast = H.fast_pitch == 48   ? k_fast_cells<48>
@@ -2184,7 +2194,8 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                      dim3(64 * ORB_DESC_WG), 0, st, a.plan, src,
 #else
   const long waves = (long)n * H.kp_slots;
-  hipLaunchKernelGGL(k_describe, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a.plan, src,
+  hipLaunchKernelGGL(k_describe, dim3((unsigned)((waves + ORB_DESC_WAVES - 1) / ORB_DESC_WAVES)),
+                     dim3(64 * ORB_DESC_WAVES), 0, st, a.plan, src,
 #endif
                      (const uint8_t*)a.pyr, (const uint8_t*)a.blur, (const uint32_t*)a.oct_out,
                      (const int*)a.oct_count, a.angle, a.desc, n);
