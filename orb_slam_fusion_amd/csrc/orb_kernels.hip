@@ -799,17 +799,35 @@ constexpr int kFastSvCarry = 64;   // + the survivors carried from the previous 
 // neighbour address is base + immediate, the score-map index i + LS + 1 (no
 // per-survivor row multiplies or offset adds).  LS = 0: pitches per cell,
 // survivors r << 7 | q.
+// One wave's LDS hand-off (its LDS operations execute in order; the fences
+// keep the compiler's order and drain lgkmcnt)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// ORB_FAST_WAVES cells (one wave each, never synchronised with each other:
+// every barrier below is the wave's own) per workgroup, each its own
+// max_roi_lds slice of the workgroup's LDS.  A/B build switch (DESIGN §11:
+// 2 and 4 measured no better than 1 and 4 less stable; a build with W > 1
+// also needs W * max_roi_lds within the LDS limit)
+#ifndef ORB_FAST_WAVES
+#define ORB_FAST_WAVES 1
+#endif
 template <int LS>
-__global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict__ P,
+__global__ __launch_bounds__(64 * ORB_FAST_WAVES) void k_fast_cells(const PlanHeader* __restrict__ P,
                                                    const Cell* __restrict__ cells, ImgSrc src,
                                                    const uint8_t* __restrict__ pyr,
                                                    uint32_t* __restrict__ slots,
-                                                   int* __restrict__ cell_count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x;
+                                                   int* __restrict__ cell_count, int n_img) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
+  const int lane = threadIdx.x & 63;
+  const int fw = ORB_FAST_WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  uint8_t* lds = lds_all + (ORB_FAST_WAVES > 1 ? fw * P->max_roi_lds : 0);
   STAMP_INIT;
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int wid = xcd_remap(blockIdx.x, gridDim.x) * ORB_FAST_WAVES + fw;
   const int img = wid / P->n_cells;
+  if (img >= n_img) return;  // (wave-uniform: the last workgroup's spare waves)
   const int ci = wid - img * P->n_cells;
   const Cell c = cells[ci];
   const int dw = c.cols - 6, dh = c.rows - 6;
@@ -899,7 +917,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   }
   // (16-byte stores: the score map's region is rounded up to 16 bytes)
   for (int i = lane; i < ((nsc + 15) >> 4); i += 64) reinterpret_cast<uint4*>(sc)[i] = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
+  wave_lds_sync();
   STAMP(6);
   STAMP_ADD(13, 1);
 
@@ -1098,7 +1116,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       }
       ns += __builtin_amdgcn_readlane(incl, 63);
     }
-    __syncthreads();
+    wave_lds_sync();
     *n_sv += ns;
     for (int j = lane; j < ns; j += 64) {
       const int i = sv[j];
@@ -1106,7 +1124,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       const uint16_t bits = __builtin_bit_cast(uint16_t, m);
       sc[sci(i)] = m >= thp1 ? (uint8_t)(bits - 1) : (uint8_t)0;
     }
-    __syncthreads();
+    wave_lds_sync();
     STAMP(1);
     int written = 0;
     if constexpr (LS != 0) {
@@ -1135,7 +1153,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       written += __popcll(km);
     }
     }
-    __syncthreads();
+    wave_lds_sync();
 #else
     // survivors, 64 group entries at a time: lane j expands entry b0 + j into
     // sv[] from the wave's inclusive scan of the entries' popcounts (raster
@@ -1153,7 +1171,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         sv[pos++] = (uint16_t)(i0 + __builtin_ctz(m));
         m &= m - 1;
       }
-      __syncthreads();
+      wave_lds_sync();
       return __builtin_amdgcn_readlane(incl, 63);
     };
     // scores of every survivor into the map: a chunk's survivors are scored
@@ -1175,10 +1193,10 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
       for (int j = lane; j < full && !(ORB_FAST_SKIP & 2); j += 64) score(sv[j]);
       pend = tot - full;
       if (full > 0 && lane < pend) sv[lane] = sv[full + lane];  // (disjoint: full >= 64 > pend)
-      __syncthreads();  // sv is rewritten by the next chunk
+      wave_lds_sync();  // sv is rewritten by the next chunk
     }
     if (lane < pend && !(ORB_FAST_SKIP & 2)) score(sv[lane]);
-    __syncthreads();
+    wave_lds_sync();
     STAMP(1);
     // NMS over the survivors again (re-expanded: the list is never held
     // whole), keypoints straight to the cell's slots in raster order: a corner
@@ -1211,7 +1229,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
         }
         written += __popcll(km);
       }
-      __syncthreads();
+      wave_lds_sync();
     }
 #endif
     STAMP(2);
@@ -1224,7 +1242,7 @@ __global__ __launch_bounds__(64) void k_fast_cells(const PlanHeader* __restrict_
   if (written == 0 && !ORB_FAST_SKIP) {
     STAMP_ADD(10, 1);
     for (int i = lane; i < ((nsc + 3) >> 2); i += 64) reinterpret_cast<uint32_t*>(sc)[i] = 0u;
-    __syncthreads();
+    wave_lds_sync();
     STAMP(3);
     ns = 0;
     written = pass(P->min_th, &ns);
@@ -2181,8 +2199,9 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
               : H.fast_pitch == 60 ? k_fast_cells<60>
               : H.fast_pitch == 64 ? k_fast_cells<64>
                                    : k_fast_cells<0>;
-  hipLaunchKernelGGL(fast, dim3(n * H.n_cells), dim3(64), H.max_roi_lds, st, a.plan,
-                     a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count);
+  hipLaunchKernelGGL(fast, dim3((unsigned)(((long)n * H.n_cells + ORB_FAST_WAVES - 1) / ORB_FAST_WAVES)),
+                     dim3(64 * ORB_FAST_WAVES), H.max_roi_lds * ORB_FAST_WAVES, st, a.plan,
+                     a.cells, src, (const uint8_t*)a.pyr, a.slots, a.cell_count, n);
   mark(3);
   hipLaunchKernelGGL(H.oct_hbm_nodes ? k_octree<true> : k_octree<false>, dim3(n * H.levels),
                      dim3(kOctThreads), a.octree_lds, st, a.plan, a.cells, (const uint32_t*)a.slots,
