@@ -46,6 +46,7 @@ extern __device__ unsigned long long g_in_stamps[64 * 32];
 #endif
 #include "f64_math_dev.h"
 #include "imu_math_dev.h"
+#include "row_halving_dev.h"
 
 namespace orbgpu {
 
@@ -662,34 +663,8 @@ __device__ void vis_sweep(InShared& sh, const VisObs* ob, const uint8_t* lv, con
       vt1 = __builtin_amdgcn_s_memtime();
 #endif
 #if ORB_IN_VIS_HALVE
-      // Row totals by recursive halving within each 16-lane row: four
-      // exchange steps (partner lane ^ 8 by row_ror:8, 7 - i within each 8 by
-      // row_half_mirror, ^ 2 and ^ 1 by quad_perm), each lane keeping the half
-      // its bit selects and adding the partner's copy of it, leave lane i of
-      // a row with the row's totals of accumulators 2i and 2i + 1: 16 + 8 +
-      // 4 + 2 exchanges instead of 4 x 27 (the sums' order differs from the
-      // row_shr chain's: parity by tolerance, as for every fp64 sum here)
-      const int li = lane & 15;
-      auto halve = [&](auto& out, const auto& in, int h, auto xch) {
-        constexpr int m = sizeof(out) / sizeof(double);
-        const bool up = (li >> h) & 1;
-#pragma unroll
-        for (int j = 0; j < m; ++j) {
-          const double lo = in[j], hi = in[j + m];
-          out[j] = (up ? hi : lo) + xch(up ? lo : hi);
-        }
-      };
-      double a32[32];
-#pragma unroll
-      for (int k = 0; k < 32; ++k) a32[k] = k < 27 ? acc[k] : 0.0;
-      double v16[16], v8[8], v4[4], v2[2];
-      halve(v16, a32, 3, [](double x) { return dpp_d<0x128, 0xf>(x); });
-      halve(v8, v16, 2, [](double x) { return dpp_d<0x141, 0xf>(x); });
-      halve(v4, v8, 1, [](double x) { return dpp_d<0x4E, 0xf>(x); });
-      halve(v2, v4, 0, [](double x) { return dpp_d<0xB1, 0xf>(x); });
-      double* dst = sh.red + (wave * 4 + (lane >> 4)) * 27;
-      if (2 * li < 27) dst[2 * li] = v2[0];
-      if (2 * li + 1 < 27) dst[2 * li + 1] = v2[1];
+      // row totals by recursive halving (row_halving_dev.h)
+      row_totals_halving<27>(acc, lane, sh.red + (wave * 4 + (lane >> 4)) * 27);
 #else
       // DPP row sums; lane 15 of each row writes its partial
 #pragma unroll
