@@ -310,9 +310,17 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   if (reduce && (size_t)n * n + 2 * (size_t)n > (size_t)INT_MAX) return ORBGPU_ERR_CAPACITY;
   const int np = pt_end - pt_begin;
   std::vector<int> cnt(np + 1, 0);
+  // point-major input (the reference adds a point's edges together, points in
+  // turn: optimizer.cc:1187-1262) needs no scatter below: the shard's edges
+  // are then the contiguous run after the i_lo edges of lower points
+  bool sorted = true;
+  int prev_pt = 0, i_lo = 0;
   for (int i = 0; i < n_edges; ++i) {
     const orbgpu_lba_edge& e = edges[i];
     if (e.point < 0 || e.point >= n_pts || e.kf < 0 || e.kf >= n_kf) return ORBGPU_ERR_INVALID;
+    sorted &= e.point >= prev_pt;
+    prev_pt = e.point;
+    i_lo += e.point < pt_begin;
     if (e.point >= pt_begin && e.point < pt_end) ++cnt[e.point - pt_begin + 1];
   }
   int n_edgeless = 0;
@@ -331,10 +339,14 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // scatter of indices, then sequential gathers), pf[j] its free-pose index
   std::vector<int> perm(std::max(ne, 1)), pf(std::max(ne, 1));  // pf: -1 = fixed pose
   {
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int i = 0; i < n_edges; ++i) {
-      const int p = edges[i].point;
-      if (p >= pt_begin && p < pt_end) perm[fill[p - pt_begin]++] = i;
+    if (sorted) {
+      std::iota(perm.begin(), perm.begin() + ne, i_lo);
+    } else {
+      std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+      for (int i = 0; i < n_edges; ++i) {
+        const int p = edges[i].point;
+        if (p >= pt_begin && p < pt_end) perm[fill[p - pt_begin]++] = i;
+      }
     }
   LBA_HOST_PHASE(2);
     auto add_pair = [&](int i, int j) {

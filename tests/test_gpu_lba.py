@@ -72,6 +72,21 @@ def test_lba_c4_window(gpu_available):
     assert got["stats"][1] < got["stats"][0]
 
 
+@pytest.mark.parametrize("order", ["shuffled", "one_swap"])
+def test_lba_edges_in_any_order(gpu_available, order):
+    # point-major input skips the layout's scatter (lba_api.cpp run_window);
+    # any other order takes it: both against the oracle on the same edge list
+    p = synth.lba_problem(seed=3, n_kf=8, n_pts=400, obs_per_pt=4, n_fixed=1, outlier_pct=10)
+    if order == "shuffled":
+        p.edges = p.edges[np.random.default_rng(11).permutation(len(p.edges))]
+    else:  # sorted but for the last two edges of different points
+        i = np.nonzero(np.diff(p.edges["point"]) > 0)[0][-1]
+        idx = np.arange(len(p.edges))
+        idx[[i, i + 1]] = idx[[i + 1, i]]
+        p.edges = p.edges[idx]
+    _compare(p)
+
+
 def test_lba_window_past_2048_rows(gpu_available):
     """344 free key frames: a 2064-row reduced system (the HBM solve path; the
     round-2 API refused it) -- one LM iteration against the oracle."""
