@@ -2355,8 +2355,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
 #pragma unroll
           for (int q = 0; q < 7; ++q) a.poses[s1][7 * k + q] = tp[7 * k + q];
       }
-      __syncthreads();
-      tposes = tp;
+      tposes = tp;  // (read after the back-substitution's barrier below)
     }
   } else {
     // the trial key-frame states, every block its own copy in LDS (block 0
@@ -2369,8 +2368,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
         if (blockIdx.x == 0)
           for (int q = 0; q < kImuStateStride; ++q) a.poses[s1][kImuStateStride * k + q] = d[q];
       }
-      __syncthreads();
-      tposes = ts;
+      tposes = ts;  // (read after the barrier below / the back-substitution's)
     }
   }
   const int i = blockIdx.x * kThreads + threadIdx.x;
@@ -2385,6 +2383,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     const int neb = (max(a.n_edges, 1) + kThreads - 1) / kThreads;
     if ((int)blockIdx.x >= neb) {
       const int l = (int)blockIdx.x - neb;
+      __syncthreads();  // the trial states' table
       if (l < a.n_imu) {  // (block-uniform)
         const double chi = lia_link<true>(a, l, threadIdx.x, tposes, nullptr, s1, lsh);
         if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
@@ -2407,7 +2406,10 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     pA = a.edges[i_first].point;
     n_bp = a.edges[min(i_first + kThreads, a.n_edges) - 1].point - pA + 1;
   }
-  for (int k = threadIdx.x; k < n_bp; k += kThreads) {
+  // (threads from the second wave on first: the first wave's lanes stage
+  // the trial poses / states above, and the two run side by side up to the
+  // one barrier below)
+  for (int k = (threadIdx.x + kThreads - 64) % kThreads; k < n_bp; k += kThreads) {
     const int p = pA + k;
     const int e0 = a.pt_begin[p], e1 = a.pt_begin[p + 1];
     const double* blp = a.bl + 3 * (size_t)p;
