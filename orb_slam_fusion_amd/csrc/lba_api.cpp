@@ -508,6 +508,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
     le[j] = LbaEdgeDev{e.point - pt_begin, e.kf, pf[j], 0, e.u, e.v, e.ur, e.inv_sigma2};
   }
   LBA_HOST_PHASE(7);
+  // the image's head (control words, the edge records) goes up now, its DMA
+  // under the host's remaining layout work; the rest after it
+  if (hipMemcpyAsync(h->arena, U, u_ints, hipMemcpyHostToDevice, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
   int* I = reinterpret_cast<int*>(U + u_ints);
   int* I_slot = I;  // int4 records first (16-B aligned)
   int* I_incl = I_slot + 4 * E;  // int4 link records
@@ -590,7 +593,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   }
   LBA_HOST_PHASE(10);
   const auto t_layout = clk::now();
-  if (hipMemcpyAsync(h->arena, U, up, hipMemcpyHostToDevice, st) != hipSuccess)
+  if (hipMemcpyAsync(h->arena + u_ints, U + u_ints, up - u_ints, hipMemcpyHostToDevice, st) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
 
   // ---- device argument block
