@@ -343,6 +343,9 @@ orbgpu_status orbgpu_lba_ctx_set_memory_limit(orbgpu_lba_ctx* c, size_t bytes);
  * the call when it is already set (optimizer.cc:1356-1357).
  * The LM loop runs on the device; with reduce == NULL the call synchronises
  * once, at its end.
+ * Edges may come in any order; a point's edges keep their order among
+ * themselves.  Edges sorted by point (the reference's insertion order,
+ * optimizer.cc:1187-1262) skip one host layout pass.
  * Outputs: optimised poses (float, unit quaternion; poses_out_d optional
  * doubles), pts_out rows of the shard's points, outlier[i] for the shard's
  * edges (chi2 > 5.991 / 7.815 or depth <= 0), stats (optional, 6 doubles):
