@@ -436,7 +436,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // kModelImu, its link-assembly blocks)
   const long nblk = (std::max(std::max(ne, np), 1) + 255) / 256 + kSumsQ * (long)nf + 1 +
                     (imu ? ((long)n * n + n + 255) / 256 + m.n_imu : 0);  // (+ the trial's link blocks)
-  const size_t n_ints = 4 * E + (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
+  const size_t n_ints = (size_t)n_kf + (np + 1) + (nf + 1) + E + 2 * (size_t)std::max(n_pairs, 1) +
                         F + (nf + 1) + std::max(inc_list.size(), (size_t)4) + E;
   // the Schur chunk layout (ints): chunk table (int4 first), tile offsets, point order
   const size_t n_sc = (sc.ok ? 4 * sc.chunk.size() + sc.tile0.size() + sc.order.size() : 1) +
@@ -485,6 +485,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
                c_imuq = take(imu ? 2 * kImuPairQ * NI : 1), c_himu = take(imu ? (size_t)n * n + n : 1),
                c_itot = take(2 + NI),  // [2 + l] per link
                c_ppart = take(27 * (size_t)kSumsQ * F),
+               c_pslot = take(2 * E),  // int4 slot records, device-built (k_lba_begin)
                c_scp = take(std::max(sc.ok ? 256 * (size_t)sc.tile0.back() : 1,
                                      sc_split > 1 ? 42 * (size_t)n_pairs * sc_split : 1));
   LBA_HOST_PHASE(6);
@@ -512,8 +513,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   // under the host's remaining layout work; the rest after it
   if (hipMemcpyAsync(h->arena, U, u_ints, hipMemcpyHostToDevice, st) != hipSuccess) return ORBGPU_ERR_DEVICE;
   int* I = reinterpret_cast<int*>(U + u_ints);
-  int* I_slot = I;  // int4 records first (16-B aligned)
-  int* I_incl = I_slot + 4 * E;  // int4 link records
+  int* I_incl = I;  // int4 link records first (16-B aligned)
   int* I_hidx = I_incl + std::max(inc_list.size(), (size_t)4);
   int* I_pt = I_hidx + n_kf;
   int* I_pb = I_pt + (np + 1);
@@ -528,8 +528,9 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   for (int f = 0; f < nf; ++f) pose_cnt[f + 1] += pose_cnt[f];
   std::copy(pose_cnt.begin(), pose_cnt.end(), I_pb);
   // one walk in point order (host-side arrays only: nothing is read back from
-  // pinned memory): each edge's pose slot, the slot records and
-  // (k_lba_schur_split) per free pose the slot where each point range starts
+  // pinned memory): each edge's pose slot (k_lba_begin builds the slot
+  // records from it) and (k_lba_schur_split) per free pose the slot where
+  // each point range starts
   // (slots are in point order within a pose).  The edge image and the free-
   // pose indices go in sequential passes of their own: interleaving them here
   // measured slower (layout 87 -> 113 µs), the pinned image taking several
@@ -555,13 +556,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
           I_es[j] = -1;
           continue;
         }
-        const int k = fill[f]++;
-        I_es[j] = k;
-        int* r = I_slot + 4 * (size_t)k;
-        r[0] = j;
-        r[1] = p;
-        r[2] = cnt[p];
-        r[3] = cnt[p + 1];
+        I_es[j] = fill[f]++;  // (k_lba_begin writes slot I_es[j]'s record)
       }
     }
     if (sc_split > 0) range_starts(np);
@@ -640,7 +635,7 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.hidx = dI + (I_hidx - I);
   a.pt_begin = dI + (I_pt - I);
   a.pose_begin = dI + (I_pb - I);
-  a.pslot = reinterpret_cast<const int4*>(dI + (I_slot - I));
+  a.pslot = reinterpret_cast<const int4*>(A + c_pslot);
   a.ef = dI + (I_ef - I);
   a.pair_i = dI + (I_pi - I);
   a.pair_j = dI + (I_pj - I);

@@ -750,6 +750,11 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   double r0 = 0;
   if (i < a.n_edges) {
     const LbaEdgeDev e = a.edges[i];
+    // the pose-slot record of a free-pose edge (read by the Schur kernels,
+    // which run after this launch): built here, not uploaded
+    const int ks = a.eslot[i];
+    if (ks >= 0)
+      const_cast<int4*>(a.pslot)[ks] = make_int4(i, e.point, a.pt_begin[e.point], a.pt_begin[e.point + 1]);
     const double* x = a.pts[0] + 3 * e.point;
     const double X[3] = {x[0], x[1], x[2]};
     double err[3];

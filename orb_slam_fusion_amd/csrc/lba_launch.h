@@ -88,7 +88,7 @@ struct LbaArgs {
   const int* hidx;           // [n_kf] free-pose index, -1 = fixed
   const int* pt_begin;       // [n_pts + 1] CSR of edges per point
   const int* pose_begin;     // [n_free + 1] CSR of edges per free pose
-  const int4* pslot;         //   {edge, point, point's first edge, end} (edge ascending)
+  const int4* pslot;         //   {edge, point, point's first edge, end} (edge ascending; k_lba_begin writes it)
   const int* ef;             // [n_edges] free-pose index of each edge (edges[i].f, packed)
   const int* pair_i;         // [n_pairs] free-pose pairs (i <= j), row-major upper triangle
   const int* pair_j;
