@@ -15,7 +15,7 @@ GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/lba_kernels
             $(CSRC)/match_api.cpp $(CSRC)/vocab_api.cpp
 GPU_HDRS := $(wildcard $(CSRC)/*.h) $(wildcard $(CSRC)/*.inc) include/orbgpu.h
 
-all: $(LIB)/liborbgpu.so $(LIB)/liborbgpu_checkuniform.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial oracle
+all: $(LIB)/liborbgpu.so $(LIB)/liborbgpu_checkuniform.so $(LIB)/liborbsynth.so build/valu_calib build/latency_inertial build/latency oracle
 
 OBJDIR   := build/obj
 GPU_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(GPU_SRCS))
@@ -80,6 +80,12 @@ build/valu_calib: tools/valu_calib.hip
 build/latency_inertial: tools/latency_inertial.cc include/orbgpu.h $(LIB)/liborbgpu.so
 	@mkdir -p build
 	$(CXX) -std=c++17 -O2 -pthread -o $@ $< -L$(LIB) -lorbgpu -Wl,-rpath,'$$ORIGIN/../$(LIB)'
+
+# C++ caller of the C ABI for the per-frame extract + PoseOptimization latency
+# (tools/bench_latency.py runs it beside its Python leg); frames from liborbsynth
+build/latency: tools/latency.cc include/orbgpu.h $(LIB)/liborbgpu.so $(LIB)/liborbsynth.so
+	@mkdir -p build
+	$(CXX) -std=c++17 -O2 -pthread -o $@ $< -L$(LIB) -lorbgpu -lorbsynth -Wl,-rpath,'$$ORIGIN/../$(LIB)'
 
 oracle:
 	$(MAKE) -C oracle

@@ -87,6 +87,20 @@ orbgpu_status orbgpu_extractor_set_stage_event(orbgpu_extractor* h, int stage, v
 #define ORBGPU_PYRAMID_FUSED 1
 orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode);
 
+/* How orbgpu_extract (one image from host buffers: the reference's
+ * per-frame call) runs on the device (same bytes either way):
+ * ORBGPU_SINGLE_DATAFLOW (default) ONE launch whose persistent workers take
+ * the stages' work items by ticket, each item waiting only for the items it
+ * reads (level 0's FAST and octree start while the resize chain runs), the
+ * image read from pinned host memory and the outputs written back to it by
+ * the launch itself; ORBGPU_SINGLE_GRAPH the batch path's per-stage launches
+ * with two copies, replayed as a hipGraph.  Plans whose octree nodes live in
+ * HBM always take the per-stage launches.  The environment variable
+ * ORBGPU_SINGLE=graph sets the default at creation. */
+#define ORBGPU_SINGLE_DATAFLOW 0
+#define ORBGPU_SINGLE_GRAPH 1
+orbgpu_status orbgpu_extractor_set_single_launch(orbgpu_extractor* h, int mode);
+
 /* Where DistributeOctTree's node list lives (orb_extractor.cc:542-742; the
  * reference's std::list has no bound, and neither does its per-level budget,
  * :432-444).  ORBGPU_OCTREE_NODES_AUTO (default): in LDS whenever the plan's
@@ -158,7 +172,8 @@ orbgpu_status orbgpu_extract_batch(orbgpu_extractor* h, const uint8_t* d_imgs, i
  *   image_pitch are that call's level-0 planes and d_kps / d_descs /
  *   cap_per_image / d_n its outputs, all still on the device.  Writes
  *   d_uright / d_depth as [n_frames][cap_per_image] floats, stream-ordered on
- *   hip_stream (NULL: the handle's stream). */
+ *   hip_stream (NULL: the handle's stream).  cap_per_image <= 65535 (the row
+ *   lists and match keys hold 16-bit keypoint indices; larger: INVALID). */
 orbgpu_status orbgpu_stereo_match_batch(orbgpu_extractor* h, int n_frames, const uint8_t* d_imgs,
                                         int stride, size_t image_pitch, const orbgpu_keypoint* d_kps,
                                         const uint8_t* d_descs, int cap_per_image, const int* d_n,
@@ -169,7 +184,8 @@ orbgpu_status orbgpu_stereo_match_batch(orbgpu_extractor* h, int n_frames, const
  *   (mpORBextractorLeft / Right) right after their orbgpu_extract calls on the
  *   frame's images (same parameters and size); their keypoints, descriptors
  *   and pyramids are used where they lie on the device.  Writes N = the left
- *   call's keypoint count floats to uright / depth (host), N <= cap. */
+ *   call's keypoint count floats to uright / depth (host), N <= cap.  Plans
+ *   with more than 65535 keypoint slots are refused (INVALID), as the batch. */
 orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* right, float bf,
                                   float mb, float* uright, float* depth, int cap);
 
@@ -317,9 +333,12 @@ orbgpu_status orbgpu_lba_ctx_set_schur(orbgpu_lba_ctx* c, int mode);
 orbgpu_status orbgpu_lba_ctx_set_relinearize(orbgpu_lba_ctx* c, int on);
 
 /* Device-memory budget of the context (bytes; 0 = none, the default).  A
- * window whose arena would exceed it returns ORBGPU_ERR_NOMEM before any
- * device work, the context stays usable -- the caller's hook for a per-window
- * memory bound (the drop-ins throw on NOMEM). */
+ * window whose device arena would exceed it returns ORBGPU_ERR_NOMEM before
+ * any device work, the context stays usable -- the caller's hook for a
+ * per-window memory bound (the drop-ins throw on NOMEM).
+ * Only the device arena is counted: the pinned host staging and result
+ * buffers, which also grow with the window (about the size of the uploaded
+ * edges and of the returned state), are outside the budget. */
 orbgpu_status orbgpu_lba_ctx_set_memory_limit(orbgpu_lba_ctx* c, size_t bytes);
 
 /* Window size: the reduced camera system (6 rows per free key frame) is

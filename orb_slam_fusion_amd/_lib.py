@@ -35,6 +35,8 @@ ORBGPU_OCTREE_NODES_AUTO = 0
 ORBGPU_OCTREE_NODES_HBM = 1
 ORBGPU_PYRAMID_PER_LEVEL = 0
 ORBGPU_PYRAMID_FUSED = 1
+ORBGPU_SINGLE_DATAFLOW = 0
+ORBGPU_SINGLE_GRAPH = 1
 
 STATUS_NAMES = {
     ORBGPU_OK: "OK",
@@ -179,6 +181,7 @@ SIGNATURES = {
     "orbgpu_extractor_set_resize_rounding": (_I, [_P, _I]),
     "orbgpu_extractor_set_octree_nodes": (_I, [_P, _I]),
     "orbgpu_extractor_set_pyramid_launch": (_I, [_P, _I]),
+    "orbgpu_extractor_set_single_launch": (_I, [_P, _I]),
     "orbgpu_extractor_set_stage_event": (_I, [_P, _I, _P]),
     "orbgpu_extractor_plan": (_I, [_P, _I, _I, _P, _P]),
     "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),

@@ -2411,9 +2411,11 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
     pA = a.edges[i_first].point;
     n_bp = a.edges[min(i_first + kThreads, a.n_edges) - 1].point - pA + 1;
   }
-  // (threads from the second wave on first: the first wave's lanes stage
-  // the trial poses / states above, and the two run side by side up to the
-  // one barrier below)
+  // (the points are dealt starting from the second wave: threads k < n_kf
+  // stage the trial poses / states above -- only wave 0 when n_kf <= 64, as
+  // in the C4 / LIA windows the overlap was measured on -- and this rotation
+  // puts wave 0 last in the back-substitution, so the two run side by side
+  // up to the one barrier below, which makes any n_kf correct)
   for (int k = (threadIdx.x + kThreads - 64) % kThreads; k < n_bp; k += kThreads) {
     const int p = pA + k;
     const int e0 = a.pt_begin[p], e1 = a.pt_begin[p + 1];

@@ -82,10 +82,20 @@ struct orbgpu_extractor {
   int* h_small = nullptr;  // n, mono, err (pinned)
   orbgpu_keypoint* h_kps = nullptr;
   uint8_t* h_descs = nullptr;
-  // pinned staging of the image: the copies are part of the graph (fixed
-  // addresses and sizes), the host only memcpys
+  // pinned (host-mapped, fine-grained) staging of the image: the graph's copy
+  // or the dataflow launch's copy items read it, the host only memcpys
   uint8_t* h_img = nullptr;
+  uint8_t* h_img_dev = nullptr;  // its device view
   size_t h_img_bytes = 0;
+  char* h_sout_dev = nullptr;    // device view of h_sout (the dataflow launch mirrors into it)
+  // the dataflow launch (k_extract_df): control block, launch record + item list
+  int single_mode = ORBGPU_SINGLE_DATAFLOW;
+  int* d_df_ctrl = nullptr;
+  DfLaunch* d_df_rec = nullptr;  // record, then the items
+  size_t df_rec_cap = 0;         // bytes of d_df_rec
+  DfLaunch df_launch{};          // what d_df_rec holds
+  bool df_valid = false;
+  int df_grid = 0;               // ORBGPU_DF_GRID (tools): workers, else the CU count
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   ExtractLaunch graph_launch{};  // what graph_exec was captured for
@@ -124,6 +134,7 @@ void drop_graphs(orbgpu_extractor* h) {
   h->graph = nullptr;
   h->graph_valid = false;
   h->eager_valid = false;
+  h->df_valid = false;  // the dataflow record names the same buffers
 }
 
 // The single-image output blocks for `slots` keypoints (see orbgpu_extractor).
@@ -136,7 +147,9 @@ orbgpu_status ensure_single_out(orbgpu_extractor* h, size_t slots) {
   if (h->h_sout) (void)hipHostFree(h->h_sout);
   h->d_sout = h->h_sout = nullptr;
   h->out_cap = 0;
-  if (hipMalloc(&h->d_sout, bytes) != hipSuccess || hipHostMalloc(&h->h_sout, bytes) != hipSuccess)
+  if (hipMalloc(&h->d_sout, bytes) != hipSuccess ||
+      hipHostMalloc(&h->h_sout, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_sout_dev), h->h_sout, 0) != hipSuccess)
     return ORBGPU_ERR_NOMEM;
   if (hipMemset(h->d_sout, 0, 16) != hipSuccess) return ORBGPU_ERR_DEVICE;
   h->sout_bytes = bytes;
@@ -394,6 +407,72 @@ static hipError_t run_single_chain(orbgpu_extractor* h, const ExtractLaunch& a) 
   return enqueue_chain(h, a);
 }
 
+// The single-image chain as one dataflow launch (k_extract_df): the launch
+// record (device pointers, lapping, the plan's item shape) lives in device
+// memory next to the item list and is rewritten only when it changes (a new
+// plan or buffer, another lapping band).  The outputs reach the host through
+// the launch's own mirror writes into the mapped h_sout: no copy commands.
+static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const int lap[2]) {
+  const PlanHeader& P = h->plan.hdr;
+  DfLaunch a;
+  std::memset(&a, 0, sizeof a);
+  a.plan = h->d_plan;
+  a.cells = h->d_cells;
+  a.rs_tab = h->d_rs;
+  a.ctrl = h->d_df_ctrl;
+  a.img_host = h->h_img_dev;
+  a.img = h->d_img;
+  a.pyr = h->d_pyr;
+  a.blur = h->d_blur;
+  a.slots = h->d_slots;
+  a.cell_count = h->d_cell_count;
+  a.dense = h->d_dense;
+  a.knode = h->d_knode;
+  a.oct_out = h->d_oct_out;
+  a.oct_count = h->d_oct_count;
+  a.angle = h->d_angle;
+  a.desc = h->d_desc;
+  a.lap0 = lap[0];
+  a.lap1 = lap[1];
+  a.kps_out = h->d_kps;
+  a.desc_out = h->d_descs;
+  a.nm = h->d_nm;
+  a.nm_host = reinterpret_cast<int*>(h->h_sout_dev);
+  a.kps_host = h->h_sout_dev + (reinterpret_cast<char*>(h->d_kps) - h->d_sout);
+  a.desc_host = h->h_sout_dev + (reinterpret_cast<char*>(h->d_descs) - h->d_sout);
+  a.cap = P.kp_slots;
+  std::vector<uint32_t> items;
+  if (h->df_valid) {
+    a.items = h->df_launch.items;
+    a.grid = h->df_launch.grid;
+    a.df = h->df_launch.df;
+  } else {
+    make_df_items(P, (int)img_bytes, a.df, items);
+    a.df.lds_bytes = (int)df_lds_bytes(P, octree_lds_bytes(P));
+    a.grid = std::min(a.df.n_items, h->df_grid > 0 ? h->df_grid : h->n_cu);
+    const size_t need = sizeof(DfLaunch) + items.size() * sizeof(uint32_t);
+    if (need > h->df_rec_cap) {
+      if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+      dfree(h->d_df_rec);
+      if (hipMalloc(reinterpret_cast<void**>(&h->d_df_rec), need) != hipSuccess) return ORBGPU_ERR_NOMEM;
+      h->df_rec_cap = need;
+    }
+    a.items = reinterpret_cast<const uint32_t*>(h->d_df_rec + 1);
+    if (set_df_lds_limit((size_t)a.df.lds_bytes) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  }
+  if (!h->df_valid || std::memcmp(&a, &h->df_launch, sizeof a) != 0) {
+    // rare (a new plan, buffer or lapping band): ordered after the stream's work
+    if (hipStreamSynchronize(h->stream) != hipSuccess ||
+        hipMemcpy(h->d_df_rec, &a, sizeof a, hipMemcpyHostToDevice) != hipSuccess ||
+        (!items.empty() && hipMemcpy(h->d_df_rec + 1, items.data(), items.size() * sizeof(uint32_t),
+                                     hipMemcpyHostToDevice) != hipSuccess))
+      return ORBGPU_ERR_DEVICE;
+    h->df_launch = a;
+    h->df_valid = true;
+  }
+  return launch_extract_df(h->df_launch, h->d_df_rec, h->stream) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+}
+
 extern "C" {
 
 orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int device, int max_width,
@@ -417,8 +496,12 @@ orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int devic
   if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       h->n_cu < 1)
     h->n_cu = 256;
+  if (const char* e = std::getenv("ORBGPU_SINGLE"))  // A/B default for tools, read once
+    if (std::strcmp(e, "graph") == 0) h->single_mode = ORBGPU_SINGLE_GRAPH;
+  if (const char* e = std::getenv("ORBGPU_DF_GRID")) h->df_grid = std::atoi(e);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1)) {
+      dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1) || dalloc(&h->d_df_ctrl, (size_t)kDfCounters * kDfCtrStride) ||
+      hipMemset(h->d_df_ctrl, 0, sizeof(int) * kDfCounters * kDfCtrStride) != hipSuccess) {
     orbgpu_extractor_destroy(h);
     return ORBGPU_ERR_DEVICE;
   }
@@ -454,6 +537,8 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_desc);
   dfree(h->d_err);
   dfree(h->d_img);
+  dfree(h->d_df_ctrl);
+  dfree(h->d_df_rec);
   if (h->d_sout) (void)hipFree(h->d_sout);
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
@@ -521,6 +606,12 @@ orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode)
   return ORBGPU_OK;
 }
 
+orbgpu_status orbgpu_extractor_set_single_launch(orbgpu_extractor* h, int mode) {
+  if (!h || (mode != ORBGPU_SINGLE_DATAFLOW && mode != ORBGPU_SINGLE_GRAPH)) return ORBGPU_ERR_INVALID;
+  h->single_mode = mode;
+  return ORBGPU_OK;
+}
+
 orbgpu_status orbgpu_extractor_plan(const orbgpu_orb_params* params, int width, int height,
                                     int* kp_slots, int* octree_hbm) {
   if (!params) return ORBGPU_ERR_INVALID;
@@ -566,7 +657,9 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
     if (h->h_img) (void)hipHostFree(h->h_img);
     h->h_img = nullptr;
     h->h_img_bytes = 0;
-    if (hipHostMalloc(&h->h_img, bytes) != hipSuccess) return ORBGPU_ERR_NOMEM;
+    if (hipHostMalloc(&h->h_img, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_img_dev), h->h_img, 0) != hipSuccess)
+      return ORBGPU_ERR_NOMEM;
     h->h_img_bytes = bytes;
   }
   if ((st = ensure_single_out(h, (size_t)P.kp_slots)) != ORBGPU_OK) return st;
@@ -578,11 +671,16 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
       std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
   }
   const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
-  ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
-                                P.kp_slots, h->d_nm, h->d_nm + 1);
-  a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs
-  if (run_single_chain(h, a) != hipSuccess || hipStreamSynchronize(h->stream))
-    return ORBGPU_ERR_DEVICE;
+  if (h->single_mode == ORBGPU_SINGLE_DATAFLOW && !P.oct_hbm_nodes) {
+    if ((st = run_single_df(h, bytes, lap)) != ORBGPU_OK) return st;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  } else {
+    ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
+                                  P.kp_slots, h->d_nm, h->d_nm + 1);
+    a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs
+    if (run_single_chain(h, a) != hipSuccess || hipStreamSynchronize(h->stream))
+      return ORBGPU_ERR_DEVICE;
+  }
   const int nm[2] = {h->h_small[0], h->h_small[1]}, err = h->h_small[2];
   h->host_pyr_valid = false;
   h->last_w = width;
@@ -765,6 +863,7 @@ orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* righ
   if (hipSetDevice(left->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
   const PlanHeader& P = left->plan.hdr;
   const int kcap = P.kp_slots;
+  if (kcap > 65535) return ORBGPU_ERR_INVALID;  // u16 row lists / match keys (k_stereo_match)
   orbgpu_status st = ensure_stereo(left, 1, kcap);
   if (st != ORBGPU_OK) return st;
   const size_t need = 4 + (size_t)2 * kcap;

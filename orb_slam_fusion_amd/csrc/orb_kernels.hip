@@ -16,6 +16,7 @@
 
 #include <algorithm>
 
+#include "orb_launch.h"
 #include "orb_math_dev.h"
 #include "orb_plan.h"
 
@@ -644,6 +645,43 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
 #ifndef ORB_BLUR_WAVES
 #define ORB_BLUR_WAVES 4
 #endif
+// One wave of blur tile t (over all levels of an image, PlanHeader::blur_tiles)
+// of image img: a full tile's R-row strip `wave` (threadIdx.x >> 6), or the
+// tail strips of tail wave 4 (t - nfull) + wave.  No synchronisation.
+// (ORB_BLUR_WAVES == 1: the wave is bid & 3 of the one-wave workgroups)
+__device__ __forceinline__ void blur_wave(const PlanHeader* __restrict__ P, ImgSrc src,
+                                          const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                          int img, int t, int bid) {
+  constexpr int R = kBlurTileH / 4;  // output rows per thread; one wave = one R-row strip
+  int l = 0;
+  while (l + 1 < P->levels && t >= P->lev[l + 1].blur_tile_begin) ++l;
+  const LevelGeom& g = P->lev[l];
+  t -= g.blur_tile_begin;
+  const int lane = threadIdx.x & 63;
+  const int wave = ORB_BLUR_WAVES == 4 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (bid & 3);
+  int sp;
+  const uint8_t* S = level_plane(P, src, pyr, img, l, sp);
+  uint8_t* dst = blur + (size_t)img * P->blur_bytes + g.blur_off;
+  const int nfull = g.tiles_x * g.tiles_y;
+  if (t < nfull) {
+    const int ty = t / g.tiles_x, tx = t - ty * g.tiles_x;
+    const int x = tx * kBlurTileW + 4 * lane;
+    // wave-uniform row origin: row addressing and row bounds stay scalar
+    const int ys = ty * kBlurTileH + R * wave;
+    if (x >= g.w || ys >= g.h) return;
+    blur_strip<false>(P, g, S, sp, dst, x, ys);
+  } else {
+    // tail wave: tail_s strips of tail_nl lanes, strip s at rows ys0 + 32 s
+    const int tw = 4 * (t - nfull) + wave;
+    const int s = lane / g.tail_nl, c = lane - s * g.tail_nl;
+    const int x = g.tiles_x * kBlurTileW + 4 * c, ys = (tw * g.tail_s + s) * R;
+    if (s >= g.tail_s || x >= g.w || ys >= g.h) return;
+    blur_strip<true>(P, g, S, sp, dst, x, ys);
+  }
+}
+
+// (the same body as blur_wave, kept verbatim: as a call of blur_wave the
+// register allocation of the edge path came out one v_mov per row longer)
 __global__ __launch_bounds__(64 * ORB_BLUR_WAVES) ORB_WPE8 ORB_BLUR_WPE void k_blur(const PlanHeader* __restrict__ P, ImgSrc src,
                                               const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur) {
@@ -814,21 +852,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef ORB_FAST_WAVES
 #define ORB_FAST_WAVES 1
 #endif
+// FAST cell ci of image img by one wave (lane 0..63) with its own LDS slice
+// of PlanHeader::max_roi_lds bytes; only wave-level synchronisation.
 template <int LS>
-__global__ __launch_bounds__(64 * ORB_FAST_WAVES) void k_fast_cells(const PlanHeader* __restrict__ P,
-                                                   const Cell* __restrict__ cells, ImgSrc src,
-                                                   const uint8_t* __restrict__ pyr,
-                                                   uint32_t* __restrict__ slots,
-                                                   int* __restrict__ cell_count, int n_img) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
-  const int lane = threadIdx.x & 63;
-  const int fw = ORB_FAST_WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  uint8_t* lds = lds_all + (ORB_FAST_WAVES > 1 ? fw * P->max_roi_lds : 0);
+__device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
+                                          const ImgSrc& src, const uint8_t* __restrict__ pyr,
+                                          uint32_t* __restrict__ slots, int* __restrict__ cell_count,
+                                          int img, int ci, uint8_t* __restrict__ lds, int lane) {
   STAMP_INIT;
-  const int wid = xcd_remap(blockIdx.x, gridDim.x) * ORB_FAST_WAVES + fw;
-  const int img = wid / P->n_cells;
-  if (img >= n_img) return;  // (wave-uniform: the last workgroup's spare waves)
-  const int ci = wid - img * P->n_cells;
   const Cell c = cells[ci];
   const int dw = c.cols - 6, dh = c.rows - 6;
   const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
@@ -1254,6 +1285,22 @@ __global__ __launch_bounds__(64 * ORB_FAST_WAVES) void k_fast_cells(const PlanHe
   STAMP_END;
 }
 
+template <int LS>
+__global__ __launch_bounds__(64 * ORB_FAST_WAVES) void k_fast_cells(const PlanHeader* __restrict__ P,
+                                                   const Cell* __restrict__ cells, ImgSrc src,
+                                                   const uint8_t* __restrict__ pyr,
+                                                   uint32_t* __restrict__ slots,
+                                                   int* __restrict__ cell_count, int n_img) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_all[];
+  const int lane = threadIdx.x & 63;
+  const int fw = ORB_FAST_WAVES > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  uint8_t* lds = lds_all + (ORB_FAST_WAVES > 1 ? fw * P->max_roi_lds : 0);
+  const int wid = xcd_remap(blockIdx.x, gridDim.x) * ORB_FAST_WAVES + fw;
+  const int img = wid / P->n_cells;
+  if (img >= n_img) return;  // (wave-uniform: the last workgroup's spare waves)
+  fast_cell<LS>(P, cells, src, pyr, slots, cell_count, img, wid - img * P->n_cells, lds, lane);
+}
+
 // --------------------------------------------------------------------------
 // Block-wide helpers for the octree (256 threads).
 // --------------------------------------------------------------------------
@@ -1360,17 +1407,17 @@ struct OctLds {
 // order; the counters' atomics are workgroup-scoped (the block's waves share
 // one CU and its L1, so the barriers order them like LDS).  Only the scan
 // scratch, the block scalars and the first kcap candidates stay in LDS.
+// DistributeOctTree of level l of image img by the whole 256-thread workgroup
+// (lds_raw: octree_lds_bytes of the plan; node_ws: this (image, level)'s HBM
+// node range when kHbm).  Every exit is workgroup-uniform.
 template <bool kHbm>
-__global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
+__device__ __forceinline__ void octree_level(
     const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
     const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
     uint32_t* __restrict__ dense, int* __restrict__ knode, uint32_t* __restrict__ oct_out,
-    int* __restrict__ oct_count, int* __restrict__ err, int n_img, int kcap,
-    uint8_t* __restrict__ node_ws) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    int* __restrict__ oct_count, int* __restrict__ err, int img, int l, int kcap,
+    uint8_t* __restrict__ node_ws, uint8_t* __restrict__ lds_raw) {
   const int L = P->levels;
-  // level-major block order: the (largest) level-0 blocks are dispatched first
-  const int l = blockIdx.x / n_img, img = blockIdx.x - l * n_img;
   const LevelGeom& g = P->lev[l];
   const int NC = P->node_cap;
   const int t = threadIdx.x;
@@ -1378,7 +1425,7 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
 
   OctLds s;
   {
-    uint8_t* nodes = kHbm ? node_ws + (size_t)blockIdx.x * oct_node_bytes(NC) : lds_raw;
+    uint8_t* nodes = kHbm ? node_ws : lds_raw;
     unsigned long long* p64 = reinterpret_cast<unsigned long long*>(nodes);
     s.best = p64;
     int* p = reinterpret_cast<int*>(p64 + NC);
@@ -1703,6 +1750,20 @@ __global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
   OSTAMP_END;
 }
 
+template <bool kHbm>
+__global__ __launch_bounds__(kOctThreads) ORB_WPE8 void k_octree(
+    const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
+    const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
+    uint32_t* __restrict__ dense, int* __restrict__ knode, uint32_t* __restrict__ oct_out,
+    int* __restrict__ oct_count, int* __restrict__ err, int n_img, int kcap,
+    uint8_t* __restrict__ node_ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+  // level-major block order: the (largest) level-0 blocks are dispatched first
+  const int l = blockIdx.x / n_img, img = blockIdx.x - l * n_img;
+  octree_level<kHbm>(P, cells, slots, cell_count, dense, knode, oct_out, oct_count, err, img, l, kcap,
+                     kHbm ? node_ws + (size_t)blockIdx.x * oct_node_bytes(P->node_cap) : nullptr, lds_raw);
+}
+
 // --------------------------------------------------------------------------
 // k_describe: one wave per octree output slot.  IC_Angle on the raw level
 // (integer moments over the 31-px circular patch, fastAtan2), then 256
@@ -1944,23 +2005,19 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
 #ifndef ORB_DESC_WAVES
 #define ORB_DESC_WAVES 4  // waves (one keypoint each) per k_describe workgroup
 #endif
-__global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
-                                                  const uint8_t* __restrict__ pyr,
-                                                  const uint8_t* __restrict__ blur,
-                                                  const uint32_t* __restrict__ oct_out,
-                                                  const int* __restrict__ oct_count,
-                                                  float* __restrict__ angle_out,
-                                                  uint64_t* __restrict__ desc_out, int n_img) {
-  constexpr int kSlice = (kDescLds + 15) & ~15;
-  __shared__ __attribute__((aligned(16))) uint8_t lds_all[ORB_DESC_WAVES * kSlice];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* raw = lds_all + wave * kSlice;
+constexpr int kDescSlice = (kDescLds + 15) & ~15;  // LDS of one describe wave
+// Octree output slot `slot` of image img by one wave (lane 0..63) with its own
+// kDescSlice bytes of LDS (raw); only wave-level synchronisation.
+__device__ __forceinline__ void describe_slot(const PlanHeader* __restrict__ P, const ImgSrc& src,
+                                              const uint8_t* __restrict__ pyr,
+                                              const uint8_t* __restrict__ blur,
+                                              const uint32_t* __restrict__ oct_out,
+                                              const int* __restrict__ oct_count,
+                                              float* __restrict__ angle_out,
+                                              uint64_t* __restrict__ desc_out, int img, int slot,
+                                              uint8_t* __restrict__ raw, int lane) {
   uint8_t* blp = raw + kRawW * kRawH;
   const int kps = P->kp_slots;
-  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * ORB_DESC_WAVES + wave;
-  if (gidx >= n_img * kps) return;  // wave-uniform
-  const int img = gidx / kps;
-  const int slot = gidx - img * kps;
   int l = 0;
   while (l + 1 < P->levels && slot >= P->lev[l + 1].out_off) ++l;
   const LevelGeom& g = P->lev[l];
@@ -2052,6 +2109,23 @@ __global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHead
   if (lane == 0) angle_out[o] = angle;
 }
 
+__global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
+                                                  const uint8_t* __restrict__ pyr,
+                                                  const uint8_t* __restrict__ blur,
+                                                  const uint32_t* __restrict__ oct_out,
+                                                  const int* __restrict__ oct_count,
+                                                  float* __restrict__ angle_out,
+                                                  uint64_t* __restrict__ desc_out, int n_img) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[ORB_DESC_WAVES * kDescSlice];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kps = P->kp_slots;
+  const int gidx = xcd_remap(blockIdx.x, gridDim.x) * ORB_DESC_WAVES + wave;
+  if (gidx >= n_img * kps) return;  // wave-uniform
+  const int img = gidx / kps;
+  describe_slot(P, src, pyr, blur, oct_out, oct_count, angle_out, desc_out, img, gidx - img * kps,
+                lds_all + wave * kDescSlice, lane);
+}
+
 #endif  // ORB_DESC_KPW
 
 // --------------------------------------------------------------------------
@@ -2065,20 +2139,24 @@ struct KeyPointOut {
   int octave, class_id;
 };
 
-__global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__ P,
-                                                  const uint32_t* __restrict__ oct_out,
-                                                  const int* __restrict__ oct_count,
-                                                  const float* __restrict__ angle_in,
-                                                  const uint64_t* __restrict__ desc_in, int lap0,
-                                                  int lap1, KeyPointOut* __restrict__ kps,
-                                                  uint64_t* __restrict__ descs, int cap,
-                                                  int* __restrict__ n_out, int* __restrict__ mono_out,
-                                                  int* __restrict__ err) {
-  __shared__ int lvl_base[kMaxLevels + 1];
-  constexpr int kChunk = 4096;  // keypoints partitioned per block scan (any n: chunks carry the count)
-  __shared__ int flags[kChunk];
-  __shared__ int scan_tmp[kOctThreads + 1];
-  const int img = blockIdx.x, t = threadIdx.x, L = P->levels;
+// kMirror: every output word also goes to the host-mapped copies (kps_h,
+// descs_h, nm_h = {n, mono, err}) of the single-image launch.  LDS: lvl_base
+// (kMaxLevels + 1 ints), flags (kAsmChunk ints), scan_tmp (kOctThreads + 1).
+constexpr int kAsmChunk = 4096;  // keypoints partitioned per block scan (any n: chunks carry the count)
+constexpr int kAsmLds = 4 * (kMaxLevels + 1 + kAsmChunk + kOctThreads + 1);
+template <bool kMirror>
+__device__ __forceinline__ void assemble_image(const PlanHeader* __restrict__ P,
+                                               const uint32_t* __restrict__ oct_out,
+                                               const int* __restrict__ oct_count,
+                                               const float* __restrict__ angle_in,
+                                               const uint64_t* __restrict__ desc_in, int lap0, int lap1,
+                                               KeyPointOut* __restrict__ kps, uint64_t* __restrict__ descs,
+                                               int cap, int* __restrict__ n_out, int* __restrict__ mono_out,
+                                               int* __restrict__ err, int img, int* lvl_base, int* flags,
+                                               int* scan_tmp, KeyPointOut* __restrict__ kps_h,
+                                               uint64_t* __restrict__ descs_h, int* __restrict__ nm_h) {
+  constexpr int kChunk = kAsmChunk;
+  const int t = threadIdx.x, L = P->levels;
   if (t == 0) {
     int acc = 0;
     for (int l = 0; l < L; ++l) {
@@ -2094,6 +2172,11 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
       n_out[img] = n;
       mono_out[img] = -1;
       atomicOr(err, kErrKpCap);
+      if (kMirror) {
+        nm_h[0] = n;
+        nm_h[1] = -1;
+        nm_h[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -2146,10 +2229,19 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
       kps[(size_t)img * cap + dst] = o;
       const uint64_t* d = desc_in + so * 4;
       uint64_t* od = descs + ((size_t)img * cap + dst) * 4;
-      od[0] = d[0];
-      od[1] = d[1];
-      od[2] = d[2];
-      od[3] = d[3];
+      const uint64_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+      od[0] = d0;
+      od[1] = d1;
+      od[2] = d2;
+      od[3] = d3;
+      if (kMirror) {
+        kps_h[(size_t)img * cap + dst] = o;
+        uint64_t* oh = descs_h + ((size_t)img * cap + dst) * 4;
+        oh[0] = d0;
+        oh[1] = d1;
+        oh[2] = d2;
+        oh[3] = d3;
+      }
     }
     n_stereo += chunk_stereo;
     __syncthreads();  // flags are the next chunk's
@@ -2157,6 +2249,199 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
   if (t == 0) {
     n_out[img] = n;
     mono_out[img] = n - n_stereo;
+    if (kMirror) {
+      nm_h[0] = n;
+      nm_h[1] = n - n_stereo;
+      nm_h[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__ P,
+                                                  const uint32_t* __restrict__ oct_out,
+                                                  const int* __restrict__ oct_count,
+                                                  const float* __restrict__ angle_in,
+                                                  const uint64_t* __restrict__ desc_in, int lap0,
+                                                  int lap1, KeyPointOut* __restrict__ kps,
+                                                  uint64_t* __restrict__ descs, int cap,
+                                                  int* __restrict__ n_out, int* __restrict__ mono_out,
+                                                  int* __restrict__ err) {
+  __shared__ int lvl_base[kMaxLevels + 1];
+  __shared__ int flags[kAsmChunk];
+  __shared__ int scan_tmp[kOctThreads + 1];
+  assemble_image<false>(P, oct_out, oct_count, angle_in, desc_in, lap0, lap1, kps, descs, cap, n_out, mono_out,
+                        err, blockIdx.x, lvl_base, flags, scan_tmp, nullptr, nullptr, nullptr);
+}
+
+
+
+// --------------------------------------------------------------------------
+// k_extract_df: the single-image host path (OrbExtractor::operator() from host
+// buffers, orbgpu_extract) as ONE launch.  One frame at a time is a chain of
+// small dependent stages (7 resize levels, blur, FAST, octree, describe,
+// assemble): as separate launches each stage pays a kernel boundary and a
+// launch that covers a fraction of the chip, and the whole chain waits for
+// its slowest level.  Here persistent 256-thread workers take work items by
+// ticket (orb_launch.h, make_df_items) and each item waits only for what it
+// reads: level 0's FAST and octree start as soon as the image is copied,
+// while the resize chain and the other levels run beside them.  Stage bodies
+// are the batch kernels' own (resize_tile / resize_tail, blur_wave,
+// fast_cell, octree_level, describe_slot, assemble_image): the same bytes.
+//
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): a producer's
+// waves drain their stores (vmcnt 0), the workgroup barrier, then one lane
+// releases at agent scope and adds to the stage's counter; a consumer's lane
+// polls the counter (agent-scope relaxed loads, s_sleep between), acquires
+// at agent scope and releases the workgroup by a barrier.  Polls are bounded:
+// a wait that never completes sets kErrDfTimeout and the item runs anyway,
+// so every worker reaches the exit.  The last describe item to finish runs
+// the assembly, mirroring the output block into host-mapped memory.
+// --------------------------------------------------------------------------
+enum : int { kErrDfTimeout = 64 };
+
+__device__ __forceinline__ void df_wait(int* ctrl, int id, int target, int* err) {
+  int* c = ctrl + id * kDfCtrStride;
+  for (int spin = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spin) {
+    if (spin > (1 << 22)) {
+      atomicOr(err, kErrDfTimeout);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void df_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__ a_dev, int* __restrict__ ctrl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ int s_item, s_last;
+  for (;;) {
+    // the launch record and the thread index laundered per item: values
+    // derived from them cannot be hoisted out of the loop (every stage's
+    // would stay live across all items); the record's fields are scalar
+    // loads from the scalar cache
+    const DfLaunch* ap = a_dev;
+    asm volatile("" : "+s"(ap));
+    const DfLaunch& a = *ap;
+    const PlanHeader* __restrict__ P = a.plan;
+    const DfPlan& df = a.df;
+    int* err = a.nm + 2;
+    const ImgSrc src{a.img, 0, P->lev[0].pitch};
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(ctrl + kDfTicket * kDfCtrStride, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      s_item = t < df.n_items ? (int)a.items[t] : -1;
+    }
+    __syncthreads();
+    const int it = s_item;
+    if (it < 0) break;
+    const int type = it & 15, l = (it >> 4) & 15, idx = (int)((uint32_t)it >> 8);
+    // ---- wait for the producers of what this item reads
+    if (type != kDfCopy) {
+      if (tid == 0) {
+        if (type == kDfDescribe) {
+          df_wait(ctrl, kDfOctDone + l, 1, err);
+          df_wait(ctrl, kDfBlurDone + l, df.blur_items[l], err);
+        } else if (type == kDfOctree) {
+          df_wait(ctrl, kDfFastDone + l, df.fast_items[l], err);
+        } else {
+          const int src_l = type == kDfResize ? l - 1 : l;  // the level plane it reads
+          if (src_l == 0)
+            df_wait(ctrl, kDfImg, df.n_bands, err);
+          else
+            df_wait(ctrl, kDfLvl + src_l, df.units[src_l], err);
+        }
+        df_acquire();
+      }
+      __syncthreads();
+    }
+    // ---- the item
+    int pub;
+    if (type == kDfCopy) {
+      const int b0 = idx * kDfBandBytes, nb = min(kDfBandBytes, df.img_bytes - b0) >> 4;
+      const uint4* s4 = reinterpret_cast<const uint4*>(a.img_host + b0);
+      uint4* d4 = reinterpret_cast<uint4*>(a.img + b0);
+      uint4 v[kDfBandBytes / 16 / 256];
+#pragma unroll
+      for (int u = 0; u < kDfBandBytes / 16 / 256; ++u)
+        if (tid + 256 * u < nb) v[u] = s4[tid + 256 * u];
+#pragma unroll
+      for (int u = 0; u < kDfBandBytes / 16 / 256; ++u)
+        if (tid + 256 * u < nb) d4[tid + 256 * u] = v[u];
+      pub = kDfImg;
+    } else if (type == kDfResize) {
+      const LevelGeom& g = P->lev[l];
+      const int nt = g.rs_tiles_x * g.rs_tiles_y;
+      if (idx < nt)
+        resize_tile(P, a.rs_tab, src, a.pyr, l, 0, idx, lds, tid, true);
+      else
+        resize_tail(P, a.rs_tab, src, a.pyr, l, 0, idx - nt, lds, tid);
+      pub = kDfLvl + l;
+    } else if (type == kDfFast) {
+      const int ci = P->lev[l].cell_begin + 4 * idx + wave;
+      if (ci < P->lev[l].cell_end) {
+        uint8_t* fl = lds + wave * P->max_roi_lds;
+        switch (P->fast_pitch) {
+          case 48: fast_cell<48>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          case 52: fast_cell<52>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          case 56: fast_cell<56>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          case 60: fast_cell<60>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          case 64: fast_cell<64>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          default: fast_cell<0>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+        }
+      }
+      pub = kDfFastDone + l;
+    } else if (type == kDfBlur) {
+      static_assert(ORB_BLUR_WAVES == 4, "k_extract_df runs a blur tile per 4-wave worker");
+      blur_wave(P, src, a.pyr, a.blur, 0, P->lev[l].blur_tile_begin + idx, 0);
+      pub = kDfBlurDone + l;
+    } else if (type == kDfOctree) {
+      // (plans whose node arrays live in HBM take the per-stage launches: one
+      // octree instance keeps the worker's registers down)
+      octree_level<false>(P, a.cells, a.slots, a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, err, 0, l,
+                          P->oct_kcap, nullptr, lds);
+      pub = kDfOctDone + l;
+    } else {  // kDfDescribe: slots out_off + 4 idx + wave of level l
+      const int k = 4 * idx + wave;
+      if (k < P->lev[l].out_cap)
+        describe_slot(P, src, a.pyr, a.blur, a.oct_out, a.oct_count, a.angle, a.desc, 0, P->lev[l].out_off + k,
+                      lds + wave * kDescSlice, lane);
+      pub = kDfDescDone;
+    }
+    // ---- publish: every wave's stores drained, one agent-scope release, the counter
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(ctrl + pub * kDfCtrStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = pub == kDfDescDone && old == df.desc_items - 1;
+      if (last) df_acquire();  // every describe (and so every octree) item's results
+      s_last = last;
+    }
+    __syncthreads();
+    if (s_last) {
+      int* ab = reinterpret_cast<int*>(lds);
+      assemble_image<true>(P, a.oct_out, a.oct_count, a.angle, a.desc, a.lap0, a.lap1,
+                           reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out), a.cap,
+                           a.nm, a.nm + 1, err, 0, ab, ab + kMaxLevels + 1, ab + kMaxLevels + 1 + kAsmChunk,
+                           reinterpret_cast<KeyPointOut*>(a.kps_host), reinterpret_cast<uint64_t*>(a.desc_host),
+                           a.nm_host);
+      __syncthreads();
+    }
+  }
+  // ---- the last worker out clears the control block for the next launch
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(ctrl + kDfExit * kDfCtrStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1)
+      for (int i = 0; i < kDfCounters; ++i)
+        __hip_atomic_store(ctrl + i * kDfCtrStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2225,6 +2510,19 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
                      reinterpret_cast<uint64_t*>(a.desc_out), a.cap, a.n_out, a.mono_out, a.err);
   mark(6);
   return hipGetLastError();
+}
+
+hipError_t launch_extract_df(const DfLaunch& a, const DfLaunch* a_dev, hipStream_t st) {
+  hipLaunchKernelGGL(k_extract_df, dim3(a.grid), dim3(256), a.df.lds_bytes, st, a_dev, a.ctrl);
+  return hipGetLastError();
+}
+
+size_t df_lds_bytes(const PlanHeader& P, size_t octree_lds) {
+  return std::max({(size_t)P.rs_lds, (size_t)4 * P.max_roi_lds, octree_lds, (size_t)4 * kDescSlice, (size_t)kAsmLds});
+}
+
+hipError_t set_df_lds_limit(size_t bytes) {
+  return bytes > 64 * 1024 ? lds_optin((const void*)k_extract_df, (int)bytes) : hipSuccess;
 }
 
 // The plan's own LDS needs, raised per (kernel, device) only as far as a plan

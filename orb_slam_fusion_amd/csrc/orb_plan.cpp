@@ -3,6 +3,7 @@
 // buffer layout -- computed once per geometry with the reference's float
 // arithmetic (compiled -ffp-contract=off).
 #include "orb_plan_host.h"
+#include "orb_launch.h"
 
 #include <algorithm>
 #include <cmath>
@@ -333,6 +334,47 @@ size_t octree_fixed_lds_bytes() { return (256 + 1) * 4 + 16 * 4; }
 size_t octree_lds_bytes(const PlanHeader& P) {
   const size_t cand = (size_t)P.oct_kcap * 8;
   return (P.oct_hbm_nodes ? 0 : oct_node_bytes(P.node_cap)) + octree_fixed_lds_bytes() + cand;
+}
+
+
+// The single-image dataflow launch's items in ticket order (orb_launch.h):
+// the image copy, then level 0's FAST cells, level 1's resize and level 0's
+// octree (the longest chain: FAST -> DistributeOctTree of level 0), level 0's
+// blur; per level l >= 1 the next level's resize, its FAST cells, octree and
+// blur; the describe items last, level 0's at the very end (its octree
+// finishes last).
+void make_df_items(const PlanHeader& P, int img_bytes, DfPlan& df, std::vector<uint32_t>& items) {
+  df = DfPlan{};
+  items.clear();
+  const int L = P.levels;
+  auto push = [&](int type, int l, int n) {
+    for (int i = 0; i < n; ++i) items.push_back((uint32_t)type | ((uint32_t)l << 4) | ((uint32_t)i << 8));
+  };
+  df.img_bytes = img_bytes;
+  df.n_bands = (img_bytes + kDfBandBytes - 1) / kDfBandBytes;
+  for (int l = 0; l < L; ++l) {
+    const LevelGeom& g = P.lev[l];
+    df.units[l] = l ? g.rs_tiles_x * g.rs_tiles_y + g.rs_tail_blocks : 0;
+    df.fast_items[l] = (g.cell_end - g.cell_begin + 3) / 4;
+    df.blur_items[l] = (l + 1 < L ? P.lev[l + 1].blur_tile_begin : P.blur_tiles) - g.blur_tile_begin;
+  }
+  push(kDfCopy, 0, df.n_bands);
+  push(kDfFast, 0, df.fast_items[0]);
+  if (L > 1) push(kDfResize, 1, df.units[1]);
+  push(kDfOctree, 0, 1);
+  push(kDfBlur, 0, df.blur_items[0]);
+  for (int l = 1; l < L; ++l) {
+    if (l + 1 < L) push(kDfResize, l + 1, df.units[l + 1]);
+    push(kDfFast, l, df.fast_items[l]);
+    push(kDfOctree, l, 1);
+    push(kDfBlur, l, df.blur_items[l]);
+  }
+  for (int l = L - 1; l >= 0; --l) {
+    const int n = (P.lev[l].out_cap + 3) / 4;
+    push(kDfDescribe, l, n);
+    df.desc_items += n;
+  }
+  df.n_items = (int)items.size();
 }
 
 }  // namespace orbgpu

@@ -171,12 +171,14 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoLaunch a) {
         const int dist = __popc(dls[0] ^ x0.x) + __popc(dls[1] ^ x0.y) + __popc(dls[2] ^ x0.z) +
                          __popc(dls[3] ^ x0.w) + __popc(dls[4] ^ x1.x) + __popc(dls[5] ^ x1.y) +
                          __popc(dls[6] ^ x1.z) + __popc(dls[7] ^ x1.w);
-        if (dist < kThHigh) key = min(key, ((uint32_t)dist << 12) | (uint32_t)iR);
+        // iR < 65536 (u16 row lists; the entry points refuse larger caps),
+        // dist < kThHigh = 100: (dist << 16) | iR orders by (dist, iR)
+        if (dist < kThHigh) key = min(key, ((uint32_t)dist << 16) | (uint32_t)iR);
       }
     }
     key = wave_umin(key);
-    if (key == 0xffffffffu || (int)(key >> 12) >= kThOrbDist) break;
-    const int best = (int)(key & 0xfff);
+    if (key == 0xffffffffu || (int)(key >> 16) >= kThOrbDist) break;
+    const int best = (int)(key & 0xffff);
 
     // ---- window sweep at the keypoint's octave (:898-935)
     const float uR0 = krf[kKpFloats * best];

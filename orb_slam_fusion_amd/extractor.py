@@ -108,6 +108,13 @@ class OrbExtractor:
         check(lib().orbgpu_extractor_set_pyramid_launch(self._h, int(mode)),
               "orbgpu_extractor_set_pyramid_launch")
 
+    def set_single_launch(self, mode: int) -> None:
+        """How __call__ runs on the device: ORBGPU_SINGLE_DATAFLOW (0, default:
+        one persistent dataflow launch) or ORBGPU_SINGLE_GRAPH (1: the per-stage
+        launches replayed as a hipGraph); same results."""
+        check(lib().orbgpu_extractor_set_single_launch(self._h, int(mode)),
+              "orbgpu_extractor_set_single_launch")
+
     def set_octree_nodes(self, mode: int) -> None:
         """Where DistributeOctTree's node list lives: ORBGPU_OCTREE_NODES_AUTO
         (0: LDS when it fits the workgroup, else HBM) or ORBGPU_OCTREE_NODES_HBM

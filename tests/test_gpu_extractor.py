@@ -52,9 +52,10 @@ def _diagnose(ex, orc, L):
     return "; ".join(lines) or "stages equal"
 
 
-def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False, fused=False):
+def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False, fused=False, single=0):
     h, w = img.shape
     ex = OrbExtractor(*params, max_width=w, max_height=h)
+    ex.set_single_launch(single)  # 0: ORBGPU_SINGLE_DATAFLOW (default), 1: ORBGPU_SINGLE_GRAPH
     if fused:
         ex.set_pyramid_launch(1)  # ORBGPU_PYRAMID_FUSED
     if rounding is not None:
@@ -68,7 +69,8 @@ def _compare(params, img, lapping=(0, 0), rounding=None, octree_hbm=False, fused
         with oracle.resize_rounding(rounding):  # the oracle's levels follow the same split
             m_ref, k_ref, d_ref = orc.extract(img, lapping)
     m, k, d = ex(img, None, lapping)
-    ctx = f"{w}x{h} params={params} lapping={lapping} rounding={rounding} octree_hbm={octree_hbm} fused={fused}"
+    ctx = (f"{w}x{h} params={params} lapping={lapping} rounding={rounding} octree_hbm={octree_hbm} "
+           f"fused={fused} single={single}")
     # the reference blurs only levels that kept keypoints (orb_extractor.cc
     # operator(): `if (nkeypointsLevel == 0) continue;`), the GPU every level
     ref_levels = set(k_ref["octave"].tolist())
@@ -377,3 +379,64 @@ def test_batch_5x_features(gpu_available):
         assert n_h[i] == len(k_ref) and mono_h[i] == m_ref
         assert kps_h[i, : n_h[i]].tobytes() == k_ref.tobytes(), f"image {i} keypoints"
         assert desc_h[i, : n_h[i]].tobytes() == d_ref.tobytes(), f"image {i} descriptors"
+
+
+@pytest.mark.parametrize("case", ["c2", "euroc", "odd", "lapping", "scale2"])
+def test_single_launch_graph_path_bit_exact(gpu_available, case):
+    """orbgpu_extract's per-stage graph path (ORBGPU_SINGLE_GRAPH) against the
+    oracle; every other host-path test runs the default dataflow launch."""
+    left, _ = synth.stereo_frame(7)
+    if case == "c2":
+        _compare(C2, left, single=1)
+    elif case == "euroc":
+        _compare(EUROC, left, single=1)
+    elif case == "odd":
+        _compare(C2, synth.stereo_frame(8, w=641, h=397)[0], single=1)
+    elif case == "lapping":
+        _compare(C2, left, lapping=(100, 400), single=1)
+    else:
+        _compare((1000, 2.0, 4, 20, 7), synth.stereo_frame(21, w=1024, h=768)[0], single=1)
+
+
+def test_dataflow_repeat_and_switches(gpu_available):
+    """The dataflow launch record is rewritten when the lapping band, the image
+    size or the mode changes; every call equals a fresh handle's graph path."""
+    imgs = [synth.stereo_frame(40 + i)[0] for i in range(3)] + [synth.stereo_frame(50, w=641, h=397)[0]]
+    laps = [(0, 0), (150, 450), (0, 0), (0, 0)]
+    ex = OrbExtractor(*C2)
+    ref = OrbExtractor(*C2)
+    ref.set_single_launch(1)
+    for rnd in range(2):
+        for img, lap in zip(imgs, laps):
+            got = ex(img, None, lap)
+            exp = ref(img, None, lap)
+            assert got[0] == exp[0] and got[1].tobytes() == exp[1].tobytes()
+            assert got[2].tobytes() == exp[2].tobytes()
+            for a, b in zip(ex.img_pyramid_, ref.img_pyramid_):
+                assert np.array_equal(a, b)
+        ex.set_single_launch(1 - rnd)  # round 2 on the graph path, then back
+
+
+def test_dataflow_two_handles_on_two_threads(gpu_available):
+    """The stereo Frame's two extractions run concurrently (frame.cc:179-182):
+    two dataflow launches in flight on two streams give each handle's
+    sequential results, frame after frame."""
+    import threading
+
+    pairs = [synth.stereo_frame(60 + i) for i in range(6)]
+    exl, exr = OrbExtractor(*C2), OrbExtractor(*C2)
+    seq = OrbExtractor(*C2)
+    expect = []
+    for l, r in pairs:
+        _, kl, dl = seq(l)
+        _, kr, dr = seq(r)
+        expect.append((kl.tobytes(), dl.tobytes(), kr.tobytes(), dr.tobytes()))
+    for rnd in range(3):
+        for (l, r), e in zip(pairs, expect):
+            out = {}
+            th = threading.Thread(target=lambda: out.__setitem__("r", exr(r)))
+            th.start()
+            _, kl, dl = exl(l)
+            th.join()
+            _, kr, dr = out["r"]
+            assert (kl.tobytes(), dl.tobytes(), kr.tobytes(), dr.tobytes()) == e

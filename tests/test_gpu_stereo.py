@@ -112,3 +112,18 @@ def test_batch_matches_oracle_per_frame(gpu_available):
         assert N == len(kl)
         got = (kl, ur[f, :N].cpu().numpy(), dep[f, :N].cpu().numpy())
         assert_same(got, (kl, ur_r, dep_r), f"batch frame {f}")
+
+
+def test_more_than_4096_right_keypoints(gpu_available):
+    """Right keypoint indices past 4095: a dense-noise pair with a
+    24 px disparity at 8000 features gives > 4096 keypoints per image, so the
+    row candidates' indices need the full 16 bits of the match key."""
+    canvas = synth.noise_image(41, 752 + 24, 480)
+    left = np.ascontiguousarray(canvas[:, :752])
+    right = np.ascontiguousarray(canvas[:, 24:])
+    params = (8000, 1.2, 8, 20, 7)
+    got = host_path(left, right, params)
+    ref = oracle_pair(left, right, params)
+    assert len(ref[0]) > 4096, len(ref[0])
+    assert_same(got, ref, "8000 features, dense noise")
+    assert (got[1] >= 0).sum() > 1000
