@@ -96,8 +96,9 @@ clean:
 # profiling variant: per-phase s_memtime totals (orbgpu_debug_stamps)
 # STAMPS=1: k_fast_cells (+ pose kernel), STAMPS=2: k_octree
 STAMPS ?= 1
+STAMP_DEFS ?=
 stamps:
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
+	$(HIPCC) $(HIPFLAGS) -DORB_STAMPS=$(STAMPS) $(STAMP_DEFS) -shared -o $(LIB)/liborbgpu_stamps.so $(GPU_SRCS)
 
 .PHONY: varB var all oracle clean stamps checkuniform

@@ -87,6 +87,9 @@ struct orbgpu_extractor {
   uint8_t* h_img = nullptr;
   uint8_t* h_img_dev = nullptr;  // its device view
   size_t h_img_bytes = 0;
+  int* h_band = nullptr;          // the dataflow launch's band flags (in the h_img block, after the image)
+  const int* h_band_dev = nullptr;
+  int df_seq = 0;                 // sequence number of the last dataflow call
   char* h_sout_dev = nullptr;    // device view of h_sout (the dataflow launch mirrors into it)
   // the dataflow launch (k_extract_df): control block, launch record + item list
   int single_mode = ORBGPU_SINGLE_DATAFLOW;
@@ -96,6 +99,8 @@ struct orbgpu_extractor {
   DfLaunch df_launch{};          // what d_df_rec holds
   bool df_valid = false;
   int df_grid = 0;               // ORBGPU_DF_GRID (tools): workers, else the CU count
+  unsigned long long* d_df_trace = nullptr;  // ORBGPU_DF_TRACE (tools/df_trace.py): per-ticket timeline
+  size_t df_trace_cap = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   ExtractLaunch graph_launch{};  // what graph_exec was captured for
@@ -412,7 +417,7 @@ static hipError_t run_single_chain(orbgpu_extractor* h, const ExtractLaunch& a) 
 // memory next to the item list and is rewritten only when it changes (a new
 // plan or buffer, another lapping band).  The outputs reach the host through
 // the launch's own mirror writes into the mapped h_sout: no copy commands.
-static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const int lap[2]) {
+static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const int lap[2], int seq) {
   const PlanHeader& P = h->plan.hdr;
   DfLaunch a;
   std::memset(&a, 0, sizeof a);
@@ -438,9 +443,11 @@ static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const 
   a.desc_out = h->d_descs;
   a.nm = h->d_nm;
   a.nm_host = reinterpret_cast<int*>(h->h_sout_dev);
+  a.done_host = reinterpret_cast<int*>(h->h_sout_dev) + 3;  // the output block's pad word
   a.kps_host = h->h_sout_dev + (reinterpret_cast<char*>(h->d_kps) - h->d_sout);
   a.desc_host = h->h_sout_dev + (reinterpret_cast<char*>(h->d_descs) - h->d_sout);
   a.cap = P.kp_slots;
+  a.trace = h->d_df_trace;
   std::vector<uint32_t> items;
   if (h->df_valid) {
     a.items = h->df_launch.items;
@@ -450,6 +457,7 @@ static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const 
     make_df_items(P, (int)img_bytes, a.df, items);
     a.df.lds_bytes = (int)df_lds_bytes(P, octree_lds_bytes(P));
     a.grid = std::min(a.df.n_items, h->df_grid > 0 ? h->df_grid : h->n_cu);
+    if (h->d_df_trace && 4 * (size_t)a.df.n_items + 2 > h->df_trace_cap) a.trace = nullptr;
     const size_t need = sizeof(DfLaunch) + items.size() * sizeof(uint32_t);
     if (need > h->df_rec_cap) {
       if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
@@ -470,7 +478,9 @@ static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const 
     h->df_launch = a;
     h->df_valid = true;
   }
-  return launch_extract_df(h->df_launch, h->d_df_rec, h->stream) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+  return launch_extract_df(h->df_launch, h->d_df_rec, h->h_band_dev, seq, h->stream) == hipSuccess
+             ? ORBGPU_OK
+             : ORBGPU_ERR_DEVICE;
 }
 
 extern "C" {
@@ -499,6 +509,13 @@ orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int devic
   if (const char* e = std::getenv("ORBGPU_SINGLE"))  // A/B default for tools, read once
     if (std::strcmp(e, "graph") == 0) h->single_mode = ORBGPU_SINGLE_GRAPH;
   if (const char* e = std::getenv("ORBGPU_DF_GRID")) h->df_grid = std::atoi(e);
+  if (std::getenv("ORBGPU_DF_TRACE")) {
+    h->df_trace_cap = 4 * 65536 + 2;
+    if (dalloc(&h->d_df_trace, h->df_trace_cap) || hipMemset(h->d_df_trace, 0, 8 * h->df_trace_cap) != hipSuccess) {
+      orbgpu_extractor_destroy(h);
+      return ORBGPU_ERR_DEVICE;
+    }
+  }
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       dalloc(&h->d_plan, 1) || dalloc(&h->d_err, 1) || dalloc(&h->d_df_ctrl, (size_t)kDfCounters * kDfCtrStride) ||
       hipMemset(h->d_df_ctrl, 0, sizeof(int) * kDfCounters * kDfCtrStride) != hipSuccess) {
@@ -539,6 +556,7 @@ void orbgpu_extractor_destroy(orbgpu_extractor* h) {
   dfree(h->d_img);
   dfree(h->d_df_ctrl);
   dfree(h->d_df_rec);
+  dfree(h->d_df_trace);
   if (h->d_sout) (void)hipFree(h->d_sout);
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
@@ -606,6 +624,24 @@ orbgpu_status orbgpu_extractor_set_pyramid_launch(orbgpu_extractor* h, int mode)
   return ORBGPU_OK;
 }
 
+// Debug (not in orbgpu.h; tools/df_trace.py): the last dataflow launch's
+// per-ticket timeline, 4 u64 per item + the assembly's start / end; returns
+// the item count, or -1 without ORBGPU_DF_TRACE.
+int orbgpu_debug_df_trace(orbgpu_extractor* h, unsigned long long* out, int cap_items) {
+  if (!h || !out || !h->d_df_trace || !h->df_valid) return -1;
+  const int n = std::min(cap_items, h->df_launch.df.n_items);
+  if (hipStreamSynchronize(h->stream) != hipSuccess ||
+      hipMemcpy(out, h->d_df_trace, 8 * (4 * (size_t)n + 2), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (n == h->df_launch.df.n_items) {  // the assembly stamps follow the items
+    out[4 * (size_t)n] = 0;
+  }
+  if (hipMemcpy(out + 4 * (size_t)n, h->d_df_trace + 4 * (size_t)h->df_launch.df.n_items, 16,
+                hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
+}
+
 orbgpu_status orbgpu_extractor_set_single_launch(orbgpu_extractor* h, int mode) {
   if (!h || (mode != ORBGPU_SINGLE_DATAFLOW && mode != ORBGPU_SINGLE_GRAPH)) return ORBGPU_ERR_INVALID;
   h->single_mode = mode;
@@ -657,24 +693,68 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
     if (h->h_img) (void)hipHostFree(h->h_img);
     h->h_img = nullptr;
     h->h_img_bytes = 0;
-    if (hipHostMalloc(&h->h_img, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+    // the image, then one flag per copy band of the dataflow launch
+    const size_t flags_off = (bytes + 63) & ~(size_t)63;
+    const size_t n_bands = (bytes + kDfBandBytes - 1) / kDfBandBytes;
+    if (hipHostMalloc(&h->h_img, flags_off + 4 * n_bands, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_img_dev), h->h_img, 0) != hipSuccess)
       return ORBGPU_ERR_NOMEM;
+    h->h_band = reinterpret_cast<int*>(h->h_img + flags_off);
+    h->h_band_dev = reinterpret_cast<const int*>(h->h_img_dev + flags_off);
+    std::memset(h->h_band, 0, 4 * n_bands);
+    h->df_seq = 0;
     h->h_img_bytes = bytes;
   }
   if ((st = ensure_single_out(h, (size_t)P.kp_slots)) != ORBGPU_OK) return st;
-  // the image into pinned staging (rows at the level-0 pitch); the graph copies it
-  if (stride == pitch0) {
-    std::memcpy(h->h_img, img, bytes);
-  } else {
-    for (int r = 0; r < height; ++r)
-      std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
-  }
+  // the image into pinned staging (rows at the level-0 pitch): before the
+  // graph's copy, or, for the dataflow launch, band by band AFTER the launch
+  // (its copy items wait for each band's flag), so the copy overlaps the
+  // launch's start
+  auto stage = [&](auto&& band_done) {
+    if (stride == pitch0) {
+      for (size_t b0 = 0; b0 < bytes; b0 += kDfBandBytes) {
+        const size_t nb = std::min((size_t)kDfBandBytes, bytes - b0);
+        std::memcpy(h->h_img + b0, img + b0, nb);
+        band_done(b0 + nb);
+      }
+    } else {
+      for (int r = 0; r < height; ++r) {
+        std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
+        band_done((size_t)(r + 1) * pitch0);
+      }
+    }
+  };
   const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
   if (h->single_mode == ORBGPU_SINGLE_DATAFLOW && !P.oct_hbm_nodes) {
-    if ((st = run_single_df(h, bytes, lap)) != ORBGPU_OK) return st;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    const int seq = h->df_seq = h->df_seq == 0x7fffffff ? 1 : h->df_seq + 1;
+    if ((st = run_single_df(h, bytes, lap, seq)) != ORBGPU_OK) return st;
+    const int n_bands = (int)((bytes + kDfBandBytes - 1) / kDfBandBytes);
+    int next = 0;
+    stage([&](size_t upto) {  // every band wholly written: its flag, after its bytes
+      while (next < n_bands && std::min((size_t)(next + 1) * kDfBandBytes, bytes) <= upto)
+        __atomic_store_n(&h->h_band[next++], seq, __ATOMIC_RELEASE);
+    });
+    // the launch writes the call's number after every output word: return as
+    // soon as it appears (the workers' exit drains on the stream behind it);
+    // past ~0.5 s, or a stream error, the stream's own synchronisation decides
+    volatile int* done = reinterpret_cast<volatile int*>(h->h_small) + 3;
+    bool seen = false;
+    for (long spin = 0; spin < (1L << 24); ++spin) {
+      if (*done == seq) {
+        seen = true;
+        break;
+      }
+      if ((spin & 4095) == 4095 && hipStreamQuery(h->stream) != hipErrorNotReady) {
+        seen = *done == seq;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (!seen && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    if (!seen && *done != seq) return ORBGPU_ERR_DEVICE;
   } else {
+    stage([](size_t) {});
     ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
                                   P.kp_slots, h->d_nm, h->d_nm + 1);
     a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs

@@ -77,7 +77,12 @@ __device__ unsigned long long g_stamps[64 * 16];  // 64 spread copies of 16 coun
 #define OSTAMP_INIT STAMP_ON_INIT
 #define OSTAMP(i) STAMP_ON(i)
 #define OSTAMP_ADD(i, v) STAMP_ON_ADD(i, v)
+#ifdef ORB_OCT_STAMP_L0  // level-0 blocks only (the single-image critical path)
+#define OSTAMP_END \
+  if (l == 0) STAMP_ON_END
+#else
 #define OSTAMP_END STAMP_ON_END
+#endif
 #else
 #define OSTAMP_INIT (void)0
 #define OSTAMP(i) (void)0
@@ -100,6 +105,30 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   const int xcd = bid & 7, idx = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
+
+// kWT (the single-image dataflow launch, k_extract_df): a payload word that
+// other workgroups of the same launch read is stored write-through (sc1: a
+// relaxed agent-scope atomic store), so its producer needs no release fence
+// before the counter that publishes it (MI355X_MICROARCH.md, inter-workgroup
+// visibility, R1); the batch kernels store plainly.
+template <bool kWT, class T>
+__device__ __forceinline__ void st_pub(T* p, T v) {
+  if constexpr (kWT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+// kWT: a wave-uniform read of another workgroup's output goes to a vector sc1
+// load -- the consumer's acquire does not refresh the scalar cache, where a
+// plain uniform load may be served from
+template <bool kWT, class T>
+__device__ __forceinline__ T ld_pub(const T* p) {
+  if constexpr (kWT)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+constexpr int kAuxSc1 = 16;  // raw buffer store cache bits: sc1 (write-through)
 
 struct ImgSrc {
   const uint8_t* base;  // image 0, level 0
@@ -234,9 +263,17 @@ __device__ __forceinline__ void rs_stage(const uint8_t* S, int sp, int sw, int c
 // LDS slice of PlanHeader::rs_lds bytes; every thread of the workgroup passes
 // its one barrier.  live = false: the group takes part in the barrier and
 // writes nothing (k_pyramid's spare groups).
+// (the dataflow launch passes `wait`: its dependency wait, called by every
+// thread once the plan-constant taps are in flight and before the source level
+// is read; the batch kernels pass nothing)
+struct NoWait {
+  __device__ void operator()() const {}
+};
+template <bool kWT = false, class Wait = NoWait>
 __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
                                             const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
-                                            int tyx, uint8_t* __restrict__ lds, int tid, bool live) {
+                                            int tyx, uint8_t* __restrict__ lds, int tid, bool live,
+                                            const Wait& wait = Wait()) {
   constexpr int RW = kResizeTileH / 4;  // output rows per wave
   const LevelGeom& g = P->lev[l];
   const int sw = P->lev[l - 1].w;
@@ -260,6 +297,7 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
   for (int k = 0; k < 4; ++k) xa[k] = xt[min(x + k, g.w - 1)];
   const int2 tl = yt[min(ys + (lane & (RW - 1)), yl)];
 
+  wait();
   rs_stage(S, sp, sw, c0, c1, rr0, nrow, lds, tid);
 
   // per-lane column taps -> byte selectors relative to the lane's LDS window
@@ -318,9 +356,9 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
     const ushort2_t p23 = as_us2(v[2] | (v[3] << 16)) >> (ushort2_t){2, 2};
     // columns past w land in the pitch padding (pitch is a multiple of 16)
     if (active)
-      *reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)y, (uint32_t)g.pitch)) =
-          __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01),
-                                0x06040200u);
+      st_pub<kWT>(reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)y, (uint32_t)g.pitch)),
+                  __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01),
+                                        0x06040200u));
   };
   for (int y = ys; y <= ye; ++y) {
     const int tx = __builtin_amdgcn_readlane(tl.x, y - ys), ty = __builtin_amdgcn_readlane(tl.y, y - ys);
@@ -364,9 +402,10 @@ __device__ __forceinline__ void resize_tile(const PlanHeader* __restrict__ P, co
 // horizontal pass on its own two source rows (no reuse across output rows)
 // and the same vertical rounding as resize_tile: the same bytes.  One barrier
 // (after staging), as resize_tile.
+template <bool kWT = false, class Wait = NoWait>
 __device__ __forceinline__ void resize_tail(const PlanHeader* __restrict__ P, const int* __restrict__ rs_tab,
                                             const ImgSrc& src, uint8_t* __restrict__ pyr, int l, int img,
-                                            int tb, uint8_t* __restrict__ lds, int tid) {
+                                            int tb, uint8_t* __restrict__ lds, int tid, const Wait& wait = Wait()) {
   const LevelGeom& g = P->lev[l];
   const int sw = P->lev[l - 1].w;
   const int2* xt = reinterpret_cast<const int2*>(rs_tab + g.rs_x);
@@ -381,6 +420,7 @@ __device__ __forceinline__ void resize_tail(const PlanHeader* __restrict__ P, co
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int y = y0 + lane;
   const int2 ty = yt[min(y, yl)];
+  wait();
   rs_stage(S, sp, sw, c0, c1, rr0, nrow, lds, tid);
   __syncthreads();
   const uint8_t* rowA = lds + ((ty.x & 0xffff) - rr0) * ncol;
@@ -424,8 +464,9 @@ __device__ __forceinline__ void resize_tail(const PlanHeader* __restrict__ P, co
     const ushort2_t p01 = as_us2(v[0] | (v[1] << 16)) >> (ushort2_t){2, 2};
     const ushort2_t p23 = as_us2(v[2] | (v[3] << 16)) >> (ushort2_t){2, 2};
     if (y <= yl)
-      *reinterpret_cast<uint32_t*>(D + x) =
-          __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01), 0x06040200u);
+      st_pub<kWT>(reinterpret_cast<uint32_t*>(D + x),
+                  __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, p23), __builtin_bit_cast(uint32_t, p01),
+                                        0x06040200u));
   }
 }
 
@@ -535,7 +576,7 @@ __device__ __forceinline__ void blur_window_sel(int x, int w, int base, uint32_t
 #endif
 // One wave's blur strip: every lane owns columns x..x+3 of R output rows from
 // ys (kTail: ys per lane -- the strips of a tail wave -- else wave-uniform).
-template <bool kTail>
+template <bool kTail, int kAux = 0>
 __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, const LevelGeom& g,
                                            const uint8_t* S, int sp, uint8_t* __restrict__ dst,
                                            int x, int ys) {
@@ -632,9 +673,9 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
         const uint32_t packed =
             __builtin_amdgcn_perm(v[1], v[0], 0x0c0c0602u) | __builtin_amdgcn_perm(v[3], v[2], 0x06020c0cu);
         if (kTail)
-          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x + (int)__umul24((uint32_t)(ys + o), (uint32_t)pitch), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x + (int)__umul24((uint32_t)(ys + o), (uint32_t)pitch), 0, kAux);
         else
-          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x, (ys + o) * pitch, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(packed, drs, x, (ys + o) * pitch, kAux);
       }
     }
   }
@@ -649,6 +690,7 @@ __device__ __forceinline__ void blur_strip(const PlanHeader* __restrict__ P, con
 // of image img: a full tile's R-row strip `wave` (threadIdx.x >> 6), or the
 // tail strips of tail wave 4 (t - nfull) + wave.  No synchronisation.
 // (ORB_BLUR_WAVES == 1: the wave is bid & 3 of the one-wave workgroups)
+template <bool kWT>
 __device__ __forceinline__ void blur_wave(const PlanHeader* __restrict__ P, ImgSrc src,
                                           const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                           int img, int t, int bid) {
@@ -669,14 +711,14 @@ __device__ __forceinline__ void blur_wave(const PlanHeader* __restrict__ P, ImgS
     // wave-uniform row origin: row addressing and row bounds stay scalar
     const int ys = ty * kBlurTileH + R * wave;
     if (x >= g.w || ys >= g.h) return;
-    blur_strip<false>(P, g, S, sp, dst, x, ys);
+    blur_strip<false, kWT ? kAuxSc1 : 0>(P, g, S, sp, dst, x, ys);
   } else {
     // tail wave: tail_s strips of tail_nl lanes, strip s at rows ys0 + 32 s
     const int tw = 4 * (t - nfull) + wave;
     const int s = lane / g.tail_nl, c = lane - s * g.tail_nl;
     const int x = g.tiles_x * kBlurTileW + 4 * c, ys = (tw * g.tail_s + s) * R;
     if (s >= g.tail_s || x >= g.w || ys >= g.h) return;
-    blur_strip<true>(P, g, S, sp, dst, x, ys);
+    blur_strip<true, kWT ? kAuxSc1 : 0>(P, g, S, sp, dst, x, ys);
   }
 }
 
@@ -854,18 +896,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 // FAST cell ci of image img by one wave (lane 0..63) with its own LDS slice
 // of PlanHeader::max_roi_lds bytes; only wave-level synchronisation.
-template <int LS>
+// (pre: the cell record, loaded by the dataflow launch before its dependency wait)
+template <int LS, bool kWT = false>
 __device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
                                           const ImgSrc& src, const uint8_t* __restrict__ pyr,
                                           uint32_t* __restrict__ slots, int* __restrict__ cell_count,
-                                          int img, int ci, uint8_t* __restrict__ lds, int lane) {
+                                          int img, int ci, uint8_t* __restrict__ lds, int lane,
+                                          const Cell* pre = nullptr) {
   STAMP_INIT;
-  const Cell c = cells[ci];
+  const Cell c = pre ? *pre : cells[ci];
   const int dw = c.cols - 6, dh = c.rows - 6;
   const int nd = (dw > 0 && dh > 0) ? dw * dh : 0;
   uint32_t* out = slots + (size_t)img * P->slots + c.slot_off;
   if (nd == 0) {
-    if (lane == 0) cell_count[(size_t)img * P->n_cells + ci] = 0;
+    if (lane == 0) st_pub<kWT>(cell_count + (size_t)img * P->n_cells + ci, 0);
     return;
   }
   // LDS (fast_cell_lds_bytes[_pitch]): ROI rows of ls bytes (ROI column x at
@@ -1121,7 +1165,7 @@ __device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, cons
             const int k = __builtin_ctz(km);
             const uint32_t sk = k < 7 ? (uint32_t)(mid >> (8 * (k + 1))) & 0xffu : m2 & 0xffu;
             if (pos < c.slot_cap)
-              out[pos] = (uint32_t)(xrel0 + q0 + k) | ((uint32_t)(yrel0 + r) << 12) | (sk << 24);
+              st_pub<kWT>(out + pos, (uint32_t)(xrel0 + q0 + k) | ((uint32_t)(yrel0 + r) << 12) | (sk << 24));
             ++pos;
             km &= km - 1;
           } while (km);
@@ -1179,7 +1223,7 @@ __device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, cons
         const int r = LS ? i / LSD : i >> QB, q = LS ? i - r * LS : i & QM;
         const int pos = written + __popcll(km & lt);
         if (pos < c.slot_cap)
-          out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
+          st_pub<kWT>(out + pos, (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24));
       }
       written += __popcll(km);
     }
@@ -1256,7 +1300,7 @@ __device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, cons
           const int r = LS ? i / LSD : i >> QB, q = LS ? i - r * LS : i & QM;
           const int pos = written + __popcll(km & lt);
           if (pos < c.slot_cap)
-            out[pos] = (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24);
+            st_pub<kWT>(out + pos, (uint32_t)(xrel0 + q) | ((uint32_t)(yrel0 + r) << 12) | ((uint32_t)s << 24));
         }
         written += __popcll(km);
       }
@@ -1280,7 +1324,7 @@ __device__ __forceinline__ void fast_cell(const PlanHeader* __restrict__ P, cons
     STAMP(4);
     STAMP_ADD(11, ns);
   }
-  if (lane == 0) cell_count[(size_t)img * P->n_cells + ci] = min(written, c.slot_cap);
+  if (lane == 0) st_pub<kWT>(cell_count + (size_t)img * P->n_cells + ci, min(written, c.slot_cap));
   STAMP(5);
   STAMP_END;
 }
@@ -1310,6 +1354,21 @@ constexpr int kOctThreads = 256;
 // kOctThreads + 1 ints of LDS.  Must be called by the whole block.
 __device__ int block_scan(int* a, int n, int* tmp) {
   const int t = threadIdx.x;
+  if (n <= kOctThreads) {
+    // one element a thread: DPP scans within the waves, the four wave totals
+    // through LDS -- two barriers instead of three (the octree's node-list
+    // scans, most of them at a few hundred nodes or fewer)
+    const int v = t < n ? a[t] : 0;
+    const int incl = wave_iscan(v);
+    const int w = t >> 6;
+    if ((t & 63) == 63) tmp[w] = incl;
+    __syncthreads();
+    const int t0 = tmp[0], t1 = tmp[1], t2 = tmp[2], t3 = tmp[3];
+    const int off = (w > 0 ? t0 : 0) + (w > 1 ? t1 : 0) + (w > 2 ? t2 : 0);
+    if (t < n) a[t] = off + incl - v;
+    __syncthreads();
+    return t0 + t1 + t2 + t3;
+  }
   const int per = (n + kOctThreads - 1) / kOctThreads;
   const int b = min(t * per, n), e = min(b + per, n);
   int s = 0;
@@ -1410,7 +1469,7 @@ struct OctLds {
 // DistributeOctTree of level l of image img by the whole 256-thread workgroup
 // (lds_raw: octree_lds_bytes of the plan; node_ws: this (image, level)'s HBM
 // node range when kHbm).  Every exit is workgroup-uniform.
-template <bool kHbm>
+template <bool kHbm, bool kWT = false>
 __device__ __forceinline__ void octree_level(
     const PlanHeader* __restrict__ P, const Cell* __restrict__ cells,
     const uint32_t* __restrict__ slots, const int* __restrict__ cell_count,
@@ -1501,7 +1560,7 @@ __device__ __forceinline__ void octree_level(
   }
   uint32_t* out = oct_out + (size_t)img * P->kp_slots + g.out_off;
   if (K == 0) {
-    if (t == 0) oct_count[img * L + l] = 0;
+    if (t == 0) st_pub<kWT>(oct_count + img * L + l, 0);
     return;
   }
   __syncthreads();
@@ -1643,7 +1702,7 @@ __device__ __forceinline__ void octree_level(
     const int S_new = T + n_stay;
     if (S_new > NC) {
       if (t == 0) atomicOr(err, kErrNodeCap);
-      if (t == 0) oct_count[img * L + l] = 0;
+      if (t == 0) st_pub<kWT>(oct_count + img * L + l, 0);
       return;  // uniform
     }
 
@@ -1738,10 +1797,10 @@ __device__ __forceinline__ void octree_level(
   const int n_out = min(S, g.out_cap);
   for (int i = t; i < n_out; i += kOctThreads) {
     const uint32_t k = 0xffffffffu - (uint32_t)(s.best[i] & 0xffffffffull);
-    out[i] = KD((int)k);
+    st_pub<kWT>(out + i, KD((int)k));
   }
   if (t == 0) {
-    oct_count[img * L + l] = n_out;
+    st_pub<kWT>(oct_count + img * L + l, n_out);
     if (S > g.out_cap) atomicOr(err, kErrOutCap);
   }
   OSTAMP(3);
@@ -2006,8 +2065,25 @@ __global__ __launch_bounds__(64 * ORB_DESC_WG) void k_describe(const PlanHeader*
 #define ORB_DESC_WAVES 4  // waves (one keypoint each) per k_describe workgroup
 #endif
 constexpr int kDescSlice = (kDescLds + 15) & ~15;  // LDS of one describe wave
+
+struct KeyPointOut {  // orbgpu_keypoint (cv::KeyPoint field order)
+  float x, y, size, angle, response;
+  int octave, class_id;
+};
+// The dataflow launch's direct output (no lapping band: keypoint i of level l
+// is output i + base, base = the keypoints of the lower levels): the wave
+// writes its keypoint record and descriptor to the device block and to its
+// host-mapped mirror itself, and the slot arrays are not written.
+struct DescFinal {
+  KeyPointOut* kps;
+  uint64_t* descs;
+  KeyPointOut* kps_h;
+  uint64_t* descs_h;
+  int base;
+};
 // Octree output slot `slot` of image img by one wave (lane 0..63) with its own
 // kDescSlice bytes of LDS (raw); only wave-level synchronisation.
+template <bool kWT = false>
 __device__ __forceinline__ void describe_slot(const PlanHeader* __restrict__ P, const ImgSrc& src,
                                               const uint8_t* __restrict__ pyr,
                                               const uint8_t* __restrict__ blur,
@@ -2015,14 +2091,15 @@ __device__ __forceinline__ void describe_slot(const PlanHeader* __restrict__ P, 
                                               const int* __restrict__ oct_count,
                                               float* __restrict__ angle_out,
                                               uint64_t* __restrict__ desc_out, int img, int slot,
-                                              uint8_t* __restrict__ raw, int lane) {
+                                              uint8_t* __restrict__ raw, int lane,
+                                              const DescFinal* fin = nullptr) {
   uint8_t* blp = raw + kRawW * kRawH;
   const int kps = P->kp_slots;
   int l = 0;
   while (l + 1 < P->levels && slot >= P->lev[l + 1].out_off) ++l;
   const LevelGeom& g = P->lev[l];
-  const int cnt = __builtin_amdgcn_readfirstlane(oct_count[img * P->levels + l]);
-  const uint32_t kp = __builtin_amdgcn_readfirstlane(oct_out[(size_t)img * kps + slot]);
+  const int cnt = __builtin_amdgcn_readfirstlane(ld_pub<kWT>(oct_count + img * P->levels + l));
+  const uint32_t kp = __builtin_amdgcn_readfirstlane(ld_pub<kWT>(oct_out + (size_t)img * kps + slot));
   if (slot - g.out_off >= cnt) return;  // wave-uniform
   const int cx = (int)(kp & 0xfff) + kFastBorder, cy = (int)((kp >> 12) & 0xfff) + kFastBorder;
 
@@ -2104,9 +2181,33 @@ __device__ __forceinline__ void describe_slot(const PlanHeader* __restrict__ P, 
     const int t1 = ctr_m[__umul24(r1, (uint32_t)kBlurW) + q1];
     words[w] = __ballot(t0 < t1);
   }
+  if (fin) {
+    const size_t dst = (size_t)fin->base + (slot - g.out_off);
+    if (lane < 4) {
+      fin->descs[dst * 4 + lane] = words[lane];
+      fin->descs_h[dst * 4 + lane] = words[lane];
+    }
+    if (lane == 0) {
+      KeyPointOut k;
+      k.x = (float)cx;
+      k.y = (float)cy;
+      if (l != 0) {
+        k.x *= g.scale;
+        k.y *= g.scale;
+      }
+      k.size = g.patch_size;
+      k.angle = angle;
+      k.response = (float)(kp >> 24);
+      k.octave = l;
+      k.class_id = -1;
+      fin->kps[dst] = k;
+      fin->kps_h[dst] = k;
+    }
+    return;
+  }
   const size_t o = (size_t)img * P->kp_slots + slot;
-  if (lane < 4) desc_out[o * 4 + lane] = words[lane];
-  if (lane == 0) angle_out[o] = angle;
+  if (lane < 4) st_pub<kWT>(desc_out + o * 4 + lane, words[lane]);
+  if (lane == 0) st_pub<kWT>(angle_out + o, angle);
 }
 
 __global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHeader* __restrict__ P, ImgSrc src,
@@ -2134,11 +2235,6 @@ __global__ __launch_bounds__(64 * ORB_DESC_WAVES) void k_describe(const PlanHead
 // multiply, level 0 untouched); points with lapping[0] <= x <= lapping[1] go
 // to the back in reverse order (stereo), the rest to the front (mono).
 // --------------------------------------------------------------------------
-struct KeyPointOut {
-  float x, y, size, angle, response;
-  int octave, class_id;
-};
-
 // kMirror: every output word also goes to the host-mapped copies (kps_h,
 // descs_h, nm_h = {n, mono, err}) of the single-image launch.  LDS: lvl_base
 // (kMaxLevels + 1 ints), flags (kAsmChunk ints), scan_tmp (kOctThreads + 1).
@@ -2157,7 +2253,14 @@ __device__ __forceinline__ void assemble_image(const PlanHeader* __restrict__ P,
                                                uint64_t* __restrict__ descs_h, int* __restrict__ nm_h) {
   constexpr int kChunk = kAsmChunk;
   const int t = threadIdx.x, L = P->levels;
-  if (t == 0) {
+  if (kMirror) {  // the level counts in one round trip (sc1 loads), then the prefix from LDS
+    if (t < L) lvl_base[t + 1] = ld_pub<kMirror>(oct_count + img * L + t);
+    __syncthreads();
+    if (t == 0) {
+      lvl_base[0] = 0;
+      for (int l = 0; l < L; ++l) lvl_base[l + 1] += lvl_base[l];
+    }
+  } else if (t == 0) {
     int acc = 0;
     for (int l = 0; l < L; ++l) {
       lvl_base[l] = acc;
@@ -2197,6 +2300,67 @@ __device__ __forceinline__ void assemble_image(const PlanHeader* __restrict__ P,
       y *= P->lev[l].scale;
     }
   };
+  if (kMirror && (lap1 < kFastBorder || lap0 > lap1)) {
+    // no keypoint can be stereo (every x >= kFastBorder): keypoint gi goes to
+    // slot gi.  The single-image path's usual case, with every load of a
+    // thread's keypoints in flight before its stores (the launch's tail)
+    constexpr int U = 4;
+    for (int b = t; b < n; b += 256 * U) {
+      uint32_t kpv[U];
+      float ang[U];
+      uint4 dv[U][2];
+      int lv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int gi = min(b + 256 * u, n - 1);
+        int l, idx;
+        locate(gi, l, idx);
+        const size_t so = (size_t)img * P->kp_slots + P->lev[l].out_off + idx;
+        lv[u] = l;
+        kpv[u] = oct_out[so];
+        ang[u] = angle_in[so];
+        const uint4* d = reinterpret_cast<const uint4*>(desc_in + so * 4);
+        dv[u][0] = d[0];
+        dv[u][1] = d[1];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int gi = b + 256 * u;
+        if (gi >= n) break;
+        const int l = lv[u];
+        const uint32_t kp = kpv[u];
+        KeyPointOut o;
+        o.x = (float)((int)(kp & 0xfff) + kFastBorder);
+        o.y = (float)((int)((kp >> 12) & 0xfff) + kFastBorder);
+        if (l != 0) {
+          o.x *= P->lev[l].scale;
+          o.y *= P->lev[l].scale;
+        }
+        o.size = P->lev[l].patch_size;
+        o.angle = ang[u];
+        o.response = (float)(kp >> 24);
+        o.octave = l;
+        o.class_id = -1;
+        const size_t dst = (size_t)img * cap + gi;
+        kps[dst] = o;
+        kps_h[dst] = o;
+        uint4* od = reinterpret_cast<uint4*>(descs + dst * 4);
+        uint4* oh = reinterpret_cast<uint4*>(descs_h + dst * 4);
+        od[0] = dv[u][0];
+        od[1] = dv[u][1];
+        oh[0] = dv[u][0];
+        oh[1] = dv[u][1];
+      }
+    }
+    if (t == 0) {
+      n_out[img] = n;
+      mono_out[img] = n;
+      nm_h[0] = n;
+      nm_h[1] = n;
+      nm_h[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   int n_stereo = 0;  // stereo keypoints before the current chunk
   for (int c0 = 0; c0 < n; c0 += kChunk) {
     const int cn = min(kChunk, n - c0);
@@ -2288,11 +2452,15 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
 // are the batch kernels' own (resize_tile / resize_tail, blur_wave,
 // fast_cell, octree_level, describe_slot, assemble_image): the same bytes.
 //
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): a producer's
-// waves drain their stores (vmcnt 0), the workgroup barrier, then one lane
-// releases at agent scope and adds to the stage's counter; a consumer's lane
-// polls the counter (agent-scope relaxed loads, s_sleep between), acquires
-// at agent scope and releases the workgroup by a barrier.  Polls are bounded:
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, R1): every
+// payload word a producer item writes for other workgroups is stored
+// write-through (sc1: st_pub / the kAuxSc1 buffer stores), its waves drain
+// them (vmcnt 0), the workgroup barrier, then one lane adds to the stage's
+// counter -- no release fence (a buffer_wbl2 per item cost 2-6 µs on every
+// hop of the resize chain); a consumer's lane polls the counter (agent-scope
+// relaxed loads, s_sleep between), acquires at agent scope and releases the
+// workgroup by a barrier; uniform reads of handed-off words are vector sc1
+// loads (ld_pub: the acquire does not refresh the scalar cache).  Polls are bounded:
 // a wait that never completes sets kErrDfTimeout and the item runs anyway,
 // so every worker reaches the exit.  The last describe item to finish runs
 // the assembly, mirroring the output block into host-mapped memory.
@@ -2315,9 +2483,10 @@ __device__ __forceinline__ void df_acquire() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__ a_dev, int* __restrict__ ctrl) {
+__global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__ a_dev, int* __restrict__ ctrl,
+                                                    const int* __restrict__ band_flags, int seq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ int s_item, s_last;
+  __shared__ int s_item, s_last, s_base;
   for (;;) {
     // the launch record and the thread index laundered per item: values
     // derived from them cannot be hoisted out of the loop (every stage's
@@ -2333,20 +2502,28 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned long long tr_grab = 0, tr_ready = 0;
+    int ticket = 0;
     if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(ctrl + kDfTicket * kDfCtrStride, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      s_item = t < df.n_items ? (int)a.items[t] : -1;
+      ticket = __hip_atomic_fetch_add(ctrl + kDfTicket * kDfCtrStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_item = ticket < df.n_items ? (int)a.items[ticket] : -1;
+      if (a.trace) tr_grab = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     const int it = s_item;
     if (it < 0) break;
     const int type = it & 15, l = (it >> 4) & 15, idx = (int)((uint32_t)it >> 8);
-    // ---- wait for the producers of what this item reads
-    if (type != kDfCopy) {
+    // ---- wait for the producers of what this item reads (resize items wait
+    // inside the tile code, once their plan-constant taps are loaded; FAST
+    // items load their cell record first)
+    Cell cell{};
+    if (type == kDfFast) {
+      const int ci = min(P->lev[l].cell_begin + 4 * idx + wave, P->lev[l].cell_end - 1);
+      cell = a.cells[ci];
+    }
+    auto wait = [&]() {
       if (tid == 0) {
         if (type == kDfDescribe) {
-          df_wait(ctrl, kDfOctDone + l, 1, err);
           df_wait(ctrl, kDfBlurDone + l, df.blur_items[l], err);
         } else if (type == kDfOctree) {
           df_wait(ctrl, kDfFastDone + l, df.fast_items[l], err);
@@ -2360,80 +2537,162 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
         df_acquire();
       }
       __syncthreads();
+    };
+    // no lapping band: every keypoint is mono and goes straight to its output
+    // slot (DescFinal), so a describe item also waits for the lower levels'
+    // octrees (the slot's base); wave 0 polls those counters lane-parallel
+    const bool direct = a.lap1 < kFastBorder || a.lap0 > a.lap1;
+    if (type == kDfDescribe && wave == 0) {
+      const int* oc = ctrl + (kDfOctDone + min(lane, kMaxLevels - 1)) * kDfCtrStride;
+      const bool need = direct ? lane <= l : lane == l;
+      for (int spin = 0;; ++spin) {
+        const bool ok = !need || __hip_atomic_load(oc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 1;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spin > (1 << 22)) {
+          if (lane == 0) atomicOr(err, kErrDfTimeout);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
+    if (type != kDfCopy && type != kDfResize) wait();
+    if (type == kDfDescribe && direct) {  // the keypoints of the lower levels (sc1 loads)
+      if (wave == 0) {
+        int c = lane < l ? ld_pub<true>(a.oct_count + lane) : 0;
+        c = wave_iscan(c);
+        if (lane == 63) s_base = c;
+      }
+      __syncthreads();
+    }
+    if (a.trace && tid == 0) tr_ready = __builtin_amdgcn_s_memrealtime();
     // ---- the item
     int pub;
     if (type == kDfCopy) {
+      // the host fills the pinned staging band by band after the launch and
+      // stamps each band's flag with the call's sequence number (fine-grained
+      // host memory: uncached on the device, so the flag read orders the data)
+      if (tid == 0)
+        for (int spin = 0; __hip_atomic_load(band_flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq;
+             ++spin) {
+          if (spin > (1 << 22)) {
+            atomicOr(err, kErrDfTimeout);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      __syncthreads();
       const int b0 = idx * kDfBandBytes, nb = min(kDfBandBytes, df.img_bytes - b0) >> 4;
       const uint4* s4 = reinterpret_cast<const uint4*>(a.img_host + b0);
-      uint4* d4 = reinterpret_cast<uint4*>(a.img + b0);
+      // write-through (sc1) 16-B stores: published without a release fence
+      const __amdgpu_buffer_rsrc_t drs =
+          __builtin_amdgcn_make_buffer_rsrc(a.img + b0, (short)0, (int)0xffffffff, kBufRsrcWord3);
       uint4 v[kDfBandBytes / 16 / 256];
 #pragma unroll
       for (int u = 0; u < kDfBandBytes / 16 / 256; ++u)
         if (tid + 256 * u < nb) v[u] = s4[tid + 256 * u];
 #pragma unroll
       for (int u = 0; u < kDfBandBytes / 16 / 256; ++u)
-        if (tid + 256 * u < nb) d4[tid + 256 * u] = v[u];
+        if (tid + 256 * u < nb)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v[u]),
+                                                 drs, 16 * (tid + 256 * u), 0, kAuxSc1);
       pub = kDfImg;
     } else if (type == kDfResize) {
       const LevelGeom& g = P->lev[l];
       const int nt = g.rs_tiles_x * g.rs_tiles_y;
       if (idx < nt)
-        resize_tile(P, a.rs_tab, src, a.pyr, l, 0, idx, lds, tid, true);
+        resize_tile<true>(P, a.rs_tab, src, a.pyr, l, 0, idx, lds, tid, true, wait);
       else
-        resize_tail(P, a.rs_tab, src, a.pyr, l, 0, idx - nt, lds, tid);
+        resize_tail<true>(P, a.rs_tab, src, a.pyr, l, 0, idx - nt, lds, tid, wait);
       pub = kDfLvl + l;
     } else if (type == kDfFast) {
       const int ci = P->lev[l].cell_begin + 4 * idx + wave;
       if (ci < P->lev[l].cell_end) {
         uint8_t* fl = lds + wave * P->max_roi_lds;
         switch (P->fast_pitch) {
-          case 48: fast_cell<48>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
-          case 52: fast_cell<52>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
-          case 56: fast_cell<56>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
-          case 60: fast_cell<60>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
-          case 64: fast_cell<64>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
-          default: fast_cell<0>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane); break;
+          case 48: fast_cell<48, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
+          case 52: fast_cell<52, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
+          case 56: fast_cell<56, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
+          case 60: fast_cell<60, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
+          case 64: fast_cell<64, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
+          default: fast_cell<0, true>(P, a.cells, src, a.pyr, a.slots, a.cell_count, 0, ci, fl, lane, &cell); break;
         }
       }
       pub = kDfFastDone + l;
     } else if (type == kDfBlur) {
       static_assert(ORB_BLUR_WAVES == 4, "k_extract_df runs a blur tile per 4-wave worker");
-      blur_wave(P, src, a.pyr, a.blur, 0, P->lev[l].blur_tile_begin + idx, 0);
+      blur_wave<true>(P, src, a.pyr, a.blur, 0, P->lev[l].blur_tile_begin + idx, 0);
       pub = kDfBlurDone + l;
     } else if (type == kDfOctree) {
       // (plans whose node arrays live in HBM take the per-stage launches: one
       // octree instance keeps the worker's registers down)
-      octree_level<false>(P, a.cells, a.slots, a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, err, 0, l,
+      octree_level<false, true>(P, a.cells, a.slots, a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, err, 0, l,
                           P->oct_kcap, nullptr, lds);
       pub = kDfOctDone + l;
     } else {  // kDfDescribe: slots out_off + 4 idx + wave of level l
       const int k = 4 * idx + wave;
+      const DescFinal fin{reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out),
+                          reinterpret_cast<KeyPointOut*>(a.kps_host), reinterpret_cast<uint64_t*>(a.desc_host),
+                          s_base};
       if (k < P->lev[l].out_cap)
-        describe_slot(P, src, a.pyr, a.blur, a.oct_out, a.oct_count, a.angle, a.desc, 0, P->lev[l].out_off + k,
-                      lds + wave * kDescSlice, lane);
+        describe_slot<true>(P, src, a.pyr, a.blur, a.oct_out, a.oct_count, a.angle, a.desc, 0, P->lev[l].out_off + k,
+                            lds + wave * kDescSlice, lane, direct ? &fin : nullptr);
       pub = kDfDescDone;
     }
-    // ---- publish: every wave's stores drained, one agent-scope release, the counter
+    // ---- publish: every payload store was write-through (sc1); every wave
+    // drains them, then one lane adds to the counter (no release fence)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(ctrl + pub * kDfCtrStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = pub == kDfDescDone && old == df.desc_items - 1;
       if (last) df_acquire();  // every describe (and so every octree) item's results
       s_last = last;
+      if (a.trace) {
+        unsigned long long* r = a.trace + 4 * (size_t)ticket;
+        r[0] = tr_grab;
+        r[1] = tr_ready;
+        r[2] = __builtin_amdgcn_s_memrealtime();
+        // HW_ID (CU / SIMD / SE ids) and XCC_ID (gfx950 hwreg 20) of this worker
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+        r[3] = (unsigned long long)(unsigned)it | ((unsigned long long)hw << 32) | ((unsigned long long)xcc << 60);
+      }
     }
     __syncthreads();
-    if (s_last) {
+    if (s_last && (a.lap1 < kFastBorder || a.lap0 > a.lap1)) {
+      // direct outputs: every record is written; the counts (n = mono)
+      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items] = __builtin_amdgcn_s_memrealtime();
+      if (wave == 0) {
+        int c = lane < P->levels ? ld_pub<true>(a.oct_count + lane) : 0;
+        c = wave_iscan(c);
+        if (lane == 63) {
+          a.nm[0] = c;
+          a.nm[1] = c;
+          a.nm_host[0] = c;
+          a.nm_host[1] = c;
+          a.nm_host[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // every other worker's output stores drained before its counter add,
+          // this lane's own before the system-scope release: then the host's word
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items + 1] = __builtin_amdgcn_s_memrealtime();
+    } else if (s_last) {
+      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items] = __builtin_amdgcn_s_memrealtime();
       int* ab = reinterpret_cast<int*>(lds);
       assemble_image<true>(P, a.oct_out, a.oct_count, a.angle, a.desc, a.lap0, a.lap1,
                            reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out), a.cap,
                            a.nm, a.nm + 1, err, 0, ab, ab + kMaxLevels + 1, ab + kMaxLevels + 1 + kAsmChunk,
                            reinterpret_cast<KeyPointOut*>(a.kps_host), reinterpret_cast<uint64_t*>(a.desc_host),
                            a.nm_host);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (tid == 0) {  // (as above: every store of the assembly drained first)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items + 1] = __builtin_amdgcn_s_memrealtime();
     }
   }
   // ---- the last worker out clears the control block for the next launch
@@ -2512,8 +2771,9 @@ hipError_t launch_extract(const ExtractLaunch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_extract_df(const DfLaunch& a, const DfLaunch* a_dev, hipStream_t st) {
-  hipLaunchKernelGGL(k_extract_df, dim3(a.grid), dim3(256), a.df.lds_bytes, st, a_dev, a.ctrl);
+hipError_t launch_extract_df(const DfLaunch& a, const DfLaunch* a_dev, const int* band_flags, int seq,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_extract_df, dim3(a.grid), dim3(256), a.df.lds_bytes, st, a_dev, a.ctrl, band_flags, seq);
   return hipGetLastError();
 }
 

@@ -99,16 +99,21 @@ struct DfLaunch {
   void* kps_host;            // host-mapped mirrors of the same three
   void* desc_host;
   int* nm_host;
+  int* done_host;            // host-mapped word: the call's sequence number once every output is written
   int cap;
   int grid;                  // workers
   DfPlan df;
+  unsigned long long* trace;  // optional (ORBGPU_DF_TRACE): per ticket {grab, ready, done, item | hw ids}
 };
 
 // host planner (orb_plan.cpp): the item list of a plan
 void make_df_items(const PlanHeader& P, int img_bytes, DfPlan& df, std::vector<uint32_t>& items);
 size_t df_lds_bytes(const PlanHeader& P, size_t octree_lds);
-// a: the host copy (grid, LDS); a_dev: the same record in device memory (read by the workers)
-hipError_t launch_extract_df(const DfLaunch& a, const DfLaunch* a_dev, hipStream_t st);
+// a: the host copy (grid, LDS); a_dev: the same record in device memory (read by
+// the workers); band_flags: one int per copy band in host-mapped memory, which
+// the host sets to `seq` once the band's bytes are in a.img_host
+hipError_t launch_extract_df(const DfLaunch& a, const DfLaunch* a_dev, const int* band_flags, int seq,
+                             hipStream_t st);
 hipError_t set_df_lds_limit(size_t bytes);
 
 // Stage boundaries recorded when ExtractLaunch::events is set.

@@ -15,7 +15,9 @@
 // frames, and per frame the keypoint counts and inliers (the Python leg checks
 // them against its own).
 //
-//   build/latency [FRAMES] [WARMUP]
+//   build/latency [FRAMES] [WARMUP] [mono]
+// (mono: the left image only, on the calling thread -- the extraction's own
+// latency without the second thread)
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -66,6 +68,7 @@ double quantile(std::vector<double> v, double q) {  // nearest rank above
 int main(int argc, char** argv) {
   const int frames = argc > 1 ? atoi(argv[1]) : 40;
   const int warmup = argc > 2 ? atoi(argv[2]) : 5;
+  const bool mono = argc > 3 && std::string(argv[3]) == "mono";
   if (frames <= 0 || warmup < 0) return 2;
 
   struct In {
@@ -105,15 +108,23 @@ int main(int argc, char** argv) {
     const In& f = in[i % frames];
     int nl = 0, nr = 0, ml = 0, mr = 0, ninl = 0;
     const auto t0 = Clock::now();
-    orbgpu_status sr = ORBGPU_OK;
-    std::thread th([&] {
-      sr = orbgpu_extract(exr, f.right.data(), kW, kH, kW, lap, kr.data(), dr.data(), cap, &nr, &mr);
-    });
-    const orbgpu_status sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
-    th.join();
+    orbgpu_status sr = ORBGPU_OK, sl = ORBGPU_OK;
+    if (mono) {
+      sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
+    } else {
+      std::thread th([&] {
+        sr = orbgpu_extract(exr, f.right.data(), kW, kH, kW, lap, kr.data(), dr.data(), cap, &nr, &mr);
+      });
+      sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
+      th.join();
+    }
     const auto t1 = Clock::now();
     CHECK(sl);
     CHECK(sr);
+    if (mono) {
+      if (i >= warmup) t_ex.push_back(ms(t0, t1)), n_left[i % frames] = nl;
+      continue;
+    }
     // ComputeStereoMatches on the two handles' resident outputs (frame.cc:189):
     // its own column, not part of the extract + pose figure
     CHECK(orbgpu_stereo_match(exl, exr, bf, mb, ur.data(), depth.data(), cap));
@@ -132,6 +143,11 @@ int main(int argc, char** argv) {
     for (size_t k = 0; k < v.size(); ++k) s += (k ? "," : "") + std::to_string(v[k]);
     return s + "]";
   };
+  if (mono) {
+    printf("{\"mode\": \"mono\", \"frames\": %d, \"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f}\n", frames,
+           quantile(t_ex, 0.5), quantile(t_ex, 0.9));
+    return 0;
+  }
   printf("{\"host\": \"C++ through the C ABI (tools/latency.cc)\", \"frames\": %d, "
          "\"gpu_ms_per_frame\": %.3f, \"gpu_ms_per_frame_p90\": %.3f, "
          "\"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f, "
