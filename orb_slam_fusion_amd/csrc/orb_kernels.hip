@@ -2072,13 +2072,12 @@ struct KeyPointOut {  // orbgpu_keypoint (cv::KeyPoint field order)
 };
 // The dataflow launch's direct output (no lapping band: keypoint i of level l
 // is output i + base, base = the keypoints of the lower levels): the wave
-// writes its keypoint record and descriptor to the device block and to its
-// host-mapped mirror itself, and the slot arrays are not written.
+// writes its keypoint record and descriptor into the device output block
+// itself (write-through: the launch's last item copies the block to the host
+// mirror), and the slot arrays are not written.
 struct DescFinal {
   KeyPointOut* kps;
   uint64_t* descs;
-  KeyPointOut* kps_h;
-  uint64_t* descs_h;
   int base;
 };
 // Octree output slot `slot` of image img by one wave (lane 0..63) with its own
@@ -2183,25 +2182,16 @@ __device__ __forceinline__ void describe_slot(const PlanHeader* __restrict__ P, 
   }
   if (fin) {
     const size_t dst = (size_t)fin->base + (slot - g.out_off);
-    if (lane < 4) {
-      fin->descs[dst * 4 + lane] = words[lane];
-      fin->descs_h[dst * 4 + lane] = words[lane];
-    }
-    if (lane == 0) {
-      KeyPointOut k;
-      k.x = (float)cx;
-      k.y = (float)cy;
+    if (lane < 4) st_pub<true>(fin->descs + dst * 4 + lane, words[lane]);
+    if (lane < 7) {  // the record's 7 words, one a lane
+      float x = (float)cx, y = (float)cy;
       if (l != 0) {
-        k.x *= g.scale;
-        k.y *= g.scale;
+        x *= g.scale;
+        y *= g.scale;
       }
-      k.size = g.patch_size;
-      k.angle = angle;
-      k.response = (float)(kp >> 24);
-      k.octave = l;
-      k.class_id = -1;
-      fin->kps[dst] = k;
-      fin->kps_h[dst] = k;
+      const float fv[5] = {x, y, g.patch_size, angle, (float)(kp >> 24)};
+      const uint32_t w = lane < 5 ? __float_as_uint(fv[lane]) : lane == 5 ? (uint32_t)l : 0xffffffffu;
+      st_pub<true>(reinterpret_cast<uint32_t*>(fin->kps + dst) + lane, w);
     }
     return;
   }
@@ -2630,9 +2620,7 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
       pub = kDfOctDone + l;
     } else {  // kDfDescribe: slots out_off + 4 idx + wave of level l
       const int k = 4 * idx + wave;
-      const DescFinal fin{reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out),
-                          reinterpret_cast<KeyPointOut*>(a.kps_host), reinterpret_cast<uint64_t*>(a.desc_host),
-                          s_base};
+      const DescFinal fin{reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out), s_base};
       if (k < P->lev[l].out_cap)
         describe_slot<true>(P, src, a.pyr, a.blur, a.oct_out, a.oct_count, a.angle, a.desc, 0, P->lev[l].out_off + k,
                             lds + wave * kDescSlice, lane, direct ? &fin : nullptr);
@@ -2668,14 +2656,41 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
         if (lane == 63) {
           a.nm[0] = c;
           a.nm[1] = c;
-          a.nm_host[0] = c;
-          a.nm_host[1] = c;
-          a.nm_host[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          // every other worker's output stores drained before its counter add,
-          // this lane's own before the system-scope release: then the host's word
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-          __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          s_base = c;
         }
+      }
+      __syncthreads();
+      // the block to its host mirror from this one workgroup (the describe
+      // items' stores were write-through and published; host-memory writes of
+      // different CUs reach the host in no promised order, so only this
+      // workgroup writes the mirror): records, descriptors, then the counts
+      const int n = s_base;
+      auto copy = [&](const void* src, void* dst, int bytes) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        const int n16 = (bytes + 15) >> 4;
+        for (int i0 = tid; i0 < n16; i0 += 256 * 4) {
+          uint4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + 256 * u < n16) v[u] = s4[i0 + 256 * u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + 256 * u < n16) d4[i0 + 256 * u] = v[u];
+        }
+      };
+      copy(a.kps_out, a.kps_host, n * (int)sizeof(KeyPointOut));
+      copy(a.desc_out, a.desc_host, n * 32);
+      if (tid == 0) {
+        a.nm_host[0] = n;
+        a.nm_host[1] = n;
+        a.nm_host[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {  // every mirror store of this workgroup drained: the host's word
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items + 1] = __builtin_amdgcn_s_memrealtime();
     } else if (s_last) {

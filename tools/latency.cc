@@ -68,7 +68,10 @@ double quantile(std::vector<double> v, double q) {  // nearest rank above
 int main(int argc, char** argv) {
   const int frames = argc > 1 ? atoi(argv[1]) : 40;
   const int warmup = argc > 2 ? atoi(argv[2]) : 5;
-  const bool mono = argc > 3 && std::string(argv[3]) == "mono";
+  const std::string mode = argc > 3 ? argv[3] : "stereo";
+  // mono: the left image on the calling thread; mono_thread: on a std::thread
+  // started per frame (the thread's own cost, as frame.cc:179-182 pays it)
+  const bool mono = mode == "mono" || mode == "mono_thread", mono_thread = mode == "mono_thread";
   if (frames <= 0 || warmup < 0) return 2;
 
   struct In {
@@ -109,7 +112,12 @@ int main(int argc, char** argv) {
     int nl = 0, nr = 0, ml = 0, mr = 0, ninl = 0;
     const auto t0 = Clock::now();
     orbgpu_status sr = ORBGPU_OK, sl = ORBGPU_OK;
-    if (mono) {
+    if (mono_thread) {
+      std::thread th([&] {
+        sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
+      });
+      th.join();
+    } else if (mono) {
       sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
     } else {
       std::thread th([&] {
@@ -144,8 +152,8 @@ int main(int argc, char** argv) {
     return s + "]";
   };
   if (mono) {
-    printf("{\"mode\": \"mono\", \"frames\": %d, \"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f}\n", frames,
-           quantile(t_ex, 0.5), quantile(t_ex, 0.9));
+    printf("{\"mode\": \"%s\", \"frames\": %d, \"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f}\n",
+           mode.c_str(), frames, quantile(t_ex, 0.5), quantile(t_ex, 0.9));
     return 0;
   }
   printf("{\"host\": \"C++ through the C ABI (tools/latency.cc)\", \"frames\": %d, "
