@@ -136,6 +136,21 @@ orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width,
                              int stride, const int lapping[2], orbgpu_keypoint* kps,
                              uint8_t* descs, int cap, int* n_out, int* mono_out);
 
+/* Both images of a stereo frame from ONE host thread: the two handles'
+ * extractions (each exactly orbgpu_extract on its image, outputs and errors
+ * included) are in flight together on the handles' own streams.  Replaces the
+ * two std::thread ExtractORB calls of the stereo Frame constructor
+ * (frame.cc:179-182, ExtractORB :467-476): on the GPU the host threads buy no
+ * parallelism and each costs a thread start per frame.  `left` and `right`
+ * must be different handles; returns the left status if it is not OK, else
+ * the right one. */
+orbgpu_status orbgpu_extract_stereo(orbgpu_extractor* left, orbgpu_extractor* right, const uint8_t* img_left,
+                                    const uint8_t* img_right, int width, int height, int stride,
+                                    const int lapping_left[2], const int lapping_right[2],
+                                    orbgpu_keypoint* kps_left, uint8_t* descs_left, int cap_left,
+                                    int* n_left, int* mono_left, orbgpu_keypoint* kps_right,
+                                    uint8_t* descs_right, int cap_right, int* n_right, int* mono_right);
+
 /* Host copy of pyramid level `level` from the last orbgpu_extract call
  * (rows *stride bytes apart, *stride >= *width).  Replaces the public member
  * std::vector<cv::Mat> img_pyramid_ (orb_extractor.h:76) read by

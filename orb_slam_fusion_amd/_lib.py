@@ -185,6 +185,7 @@ SIGNATURES = {
     "orbgpu_extractor_set_stage_event": (_I, [_P, _I, _P]),
     "orbgpu_extractor_plan": (_I, [_P, _I, _I, _P, _P]),
     "orbgpu_extract": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P]),
+    "orbgpu_extract_stereo": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _P]),
     "orbgpu_extractor_pyramid_level": (_I, [_P, _I, ctypes.POINTER(_P), _P, _P, _P]),
     "orbgpu_extract_batch": (
         _I,

@@ -483,6 +483,157 @@ static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const 
              : ORBGPU_ERR_DEVICE;
 }
 
+// One host-buffer extraction (orbgpu_extract, and each image of
+// orbgpu_extract_stereo) in phases, so a stereo pair can have both launches in
+// flight from one host thread: prepare (validation, plan, buffers), launch
+// (the dataflow launch before its image is staged; the graph path stages the
+// image and enqueues its copy + chain), stage_df (the dataflow launch's image,
+// band by band), wait, finish (the outputs to the caller's arrays).
+struct SingleCall {
+  orbgpu_extractor* h;
+  const uint8_t* img;
+  int width, height, stride;
+  const int* lapping;
+  orbgpu_keypoint* kps;
+  uint8_t* descs;
+  int cap;
+  int* n_out;
+  int* mono_out;
+  size_t bytes = 0;
+  int pitch0 = 0, seq = 0;
+  int lap[2] = {0, 0};
+  bool df = false;
+
+  orbgpu_status prepare() {
+    if (!h || !n_out) return ORBGPU_ERR_INVALID;
+    *n_out = 0;
+    if (mono_out) *mono_out = -1;
+    if (!img || width <= 0 || height <= 0) return ORBGPU_ERR_EMPTY;
+    if (stride < width || cap < 0 || (cap > 0 && (!kps || !descs))) return ORBGPU_ERR_INVALID;
+    if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    orbgpu_status st = ensure_plan(h, width, height);
+    if (st == ORBGPU_OK) st = ensure_workspace(h, 1);
+    if (st != ORBGPU_OK) return st;
+    const PlanHeader& P = h->plan.hdr;
+    pitch0 = P.lev[0].pitch;  // 16-byte aligned rows for the vector loads
+    bytes = (size_t)pitch0 * height;
+    if (bytes > h->d_img_bytes || bytes > h->h_img_bytes) drop_graphs(h);  // image staging about to be reallocated
+    if (bytes > h->d_img_bytes) {
+      dfree(h->d_img);
+      if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
+      h->d_img_bytes = bytes;
+    }
+    if (bytes > h->h_img_bytes) {
+      if (h->h_img) (void)hipHostFree(h->h_img);
+      h->h_img = nullptr;
+      h->h_img_bytes = 0;
+      // the image, then one flag per copy band of the dataflow launch
+      const size_t flags_off = (bytes + 63) & ~(size_t)63;
+      const size_t n_bands = (bytes + kDfBandBytes - 1) / kDfBandBytes;
+      if (hipHostMalloc(&h->h_img, flags_off + 4 * n_bands, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_img_dev), h->h_img, 0) != hipSuccess)
+        return ORBGPU_ERR_NOMEM;
+      h->h_band = reinterpret_cast<int*>(h->h_img + flags_off);
+      h->h_band_dev = reinterpret_cast<const int*>(h->h_img_dev + flags_off);
+      std::memset(h->h_band, 0, 4 * n_bands);
+      h->df_seq = 0;
+      h->h_img_bytes = bytes;
+    }
+    if ((st = ensure_single_out(h, (size_t)P.kp_slots)) != ORBGPU_OK) return st;
+    lap[0] = lapping ? lapping[0] : 0;
+    lap[1] = lapping ? lapping[1] : 0;
+    df = h->single_mode == ORBGPU_SINGLE_DATAFLOW && !P.oct_hbm_nodes;
+    return ORBGPU_OK;
+  }
+
+  // the image into pinned staging (rows at the level-0 pitch); band_done(b)
+  // after each piece: the bytes below b are in place
+  template <class F>
+  void stage(F&& band_done) {
+    if (stride == pitch0) {
+      for (size_t b0 = 0; b0 < bytes; b0 += kDfBandBytes) {
+        const size_t nb = std::min((size_t)kDfBandBytes, bytes - b0);
+        std::memcpy(h->h_img + b0, img + b0, nb);
+        band_done(b0 + nb);
+      }
+    } else {
+      for (int r = 0; r < height; ++r) {
+        std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
+        band_done((size_t)(r + 1) * pitch0);
+      }
+    }
+  }
+
+  orbgpu_status launch() {
+    if (df) {
+      seq = h->df_seq = h->df_seq == 0x7fffffff ? 1 : h->df_seq + 1;
+      return run_single_df(h, bytes, lap, seq);
+    }
+    stage([](size_t) {});
+    const PlanHeader& P = h->plan.hdr;
+    ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs, P.kp_slots, h->d_nm,
+                                  h->d_nm + 1);
+    a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs
+    return run_single_chain(h, a) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+  }
+
+  // the dataflow launch's image, after the launch: each band's flag once its
+  // bytes are written (the launch's copy items wait for them), so the copy
+  // overlaps the launch's start
+  void stage_df() {
+    if (!df) return;
+    const int n_bands = (int)((bytes + kDfBandBytes - 1) / kDfBandBytes);
+    int next = 0;
+    stage([&](size_t upto) {
+      while (next < n_bands && std::min((size_t)(next + 1) * kDfBandBytes, bytes) <= upto)
+        __atomic_store_n(&h->h_band[next++], seq, __ATOMIC_RELEASE);
+    });
+  }
+
+  orbgpu_status wait() {
+    if (!df) return hipStreamSynchronize(h->stream) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
+    // the launch writes the call's number after every output word: return as
+    // soon as it appears (the workers' exit drains on the stream behind it);
+    // past ~0.5 s, or a stream error, the stream's own synchronisation decides
+    volatile int* done = reinterpret_cast<volatile int*>(h->h_small) + 3;
+    bool seen = false;
+    for (long spin = 0; spin < (1L << 24); ++spin) {
+      if (*done == seq) {
+        seen = true;
+        break;
+      }
+      if ((spin & 4095) == 4095 && hipStreamQuery(h->stream) != hipErrorNotReady) {
+        seen = *done == seq;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (!seen && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+    if (!seen && *done != seq) return ORBGPU_ERR_DEVICE;
+    return ORBGPU_OK;
+  }
+
+  orbgpu_status finish() {
+    const int nm[2] = {h->h_small[0], h->h_small[1]}, err = h->h_small[2];
+    h->host_pyr_valid = false;
+    h->last_w = width;
+    h->last_h = height;
+    if (err) {
+      (void)hipMemset(h->d_nm + 2, 0, sizeof(int));
+      return ORBGPU_ERR_CAPACITY;
+    }
+    *n_out = nm[0];
+    if (mono_out) *mono_out = nm[1];
+    if (nm[0] > cap) return ORBGPU_ERR_CAPACITY;
+    if (nm[0] > 0) {
+      std::memcpy(kps, h->h_kps, (size_t)nm[0] * sizeof(orbgpu_keypoint));
+      std::memcpy(descs, h->h_descs, (size_t)nm[0] * 32);
+    }
+    return ORBGPU_OK;
+  }
+};
+
 extern "C" {
 
 orbgpu_status orbgpu_extractor_create(const orbgpu_orb_params* params, int device, int max_width,
@@ -670,113 +821,38 @@ int orbgpu_extractor_max_keypoints(orbgpu_extractor* h, int width, int height) {
 orbgpu_status orbgpu_extract(orbgpu_extractor* h, const uint8_t* img, int width, int height,
                              int stride, const int lapping[2], orbgpu_keypoint* kps,
                              uint8_t* descs, int cap, int* n_out, int* mono_out) {
-  if (!h || !n_out) return ORBGPU_ERR_INVALID;
-  *n_out = 0;
-  if (mono_out) *mono_out = -1;
-  if (!img || width <= 0 || height <= 0) return ORBGPU_ERR_EMPTY;
-  if (stride < width || cap < 0 || (cap > 0 && (!kps || !descs))) return ORBGPU_ERR_INVALID;
-  if (hipSetDevice(h->device) != hipSuccess) return ORBGPU_ERR_DEVICE;
-  orbgpu_status st = ensure_plan(h, width, height);
-  if (st == ORBGPU_OK) st = ensure_workspace(h, 1);
-  if (st != ORBGPU_OK) return st;
-  const PlanHeader& P = h->plan.hdr;
-  const int pitch0 = P.lev[0].pitch;  // 16-byte aligned rows for the vector loads
-  const size_t bytes = (size_t)pitch0 * height;
-  if (bytes > h->d_img_bytes || bytes > h->h_img_bytes)
-    drop_graphs(h);  // image staging about to be reallocated
-  if (bytes > h->d_img_bytes) {
-    dfree(h->d_img);
-    if (dalloc(&h->d_img, bytes)) return ORBGPU_ERR_NOMEM;
-    h->d_img_bytes = bytes;
-  }
-  if (bytes > h->h_img_bytes) {
-    if (h->h_img) (void)hipHostFree(h->h_img);
-    h->h_img = nullptr;
-    h->h_img_bytes = 0;
-    // the image, then one flag per copy band of the dataflow launch
-    const size_t flags_off = (bytes + 63) & ~(size_t)63;
-    const size_t n_bands = (bytes + kDfBandBytes - 1) / kDfBandBytes;
-    if (hipHostMalloc(&h->h_img, flags_off + 4 * n_bands, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_img_dev), h->h_img, 0) != hipSuccess)
-      return ORBGPU_ERR_NOMEM;
-    h->h_band = reinterpret_cast<int*>(h->h_img + flags_off);
-    h->h_band_dev = reinterpret_cast<const int*>(h->h_img_dev + flags_off);
-    std::memset(h->h_band, 0, 4 * n_bands);
-    h->df_seq = 0;
-    h->h_img_bytes = bytes;
-  }
-  if ((st = ensure_single_out(h, (size_t)P.kp_slots)) != ORBGPU_OK) return st;
-  // the image into pinned staging (rows at the level-0 pitch): before the
-  // graph's copy, or, for the dataflow launch, band by band AFTER the launch
-  // (its copy items wait for each band's flag), so the copy overlaps the
-  // launch's start
-  auto stage = [&](auto&& band_done) {
-    if (stride == pitch0) {
-      for (size_t b0 = 0; b0 < bytes; b0 += kDfBandBytes) {
-        const size_t nb = std::min((size_t)kDfBandBytes, bytes - b0);
-        std::memcpy(h->h_img + b0, img + b0, nb);
-        band_done(b0 + nb);
-      }
-    } else {
-      for (int r = 0; r < height; ++r) {
-        std::memcpy(h->h_img + (size_t)r * pitch0, img + (size_t)r * stride, (size_t)width);
-        band_done((size_t)(r + 1) * pitch0);
-      }
-    }
-  };
-  const int lap[2] = {lapping ? lapping[0] : 0, lapping ? lapping[1] : 0};
-  if (h->single_mode == ORBGPU_SINGLE_DATAFLOW && !P.oct_hbm_nodes) {
-    const int seq = h->df_seq = h->df_seq == 0x7fffffff ? 1 : h->df_seq + 1;
-    if ((st = run_single_df(h, bytes, lap, seq)) != ORBGPU_OK) return st;
-    const int n_bands = (int)((bytes + kDfBandBytes - 1) / kDfBandBytes);
-    int next = 0;
-    stage([&](size_t upto) {  // every band wholly written: its flag, after its bytes
-      while (next < n_bands && std::min((size_t)(next + 1) * kDfBandBytes, bytes) <= upto)
-        __atomic_store_n(&h->h_band[next++], seq, __ATOMIC_RELEASE);
-    });
-    // the launch writes the call's number after every output word: return as
-    // soon as it appears (the workers' exit drains on the stream behind it);
-    // past ~0.5 s, or a stream error, the stream's own synchronisation decides
-    volatile int* done = reinterpret_cast<volatile int*>(h->h_small) + 3;
-    bool seen = false;
-    for (long spin = 0; spin < (1L << 24); ++spin) {
-      if (*done == seq) {
-        seen = true;
-        break;
-      }
-      if ((spin & 4095) == 4095 && hipStreamQuery(h->stream) != hipErrorNotReady) {
-        seen = *done == seq;
-        break;
-      }
-      __builtin_ia32_pause();
-    }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    if (!seen && hipStreamSynchronize(h->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
-    if (!seen && *done != seq) return ORBGPU_ERR_DEVICE;
-  } else {
-    stage([](size_t) {});
-    ExtractLaunch a = make_launch(h, h->d_img, bytes, pitch0, 1, lap, h->d_kps, h->d_descs,
-                                  P.kp_slots, h->d_nm, h->d_nm + 1);
-    a.err = h->d_nm + 2;  // the block's error word: copied back with the outputs
-    if (run_single_chain(h, a) != hipSuccess || hipStreamSynchronize(h->stream))
-      return ORBGPU_ERR_DEVICE;
-  }
-  const int nm[2] = {h->h_small[0], h->h_small[1]}, err = h->h_small[2];
-  h->host_pyr_valid = false;
-  h->last_w = width;
-  h->last_h = height;
-  if (err) {
-    (void)hipMemset(h->d_nm + 2, 0, sizeof(int));
-    return ORBGPU_ERR_CAPACITY;
-  }
-  *n_out = nm[0];
-  if (mono_out) *mono_out = nm[1];
-  if (nm[0] > cap) return ORBGPU_ERR_CAPACITY;
-  if (nm[0] > 0) {
-    std::memcpy(kps, h->h_kps, (size_t)nm[0] * sizeof(orbgpu_keypoint));
-    std::memcpy(descs, h->h_descs, (size_t)nm[0] * 32);
-  }
-  return ORBGPU_OK;
+  SingleCall c{h, img, width, height, stride, lapping, kps, descs, cap, n_out, mono_out};
+  orbgpu_status st = c.prepare();
+  if (st == ORBGPU_OK) st = c.launch();
+  if (st == ORBGPU_OK) c.stage_df();
+  if (st == ORBGPU_OK) st = c.wait();
+  return st == ORBGPU_OK ? c.finish() : st;
+}
+
+orbgpu_status orbgpu_extract_stereo(orbgpu_extractor* left, orbgpu_extractor* right, const uint8_t* img_left,
+                                    const uint8_t* img_right, int width, int height, int stride,
+                                    const int lapping_left[2], const int lapping_right[2],
+                                    orbgpu_keypoint* kps_left, uint8_t* descs_left, int cap_left,
+                                    int* n_left, int* mono_left, orbgpu_keypoint* kps_right,
+                                    uint8_t* descs_right, int cap_right, int* n_right, int* mono_right) {
+  if (!left || !right || left == right) return ORBGPU_ERR_INVALID;
+  SingleCall c[2] = {{left, img_left, width, height, stride, lapping_left, kps_left, descs_left, cap_left, n_left,
+                      mono_left},
+                     {right, img_right, width, height, stride, lapping_right, kps_right, descs_right, cap_right,
+                      n_right, mono_right}};
+  orbgpu_status st[2];
+  for (int k = 0; k < 2; ++k) st[k] = c[k].prepare();
+  // both launches first (each handle's own stream), then both images
+  // (each launch's copy items wait for their bands), then the results
+  for (int k = 0; k < 2; ++k)
+    if (st[k] == ORBGPU_OK) st[k] = c[k].launch();
+  for (int k = 0; k < 2; ++k)
+    if (st[k] == ORBGPU_OK) c[k].stage_df();
+  for (int k = 0; k < 2; ++k)
+    if (st[k] == ORBGPU_OK) st[k] = c[k].wait();
+  for (int k = 0; k < 2; ++k)
+    if (st[k] == ORBGPU_OK) st[k] = c[k].finish();
+  return st[0] != ORBGPU_OK ? st[0] : st[1];
 }
 
 orbgpu_status orbgpu_extractor_pyramid_level(orbgpu_extractor* h, int level, const uint8_t** data,

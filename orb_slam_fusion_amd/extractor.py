@@ -155,6 +155,34 @@ class OrbExtractor:
         N = n.value
         return mono.value, kps[:N].copy(), (descs[:N].copy() if N > 0 else None)
 
+    def extract_stereo(self, right: "OrbExtractor", img_left: np.ndarray, img_right: np.ndarray,
+                       lapping_left: Sequence[int] = (0, 0), lapping_right: Sequence[int] = (0, 0)):
+        """Both images of a stereo frame from this thread (orbgpu_extract_stereo):
+        this handle takes the left image, `right` the right one; returns the
+        two operator() results ((mono, keypoints, descriptors) each)."""
+        outs = []
+        args = []
+        for ex, img, lp in ((self, img_left, lapping_left), (right, img_right, lapping_right)):
+            img = np.ascontiguousarray(img)
+            if img.dtype != np.uint8 or img.ndim != 2:
+                raise AssertionError("OrbExtractor expects a CV_8UC1 image")
+            cap = max(ex.max_keypoints(img.shape[1], img.shape[0]), 1)
+            o = (np.zeros(cap, KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8), ctypes.c_int(), ctypes.c_int(),
+                 (ctypes.c_int * 2)(int(lp[0]), int(lp[1])), img, cap)
+            outs.append(o)
+        (kl, dl, nl, ml, ll, il, cl), (kr, dr, nr, mr, lr, ir, cr) = outs
+        if il.shape != ir.shape:
+            raise ValueError("the stereo images differ in size")
+        h, w = il.shape
+        st = lib().orbgpu_extract_stereo(
+            self._h, right._h, ptr(il), ptr(ir), w, h, w, ll, lr, ptr(kl), ptr(dl), cl, ctypes.byref(nl),
+            ctypes.byref(ml), ptr(kr), ptr(dr), cr, ctypes.byref(nr), ctypes.byref(mr))
+        check(st, "orbgpu_extract_stereo")
+        self._pyr_valid = False
+        right._pyr_valid = False
+        return tuple((m.value, k[:n.value].copy(), d[:n.value].copy() if n.value > 0 else None)
+                     for k, d, n, m in ((kl, dl, nl, ml), (kr, dr, nr, mr)))
+
     @property
     def img_pyramid_(self):
         if not self._pyr_valid:

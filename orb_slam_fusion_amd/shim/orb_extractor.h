@@ -7,6 +7,7 @@
 #define ORBEXTRACTOR_H
 
 #include <list>
+#include <utility>
 #include <opencv2/opencv.hpp>
 #include <vector>
 
@@ -51,6 +52,17 @@ class OrbExtractor {
 
   void ComputePyramid(cv::Mat img);
 
+  // Both images of a stereo frame from the calling thread (orbgpu_extract_stereo):
+  // left's operator() on im_left and right's on im_right, both launches in
+  // flight together.  Returns {left mono index, right mono index}; used by the
+  // stereo Frame constructor in place of its two ExtractORB threads
+  // (frame.cc:179-182, frame_stereo_gpu.cc).
+  static std::pair<int, int> ExtractStereo(OrbExtractor &left, OrbExtractor &right, cv::InputArray im_left,
+                                           cv::InputArray im_right, std::vector<cv::KeyPoint> &kps_left,
+                                           cv::OutputArray descs_left, std::vector<cv::KeyPoint> &kps_right,
+                                           cv::OutputArray descs_right, std::vector<int> &lapping_left,
+                                           std::vector<int> &lapping_right);
+
   // The device handle (frame_stereo_gpu.cc matches on its resident outputs).
   orbgpu_extractor *gpu() const { return gpu_; }
 
@@ -66,6 +78,10 @@ class OrbExtractor {
   std::vector<float> inv_lev_sigma_2_;
 
  private:
+  // the call's outputs from kp_buf_ / desc_buf_ (and img_pyramid_ without ORBGPU_STEREO)
+  void finish_call(int n, std::vector<cv::KeyPoint> &kps, cv::OutputArray descs);
+  int reserve_call(const cv::Mat &im);  // sizes the buffers; returns the keypoint capacity
+
   orbgpu_extractor *gpu_ = nullptr;
   std::vector<orbgpu_keypoint> kp_buf_;
   cv::Mat desc_buf_;

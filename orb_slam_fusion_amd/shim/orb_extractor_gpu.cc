@@ -39,23 +39,15 @@ OrbExtractor::OrbExtractor(int num_feats, float scale_factor, int num_levs, int 
 
 OrbExtractor::~OrbExtractor() { orbgpu_extractor_destroy(gpu_); }
 
-int OrbExtractor::operator()(cv::InputArray img, cv::InputArray /*msk*/,
-                             std::vector<cv::KeyPoint> &kps, cv::OutputArray descs,
-                             std::vector<int> &lapping_areas) {
-  if (img.empty()) return -1;
-  cv::Mat im = img.getMat();
+int OrbExtractor::reserve_call(const cv::Mat &im) {
   assert(im.type() == CV_8UC1);
   const int cap = orbgpu_extractor_max_keypoints(gpu_, im.cols, im.rows);
   kp_buf_.resize(cap > 0 ? cap : 1);
   desc_buf_.create(cap > 0 ? cap : 1, 32, CV_8U);
-  int n = 0, mono = 0;
-  const int lap[2] = {lapping_areas.size() > 0 ? lapping_areas[0] : 0,
-                      lapping_areas.size() > 1 ? lapping_areas[1] : 0};
-  const orbgpu_status st =
-      orbgpu_extract(gpu_, im.data, im.cols, im.rows, (int)im.step, lap, kp_buf_.data(),
-                     desc_buf_.data, cap, &n, &mono);
-  if (st != ORBGPU_OK) throw std::runtime_error("orbgpu_extract failed");
+  return cap;
+}
 
+void OrbExtractor::finish_call(int n, std::vector<cv::KeyPoint> &kps, cv::OutputArray descs) {
   kps = std::vector<cv::KeyPoint>(n);
   static_assert(sizeof(cv::KeyPoint) == sizeof(orbgpu_keypoint), "cv::KeyPoint layout");
   std::memcpy(kps.data(), kp_buf_.data(), sizeof(orbgpu_keypoint) * n);
@@ -82,8 +74,51 @@ int OrbExtractor::operator()(cv::InputArray img, cv::InputArray /*msk*/,
     img_pyramid_[l] = tmp(cv::Rect(kEdgeThreshold, kEdgeThreshold, w, h));
   }
 #endif
+}
 
+int OrbExtractor::operator()(cv::InputArray img, cv::InputArray /*msk*/,
+                             std::vector<cv::KeyPoint> &kps, cv::OutputArray descs,
+                             std::vector<int> &lapping_areas) {
+  if (img.empty()) return -1;
+  cv::Mat im = img.getMat();
+  const int cap = reserve_call(im);
+  int n = 0, mono = 0;
+  const int lap[2] = {lapping_areas.size() > 0 ? lapping_areas[0] : 0,
+                      lapping_areas.size() > 1 ? lapping_areas[1] : 0};
+  const orbgpu_status st =
+      orbgpu_extract(gpu_, im.data, im.cols, im.rows, (int)im.step, lap, kp_buf_.data(),
+                     desc_buf_.data, cap, &n, &mono);
+  if (st != ORBGPU_OK) throw std::runtime_error("orbgpu_extract failed");
+  finish_call(n, kps, descs);
   return mono;
+}
+
+std::pair<int, int> OrbExtractor::ExtractStereo(OrbExtractor &left, OrbExtractor &right, cv::InputArray im_left,
+                                                cv::InputArray im_right, std::vector<cv::KeyPoint> &kps_left,
+                                                cv::OutputArray descs_left, std::vector<cv::KeyPoint> &kps_right,
+                                                cv::OutputArray descs_right, std::vector<int> &lapping_left,
+                                                std::vector<int> &lapping_right) {
+  if (im_left.empty() || im_right.empty() || im_left.size() != im_right.size() ||
+      im_left.getMat().step != im_right.getMat().step)  // one geometry: otherwise one image at a time
+    return {left(im_left, cv::Mat(), kps_left, descs_left, lapping_left),
+            right(im_right, cv::Mat(), kps_right, descs_right, lapping_right)};
+  cv::Mat iml = im_left.getMat(), imr = im_right.getMat();
+  const int cap_l = left.reserve_call(iml), cap_r = right.reserve_call(imr);
+  auto lap_of = [](const std::vector<int> &v, int (&l)[2]) {
+    l[0] = v.size() > 0 ? v[0] : 0;
+    l[1] = v.size() > 1 ? v[1] : 0;
+  };
+  int lap_l[2], lap_r[2];
+  lap_of(lapping_left, lap_l);
+  lap_of(lapping_right, lap_r);
+  int n_l = 0, n_r = 0, mono_l = 0, mono_r = 0;
+  if (orbgpu_extract_stereo(left.gpu_, right.gpu_, iml.data, imr.data, iml.cols, iml.rows, (int)iml.step, lap_l,
+                            lap_r, left.kp_buf_.data(), left.desc_buf_.data, cap_l, &n_l, &mono_l,
+                            right.kp_buf_.data(), right.desc_buf_.data, cap_r, &n_r, &mono_r) != ORBGPU_OK)
+    throw std::runtime_error("orbgpu_extract_stereo failed");
+  left.finish_call(n_l, kps_left, descs_left);
+  right.finish_call(n_r, kps_right, descs_right);
+  return {mono_l, mono_r};
 }
 
 void OrbExtractor::ComputePyramid(cv::Mat img) {

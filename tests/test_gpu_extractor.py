@@ -440,3 +440,29 @@ def test_dataflow_two_handles_on_two_threads(gpu_available):
             th.join()
             _, kr, dr = out["r"]
             assert (kl.tobytes(), dl.tobytes(), kr.tobytes(), dr.tobytes()) == e
+
+
+@pytest.mark.parametrize("single", [0, 1])
+def test_extract_stereo_pair_equals_two_calls(gpu_available, single):
+    """orbgpu_extract_stereo (both images from one host thread) gives each
+    handle's orbgpu_extract results, on both launch paths, frame after frame
+    -- and the pair's pyramids / stereo match read back as after two calls."""
+    from orb_slam_fusion_amd import compute_stereo_matches
+
+    pairs = [synth.stereo_frame(70 + i) for i in range(4)]
+    exl, exr = OrbExtractor(*C2), OrbExtractor(*C2)
+    for e in (exl, exr):
+        e.set_single_launch(single)
+    ref_l, ref_r = OrbExtractor(*C2), OrbExtractor(*C2)
+    for rnd in range(2):
+        for l, r in pairs:
+            (ml, kl, dl), (mr, kr, dr) = exl.extract_stereo(exr, l, r)
+            el, er = ref_l(l), ref_r(r)
+            assert (ml, kl.tobytes(), dl.tobytes()) == (el[0], el[1].tobytes(), el[2].tobytes())
+            assert (mr, kr.tobytes(), dr.tobytes()) == (er[0], er[1].tobytes(), er[2].tobytes())
+            bf, mb = np.float32(435.2 * 0.11), np.float32(np.float32(435.2 * 0.11) / np.float32(435.2))
+            u1, d1 = compute_stereo_matches(exl, exr, len(kl), bf, mb)
+            u2, d2 = compute_stereo_matches(ref_l, ref_r, len(el[1]), bf, mb)
+            assert u1.tobytes() == u2.tobytes() and d1.tobytes() == d2.tobytes()
+    (ml, kl, _), _ = exl.extract_stereo(exr, pairs[0][0], pairs[0][1], (100, 400), (0, 0))
+    assert kl.tobytes() == ref_l(pairs[0][0], None, (100, 400))[1].tobytes()

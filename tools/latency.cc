@@ -15,7 +15,7 @@
 // frames, and per frame the keypoint counts and inliers (the Python leg checks
 // them against its own).
 //
-//   build/latency [FRAMES] [WARMUP] [mono]
+//   build/latency [FRAMES] [WARMUP] [stereo | pair | mono | mono_thread]
 // (mono: the left image only, on the calling thread -- the extraction's own
 // latency without the second thread)
 #include <algorithm>
@@ -72,6 +72,10 @@ int main(int argc, char** argv) {
   // mono: the left image on the calling thread; mono_thread: on a std::thread
   // started per frame (the thread's own cost, as frame.cc:179-182 pays it)
   const bool mono = mode == "mono" || mode == "mono_thread", mono_thread = mode == "mono_thread";
+  // pair: both images by orbgpu_extract_stereo from this thread (the Frame
+  // drop-in, shim/frame_stereo_gpu.cc); stereo: a std::thread for the right
+  // image per frame, as the reference's Frame constructor starts them
+  const bool pair = mode == "pair";
   if (frames <= 0 || warmup < 0) return 2;
 
   struct In {
@@ -119,6 +123,9 @@ int main(int argc, char** argv) {
       th.join();
     } else if (mono) {
       sl = orbgpu_extract(exl, f.left.data(), kW, kH, kW, lap, kl.data(), dl.data(), cap, &nl, &ml);
+    } else if (pair) {
+      sl = orbgpu_extract_stereo(exl, exr, f.left.data(), f.right.data(), kW, kH, kW, lap, lap, kl.data(), dl.data(),
+                                 cap, &nl, &ml, kr.data(), dr.data(), cap, &nr, &mr);
     } else {
       std::thread th([&] {
         sr = orbgpu_extract(exr, f.right.data(), kW, kH, kW, lap, kr.data(), dr.data(), cap, &nr, &mr);
@@ -156,12 +163,12 @@ int main(int argc, char** argv) {
            mode.c_str(), frames, quantile(t_ex, 0.5), quantile(t_ex, 0.9));
     return 0;
   }
-  printf("{\"host\": \"C++ through the C ABI (tools/latency.cc)\", \"frames\": %d, "
+  printf("{\"host\": \"C++ through the C ABI (tools/latency.cc)\", \"mode\": \"%s\", \"frames\": %d, "
          "\"gpu_ms_per_frame\": %.3f, \"gpu_ms_per_frame_p90\": %.3f, "
          "\"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f, "
          "\"gpu_pose_ms\": %.3f, \"gpu_pose_ms_p90\": %.3f, "
          "\"gpu_stereo_ms\": %.3f, \"n_left\": %s, \"n_right\": %s, \"inliers\": %s}\n",
-         frames, quantile(t_tot, 0.5), quantile(t_tot, 0.9), quantile(t_ex, 0.5), quantile(t_ex, 0.9),
+         mode.c_str(), frames, quantile(t_tot, 0.5), quantile(t_tot, 0.9), quantile(t_ex, 0.5), quantile(t_ex, 0.9),
          quantile(t_po, 0.5), quantile(t_po, 0.9), quantile(t_st, 0.5), list(n_left).c_str(),
          list(n_right).c_str(), list(inliers).c_str());
   orbgpu_pose_ctx_destroy(pc);
