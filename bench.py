@@ -494,7 +494,7 @@ def main() -> int:
         sys.path.insert(0, str(REPO / "tools"))
         from bench_latency import measure as measure_latency  # noqa: E402
 
-        result["latency"] = measure_latency(frames=40, cpu_frames=0 if args.no_cpu_baseline else 8)
+        result["latency"] = measure_latency(frames=100, cpu_frames=0 if args.no_cpu_baseline else 8)
     if rank == 0 and world == 1 and not args.no_latency_inertial:
         # the same target in the mode EuRoC MH01 runs (stereo-inertial after IMU
         # initialisation): extract + stereo + SearchLocalPoints +

@@ -223,8 +223,8 @@ orbgpu_status run_host(HostCall& c, int n, int32_t* match, int* nmatches,
                        orbgpu_track_view* views_out, int n_pts) {
   orbgpu_matcher* m = c.m;
   hipStream_t s = m->stream;
-  if (hipMemsetAsync(c.d_call_err, 0, sizeof(int), s) ||
-      hipMemcpyAsync(m->in.d, m->in.h, c.bi.off, hipMemcpyHostToDevice, s) ||
+  c.L.zero_err = 1;  // k_mt_grid writes the call's error word first (no memset)
+  if (hipMemcpyAsync(m->in.d, m->in.h, c.bi.off, hipMemcpyHostToDevice, s) ||
       orbgpu::launch_match(c.L, s) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
   // outputs: the error word, match, nmatches (+ views) are contiguous at the

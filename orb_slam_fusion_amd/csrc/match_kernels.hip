@@ -358,78 +358,97 @@ __device__ __forceinline__ Query make_query(const MatchLaunch& a, int f, int q, 
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_mt_grid(MatchLaunch a) {
+// 1024 threads: a thread's keypoints' cells are computed once and kept in
+// registers (n <= kMatchMaxKeypoints = 8 x 1024), the cell counts scanned by
+// wave prefix sums (3 cells a thread) and one pass over the 16 wave totals.
+constexpr int kGridThreads = 1024;
+constexpr int kGridPerThread = kMatchMaxKeypoints / kGridThreads;
+static_assert(kGridCells % kGridThreads == 0, "cells per thread");
+__global__ __launch_bounds__(kGridThreads) void k_mt_grid(MatchLaunch a) {
   __shared__ int cnt[kGridCells];
   __shared__ int start[kGridCells];
   __shared__ uint16_t lidx[kMatchMaxKeypoints];
-  __shared__ int part[256];
-  const int f = blockIdx.x, t = threadIdx.x;
+  __shared__ int wtot[kGridThreads / 64];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = a.n[f];
-  if (t == 0 && a.npts[f] > a.pt_stride) atomicOr(a.err, 4);  // searched up to pt_stride only
-  if (n > kMatchMaxKeypoints || n > a.kp_stride) {
-    if (t == 0) atomicOr(a.err, 1);
-    return;
+  if (t == 0) {
+    const int e = (a.npts[f] > a.pt_stride ? 4 : 0) |  // searched up to pt_stride only
+                  (n > kMatchMaxKeypoints || n > a.kp_stride ? 1 : 0);
+    if (a.zero_err)
+      *a.err = e;  // single-frame call: this call's own word, no memset before it
+    else if (e)
+      atomicOr(a.err, e);
   }
+  if (n > kMatchMaxKeypoints || n > a.kp_stride) return;
   const float* kps = a.kps + (size_t)f * a.kp_stride * kKpFloats;
-  for (int c = t; c < kGridCells; c += 256) cnt[c] = 0;
-  __syncthreads();
-  // Frame::PosInGrid (frame.cc:748-759)
-  auto cell_of = [&](int i) -> int {
-    const float* k = kps + (size_t)i * kKpFloats;
-    const int px = (int)roundf((k[0] - a.p.min_x) * a.p.inv_w);
-    const int py = (int)roundf((k[1] - a.p.min_y) * a.p.inv_h);
-    if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) return -1;
-    return px * kGridRows + py;
-  };
-  for (int i = t; i < n; i += 256) {
-    const int c = cell_of(i);
-    if (c >= 0) atomicAdd(&cnt[c], 1);
-  }
-  __syncthreads();
-  constexpr int kPer = kGridCells / 256;  // 12 cells per thread
-  int sum = 0;
+  for (int c = t; c < kGridCells; c += kGridThreads) cnt[c] = 0;
+  // Frame::PosInGrid (frame.cc:748-759), keypoints t + 1024 j
+  int cell[kGridPerThread];
 #pragma unroll
-  for (int j = 0; j < kPer; ++j) sum += cnt[t * kPer + j];
-  part[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {  // inclusive scan of the partials
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  for (int j = 0; j < kGridPerThread; ++j) {
+    const int i = t + kGridThreads * j;
+    cell[j] = -1;
+    if (i < n) {
+      const float* k = kps + (size_t)i * kKpFloats;
+      const int px = (int)roundf((k[0] - a.p.min_x) * a.p.inv_w);
+      const int py = (int)roundf((k[1] - a.p.min_y) * a.p.inv_h);
+      if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) cell[j] = px * kGridRows + py;
+    }
   }
-  int run = part[t] - sum;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kGridPerThread; ++j)
+    if (cell[j] >= 0) atomicAdd(&cnt[cell[j]], 1);
+  __syncthreads();
+  constexpr int kPer = kGridCells / kGridThreads;  // 3 cells per thread
+  int v[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) v[j] = cnt[t * kPer + j], sum += v[j];
+  int incl = sum;  // inclusive wave scan
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
+  }
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  int run = incl - sum, total = 0;
+#pragma unroll
+  for (int q = 0; q < kGridThreads / 64; ++q) {
+    const int x = wtot[q];
+    run += q < w ? x : 0;
+    total += x;
+  }
   int* cs = a.cell_start + (size_t)f * (kGridCells + 1);
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int c = t * kPer + j;
-    const int v = cnt[c];
     start[c] = run;
     cs[c] = run;
     cnt[c] = run;  // cursor
-    run += v;
+    run += v[j];
   }
-  if (t == 255) cs[kGridCells] = part[255];
+  if (t == 0) cs[kGridCells] = total;
   __syncthreads();
-  for (int i = t; i < n; i += 256) {
-    const int c = cell_of(i);
-    if (c >= 0) lidx[atomicAdd(&cnt[c], 1)] = (uint16_t)i;
-  }
+#pragma unroll
+  for (int j = 0; j < kGridPerThread; ++j)
+    if (cell[j] >= 0) lidx[atomicAdd(&cnt[cell[j]], 1)] = (uint16_t)(t + kGridThreads * j);
   __syncthreads();
   // ascending keypoint index inside each cell (push_back order, frame.cc:452-464)
-  for (int c = t; c < kGridCells; c += 256) {
-    const int s = start[c], e = cnt[c];
-    for (int i = s + 1; i < e; ++i) {
-      const uint16_t v = lidx[i];
-      int j = i - 1;
-      while (j >= s && lidx[j] > v) lidx[j + 1] = lidx[j], --j;
-      lidx[j + 1] = v;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int c = t * kPer + j;
+    const int s0 = start[c], e = cnt[c];
+    for (int i = s0 + 1; i < e; ++i) {
+      const uint16_t x = lidx[i];
+      int q = i - 1;
+      while (q >= s0 && lidx[q] > x) lidx[q + 1] = lidx[q], --q;
+      lidx[q + 1] = x;
     }
   }
   __syncthreads();
-  const int total = part[255];
   uint16_t* out = a.cell_idx + (size_t)f * a.kp_stride;
-  for (int i = t; i < total; i += 256) out[i] = lidx[i];
+  for (int i = t; i < total; i += kGridThreads) out[i] = lidx[i];
 }
 
 __global__ __launch_bounds__(256) void k_mt_search(MatchLaunch a) {
@@ -454,20 +473,6 @@ __device__ __forceinline__ int accept_dist(const MatchLaunch& a) {
   return a.mode == kModeKeyFrame ? a.p.orb_dist : kThHigh;
 }
 
-// accept decision of one query from its (best, second)
-__device__ __forceinline__ bool accept_of(const MatchLaunch& a, const float* kps, uint32_t best,
-                                          uint32_t second) {
-  if (best == kNone) return false;
-  const int d1 = (int)(best >> 16);
-  if (d1 > accept_dist(a)) return false;
-  if (a.mode == kModeLast || a.mode == kModeKeyFrame) return true;
-  // orb_matcher.cc:117-121: reject iff same level and d1 > ratio * d2
-  const int l1 = kp_octave(kps + (size_t)(best & 0xFFFF) * kKpFloats);
-  const int l2 = second == kNone ? -1 : kp_octave(kps + (size_t)(second & 0xFFFF) * kKpFloats);
-  const int d2 = second == kNone ? 256 : (int)(second >> 16);
-  return !(l1 == l2 && (float)d1 > a.p.nn_ratio * (float)d2);
-}
-
 // does a match by query q hide its keypoint from later queries?  (the key
 // frame search skips every keypoint holding a point, orb_matcher.cc:1791)
 __device__ __forceinline__ bool has_obs(const MatchLaunch& a, int f, int q) {
@@ -489,8 +494,14 @@ __device__ __forceinline__ int rot_bin(const MatchLaunch& a, const float* kps, i
   return bin;
 }
 
+// One wave per frame.  The call's mvpMapPoints row and the keypoint octaves
+// live in LDS (the rounds below touch no global memory on the local-map and
+// last-frame paths but the output stores), and the next 64 queries' top-K
+// lists are loaded while the current ones resolve.
 __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   __shared__ uint32_t owner[kMatchMaxKeypoints];  // in-round first claiming lane, 64 = none
+  __shared__ int32_t lmatch[kMatchMaxKeypoints];
+  __shared__ uint8_t loct[kMatchMaxKeypoints];
   __shared__ uint32_t claims[kMatchMaxKeypoints / 32];
   __shared__ uint32_t removed[kMatchMaxKeypoints / 32];
   __shared__ int hist[kHistoLength];
@@ -501,9 +512,9 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   const bool rot_check = (a.mode == kModeLast || a.mode == kModeKeyFrame) && a.p.check_ori;
   const bool local = a.mode == kModeLocal || a.mode == kModeLocalFrustum;
   // mvpMapPoints of this call: the last matching query (later matches
-  // overwrite, orb_matcher.cc:122, 1611), kept with atomicMax in the output
-  int32_t* match = a.match + (size_t)f * a.kp_stride;
-  for (int i = lane; i < n; i += 64) match[i] = -1, owner[i] = 64;
+  // overwrite, orb_matcher.cc:122, 1611), kept with atomicMax
+  for (int i = lane; i < n; i += 64)
+    lmatch[i] = -1, owner[i] = 64, loct[i] = (uint8_t)kp_octave(F.kps + (size_t)i * kKpFloats);
   for (int i = lane; i < kMatchMaxKeypoints / 32; i += 64) claims[i] = 0, removed[i] = 0;
   if (lane < kHistoLength) hist[lane] = 0;
   __syncthreads();
@@ -514,15 +525,38 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     const int idx = key & 0xFFFF;
     return (claims[idx >> 5] >> (idx & 31)) & 1u;
   };
+  // (best, second) acceptance with the octaves from LDS (accept_of)
+  auto accept = [&](uint32_t best, uint32_t second) -> bool {
+    if (best == kNone) return false;
+    const int d1 = (int)(best >> 16);
+    if (d1 > accept_dist(a)) return false;
+    if (a.mode == kModeLast || a.mode == kModeKeyFrame) return true;
+    const int l1 = loct[best & 0xFFFF];
+    const int l2 = second == kNone ? -1 : loct[second & 0xFFFF];
+    const int d2 = second == kNone ? 256 : (int)(second >> 16);
+    return !(l1 == l2 && (float)d1 > a.p.nn_ratio * (float)d2);
+  };
+  uint32_t ntop[kMatchTopK];  // the next chunk's lists, in flight
+  int ncount = 0;
+  bool nobs = false;
+  auto fetch = [&](int base) {
+    const int q = base + lane;
+    const bool valid = q < nq;
+#pragma unroll
+    for (int i = 0; i < kMatchTopK; ++i) ntop[i] = valid ? res[(size_t)kMatchResWords * q + i] : kNone;
+    ncount = valid ? (int)res[(size_t)kMatchResWords * q + kMatchTopK] : 0;
+    nobs = valid && has_obs(a, f, q);
+  };
+  fetch(0);
   for (int base = 0; base < nq; base += 64) {
     const int q = base + lane;
     const bool valid = q < nq;
     uint32_t top[kMatchTopK];
-    int count = 0;
 #pragma unroll
-    for (int i = 0; i < kMatchTopK; ++i) top[i] = valid ? res[(size_t)kMatchResWords * q + i] : kNone;
-    if (valid) count = (int)res[(size_t)kMatchResWords * q + kMatchTopK];
-    const bool obs = valid && has_obs(a, f, q);
+    for (int i = 0; i < kMatchTopK; ++i) top[i] = ntop[i];
+    int count = ncount;
+    const bool obs = nobs;
+    if (base + 64 < nq) fetch(base + 64);
     bool done = !valid;
     // Rounds: every pending query takes its best / second unclaimed entries;
     // the queries before the first one that an earlier pending claimer hits
@@ -542,7 +576,7 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
       const bool hopeless = b != kNone && (int)(b >> 16) > accept_dist(a);
       const int need = local ? 2 : 1;
       const bool exhausted = !done && !hopeless && found < need && count > kMatchTopK;
-      const bool ok = !done && !exhausted && accept_of(a, F.kps, b, s2);
+      const bool ok = !done && !exhausted && accept(b, s2);
       const bool claimer = ok && obs;
       if (claimer) atomicMin(&owner[b & 0xFFFF], (uint32_t)lane);
       __syncthreads();
@@ -559,7 +593,7 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
       if (commit) {
         if (ok) {
           const int idx = b & 0xFFFF;
-          atomicMax(&match[idx], q);
+          atomicMax(&lmatch[idx], q);
           if (claimer) atomicOr(&claims[idx >> 5], 1u << (idx & 31));
           int bin = 0;
           if (rot_check) {
@@ -625,8 +659,11 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     nmatch -= dropped;
     __syncthreads();
     for (int i = lane; i < n; i += 64)
-      if ((removed[i >> 5] >> (i & 31)) & 1u) atomicExch(&match[i], -2);
+      if ((removed[i >> 5] >> (i & 31)) & 1u) lmatch[i] = -2;
+    __syncthreads();
   }
+  int32_t* match = a.match + (size_t)f * a.kp_stride;
+  for (int i = lane; i < n; i += 64) match[i] = lmatch[i];
   if (lane == 0) a.nmatches[f] = nmatch;
 }
 
@@ -911,7 +948,7 @@ hipError_t launch_bow_search(const BowSearchLaunch& a, hipStream_t st) {
 
 hipError_t launch_match(const MatchLaunch& a, hipStream_t st) {
   if (a.n_frames <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_mt_grid, dim3(a.n_frames), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_mt_grid, dim3(a.n_frames), dim3(kGridThreads), 0, st, a);
   if (a.max_pts > 0) {
     hipLaunchKernelGGL(k_mt_search, dim3((unsigned)((a.max_pts + 3) / 4), a.n_frames), dim3(256),
                        0, st, a);

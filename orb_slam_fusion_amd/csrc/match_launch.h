@@ -75,6 +75,7 @@ struct MatchLaunch {
   int32_t* match;       // [n_frames][kp_stride]
   int* nmatches;        // [n_frames]
   int* err;
+  int zero_err;         // k_mt_grid stores err (a one-frame call's own word) instead of OR-ing into it
 };
 
 hipError_t launch_match(const MatchLaunch& a, hipStream_t st);

@@ -125,6 +125,16 @@ class OrbExtractor:
     def max_keypoints(self, width: int, height: int) -> int:
         return int(lib().orbgpu_extractor_max_keypoints(self._h, width, height))
 
+    def _out_buffers(self, w: int, h: int):
+        """(cap, keypoints, descriptors) staging arrays for a w x h image, kept
+        between calls (every result is returned as a copy of its first n rows)."""
+        key = (w, h)
+        if getattr(self, "_out_key", None) != key:
+            cap = max(self.max_keypoints(w, h), 1)
+            self._out = (cap, np.zeros(cap, KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8))
+            self._out_key = key
+        return self._out
+
     # -- operator() (orb_extractor.cc:1011-1091)
     def __call__(
         self,
@@ -138,9 +148,7 @@ class OrbExtractor:
             raise AssertionError("OrbExtractor expects a CV_8UC1 image")
         img = np.ascontiguousarray(img)
         h, w = img.shape
-        cap = max(self.max_keypoints(w, h), 1)
-        kps = np.zeros(cap, KEYPOINT_DTYPE)
-        descs = np.zeros((cap, 32), np.uint8)
+        cap, kps, descs = self._out_buffers(w, h)
         n = ctypes.c_int()
         mono = ctypes.c_int()
         lap = (ctypes.c_int * 2)(int(lapping_areas[0]), int(lapping_areas[1]))
@@ -166,9 +174,8 @@ class OrbExtractor:
             img = np.ascontiguousarray(img)
             if img.dtype != np.uint8 or img.ndim != 2:
                 raise AssertionError("OrbExtractor expects a CV_8UC1 image")
-            cap = max(ex.max_keypoints(img.shape[1], img.shape[0]), 1)
-            o = (np.zeros(cap, KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8), ctypes.c_int(), ctypes.c_int(),
-                 (ctypes.c_int * 2)(int(lp[0]), int(lp[1])), img, cap)
+            cap, kb, db = ex._out_buffers(img.shape[1], img.shape[0])
+            o = (kb, db, ctypes.c_int(), ctypes.c_int(), (ctypes.c_int * 2)(int(lp[0]), int(lp[1])), img, cap)
             outs.append(o)
         (kl, dl, nl, ml, ll, il, cl), (kr, dr, nr, mr, lr, ir, cr) = outs
         if il.shape != ir.shape:

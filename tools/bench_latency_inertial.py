@@ -2,8 +2,9 @@
 initialisation (the mode EuRoC MH01 runs, tests/slam_euroc_si.cc): one frame
 at a time through the host-buffer ABI, as the reference calls it --
 
-  Frame(): the left / right OrbExtractor::operator() on two threads
-           (frame.cc:179-182) + ComputeStereoMatches (:189);
+  Frame(): the left / right extraction of frame.cc:179-182 from the tracking
+           thread, both launches in flight (orbgpu_extract_stereo, the
+           ORBGPU_STEREO Frame shim) + ComputeStereoMatches (:189);
   TrackWithMotionModel: PredictStateIMU only, no search (tracking.cc:2170-2176);
   TrackLocalMap: SearchLocalPoints = isInFrustum + SearchByProjection(F,
            vpMapPoints, th 6, nn 0.8) (:2626-2690), then
@@ -37,6 +38,7 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tools"))
 
 PARAMS = (1000, 1.2, 8, 20, 7)
+CPP_REPS = 4  # passes over the frames in the C++ leg (a p90 over 4 x frames samples)
 TH_LOCAL = 6.0  # SearchLocalPoints after IMU init, before InertialBA2 (tracking.cc:2669-2673)
 NN_LOCAL = 0.8
 
@@ -118,10 +120,14 @@ def _cpp_leg(c, maps, imus, inv_sigma2, n_obs, good, warmup):
     exe = REPO / "build" / "latency_inertial"
     if not exe.exists():
         raise RuntimeError(f"{exe} missing: run make")
+    import os
+
     with tempfile.TemporaryDirectory() as tmp:
-        path = Path(tmp) / "latin.bin"
+        # ORBGPU_LATIN_DUMP=path keeps the inputs (e.g. to profile build/latency_inertial alone)
+        path = Path(os.environ.get("ORBGPU_LATIN_DUMP") or Path(tmp) / "latin.bin")
         _dump(path, c, maps, imus, inv_sigma2, n_obs, good)
-        r = subprocess.run([str(exe), str(path), str(warmup)], capture_output=True, text=True,
+        r = subprocess.run([str(exe), str(path), str(warmup), "stereo", str(CPP_REPS)], capture_output=True,
+                           text=True,
                            timeout=120)
     if r.returncode != 0:
         raise RuntimeError(f"latency_inertial exited {r.returncode}: {r.stderr.strip()[-400:]} "
@@ -150,11 +156,7 @@ def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4, cpp_host: bo
     def one(f):
         _, _, cl, cr = c.quads[f]
         t0 = time.perf_counter()
-        out = {}
-        th = threading.Thread(target=lambda: out.__setitem__("r", exr(cr)))
-        th.start()
-        _, kl, dl = exl(cl)
-        th.join()
+        (_, kl, dl), _ = exl.extract_stereo(exr, cl, cr)
         t1 = time.perf_counter()
         ur, _ = compute_stereo_matches(exl, exr, len(kl), c.bf, c.mb)
         t2 = time.perf_counter()
@@ -191,9 +193,10 @@ def measure(frames: int = 16, warmup: int = 3, cpu_frames: int = 4, cpp_host: bo
     }
     out = {
         "workload": "stereo-inertial tracking after IMU init, one 752x480 frame at a time through "
-                    "the host ABI: 2-thread extraction (1000 kp, 8 levels) + ComputeStereoMatches + "
-                    "SearchLocalPoints (isInFrustum + SearchByProjection th 6, nn 0.8) + "
-                    f"PoseInertialOptimizationLastFrame; median of {frames} frames",
+                    "the host ABI: one-thread stereo extraction (orbgpu_extract_stereo; 1000 kp, "
+                    "8 levels) + ComputeStereoMatches + SearchLocalPoints (isInFrustum + "
+                    "SearchByProjection th 6, nn 0.8) + PoseInertialOptimizationLastFrame; median "
+                    f"(and, C++ leg, p90 over {CPP_REPS} passes) of {frames} frames",
         "observations_per_frame": round(float(np.mean(n_obs)), 1),
         "inliers_per_frame": round(float(np.mean(good)), 1),
     }

@@ -4,9 +4,11 @@
 // (the same frames, local maps and IMU states its Python leg times), one frame
 // at a time --
 //
-//   Frame():        the left / right OrbExtractor::operator() on two threads,
-//                   a std::thread per frame as frame.cc:179-182 starts them,
-//                   then ComputeStereoMatches (:189) = orbgpu_stereo_match;
+//   Frame():        the left / right extraction of frame.cc:179-182 from this
+//                   thread, both launches in flight (orbgpu_extract_stereo, the
+//                   ORBGPU_STEREO Frame shim; "threads" as 2nd argument: a
+//                   std::thread per frame as the reference starts them), then
+//                   ComputeStereoMatches (:189) = orbgpu_stereo_match;
 //   SearchLocalPoints: isInFrustum + SearchByProjection(F, vpMapPoints, th 6,
 //                   nn 0.8) = orbgpu_search_local_points (tracking.cc:2626-2690);
 //   PoseInertialOptimizationLastFrame over the matches it left: the
@@ -14,10 +16,11 @@
 //                   as the reference's graph build does (optimizer.cc:4806-4880),
 //                   then orbgpu_pose_inertial.
 //
-// Prints one JSON object: medians per part and per frame, and whether every
-// frame's observation count and n_good equal the Python leg's (same work).
+// Prints one JSON object: medians (and p90s) per part and per frame, and
+// whether every frame's observation count and n_good equal the Python leg's
+// (same work).
 //
-//   build/latency_inertial DUMP [WARMUP]
+//   build/latency_inertial DUMP [WARMUP] [stereo|threads] [REPS]  (REPS passes over the frames)
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -113,6 +116,11 @@ double median(std::vector<double> v) {
   const size_t n = v.size();
   return n == 0 ? 0.0 : (n % 2 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]));
 }
+double p90(std::vector<double> v) {  // nearest rank
+  if (v.empty()) return 0.0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, (size_t)(0.9 * (double)v.size()))];
+}
 
 }  // namespace
 
@@ -122,6 +130,8 @@ int main(int argc, char** argv) {
     return 2;
   }
   const int warmup = argc > 2 ? atoi(argv[2]) : 3;
+  const bool two_threads = argc > 3 && strcmp(argv[3], "threads") == 0;
+  const int reps = argc > 4 ? std::max(1, atoi(argv[4])) : 1;
   Dump d;
   if (!load(argv[1], d)) return 1;
 
@@ -148,19 +158,24 @@ int main(int argc, char** argv) {
 
   std::vector<double> t_ex, t_st, t_sl, t_pi, t_tot;
   bool same = true;
-  for (int i = 0; i < warmup + d.frames; ++i) {
+  for (int i = 0; i < warmup + d.frames * reps; ++i) {
     const Frame& f = d.f[i % d.frames];
     const auto t0 = Clock::now();
     int nl = 0, nr = 0, ml = 0, mr = 0;
-    orbgpu_status sr = ORBGPU_OK;
-    std::thread th([&] {
-      sr = orbgpu_extract(exr, f.right.data(), d.W, d.H, d.W, lap, kr.data(), dr.data(), d.cap, &nr, &mr);
-    });
-    const orbgpu_status sl =
-        orbgpu_extract(exl, f.left.data(), d.W, d.H, d.W, lap, kl.data(), dl.data(), d.cap, &nl, &ml);
-    th.join();
-    CHECK(sl);
-    CHECK(sr);
+    if (two_threads) {
+      orbgpu_status sr = ORBGPU_OK;
+      std::thread th([&] {
+        sr = orbgpu_extract(exr, f.right.data(), d.W, d.H, d.W, lap, kr.data(), dr.data(), d.cap, &nr, &mr);
+      });
+      const orbgpu_status sl =
+          orbgpu_extract(exl, f.left.data(), d.W, d.H, d.W, lap, kl.data(), dl.data(), d.cap, &nl, &ml);
+      th.join();
+      CHECK(sl);
+      CHECK(sr);
+    } else {
+      CHECK(orbgpu_extract_stereo(exl, exr, f.left.data(), f.right.data(), d.W, d.H, d.W, lap, lap, kl.data(),
+                                  dl.data(), d.cap, &nl, &ml, kr.data(), dr.data(), d.cap, &nr, &mr));
+    }
     const auto t1 = Clock::now();
     CHECK(orbgpu_stereo_match(exl, exr, d.bf, d.mb, ur.data(), depth.data(), d.cap));
     const auto t2 = Clock::now();
@@ -192,11 +207,13 @@ int main(int argc, char** argv) {
       }
     }
   }
-  printf("{\"host\": \"C++ through the C ABI (tools/latency_inertial.cc)\", \"frames\": %d, "
-         "\"gpu_ms_per_frame\": %.3f, \"gpu_extract_ms\": %.3f, \"gpu_stereo_ms\": %.3f, "
-         "\"gpu_search_local_ms\": %.3f, \"gpu_pose_inertial_ms\": %.3f, "
+  printf("{\"host\": \"C++ through the C ABI (tools/latency_inertial.cc)\", \"extraction\": \"%s\", "
+         "\"frames\": %d, \"gpu_ms_per_frame\": %.3f, \"gpu_ms_per_frame_p90\": %.3f, "
+         "\"gpu_extract_ms\": %.3f, \"gpu_extract_ms_p90\": %.3f, \"gpu_stereo_ms\": %.3f, "
+         "\"gpu_search_local_ms\": %.3f, \"gpu_pose_inertial_ms\": %.3f, \"gpu_pose_inertial_ms_p90\": %.3f, "
          "\"same_work_as_python_leg\": %s}\n",
-         d.frames, median(t_tot), median(t_ex), median(t_st), median(t_sl), median(t_pi),
+         two_threads ? "two std::threads (frame.cc:179-182)" : "orbgpu_extract_stereo from one thread", d.frames,
+         median(t_tot), p90(t_tot), median(t_ex), p90(t_ex), median(t_st), median(t_sl), median(t_pi), p90(t_pi),
          same ? "true" : "false");
   orbgpu_inertial_ctx_destroy(ic);
   orbgpu_matcher_destroy(mt);

@@ -1,7 +1,10 @@
 """Per-phase cycle shares of the pose kernel from the ORB_STAMPS build.
 
-    ORBGPU_LIB=orb_slam_fusion_amd/lib/liborbgpu_stamps.so python tools/pose_stamps.py
+    ORBGPU_LIB=orb_slam_fusion_amd/lib/liborbgpu_stamps.so python tools/pose_stamps.py [--batch B]
+
+(--batch 1: the single-problem latency case; s_memtime ticks at 100 MHz)
 """
+import argparse
 import ctypes
 import json
 import sys
@@ -19,7 +22,9 @@ def main():
     from orb_slam_fusion_amd import PoseOptimizer, synth
     from orb_slam_fusion_amd._lib import library_path
 
-    B = 64
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    B = ap.parse_args().batch
     probs = [synth.pose_problem(7 + i, 600, 10) for i in range(B)]
     obs = torch.from_numpy(np.stack([p[3] for p in probs]).view(np.float32).reshape(B, 600, 7).copy()).cuda()
     pin = torch.from_numpy(np.stack([p[1] for p in probs])).cuda()
@@ -41,7 +46,7 @@ def main():
     v = list(buf)
     tot = sum(v[i] for i in range(8))
     names = {0: "control", 1: "build_sweep", 2: "ldlt", 3: "se3_exp", 4: "chi_sweep", 5: "classify"}
-    print(json.dumps({"ticks_per_problem": tot / (B * iters), "builds_per_problem": v[8] / (B * iters),
+    print(json.dumps({"batch": B, "ticks_per_problem": tot / (B * iters), "us_per_problem_at_100MHz": tot / (B * iters) / 100, "builds_per_problem": v[8] / (B * iters),
                       "trials_per_problem": v[9] / (B * iters),
                       "trial_rounds_per_problem": v[10] / (B * iters),
                       "share": {names[i]: round(v[i] / max(tot, 1), 3) for i in names}}))
