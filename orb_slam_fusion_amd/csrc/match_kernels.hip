@@ -37,6 +37,11 @@
 
 namespace orbgpu {
 
+#ifdef ORB_STAMPS
+// profiling build only: k_mt_resolve chunks, rounds, list re-searches, queries
+__device__ unsigned long long g_mt_stats[8];
+#endif
+
 namespace {
 
 constexpr int kThHigh = 100;      // ORBmatcher::TH_HIGH (orb_matcher.cc:35)
@@ -81,6 +86,12 @@ __device__ __forceinline__ float dot3(V3 a, V3 b) {
 }
 
 __device__ __forceinline__ int kp_octave(const float* k) { return __float_as_int(k[5]); }
+
+// A barrier for LDS hand-offs only: each wave waits for its own LDS operations,
+// not for its global loads and stores, which __syncthreads' release fence also
+// drains (a ~1 us store acknowledgement per round in k_mt_resolve, and the
+// prefetch of the next queries).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
@@ -395,11 +406,11 @@ __global__ __launch_bounds__(kGridThreads) void k_mt_grid(MatchLaunch a) {
       if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) cell[j] = px * kGridRows + py;
     }
   }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < kGridPerThread; ++j)
     if (cell[j] >= 0) atomicAdd(&cnt[cell[j]], 1);
-  __syncthreads();
+  lds_barrier();
   constexpr int kPer = kGridCells / kGridThreads;  // 3 cells per thread
   int v[kPer], sum = 0;
 #pragma unroll
@@ -411,7 +422,7 @@ __global__ __launch_bounds__(kGridThreads) void k_mt_grid(MatchLaunch a) {
     if (lane >= off) incl += o;
   }
   if (lane == 63) wtot[w] = incl;
-  __syncthreads();
+  lds_barrier();
   int run = incl - sum, total = 0;
 #pragma unroll
   for (int q = 0; q < kGridThreads / 64; ++q) {
@@ -429,11 +440,11 @@ __global__ __launch_bounds__(kGridThreads) void k_mt_grid(MatchLaunch a) {
     run += v[j];
   }
   if (t == 0) cs[kGridCells] = total;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < kGridPerThread; ++j)
     if (cell[j] >= 0) lidx[atomicAdd(&cnt[cell[j]], 1)] = (uint16_t)(t + kGridThreads * j);
-  __syncthreads();
+  lds_barrier();
   // ascending keypoint index inside each cell (push_back order, frame.cc:452-464)
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(kGridThreads) void k_mt_grid(MatchLaunch a) {
       lidx[q + 1] = x;
     }
   }
-  __syncthreads();
+  lds_barrier();
   uint16_t* out = a.cell_idx + (size_t)f * a.kp_stride;
   for (int i = t; i < total; i += kGridThreads) out[i] = lidx[i];
 }
@@ -517,7 +528,7 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     lmatch[i] = -1, owner[i] = 64, loct[i] = (uint8_t)kp_octave(F.kps + (size_t)i * kKpFloats);
   for (int i = lane; i < kMatchMaxKeypoints / 32; i += 64) claims[i] = 0, removed[i] = 0;
   if (lane < kHistoLength) hist[lane] = 0;
-  __syncthreads();
+  lds_barrier();
   const uint32_t* res = a.res + (size_t)kMatchResWords * f * a.pt_stride;
   int32_t* acc = a.acc + (size_t)f * a.pt_stride;
   int nmatch = 0;
@@ -548,6 +559,9 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     nobs = valid && has_obs(a, f, q);
   };
   fetch(0);
+#ifdef ORB_STAMPS
+  const unsigned long long t_setup = __builtin_amdgcn_s_memtime();
+#endif
   for (int base = 0; base < nq; base += 64) {
     const int q = base + lane;
     const bool valid = q < nq;
@@ -579,13 +593,13 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
       const bool ok = !done && !exhausted && accept(b, s2);
       const bool claimer = ok && obs;
       if (claimer) atomicMin(&owner[b & 0xFFFF], (uint32_t)lane);
-      __syncthreads();
+      lds_barrier();
       bool hit = false;
       if (!done && !exhausted && b != kNone && !hopeless) {
         hit = owner[b & 0xFFFF] < (uint32_t)lane;
         if (local && s2 != kNone) hit = hit || owner[s2 & 0xFFFF] < (uint32_t)lane;
       }
-      __syncthreads();
+      lds_barrier();
       if (claimer) owner[b & 0xFFFF] = 64;
       const uint64_t stop_mask = __ballot(hit || exhausted);
       const int stop = stop_mask ? __builtin_ctzll(stop_mask) : 64;
@@ -607,12 +621,19 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
         done = true;
       }
       nmatch += __popcll(__ballot(commit && ok));
-      __syncthreads();
+      lds_barrier();
+#ifdef ORB_STAMPS
+      if (lane == 0) atomicAdd(&g_mt_stats[1], 1ull);
+#endif
       if (stop == 64) break;
       // the first stopped query: hit by a claim now committed (its next round
       // sees it), or its list ran out -> full search with the claims masked
       const bool ex_stop = (stop_mask >> stop) & 1 && __builtin_amdgcn_readlane((int)exhausted, stop);
       if (ex_stop) {
+#ifdef ORB_STAMPS
+        if (lane == 0) atomicAdd(&g_mt_stats[2], 1ull);
+        const unsigned long long rs0 = __builtin_amdgcn_s_memtime();
+#endif
         const Query Q = make_query(a, f, base + stop, false);
         uint32_t t2[kMatchTopK];
         int c2;
@@ -622,10 +643,13 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
           for (int i = 0; i < kMatchTopK; ++i) top[i] = t2[i];
           count = c2;
         }
+#ifdef ORB_STAMPS
+        if (lane == 0) atomicAdd(&g_mt_stats[5], __builtin_amdgcn_s_memtime() - rs0);
+#endif
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (rot_check) {
     // ComputeThreeMaxima (orb_matcher.cc:1841-1873), every lane
     int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -657,13 +681,20 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     }
     for (int off = 32; off >= 1; off >>= 1) dropped += __shfl_xor(dropped, off, 64);
     nmatch -= dropped;
-    __syncthreads();
+    lds_barrier();
     for (int i = lane; i < n; i += 64)
       if ((removed[i >> 5] >> (i & 31)) & 1u) lmatch[i] = -2;
-    __syncthreads();
+    lds_barrier();
   }
   int32_t* match = a.match + (size_t)f * a.kp_stride;
   for (int i = lane; i < n; i += 64) match[i] = lmatch[i];
+#ifdef ORB_STAMPS
+  if (lane == 0) {
+    atomicAdd(&g_mt_stats[0], (unsigned long long)((nq + 63) / 64));
+    atomicAdd(&g_mt_stats[3], (unsigned long long)nq);
+    atomicAdd(&g_mt_stats[4], __builtin_amdgcn_s_memtime() - t_setup);  // chunks .. end
+  }
+#endif
   if (lane == 0) a.nmatches[f] = nmatch;
 }
 
@@ -958,3 +989,14 @@ hipError_t launch_match(const MatchLaunch& a, hipStream_t st) {
 }
 
 }  // namespace orbgpu
+
+#ifdef ORB_STAMPS
+// profiling build only: the k_mt_resolve counters since the last call (chunks,
+// rounds, re-searches, queries), then cleared
+extern "C" int orbgpu_debug_mt_stats(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(orbgpu::g_mt_stats), 6 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  static const unsigned long long z[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(orbgpu::g_mt_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

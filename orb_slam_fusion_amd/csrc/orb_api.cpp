@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -417,7 +418,12 @@ static hipError_t run_single_chain(orbgpu_extractor* h, const ExtractLaunch& a) 
 // memory next to the item list and is rewritten only when it changes (a new
 // plan or buffer, another lapping band).  The outputs reach the host through
 // the launch's own mirror writes into the mapped h_sout: no copy commands.
-static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const int lap[2], int seq) {
+// The launch record of a dataflow call, uploaded when it changes -- in the
+// call's prepare phase, before any launch: its synchronous copy must not be
+// issued while another dataflow launch of this thread waits for its image (a
+// copy queued behind that launch on a shared hardware queue would wait for
+// the staging this thread has not done yet).
+static orbgpu_status prepare_single_df(orbgpu_extractor* h, size_t img_bytes, const int lap[2]) {
   const PlanHeader& P = h->plan.hdr;
   DfLaunch a;
   std::memset(&a, 0, sizeof a);
@@ -478,9 +484,7 @@ static orbgpu_status run_single_df(orbgpu_extractor* h, size_t img_bytes, const 
     h->df_launch = a;
     h->df_valid = true;
   }
-  return launch_extract_df(h->df_launch, h->d_df_rec, h->h_band_dev, seq, h->stream) == hipSuccess
-             ? ORBGPU_OK
-             : ORBGPU_ERR_DEVICE;
+  return ORBGPU_OK;
 }
 
 // One host-buffer extraction (orbgpu_extract, and each image of
@@ -543,7 +547,7 @@ struct SingleCall {
     lap[0] = lapping ? lapping[0] : 0;
     lap[1] = lapping ? lapping[1] : 0;
     df = h->single_mode == ORBGPU_SINGLE_DATAFLOW && !P.oct_hbm_nodes;
-    return ORBGPU_OK;
+    return df ? prepare_single_df(h, bytes, lap) : ORBGPU_OK;
   }
 
   // the image into pinned staging (rows at the level-0 pitch); band_done(b)
@@ -567,7 +571,9 @@ struct SingleCall {
   orbgpu_status launch() {
     if (df) {
       seq = h->df_seq = h->df_seq == 0x7fffffff ? 1 : h->df_seq + 1;
-      return run_single_df(h, bytes, lap, seq);
+      return launch_extract_df(h->df_launch, h->d_df_rec, h->h_band_dev, seq, h->stream) == hipSuccess
+                 ? ORBGPU_OK
+                 : ORBGPU_ERR_DEVICE;
     }
     stage([](size_t) {});
     const PlanHeader& P = h->plan.hdr;
@@ -620,6 +626,7 @@ struct SingleCall {
     h->last_w = width;
     h->last_h = height;
     if (err) {
+      if (std::getenv("ORBGPU_DEBUG")) fprintf(stderr, "orbgpu_extract: device error word 0x%x (df %d)\n", err, (int)df);
       (void)hipMemset(h->d_nm + 2, 0, sizeof(int));
       return ORBGPU_ERR_CAPACITY;
     }
@@ -842,12 +849,19 @@ orbgpu_status orbgpu_extract_stereo(orbgpu_extractor* left, orbgpu_extractor* ri
                       n_right, mono_right}};
   orbgpu_status st[2];
   for (int k = 0; k < 2; ++k) st[k] = c[k].prepare();
-  // both launches first (each handle's own stream), then both images
-  // (each launch's copy items wait for their bands), then the results
-  for (int k = 0; k < 2; ++k)
-    if (st[k] == ORBGPU_OK) st[k] = c[k].launch();
-  for (int k = 0; k < 2; ++k)
-    if (st[k] == ORBGPU_OK) c[k].stage_df();
+  // both dataflow launches first (each handle's own stream), then both images
+  // (each launch's copy items wait for their bands), then the results.  A
+  // graph-path launch may block (capture, instantiation), so with one in the
+  // pair each image is staged right after its own launch.
+  if (c[0].df && c[1].df) {
+    for (int k = 0; k < 2; ++k)
+      if (st[k] == ORBGPU_OK) st[k] = c[k].launch();
+    for (int k = 0; k < 2; ++k)
+      if (st[k] == ORBGPU_OK) c[k].stage_df();
+  } else {
+    for (int k = 0; k < 2; ++k)
+      if (st[k] == ORBGPU_OK && (st[k] = c[k].launch()) == ORBGPU_OK) c[k].stage_df();
+  }
   for (int k = 0; k < 2; ++k)
     if (st[k] == ORBGPU_OK) st[k] = c[k].wait();
   for (int k = 0; k < 2; ++k)
