@@ -15,7 +15,7 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
                                 const orbgpu_imu_preint* d_preint, const orbgpu_imu_prior* d_prior,
                                 const orbgpu_inertial_obs* d_obs, const int* d_nobs, int obs_stride,
                                 int rec_init, orbgpu_inertial_result* d_res, uint8_t* d_outlier,
-                                hipStream_t st);
+                                hipStream_t st, int* done_host = nullptr, const int* seq_src = nullptr);
 }
 
 static_assert(sizeof(orbgpu_imu_state) == 132, "orbgpu_imu_state layout");
@@ -28,16 +28,20 @@ struct orbgpu_inertial_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_problems = 0, max_obs = 0;
-  // single-problem path: the input and the output as one block each, pinned
-  // on the host and mirrored on the device -- in: [cur | prev | preint |
-  // prior | n_obs | obs], out: [result | outlier flags] -- so a call is one
-  // H2D copy, the kernel and one D2H copy, sized by the observation count's
-  // bucket, replayed as a hipGraph per (mode, bucket, rec_init, calibration)
-  // from the second call of that key on
+  // single-problem path: the input as one pinned block mirrored on the device
+  // -- [cur | prev | preint | prior | n_obs | call number | obs] -- and the
+  // output block [result | outlier flags] in host-mapped memory, written by
+  // the kernel itself, which then stores the call number into h_done (the
+  // host polls it): a call is one H2D copy and the kernel, sized by the
+  // observation count's bucket, replayed as a hipGraph per (mode, bucket,
+  // rec_init, calibration) from the second call of that key on
   uint8_t* h_in = nullptr;
   uint8_t* h_out = nullptr;
+  uint8_t* h_out_dev = nullptr;
   uint8_t* d_in = nullptr;
-  uint8_t* d_out = nullptr;
+  int* h_done = nullptr;
+  int* h_done_dev = nullptr;
+  int seq = 0;
   struct Graph {
     int mode = 0, bucket = 0, rec_init = 0;
     orbgpu_imu_calib calib{};
@@ -48,7 +52,7 @@ struct orbgpu_inertial_ctx {
 };
 
 namespace {
-constexpr size_t kOffPrev = 136, kOffPreint = 272, kOffPrior = 1336, kOffN = 3304, kInBytes = 3312;
+constexpr size_t kOffPrev = 136, kOffPreint = 272, kOffPrior = 1336, kOffN = 3304, kOffSeq = 3308, kInBytes = 3312;
 static_assert(kOffPrev >= sizeof(orbgpu_imu_state) && kOffPreint - kOffPrev >= sizeof(orbgpu_imu_state) &&
                   kOffPrior - kOffPreint >= sizeof(orbgpu_imu_preint) &&
                   kOffN - kOffPrior >= sizeof(orbgpu_imu_prior) && kOffPreint % 8 == 0 &&
@@ -76,8 +80,8 @@ hipError_t enqueue_single(orbgpu_inertial_ctx* c, int mode, const orbgpu_imu_cal
         reinterpret_cast<const orbgpu_imu_prior*>(c->d_in + kOffPrior),
         reinterpret_cast<const orbgpu_inertial_obs*>(c->d_in + kInBytes),
         reinterpret_cast<const int*>(c->d_in + kOffN), bucket, rec_init,
-        reinterpret_cast<orbgpu_inertial_result*>(c->d_out), c->d_out + kOutFlags, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out, c->d_out, kOutFlags + bucket, hipMemcpyDeviceToHost, st);
+        reinterpret_cast<orbgpu_inertial_result*>(c->h_out_dev), c->h_out_dev + kOutFlags, st, c->h_done_dev,
+        reinterpret_cast<const int*>(c->d_in + kOffSeq));
   return e;
 }
 
@@ -103,12 +107,17 @@ orbgpu_status orbgpu_inertial_ctx_create(int device, int max_problems, int max_o
   c->max_obs = max_obs;
   const size_t nb = (size_t)(max_obs + kObsBucket - 1) / kObsBucket * kObsBucket;
   const size_t in_bytes = kInBytes + sizeof(orbgpu_inertial_obs) * nb, out_bytes = kOutFlags + nb;
+  const unsigned hflags = hipHostMallocMapped | hipHostMallocCoherent;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_in, in_bytes) != hipSuccess || hipMalloc(&c->d_out, out_bytes) != hipSuccess ||
-      hipHostMalloc(&c->h_in, in_bytes) != hipSuccess || hipHostMalloc(&c->h_out, out_bytes) != hipSuccess) {
+      hipMalloc(&c->d_in, in_bytes) != hipSuccess || hipHostMalloc(&c->h_in, in_bytes) != hipSuccess ||
+      hipHostMalloc(&c->h_out, out_bytes, hflags) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_out_dev), c->h_out, 0) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_done), 64, hflags) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_done_dev), c->h_done, 0) != hipSuccess) {
     orbgpu_inertial_ctx_destroy(c);
     return ORBGPU_ERR_DEVICE;
   }
+  *c->h_done = 0;
   *out = c;
   return ORBGPU_OK;
 }
@@ -119,9 +128,10 @@ void orbgpu_inertial_ctx_destroy(orbgpu_inertial_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& g : c->graphs) destroy_graph(g);
   if (c->d_in) (void)hipFree(c->d_in);
-  if (c->d_out) (void)hipFree(c->d_out);
+
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_done) (void)hipHostFree(c->h_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -147,6 +157,8 @@ orbgpu_status orbgpu_pose_inertial(orbgpu_inertial_ctx* c, int mode, const orbgp
   else
     std::memset(host + kOffPrior, 0, sizeof(orbgpu_imu_prior));
   std::memcpy(host + kOffN, &n_obs, sizeof(int));
+  const int seq = c->seq = c->seq == 0x7fffffff ? 1 : c->seq + 1;
+  std::memcpy(host + kOffSeq, &seq, sizeof(int));
   if (n_obs > 0) std::memcpy(host + kInBytes, obs, sizeof(*obs) * n_obs);
   const int bucket = std::min(c->max_obs, std::max(1, (n_obs + kObsBucket - 1) / kObsBucket) * kObsBucket);
   const int ri = rec_init ? 1 : 0;
@@ -185,7 +197,24 @@ orbgpu_status orbgpu_pose_inertial(orbgpu_inertial_ctx* c, int mode, const orbgp
     ng.calib = *calib;
     c->graphs.push_back(ng);
   }
-  if (e != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  if (e != hipSuccess) return ORBGPU_ERR_DEVICE;
+  // poll the completion word (the stream's own synchronisation decides past
+  // ~0.5 s or on a stream error)
+  volatile int* done = c->h_done;
+  bool seen = false;
+  for (long spin = 0; spin < (1L << 24); ++spin) {
+    if (*done == seq) {
+      seen = true;
+      break;
+    }
+    if ((spin & 4095) == 4095 && hipStreamQuery(c->stream) != hipErrorNotReady) {
+      seen = *done == seq;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  if (!seen && (hipStreamSynchronize(c->stream) != hipSuccess || *done != seq)) return ORBGPU_ERR_DEVICE;
   std::memcpy(res, c->h_out, sizeof(*res));
   if (n_obs > 0) std::memcpy(outlier, c->h_out + kOutFlags, n_obs);
   return ORBGPU_OK;

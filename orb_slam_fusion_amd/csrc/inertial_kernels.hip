@@ -754,7 +754,8 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     CalibD cal, const orbgpu_imu_state* __restrict__ g_cur, const orbgpu_imu_state* __restrict__ g_prev,
     const orbgpu_imu_preint* __restrict__ g_preint, const orbgpu_imu_prior* __restrict__ g_prior,
     const VisObs* __restrict__ g_obs, const int* __restrict__ g_nobs, int obs_stride, int rec_init,
-    orbgpu_inertial_result* __restrict__ g_res, uint8_t* __restrict__ g_out, int lds_obs) {
+    orbgpu_inertial_result* __restrict__ g_res, uint8_t* __restrict__ g_out, int lds_obs,
+    int* __restrict__ done_host, const int* __restrict__ seq_src) {
   constexpr int n = MODE == ORBGPU_INERTIAL_LAST_FRAME ? 30 : 15;
   __shared__ InShared sh;
   extern __shared__ __attribute__((aligned(16))) uint8_t in_lds[];
@@ -1175,6 +1176,16 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     res->n_good = nobs - nBad;
     res->n_inliers = nInl;
   }
+  if (done_host) {
+    // single-problem host call (outputs in host-mapped memory): the call's
+    // number, from its input block, stored at system scope after every
+    // output word of the workgroup -- the host polls it
+    __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      __hip_atomic_store(done_host, *seq_src, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   ISTAMP(5);
   ISTAMP_END;
 }
@@ -1184,7 +1195,7 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
                                 const orbgpu_imu_preint* d_preint, const orbgpu_imu_prior* d_prior,
                                 const orbgpu_inertial_obs* d_obs, const int* d_nobs, int obs_stride,
                                 int rec_init, orbgpu_inertial_result* d_res, uint8_t* d_outlier,
-                                hipStream_t st) {
+                                hipStream_t st, int* done_host, const int* seq_src) {
   CalibD cd;
   cd.fx = c.fx;
   cd.fy = c.fy;
@@ -1211,11 +1222,11 @@ hipError_t launch_pose_inertial(int mode, const orbgpu_imu_calib& c, int n_probl
   if (mode == ORBGPU_INERTIAL_LAST_FRAME)
     hipLaunchKernelGGL(k_pose_inertial<ORBGPU_INERTIAL_LAST_FRAME>, dim3(n_problems),
                        dim3(kInThreads), lds, st, cd, d_cur, d_prev, d_preint, d_prior, obs, d_nobs,
-                       obs_stride, rec_init, d_res, d_outlier, lds_obs);
+                       obs_stride, rec_init, d_res, d_outlier, lds_obs, done_host, seq_src);
   else
     hipLaunchKernelGGL(k_pose_inertial<ORBGPU_INERTIAL_LAST_KEYFRAME>, dim3(n_problems),
                        dim3(kInThreads), lds, st, cd, d_cur, d_prev, d_preint, d_prior, obs, d_nobs,
-                       obs_stride, rec_init, d_res, d_outlier, lds_obs);
+                       obs_stride, rec_init, d_res, d_outlier, lds_obs, done_host, seq_src);
   return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ namespace orbgpu {
 hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const void* d_obs,
                            const int* d_nobs, int obs_stride, int n_problems, float* d_pose_out,
                            uint8_t* d_outlier, int* d_inliers, double* d_pose_out_d,
-                           hipStream_t st, int groups);
+                           hipStream_t st, int groups, int* done_host = nullptr, int seq = 0);
 }
 
 static_assert(sizeof(orbgpu_pose) == 7 * sizeof(float), "orbgpu_pose layout");
@@ -45,6 +45,11 @@ struct orbgpu_pose_ctx {
   bool zero_copy = true;
   uint8_t* h_in_dev = nullptr;
   uint8_t* h_out_dev = nullptr;
+  // the zero-copy call's completion word (host-mapped): the kernel stores the
+  // call's number after its outputs; the host polls it
+  int* h_done = nullptr;
+  int* h_done_dev = nullptr;
+  int seq = 0;
   struct Graph {
     int bucket = 0, groups = 0;
     double cam[5] = {};
@@ -110,10 +115,13 @@ orbgpu_status orbgpu_pose_ctx_create(int device, int max_problems, int max_obs,
       hipHostMalloc(&c->h_in, in_bytes, hflags) != hipSuccess ||
       hipHostMalloc(&c->h_out, out_bytes, hflags) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_in_dev), c->h_in, 0) != hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_out_dev), c->h_out, 0) != hipSuccess) {
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_out_dev), c->h_out, 0) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_done), 64, hflags) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_done_dev), c->h_done, 0) != hipSuccess) {
     orbgpu_pose_ctx_destroy(c);
     return ORBGPU_ERR_DEVICE;
   }
+  *c->h_done = 0;
   *out = c;
   return ORBGPU_OK;
 }
@@ -136,6 +144,7 @@ void orbgpu_pose_ctx_destroy(orbgpu_pose_ctx* c) {
   for (auto& g : c->graphs) destroy_graph(g);
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_done) (void)hipHostFree(c->h_done);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -157,12 +166,30 @@ orbgpu_status orbgpu_pose_opt(orbgpu_pose_ctx* c, const orbgpu_camera* cam,
   const int bucket = std::min(c->max_obs, std::max(1, (n_obs + kObsBucket - 1) / kObsBucket) * kObsBucket);
   const int groups = c->groups_single;
   if (c->zero_copy) {
+    const int seq = c->seq = c->seq == 0x7fffffff ? 1 : c->seq + 1;
     const hipError_t ze = orbgpu::launch_pose_opt(
         cd, reinterpret_cast<const float*>(c->h_in_dev + kInPose), c->h_in_dev + kInObs,
         reinterpret_cast<const int*>(c->h_in_dev + kInN), bucket, 1,
         reinterpret_cast<float*>(c->h_out_dev + kOutPose), c->h_out_dev + kOutFlags,
-        reinterpret_cast<int*>(c->h_out_dev + kOutInl), nullptr, c->stream, groups);
-    if (ze != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+        reinterpret_cast<int*>(c->h_out_dev + kOutInl), nullptr, c->stream, groups, c->h_done_dev, seq);
+    if (ze != hipSuccess) return ORBGPU_ERR_DEVICE;
+    // poll the completion word (the stream's own synchronisation decides past
+    // ~0.5 s or on a stream error), as the extractor's single-image path
+    volatile int* done = c->h_done;
+    bool seen = false;
+    for (long spin = 0; spin < (1L << 24); ++spin) {
+      if (*done == seq) {
+        seen = true;
+        break;
+      }
+      if ((spin & 4095) == 4095 && hipStreamQuery(c->stream) != hipErrorNotReady) {
+        seen = *done == seq;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (!seen && (hipStreamSynchronize(c->stream) != hipSuccess || *done != seq)) return ORBGPU_ERR_DEVICE;
     memcpy(Tcw_out, c->h_out + kOutPose, sizeof(orbgpu_pose));
     memcpy(n_inliers, c->h_out + kOutInl, sizeof(int));
     if (n_obs > 0) memcpy(outlier, c->h_out + kOutFlags, n_obs);

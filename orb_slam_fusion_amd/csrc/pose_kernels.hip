@@ -381,7 +381,18 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     CamDev cam, const float* __restrict__ pose_in, const PoseObsDev* __restrict__ obs_all,
     const int* __restrict__ nobs, int obs_stride, float* __restrict__ pose_out,
     uint8_t* __restrict__ outlier_all, int* __restrict__ inliers, double* __restrict__ pose_out_d,
-    int lds_obs) {
+    int lds_obs, int* __restrict__ done_host, int seq) {
+  // done_host (single-problem host call, outputs in host-mapped memory): the
+  // call's number, stored at system scope after every output word of the
+  // workgroup -- the host polls it instead of synchronising the stream
+  auto signal_done = [&]() {
+    if (!done_host) return;
+    __syncthreads();  // every lane's output stores drained (vmcnt 0) before the barrier
+    if (threadIdx.x == 0) {
+      __threadfence_system();
+      __hip_atomic_store(done_host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
   constexpr int NT = kPoseThreads * G, NW = NT / 64;
   __shared__ PoseShared<G> sh;
   const int p = blockIdx.x;
@@ -410,6 +421,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
   if (n < 3) {  // optimizer.cc:951
     if (t < 7) pose_out[7 * p + t] = pin[t];
     if (t == 0) inliers[p] = 0;
+    signal_done();
     return;
   }
   // observations (and their levels) live in LDS for the whole call: one
@@ -778,6 +790,7 @@ __global__ __launch_bounds__(kPoseThreads * G) void k_pose_opt(
     for (int i = 0; i < 7; ++i) pose_out[7 * p + i] = f[i];
     inliers[p] = n - nbad_round;
   }
+  signal_done();
   PSTAMP(0);
   PSTAMP_END;
 }
@@ -786,7 +799,7 @@ template <int G>
 static hipError_t launch_pose_opt_g(const CamDev& c, const float* d_pose_in, const void* d_obs,
                                     const int* d_nobs, int obs_stride, int n_problems,
                                     float* d_pose_out, uint8_t* d_outlier, int* d_inliers,
-                                    double* d_pose_out_d, hipStream_t st) {
+                                    double* d_pose_out_d, hipStream_t st, int* done_host, int seq) {
   // observations staged in LDS: up to kPoseLdsObs, and what fits beside the
   // static part and (G == 1) the reduction buffer in 160 KB
   const size_t fixed = sizeof(PoseShared<G>) + (G == 1 ? kPoseRedT : 0) + 64;
@@ -802,7 +815,7 @@ static hipError_t launch_pose_opt_g(const CamDev& c, const float* d_pose_in, con
   }
   hipLaunchKernelGGL(k_pose_opt<G>, dim3(n_problems), dim3(kPoseThreads * G), lds, st, c,
                      d_pose_in, reinterpret_cast<const PoseObsDev*>(d_obs), d_nobs, obs_stride,
-                     d_pose_out, d_outlier, d_inliers, d_pose_out_d, lds_obs);
+                     d_pose_out, d_outlier, d_inliers, d_pose_out_d, lds_obs, done_host, seq);
   return hipGetLastError();
 }
 
@@ -812,15 +825,15 @@ static hipError_t launch_pose_opt_g(const CamDev& c, const float* d_pose_in, con
 hipError_t launch_pose_opt(const double cam[5], const float* d_pose_in, const void* d_obs,
                            const int* d_nobs, int obs_stride, int n_problems, float* d_pose_out,
                            uint8_t* d_outlier, int* d_inliers, double* d_pose_out_d,
-                           hipStream_t st, int groups) {
+                           hipStream_t st, int groups, int* done_host, int seq) {
   CamDev c{cam[0], cam[1], cam[2], cam[3], cam[4]};
   switch (groups) {
     case 1:
       return launch_pose_opt_g<1>(c, d_pose_in, d_obs, d_nobs, obs_stride, n_problems, d_pose_out,
-                                  d_outlier, d_inliers, d_pose_out_d, st);
+                                  d_outlier, d_inliers, d_pose_out_d, st, done_host, seq);
     case 2:
       return launch_pose_opt_g<2>(c, d_pose_in, d_obs, d_nobs, obs_stride, n_problems, d_pose_out,
-                                  d_outlier, d_inliers, d_pose_out_d, st);
+                                  d_outlier, d_inliers, d_pose_out_d, st, done_host, seq);
     default:
       return hipErrorInvalidValue;
   }

@@ -41,6 +41,25 @@ python3 tools/pmc_kernels.py --traffic $O/traffic --sq $O/sq --calib $O/calib \
   --stats $O/bench_kernel_stats.csv --images-per-launch $((2 * FR)) --out $O/kernels.json > $O/kernels.log 2>&1 \
   || { echo "summary failed"; tail -5 $O/kernels.log; exit 1; }
 echo "kernels.json ok"
+if [ "${VMEM:-1}" = "1" ]; then
+  # the vector-memory pipeline groups over the same
+  # workload, reduced per kernel and merged into kernels.json under "vmem"
+  rm -rf gpurun_out/pmc
+  PMC_GROUPS=tools/pmc_groups_vmem.txt PROF_ARGS="--frames $FR --iters 3 --mode ext" bash tools/pmc_run.sh \
+    > $O/vmem_passes.log 2>&1 || { echo "vmem passes failed"; tail -5 $O/vmem_passes.log; exit 1; }
+  python3 tools/pmc_vmem.py gpurun_out/pmc --out $O/vmem.json > $O/vmem.log 2>&1 \
+    || { echo "vmem summary failed"; tail -5 $O/vmem.log; exit 1; }
+  python3 - "$O" <<'PY'
+import json, sys
+o = sys.argv[1]
+k = json.load(open(f"{o}/kernels.json"))
+v = json.load(open(f"{o}/vmem.json"))
+k["vmem"] = {n: {kk: vv for kk, vv in d.items() if kk != "counters_per_dispatch"} for n, d in v.items()}
+k["vmem_source"] = "tools/pmc_groups_vmem.txt passes (tools/pmc_run.sh) reduced by tools/pmc_vmem.py"
+json.dump(k, open(f"{o}/kernels.json", "w"), indent=1)
+PY
+  echo "vmem ok"
+fi
 if [ "${RUN_BENCH:-1}" = "1" ]; then
   BENCH_KERNELS_JSON=$O/kernels.json timeout -k 10 400 python3 bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err \
     || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
