@@ -26,7 +26,9 @@ namespace {
 struct Arena {
   size_t bytes = 0;
   uint8_t* d = nullptr;
-  uint8_t* h = nullptr;  // pinned staging, same size
+  uint8_t* h = nullptr;   // pinned staging, same size (the output arena: host-mapped)
+  uint8_t* hd = nullptr;  // the device's address of h (mapped arenas)
+  bool mapped = false;
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -49,6 +51,10 @@ struct orbgpu_matcher {
   float thr_lsf = 0.0f;
   int thr_levels = -1;
   float thr[ORBGPU_MAX_LEVELS] = {};
+  // one-frame calls: the completion word k_mt_resolve stores (host-mapped)
+  int* h_done = nullptr;
+  int* h_done_dev = nullptr;
+  int seq = 0;
 };
 
 namespace {
@@ -134,7 +140,9 @@ orbgpu_status arena_reserve(Arena& a, size_t bytes) {
   if (a.h) (void)hipHostFree(a.h);
   a.d = a.h = nullptr;
   a.bytes = 0;
-  if (hipMalloc(&a.d, bytes) != hipSuccess || hipHostMalloc(&a.h, bytes) != hipSuccess)
+  if (hipMalloc(&a.d, bytes) != hipSuccess ||
+      hipHostMalloc(&a.h, bytes, a.mapped ? hipHostMallocMapped | hipHostMallocCoherent : 0) != hipSuccess ||
+      (a.mapped && hipHostGetDevicePointer(reinterpret_cast<void**>(&a.hd), a.h, 0) != hipSuccess))
     return ORBGPU_ERR_NOMEM;
   a.bytes = bytes;
   return ORBGPU_OK;
@@ -224,16 +232,36 @@ orbgpu_status run_host(HostCall& c, int n, int32_t* match, int* nmatches,
   orbgpu_matcher* m = c.m;
   hipStream_t s = m->stream;
   c.L.zero_err = 1;  // k_mt_grid writes the call's error word first (no memset)
-  if (hipMemcpyAsync(m->in.d, m->in.h, c.bi.off, hipMemcpyHostToDevice, s) ||
-      orbgpu::launch_match(c.L, s) != hipSuccess)
-    return ORBGPU_ERR_DEVICE;
   // outputs: the error word, match, nmatches (+ views) are contiguous at the
-  // front of `out`: one copy back
+  // front of `out`; k_mt_resolve mirrors them into the host-mapped arena and
+  // then stores the call's number into h_done
   const size_t dl = views_out ? (size_t)((uint8_t*)c.d_views_out - m->out.d) +
                                     sizeof(orbgpu_track_view) * n_pts
                               : (size_t)((uint8_t*)c.d_nm - m->out.d) + sizeof(int);
-  if (hipMemcpyAsync(m->out.h, m->out.d, dl, hipMemcpyDeviceToHost, s) || hipStreamSynchronize(s))
+  const int seq = m->seq = m->seq == 0x7fffffff ? 1 : m->seq + 1;
+  c.L.mirror_src = m->out.d;
+  c.L.mirror_dst = m->out.hd;
+  c.L.mirror_bytes = (int)dl;
+  c.L.done_host = m->h_done_dev;
+  c.L.seq = seq;
+  if (hipMemcpyAsync(m->in.d, m->in.h, c.bi.off, hipMemcpyHostToDevice, s) ||
+      orbgpu::launch_match(c.L, s) != hipSuccess)
     return ORBGPU_ERR_DEVICE;
+  volatile int* done = m->h_done;
+  bool seen = false;
+  for (long spin = 0; spin < (1L << 24); ++spin) {
+    if (*done == seq) {
+      seen = true;
+      break;
+    }
+    if ((spin & 4095) == 4095 && hipStreamQuery(s) != hipErrorNotReady) {
+      seen = *done == seq;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  if (!seen && (hipStreamSynchronize(s) != hipSuccess || *done != seq)) return ORBGPU_ERR_DEVICE;
   int err = 0;
   std::memcpy(&err, m->out.h + ((uint8_t*)c.d_call_err - m->out.d), sizeof(int));
   if (err) return ORBGPU_ERR_CAPACITY;
@@ -268,7 +296,11 @@ orbgpu_status orbgpu_matcher_create(int device, int max_keypoints, int max_point
   m->max_kp = max_keypoints;
   m->max_pts = max_points;
   const size_t pt = sizeof(orbgpu_map_point);
+  m->out.mapped = true;  // k_mt_resolve writes a one-frame call's outputs into it
+  const unsigned hflags = hipHostMallocMapped | hipHostMallocCoherent;
   if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&m->h_done), 64, hflags) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&m->h_done_dev), m->h_done, 0) != hipSuccess ||
       hipMalloc(&m->d_err, sizeof(int)) != hipSuccess ||
       hipMemset(m->d_err, 0, sizeof(int)) != hipSuccess ||
       arena_reserve(m->in, in_bytes(max_keypoints, max_points, pt)) != ORBGPU_OK ||
@@ -277,6 +309,7 @@ orbgpu_status orbgpu_matcher_create(int device, int max_keypoints, int max_point
     orbgpu_matcher_destroy(m);
     return ORBGPU_ERR_NOMEM;
   }
+  *m->h_done = 0;
   *out = m;
   return ORBGPU_OK;
 }
@@ -294,6 +327,7 @@ void orbgpu_matcher_destroy(orbgpu_matcher* m) {
   if (m->d_res) (void)hipFree(m->d_res);
   if (m->d_acc) (void)hipFree(m->d_acc);
   if (m->d_err) (void)hipFree(m->d_err);
+  if (m->h_done) (void)hipHostFree(m->h_done);
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
 }

@@ -688,6 +688,20 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   }
   int32_t* match = a.match + (size_t)f * a.kp_stride;
   for (int i = lane; i < n; i += 64) match[i] = lmatch[i];
+  if (a.mirror_dst) {  // one-frame host call: the outputs into host memory by this one workgroup
+    if (lane == 0) a.nmatches[f] = nmatch;
+    __syncthreads();                                  // this wave's stores drained
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // fresh lines of the other kernels' outputs
+    const uint4* s4 = reinterpret_cast<const uint4*>(a.mirror_src);
+    uint4* d4 = reinterpret_cast<uint4*>(a.mirror_dst);
+    for (int i = lane; i < (a.mirror_bytes + 15) >> 4; i += 64) d4[i] = s4[i];
+    __syncthreads();
+    if (lane == 0) {
+      __threadfence_system();
+      __hip_atomic_store(a.done_host, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
 #ifdef ORB_STAMPS
   if (lane == 0) {
     atomicAdd(&g_mt_stats[0], (unsigned long long)((nq + 63) / 64));

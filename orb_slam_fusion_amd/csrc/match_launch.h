@@ -76,6 +76,15 @@ struct MatchLaunch {
   int* nmatches;        // [n_frames]
   int* err;
   int zero_err;         // k_mt_grid stores err (a one-frame call's own word) instead of OR-ing into it
+  // one-frame host call: k_mt_resolve copies the output range [mirror_src,
+  // + mirror_bytes) of the device arena (error word, match row, count, views)
+  // into the host-mapped arena, then stores seq into done_host (the host
+  // polls it: no copy command, no stream synchronisation)
+  const uint8_t* mirror_src;
+  uint8_t* mirror_dst;
+  int mirror_bytes;
+  int* done_host;
+  int seq;
 };
 
 hipError_t launch_match(const MatchLaunch& a, hipStream_t st);
