@@ -119,7 +119,9 @@ struct orbgpu_extractor {
   // host path block [error word, pad x3 | uright x kcap | depth x kcap] on the
   // device and its pinned mirror: one copy back per call
   float* d_st_out = nullptr;
-  float* h_st_out = nullptr;
+  float* h_st_out = nullptr;      // host-mapped: [error word | uright | depth], then the completion word
+  float* h_st_out_dev = nullptr;
+  int st_seq = 0;
   size_t st_lists = 0, st_rowend = 0, st_sad = 0, st_out = 0;
 
   // optional per-stage event profiling of batch calls (a ring of event sets)
@@ -1043,8 +1045,11 @@ orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* righ
     left->h_st_out = nullptr;
     left->st_out = 0;
     if (dalloc(&left->d_st_out, need) ||
-        hipHostMalloc(&left->h_st_out, need * sizeof(float)) != hipSuccess)
+        hipHostMalloc(&left->h_st_out, (need + 16) * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&left->h_st_out_dev), left->h_st_out, 0) != hipSuccess)
       return ORBGPU_ERR_NOMEM;
+    reinterpret_cast<int*>(left->h_st_out)[need] = 0;
     left->st_out = need;
   }
   float* dur = left->d_st_out + 4;
@@ -1064,13 +1069,32 @@ orbgpu_status orbgpu_stereo_match(orbgpu_extractor* left, orbgpu_extractor* righ
   // the left call's keypoint count (its pinned output block, already synchronised)
   const int n = std::min(left->h_small[0], kcap);
   if (n > cap) return ORBGPU_ERR_CAPACITY;
-  // error word, uright[0, kcap), depth[0, n): one copy back
+  // error word, uright[0, kcap), depth[0, n): mirrored into the host-mapped
+  // block by k_stereo_median, which then stores the call's number after it
   const size_t bytes = (4 + (size_t)kcap + (size_t)n) * sizeof(float);
-  if (hipMemsetAsync(d_call_err, 0, sizeof(int), left->stream) ||
-      launch_stereo(a, left->stream) != hipSuccess ||
-      hipMemcpyAsync(left->h_st_out, left->d_st_out, bytes, hipMemcpyDeviceToHost, left->stream) ||
-      hipStreamSynchronize(left->stream))
-    return ORBGPU_ERR_DEVICE;
+  const int seq = left->st_seq = left->st_seq == 0x7fffffff ? 1 : left->st_seq + 1;
+  a.zero_err = 1;  // k_stereo_rows writes the error word (no memset)
+  a.mirror_src = reinterpret_cast<const uint8_t*>(left->d_st_out);
+  a.mirror_dst = reinterpret_cast<uint8_t*>(left->h_st_out_dev);
+  a.mirror_bytes = (int)bytes;
+  a.done_host = reinterpret_cast<int*>(left->h_st_out_dev) + left->st_out;
+  a.seq = seq;
+  if (launch_stereo(a, left->stream) != hipSuccess) return ORBGPU_ERR_DEVICE;
+  volatile int* done = reinterpret_cast<volatile int*>(left->h_st_out) + left->st_out;
+  bool seen = false;
+  for (long spin = 0; spin < (1L << 24); ++spin) {
+    if (*done == seq) {
+      seen = true;
+      break;
+    }
+    if ((spin & 4095) == 4095 && hipStreamQuery(left->stream) != hipErrorNotReady) {
+      seen = *done == seq;
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  if (!seen && (hipStreamSynchronize(left->stream) != hipSuccess || *done != seq)) return ORBGPU_ERR_DEVICE;
   int err = 0;
   std::memcpy(&err, left->h_st_out, sizeof(int));
   if (err) return ORBGPU_ERR_CAPACITY;

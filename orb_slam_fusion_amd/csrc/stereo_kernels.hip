@@ -109,7 +109,12 @@ __global__ __launch_bounds__(256) void k_stereo_rows(StereoLaunch a) {
     cnt[y] = base;
     base += c;
   }
-  if (threadIdx.x == 255 && incl > a.list_cap) atomicOr(a.err, 16);
+  if (threadIdx.x == 255) {
+    if (a.zero_err)
+      *a.err = incl > a.list_cap ? 16 : 0;  // the one-frame call's own word (one block)
+    else if (incl > a.list_cap)
+      atomicOr(a.err, 16);
+  }
   __syncthreads();
   uint16_t* list = a.lists + (size_t)f * a.list_cap;
   for (int i = threadIdx.x; i < nr; i += 256) {
@@ -260,23 +265,11 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoLaunch a) {
 }
 
 // Median filter of frame blockIdx.x (:965-980): the (m/2)-th smallest kept
-// window distance by a two-pass radix select (distances < 2^15).
-__global__ __launch_bounds__(256) void k_stereo_median(StereoLaunch a) {
-  __shared__ int hist[256];
-  __shared__ int tmp[256];
-  __shared__ int sel[2];
-  const int f = blockIdx.x;
-  const int nl = min(a.L.n[(size_t)f * a.L.n_fstride], a.cap);
-  const int* sad = a.sad + (size_t)f * a.out_fstride;
-  hist[threadIdx.x] = 0;
-  __syncthreads();
-  for (int i = threadIdx.x; i < nl; i += 256)
-    if (sad[i] >= 0) atomicAdd(&hist[sad[i] >> 7], 1);
-  __syncthreads();
-  int h = hist[threadIdx.x];
-  int incl = block_scan256(h, tmp);
-  const int m = tmp[255];
-  if (m == 0) return;  // uniform: the reference would read vDistIdx[0] of an empty list
+// window distance by a two-pass radix select (distances < 2^15).  m: kept
+// matches (> 0), h / incl: this thread's first-pass bucket count and
+// inclusive scan.
+__device__ __forceinline__ void median_filter(const StereoLaunch& a, int f, int nl, const int* sad, int* hist,
+                                              int* tmp, int* sel, int h, int incl, int m) {
   const int k = m / 2;
   if (incl > k && incl - h <= k) sel[0] = threadIdx.x, sel[1] = k - (incl - h);
   __syncthreads();
@@ -298,6 +291,37 @@ __global__ __launch_bounds__(256) void k_stereo_median(StereoLaunch a) {
       a.uright[o] = -1;
       a.depth[o] = -1;
     }
+}
+
+__global__ __launch_bounds__(256) void k_stereo_median(StereoLaunch a) {
+  __shared__ int hist[256];
+  __shared__ int tmp[256];
+  __shared__ int sel[2];
+  const int f = blockIdx.x;
+  const int nl = min(a.L.n[(size_t)f * a.L.n_fstride], a.cap);
+  const int* sad = a.sad + (size_t)f * a.out_fstride;
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nl; i += 256)
+    if (sad[i] >= 0) atomicAdd(&hist[sad[i] >> 7], 1);
+  __syncthreads();
+  const int h = hist[threadIdx.x];
+  const int incl = block_scan256(h, tmp);
+  const int m = tmp[255];
+  // m == 0 (uniform): the reference would read vDistIdx[0] of an empty list; nothing to filter
+  if (m > 0) median_filter(a, f, nl, sad, hist, tmp, sel, h, incl, m);
+  if (a.mirror_dst) {  // one-frame host call: the outputs into host memory by this one workgroup
+    __syncthreads();                                   // this block's stores drained
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // fresh lines of k_stereo_match's outputs
+    const uint4* s4 = reinterpret_cast<const uint4*>(a.mirror_src);
+    uint4* d4 = reinterpret_cast<uint4*>(a.mirror_dst);
+    for (int i = threadIdx.x; i < (a.mirror_bytes + 15) >> 4; i += 256) d4[i] = s4[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence_system();
+      __hip_atomic_store(a.done_host, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st) {

@@ -39,6 +39,16 @@ struct StereoLaunch {
   int* row_end;     // [n_frames][rows] end offset of each row's list
   int* sad;         // [n_frames][cap] window distance of kept matches, else -1
   int* err;
+  // one-frame host call (orbgpu_stereo_match): k_stereo_rows stores the
+  // call's error word (no memset before it); k_stereo_median copies the
+  // output range [mirror_src, + mirror_bytes) into host-mapped memory and then
+  // stores seq into done_host (the host polls it: no copy, no stream sync)
+  int zero_err;
+  const uint8_t* mirror_src;
+  uint8_t* mirror_dst;
+  int mirror_bytes;
+  int* done_host;
+  int seq;
 };
 
 hipError_t launch_stereo(const StereoLaunch& a, hipStream_t st);
