@@ -510,7 +510,8 @@ __device__ __forceinline__ int rot_bin(const MatchLaunch& a, const float* kps, i
 // last-frame paths but the output stores), and the next 64 queries' top-K
 // lists are loaded while the current ones resolve.
 __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
-  __shared__ uint32_t owner[kMatchMaxKeypoints];  // in-round first claiming lane, 64 = none
+  __shared__ uint32_t owner[kMatchMaxKeypoints];    // in-round first claiming lane, 64 = none
+  __shared__ uint32_t blocked[kMatchMaxKeypoints];  // in-round first stopped lane listing it, 64 = none
   __shared__ int32_t lmatch[kMatchMaxKeypoints];
   __shared__ uint8_t loct[kMatchMaxKeypoints];
   __shared__ uint32_t claims[kMatchMaxKeypoints / 32];
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   // mvpMapPoints of this call: the last matching query (later matches
   // overwrite, orb_matcher.cc:122, 1611), kept with atomicMax
   for (int i = lane; i < n; i += 64)
-    lmatch[i] = -1, owner[i] = 64, loct[i] = (uint8_t)kp_octave(F.kps + (size_t)i * kKpFloats);
+    lmatch[i] = -1, owner[i] = 64, blocked[i] = 64, loct[i] = (uint8_t)kp_octave(F.kps + (size_t)i * kKpFloats);
   for (int i = lane; i < kMatchMaxKeypoints / 32; i += 64) claims[i] = 0, removed[i] = 0;
   if (lane < kHistoLength) hist[lane] = 0;
   lds_barrier();
@@ -601,9 +602,43 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
       }
       lds_barrier();
       if (claimer) owner[b & 0xFFFF] = 64;
-      const uint64_t stop_mask = __ballot(hit || exhausted);
+      // Stopped: hit or exhausted, and every later query a stopped one could
+      // still affect.  A stopped query whose top-K list is its complete
+      // candidate set (count <= K) can only ever take an entry of that list,
+      // so a later query whose best (and, local, second) is in no such list
+      // is final now and commits past it -- its own claim cannot reach the
+      // stopped one.  A stopped query whose list may run out (a full search
+      // later, against every claim then made) blocks all later ones.  Hopeless
+      // queries and queries with no candidate are final anyway.
+      uint64_t stop_mask = __ballot(hit || exhausted);
+      if (stop_mask) {
+        const uint64_t inc = __ballot(!done && count > kMatchTopK);
+        const bool live = !done && !hopeless && b != kNone;
+        for (;;) {
+          const uint64_t si = stop_mask & inc;
+          const int first_inc = si ? __builtin_ctzll(si) : 64;
+          if ((stop_mask >> lane) & 1)
+#pragma unroll
+            for (int i = 0; i < kMatchTopK; ++i)
+              if (top[i] != kNone) atomicMin(&blocked[top[i] & 0xFFFF], (uint32_t)lane);
+          lds_barrier();
+          bool blk = false;
+          if (live) {
+            blk = lane > first_inc || blocked[b & 0xFFFF] < (uint32_t)lane;
+            if (local && s2 != kNone) blk = blk || blocked[s2 & 0xFFFF] < (uint32_t)lane;
+          }
+          const uint64_t grown = stop_mask | __ballot(blk);
+          lds_barrier();
+          if (grown == stop_mask) break;
+          stop_mask = grown;
+        }
+        if ((stop_mask >> lane) & 1)
+#pragma unroll
+          for (int i = 0; i < kMatchTopK; ++i)
+            if (top[i] != kNone) blocked[top[i] & 0xFFFF] = 64;
+      }
       const int stop = stop_mask ? __builtin_ctzll(stop_mask) : 64;
-      const bool commit = !done && lane < stop;
+      const bool commit = !done && !((stop_mask >> lane) & 1);
       if (commit) {
         if (ok) {
           const int idx = b & 0xFFFF;
@@ -688,6 +723,13 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
   }
   int32_t* match = a.match + (size_t)f * a.kp_stride;
   for (int i = lane; i < n; i += 64) match[i] = lmatch[i];
+#ifdef ORB_STAMPS
+  if (lane == 0) {
+    atomicAdd(&g_mt_stats[0], (unsigned long long)((nq + 63) / 64));
+    atomicAdd(&g_mt_stats[3], (unsigned long long)nq);
+    atomicAdd(&g_mt_stats[4], __builtin_amdgcn_s_memtime() - t_setup);  // chunks .. end
+  }
+#endif
   if (a.mirror_dst) {  // one-frame host call: the outputs into host memory by this one workgroup
     if (lane == 0) a.nmatches[f] = nmatch;
     __syncthreads();                                  // this wave's stores drained
@@ -702,13 +744,6 @@ __global__ __launch_bounds__(64) void k_mt_resolve(MatchLaunch a) {
     }
     return;
   }
-#ifdef ORB_STAMPS
-  if (lane == 0) {
-    atomicAdd(&g_mt_stats[0], (unsigned long long)((nq + 63) / 64));
-    atomicAdd(&g_mt_stats[3], (unsigned long long)nq);
-    atomicAdd(&g_mt_stats[4], __builtin_amdgcn_s_memtime() - t_setup);  // chunks .. end
-  }
-#endif
   if (lane == 0) a.nmatches[f] = nmatch;
 }
 
