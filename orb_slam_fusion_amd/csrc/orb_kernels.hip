@@ -1352,9 +1352,15 @@ constexpr int kOctThreads = 256;
 
 // In-place exclusive scan of a[0..n) in LDS; returns the total.  `tmp` holds
 // kOctThreads + 1 ints of LDS.  Must be called by the whole block.
+// kSmall: n <= 256 as one element a thread in two barriers -- the
+// single-image dataflow launch's octree (its latency chain); the batch
+// kernels keep the three-barrier form (the small path's registers cost the
+// batch octree its co-residency in the bench mix: 146.7k vs 149.7k frames/s
+// over three interleaved rounds, though 12 % faster alone)
+template <bool kSmall = false>
 __device__ int block_scan(int* a, int n, int* tmp) {
   const int t = threadIdx.x;
-  if (n <= kOctThreads) {
+  if (kSmall && n <= kOctThreads) {
     // one element a thread: DPP scans within the waves, the four wave totals
     // through LDS -- two barriers instead of three (the octree's node-list
     // scans, most of them at a few hundred nodes or fewer)
@@ -1518,7 +1524,7 @@ __device__ __forceinline__ void octree_level(
     cell_src[i] = cells[g.cell_begin + i].slot_off;
   }
   __syncthreads();
-  const int K = block_scan(cell_off, nc, s.scan_tmp);
+  const int K = block_scan<kWT>(cell_off, nc, s.scan_tmp);
   uint32_t* kd = dense + (size_t)img * P->slots + g.slot_begin;  // overflow beyond kcap
   int* kn = knode + (size_t)img * P->slots + g.slot_begin;
   // candidate k: packed x|y<<12|score<<24 and its node; LDS below kcap, HBM above
@@ -1585,7 +1591,7 @@ __device__ __forceinline__ void octree_level(
   __syncthreads();
   for (int i = t; i < R; i += kOctThreads) s.tmp2[i] = s.ccnt[i] > 0 ? 1 : 0;
   __syncthreads();
-  int S = block_scan(s.tmp2, R, s.scan_tmp);
+  int S = block_scan<kWT>(s.tmp2, R, s.scan_tmp);
   for (int i = t; i < R; i += kOctThreads) {
     if (s.ccnt[i] > 0) {
       const int p = s.tmp2[i];
@@ -1621,7 +1627,7 @@ __device__ __forceinline__ void octree_level(
     int m;  // |D|
     OSTAMP_ADD(12 + (phase == 2), 1);
     if (phase == 1) {
-      m = block_scan(s.ncnt, S, s.scan_tmp);  // ranks of the nodes with cnt >= 2
+      m = block_scan<kWT>(s.ncnt, S, s.scan_tmp);  // ranks of the nodes with cnt >= 2
       for (int i = t; i < S; i += kOctThreads)
         if (s.cnt[i] >= 2) s.rank[i] = s.ncnt[i];
     } else {
@@ -1675,7 +1681,7 @@ __device__ __forceinline__ void octree_level(
     if (phase == 2) {
       for (int r = t; r < m; r += kOctThreads) s.tmp2[r] = s.pc[r] - 1;
       __syncthreads();
-      const int tot = block_scan(s.tmp2, m, s.scan_tmp);
+      const int tot = block_scan<kWT>(s.tmp2, m, s.scan_tmp);
       // size after processing rank r = S + (exclusive[r] + pc[r] - 1)
       if (t == 0) s.scal[0] = m;
       __syncthreads();
@@ -1695,10 +1701,10 @@ __device__ __forceinline__ void octree_level(
 
     OSTAMP(6);
     // ---- push offsets (processing order) and stay offsets (list order)
-    const int T = block_scan(s.pc, m, s.scan_tmp);  // s.pc[r] = push offset of rank r
+    const int T = block_scan<kWT>(s.pc, m, s.scan_tmp);  // s.pc[r] = push offset of rank r
     for (int i = t; i < S; i += kOctThreads) s.stay[i] = s.rank[i] < 0 ? 1 : 0;
     __syncthreads();
-    const int n_stay = block_scan(s.stay, S, s.scan_tmp);
+    const int n_stay = block_scan<kWT>(s.stay, S, s.scan_tmp);
     const int S_new = T + n_stay;
     if (S_new > NC) {
       if (t == 0) atomicOr(err, kErrNodeCap);
@@ -1760,7 +1766,7 @@ __device__ __forceinline__ void octree_level(
     // expandable children in push order = positions T-1, T-2, ..., 0
     for (int i = t; i < T; i += kOctThreads) s.pc[i] = s.tmp2[T - 1 - i];
     __syncthreads();
-    const int e = block_scan(s.pc, T, s.scan_tmp);
+    const int e = block_scan<kWT>(s.pc, T, s.scan_tmp);
     for (int i = t; i < T; i += kOctThreads)
       if (s.tmp2[T - 1 - i]) s.exp_list[s.pc[i]] = T - 1 - i;
     for (int i = t; i < S_new; i += kOctThreads) {
