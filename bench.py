@@ -35,7 +35,7 @@ W, H = 752, 480
 PARAMS = (1000, 1.2, 8, 20, 7)
 POSE_OBS = 600
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PROFILE_ROUND = "r05"  # profiles/<round>/kernels.json (tools/profile_round.sh)
+PROFILE_ROUND = "r06"  # profiles/<round>/kernels.json (tools/profile_round.sh)
 SIDE_BATCH = 256  # frames / problems per call of the side lines (stereo, match, BoW, inertial, track)
 
 

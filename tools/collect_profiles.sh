@@ -10,7 +10,7 @@ S=gpurun_out/prof_$R
 D=profiles/$R
 mkdir -p $D
 cp $S/kernels.json $S/bench_kernel_stats.csv $D/
-for f in $S/bench_under_rocprof.json $S/bench.json; do [ -f "$f" ] && cp "$f" $D/; done
+for f in $S/bench_under_rocprof.json $S/bench.json $S/vmem.json; do [ -f "$f" ] && cp "$f" $D/; done
 T=$(mktemp -d)
 for sub in traffic sq calib; do
   find $S/$sub -name '*counter_collection.csv' | while read -r f; do
