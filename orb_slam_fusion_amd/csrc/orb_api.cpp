@@ -598,6 +598,17 @@ struct SingleCall {
     });
   }
 
+  // band b of the dataflow launch's image (rows at the level-0 pitch, the
+  // caller's stride equal to it): false past the last band
+  bool stage_band(int b) {
+    const size_t b0 = (size_t)b * kDfBandBytes;
+    if (!df || stride != pitch0 || b0 >= bytes) return false;
+    const size_t nb = std::min((size_t)kDfBandBytes, bytes - b0);
+    std::memcpy(h->h_img + b0, img + b0, nb);
+    __atomic_store_n(&h->h_band[b], seq, __ATOMIC_RELEASE);
+    return true;
+  }
+
   orbgpu_status wait() {
     if (!df) return hipStreamSynchronize(h->stream) == hipSuccess ? ORBGPU_OK : ORBGPU_ERR_DEVICE;
     // the launch writes the call's number after every output word: return as
@@ -858,8 +869,17 @@ orbgpu_status orbgpu_extract_stereo(orbgpu_extractor* left, orbgpu_extractor* ri
   if (c[0].df && c[1].df) {
     for (int k = 0; k < 2; ++k)
       if (st[k] == ORBGPU_OK) st[k] = c[k].launch();
-    for (int k = 0; k < 2; ++k)
-      if (st[k] == ORBGPU_OK) c[k].stage_df();
+    if (st[0] == ORBGPU_OK && st[1] == ORBGPU_OK && c[0].stride == c[0].pitch0 && c[1].stride == c[1].pitch0) {
+      // the two images' bands in alternation: both launches start on level 0
+      // together instead of the right one waiting for the whole left image
+      for (int b = 0;; ++b) {
+        const bool l = c[0].stage_band(b), r = c[1].stage_band(b);
+        if (!l && !r) break;
+      }
+    } else {
+      for (int k = 0; k < 2; ++k)
+        if (st[k] == ORBGPU_OK) c[k].stage_df();
+    }
   } else {
     for (int k = 0; k < 2; ++k)
       if (st[k] == ORBGPU_OK && (st[k] = c[k].launch()) == ORBGPU_OK) c[k].stage_df();
