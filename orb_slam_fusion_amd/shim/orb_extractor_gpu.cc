@@ -4,6 +4,7 @@
 #include "orb_extractor.h"
 
 #include <cassert>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
