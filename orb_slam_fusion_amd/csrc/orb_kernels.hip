@@ -2624,6 +2624,64 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
       octree_level<false, true>(P, a.cells, a.slots, a.cell_count, a.dense, a.knode, a.oct_out, a.oct_count, err, 0, l,
                           P->oct_kcap, nullptr, lds);
       pub = kDfOctDone + l;
+    } else if (type == kDfMirror) {
+      // the output block's host mirror by this one workgroup (host-memory
+      // writes of different CUs reach the host in no promised order), level
+      // by level in output order as each level's describe items finish, so
+      // only the last levels' few records are left when the final one lands;
+      // then the counts and the call's number.  With a lapping band the last
+      // describe item assembles and mirrors instead.
+      if (direct) {
+        if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items] = __builtin_amdgcn_s_memrealtime();
+        auto copy = [&](const void* src, void* dst, int bytes) {
+          const uint4* s4 = reinterpret_cast<const uint4*>(src);
+          uint4* d4 = reinterpret_cast<uint4*>(dst);
+          const int n16 = (bytes + 15) >> 4;
+          for (int i0 = tid; i0 < n16; i0 += 256 * 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (i0 + 256 * u < n16) v[u] = s4[i0 + 256 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (i0 + 256 * u < n16) d4[i0 + 256 * u] = v[u];
+          }
+        };
+        int base = 0;
+        for (int lv = 0; lv < P->levels; ++lv) {
+          if (tid == 0) {
+            df_wait(ctrl, kDfDescLvl + lv, (P->lev[lv].out_cap + 3) / 4, err);
+            df_acquire();
+            s_base = ld_pub<true>(a.oct_count + lv);
+          }
+          __syncthreads();
+          const int nl = s_base;
+          __syncthreads();
+          {  // 28-B records: dwords (a level's range need not be 16-B aligned)
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(a.kps_out) + 7 * (size_t)base;
+            uint32_t* d1 = reinterpret_cast<uint32_t*>(a.kps_host) + 7 * (size_t)base;
+            for (int i = tid; i < 7 * nl; i += 256) d1[i] = s1[i];
+          }
+          copy(reinterpret_cast<const uint64_t*>(a.desc_out) + 4 * (size_t)base,
+               reinterpret_cast<uint64_t*>(a.desc_host) + 4 * (size_t)base, nl * 32);
+          base += nl;
+        }
+        if (tid == 0) {
+          a.nm[0] = base;  // device counts (read by the stereo matcher)
+          a.nm[1] = base;
+          a.nm_host[0] = base;
+          a.nm_host[1] = base;
+          a.nm_host[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {  // every mirror store of this workgroup drained: the host's word
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items + 1] = __builtin_amdgcn_s_memrealtime();
+      }
+      pub = kDfMirrorDone;
     } else {  // kDfDescribe: slots out_off + 4 idx + wave of level l
       const int k = 4 * idx + wave;
       const DescFinal fin{reinterpret_cast<KeyPointOut*>(a.kps_out), reinterpret_cast<uint64_t*>(a.desc_out), s_base};
@@ -2637,6 +2695,9 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+      if (pub == kDfDescDone)  // the level's own count too (the host mirror's item waits on it)
+        (void)__hip_atomic_fetch_add(ctrl + (kDfDescLvl + l) * kDfCtrStride, 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
       const int old = __hip_atomic_fetch_add(ctrl + pub * kDfCtrStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = pub == kDfDescDone && old == df.desc_items - 1;
       if (last) df_acquire();  // every describe (and so every octree) item's results
@@ -2653,53 +2714,7 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
       }
     }
     __syncthreads();
-    if (s_last && (a.lap1 < kFastBorder || a.lap0 > a.lap1)) {
-      // direct outputs: every record is written; the counts (n = mono)
-      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items] = __builtin_amdgcn_s_memrealtime();
-      if (wave == 0) {
-        int c = lane < P->levels ? ld_pub<true>(a.oct_count + lane) : 0;
-        c = wave_iscan(c);
-        if (lane == 63) {
-          a.nm[0] = c;
-          a.nm[1] = c;
-          s_base = c;
-        }
-      }
-      __syncthreads();
-      // the block to its host mirror from this one workgroup (the describe
-      // items' stores were write-through and published; host-memory writes of
-      // different CUs reach the host in no promised order, so only this
-      // workgroup writes the mirror): records, descriptors, then the counts
-      const int n = s_base;
-      auto copy = [&](const void* src, void* dst, int bytes) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(src);
-        uint4* d4 = reinterpret_cast<uint4*>(dst);
-        const int n16 = (bytes + 15) >> 4;
-        for (int i0 = tid; i0 < n16; i0 += 256 * 4) {
-          uint4 v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (i0 + 256 * u < n16) v[u] = s4[i0 + 256 * u];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (i0 + 256 * u < n16) d4[i0 + 256 * u] = v[u];
-        }
-      };
-      copy(a.kps_out, a.kps_host, n * (int)sizeof(KeyPointOut));
-      copy(a.desc_out, a.desc_host, n * 32);
-      if (tid == 0) {
-        a.nm_host[0] = n;
-        a.nm_host[1] = n;
-        a.nm_host[2] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {  // every mirror store of this workgroup drained: the host's word
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        __hip_atomic_store(a.done_host, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items + 1] = __builtin_amdgcn_s_memrealtime();
-    } else if (s_last) {
+    if (s_last && !direct) {
       if (a.trace && tid == 0) a.trace[4 * (size_t)df.n_items] = __builtin_amdgcn_s_memrealtime();
       int* ab = reinterpret_cast<int*>(lds);
       assemble_image<true>(P, a.oct_out, a.oct_count, a.angle, a.desc, a.lap0, a.lap1,

@@ -50,7 +50,7 @@ struct ExtractLaunch {
 // ticket order the workers take them; an item depends only on items of
 // smaller tickets, so a worker that holds a ticket always finds its
 // producers running or done (no residency assumption).
-enum DfType : int { kDfCopy, kDfResize, kDfFast, kDfBlur, kDfOctree, kDfDescribe };
+enum DfType : int { kDfCopy, kDfResize, kDfFast, kDfBlur, kDfOctree, kDfDescribe, kDfMirror };
 // Counters in the handle's control block, one 128-B line each; zero at the
 // start of every launch (the last workgroup to leave resets them).
 enum DfCounter : int {
@@ -60,6 +60,8 @@ enum DfCounter : int {
   kDfBlurDone = kDfFastDone + kMaxLevels,
   kDfOctDone = kDfBlurDone + kMaxLevels,
   kDfDescDone = kDfOctDone + kMaxLevels,
+  kDfDescLvl,                        // + level: describe items of level l done
+  kDfMirrorDone = kDfDescLvl + kMaxLevels,
   kDfCounters
 };
 constexpr int kDfCtrStride = 32;  // ints between counters (128 B)

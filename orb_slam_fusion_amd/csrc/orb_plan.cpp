@@ -374,6 +374,9 @@ void make_df_items(const PlanHeader& P, int img_bytes, DfPlan& df, std::vector<u
     push(kDfDescribe, l, n);
     df.desc_items += n;
   }
+  // last: the host mirror, level by level as each level's descriptors land
+  // (no lapping band; with one, the last describe item assembles)
+  push(kDfMirror, 0, 1);
   df.n_items = (int)items.size();
 }
 

@@ -19,7 +19,7 @@ import numpy as np
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
-TYPES = ["copy", "resize", "fast", "blur", "octree", "describe"]
+TYPES = ["copy", "resize", "fast", "blur", "octree", "describe", "mirror"]
 
 
 def main():
