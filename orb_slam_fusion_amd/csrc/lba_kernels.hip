@@ -354,6 +354,40 @@ __device__ __forceinline__ bool last_block(unsigned* counter) {
   return last != 0;
 }
 
+// The same ticket for launches whose cross-block payload (what the last
+// block reads: the partials, pose quarters, link chi2s) is stored
+// write-through (st_wt: agent-scope relaxed atomic stores, sc1, straight to
+// L2) and drained before the barrier -- no release fence per block (its L2
+// write-back cost each block several microseconds at the kernel's tail).
+// The last block still acquires (an L1 / L2 invalidate) before reading.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#ifndef ORB_LBA_WT_TICKET
+#define ORB_LBA_WT_TICKET 1  // 0: the release-fence ticket everywhere (A/B)
+#endif
+__device__ __forceinline__ bool last_block_wt(unsigned* counter) {
+#if !ORB_LBA_WT_TICKET
+  return last_block(counter);
+#else
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return last != 0;
+#endif
+}
+
 // Sum of K per-block partials (partials[K * b + k]) in a fixed tree, by the
 // last block; valid in every thread.
 template <int K>
@@ -739,7 +773,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
     const int l = (int)blockIdx.x - neb;
     if (l >= 0 && l < a.n_imu) {  // (block-uniform)
       const double chi = lia_link<true>(a, l, threadIdx.x, a.poses[0], nullptr, 0, lsh);
-      if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
+      if (threadIdx.x == 0) st_wt(a.imu_tot + 2 + l, chi);
     }
   }
   // the system's blocks no pose pair writes (and, kModelImu, the IMU rows,
@@ -770,8 +804,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_begin(LbaArgs a) {
   }
   double v[1] = {r0};
   block_sum<1>(v, red);
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = v[0];
-  if (!last_block(a.counter + 0)) return;
+  if (threadIdx.x == 0) st_wt(a.partials + blockIdx.x, v[0]);
+  if (!last_block_wt(a.counter + 0)) return;
   double s[1];
   sum_partials<1>(a.partials, gridDim.x, s, red);
   if (threadIdx.x == 0) {
@@ -966,7 +1000,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
       double v = 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) v += red[r * 27 + k];
-      a.pose_part[27 * (size_t)blockIdx.x + k] = v;
+      st_wt(a.pose_part + 27 * (size_t)blockIdx.x + k, v);
     }
   } else if ((int)blockIdx.x >= n_pose_blocks + n_pt_blocks) {
     // kModelImu: the links' part of the system (lia_assemble_entry)
@@ -1001,8 +1035,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_sums(LbaArgs a) {
     __syncthreads();
     hmax = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
   }
-  if (threadIdx.x == 0) a.partials[blockIdx.x] = hmax;
-  if (!last_block(a.counter + 1)) return;
+  if (threadIdx.x == 0) st_wt(a.partials + blockIdx.x, hmax);
+  if (!last_block_wt(a.counter + 1)) return;
   // each pose's quarters in order -> Hpp (6 x 6 full), bp, the pose diagonal
   for (int idx = threadIdx.x; idx < 27 * a.n_free; idx += kThreads) {
     const int f = idx / 27, k = idx - 27 * f;
@@ -1288,20 +1322,27 @@ __global__ __launch_bounds__(kSplitThreads) void k_lba_schur_split(LbaArgs a) {
     if (t < nk) schur_write(a, fi, fj, t, sum);
     return;
   }
-  if (t < nk) a.sc_part[42 * (size_t)blockIdx.x + t] = sum;
-  if (!a.sc_fold_inline) return;  // k_lba_schur_fold adds the ranges
+  if (!a.sc_fold_inline) {  // k_lba_schur_fold adds the ranges
+    if (t < nk) a.sc_part[42 * (size_t)blockIdx.x + t] = sum;
+    return;
+  }
   // the pair's last block to finish (a ticket per pair, self-resetting) adds
   // its S range partials in range order -- k_lba_schur_fold's sum, without
-  // the launch
+  // the launch.  The partials are stored write-through (agent-scope relaxed
+  // atomic stores: sc1, straight to L2) and drained (vmcnt 0) before the
+  // barrier and the ticket -- no release fence (its L2 write-back made the
+  // first form of this, 17.9 us, slower than the extra launch)
+  if (t < nk)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.sc_part) + 42 * (size_t)blockIdx.x + t,
+                       (unsigned long long)__double_as_longlong(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned tk = __hip_atomic_fetch_add(a.pair_cnt + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = tk == (unsigned)(S - 1);
     if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (an L1 invalidate: the partials come from L2)
       __hip_atomic_store(a.pair_cnt + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -2391,7 +2432,7 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
       __syncthreads();  // the trial states' table
       if (l < a.n_imu) {  // (block-uniform)
         const double chi = lia_link<true>(a, l, threadIdx.x, tposes, nullptr, s1, lsh);
-        if (threadIdx.x == 0) a.imu_tot[2 + l] = chi;
+        if (threadIdx.x == 0) st_wt(a.imu_tot + 2 + l, chi);
       }
       link_block = true;
     }
@@ -2482,8 +2523,8 @@ __global__ __launch_bounds__(kThreads) void k_lba_trial(LbaArgs a) {
   block_sum<3>(part, red);
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.partials[3 * blockIdx.x + k] = part[k];
-  if (!last_block(a.counter + 2)) return;
+    for (int k = 0; k < 3; ++k) st_wt(a.partials + 3 * blockIdx.x + k, part[k]);
+  if (!last_block_wt(a.counter + 2)) return;
   double s[3];
   sum_partials<3>(a.partials, gridDim.x, s, red);
   if (threadIdx.x == 0) {
