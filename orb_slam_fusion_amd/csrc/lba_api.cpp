@@ -608,13 +608,13 @@ orbgpu_status run_window(orbgpu_lba_ctx* h, const orbgpu_camera* cam, int n_kf, 
   a.force_lin = h->relinearize;
   a.pose_split = reinterpret_cast<const int*>(A + u_sc) + (SP - SC);
   a.pair_cnt = reinterpret_cast<unsigned*>(A + u_pcnt);
-  // each pair's ranges folded by k_lba_schur_fold; ORBGPU_SCHUR_FOLD=inline:
-  // by the pair's last range block instead (a per-pair ticket: measured
-  // slower, 17.9 µs against 8.7 + 4.8 at C4 -- every block's agent-scope
-  // release costs more than the launch it saves)
+  // each pair's ranges folded by the pair's last range block (a per-pair
+  // ticket over write-through partials: one launch fewer a step; with an
+  // agent-scope release per block this measured slower, 17.9 µs against 8.7
+  // + 4.8 at C4); ORBGPU_SCHUR_FOLD=launch: by k_lba_schur_fold (A/B)
   static const bool fold_inline = [] {
     const char* e = std::getenv("ORBGPU_SCHUR_FOLD");
-    return e && std::strcmp(e, "inline") == 0;
+    return !(e && std::strcmp(e, "launch") == 0);
   }();
   a.sc_fold_inline = fold_inline ? 1 : 0;
   if (sc_split > 1) a.sc_part = dp(c_scp);
