@@ -13,12 +13,12 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 
-PROFILE = REPO / "profiles" / "r05" / "ba" / "ba_kernels.json"
+PROFILE = REPO / "profiles" / "r06" / "ba" / "ba_kernels.json"
 
 
 def roofline(window: str, n_sys: int) -> dict:
     """The back-end's roofline block from the committed rocprofv3 evidence
-    (tools/ba_prof.sh -> tools/ba_roofline.py -> profiles/r05/ba/): fp64
+    (tools/ba_prof.sh -> tools/ba_roofline.py -> profiles/r06/ba/): fp64
     FLOP/s and MFMA busy of k_lba_solve against the gfx950 fp64 matrix peak
     (the chip's, and the one CU a single-workgroup solve can use), HBM GB/s
     of the per-edge / per-pair stages against 8 TB/s.  Recomputable from the
