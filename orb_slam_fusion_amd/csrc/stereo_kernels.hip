@@ -64,18 +64,25 @@ __device__ __forceinline__ void kp_rows(const PlanHeader* P, const float* k, int
   y0 = max((int)floorf(y - r), 0);
 }
 
-// Block-wide inclusive scan of one int per thread (256 threads).
+// Block-wide inclusive scan of one int per thread (256 threads): wave scans
+// by lane shuffles, the four wave totals through LDS -- two barriers (the
+// LDS ladder it replaces took seventeen).  tmp[t] holds thread t's inclusive
+// value on return (tmp[255]: the total).
 __device__ __forceinline__ int block_scan256(int v, int* tmp) {
-  tmp[threadIdx.x] = v;
-  __syncthreads();
+  __shared__ int wtot[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = v;
 #pragma unroll
-  for (int d = 1; d < 256; d <<= 1) {
-    const int t = threadIdx.x >= (unsigned)d ? tmp[threadIdx.x - d] : 0;
-    __syncthreads();
-    tmp[threadIdx.x] += t;
-    __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += o;
   }
-  return tmp[threadIdx.x];
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  incl += (w > 0 ? wtot[0] : 0) + (w > 1 ? wtot[1] : 0) + (w > 2 ? wtot[2] : 0);
+  tmp[threadIdx.x] = incl;
+  __syncthreads();
+  return incl;
 }
 
 }  // namespace
