@@ -2462,6 +2462,9 @@ __global__ __launch_bounds__(256) void k_assemble(const PlanHeader* __restrict__
 // the assembly, mirroring the output block into host-mapped memory.
 // --------------------------------------------------------------------------
 enum : int { kErrDfTimeout = 64 };
+#ifndef ORB_DF_SLEEP
+#define ORB_DF_SLEEP 1  // s_sleep between a waiting worker's polls (x 64 clocks)
+#endif
 
 __device__ __forceinline__ void df_wait(int* ctrl, int id, int target, int* err) {
   int* c = ctrl + id * kDfCtrStride;
@@ -2470,7 +2473,7 @@ __device__ __forceinline__ void df_wait(int* ctrl, int id, int target, int* err)
       atomicOr(err, kErrDfTimeout);
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(ORB_DF_SLEEP);
   }
 }
 
@@ -2548,7 +2551,7 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
           if (lane == 0) atomicOr(err, kErrDfTimeout);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(ORB_DF_SLEEP);
       }
     }
     if (type != kDfCopy && type != kDfResize) wait();
@@ -2574,7 +2577,7 @@ __global__ __launch_bounds__(256) void k_extract_df(const DfLaunch* __restrict__
             atomicOr(err, kErrDfTimeout);
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          __builtin_amdgcn_s_sleep(ORB_DF_SLEEP);
         }
       __syncthreads();
       const int b0 = idx * kDfBandBytes, nb = min(kDfBandBytes, df.img_bytes - b0) >> 4;
