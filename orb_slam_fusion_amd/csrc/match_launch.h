@@ -16,7 +16,7 @@ constexpr int kMatchMaxPoints = 1 << 20;  // per frame
 // Per query the search keeps its kMatchTopK best candidates (in the
 // reference's order) plus the candidate count: claims by earlier queries are
 // then resolved from the list, a full re-search only when it runs out.
-constexpr int kMatchTopK = 4;
+constexpr int kMatchTopK = 6;
 constexpr int kMatchResWords = kMatchTopK + 1;
 
 // kModeLast: SearchByProjection(CurrentFrame, LastFrame); kModeLocal /
