@@ -5,5 +5,5 @@ tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
 timeout -k 10 300 python tools/bench_latency_inertial.py --frames 100 > gpurun_out/lat_inertial.json 2>gpurun_out/lat_inertial.err || exit 1
 tail -1 gpurun_out/lat_inertial.json
-timeout -k 10 600 python bench.py > gpurun_out/bench_k6.json 2>gpurun_out/bench_k6.err || exit 1
-tail -1 gpurun_out/bench_k6.json
+timeout -k 10 600 python bench.py > gpurun_out/bench_val.json 2>gpurun_out/bench_val.err || exit 1
+tail -1 gpurun_out/bench_val.json
