@@ -98,10 +98,12 @@ def gen(n):
         out.append(f"    double d;\n    asm volatile(\"s_nop 1\\n\\tv_mov_b64_dpp %0, %1 row_newbcast:{k % 16} "
                    f"row_mask:0xf bank_mask:0xf\" : \"=v\"(d) : \"v\"({src}[{k}]));\n")
         out.append("    flags |= (d < 0.0 ? 1 : 0) | (fabs(d) <= tiny ? 2 : 0);\n")
+        # the select and the flags at the pivot itself (an empty asm pins
+        # them): sunk to the solve's end they kept every pivot's d live
         if k < 16:
-            out.append(f"    dA = li == {k} ? d : dA;\n")
+            out.append(f"    dA = li == {k} ? d : dA;\n    asm volatile(\"\" : \"+v\"(dA), \"+v\"(flags));\n")
         else:
-            out.append(f"    dB = li == {k - 16} ? d : dB;\n")
+            out.append(f"    dB = li == {k - 16} ? d : dB;\n    asm volatile(\"\" : \"+v\"(dB), \"+v\"(flags));\n")
         rows_k = [i for i in range(n) if i != k and (i, k) in nz]
         cols_k = [j for j in range(k + 1, n) if (k, j) in nz] + [n]
         for i in rows_k:
