@@ -725,26 +725,29 @@ __device__ __forceinline__ bool ldlt15(double* A, int lane) {
 }
 
 // X = A^-1 (15 x 15, row stride 16) from the LDL^T factors in A: column c of
-// L^-1 by forward substitution (lane c, in place in X: a lane reads only the
-// entries it wrote), D^-1, then L^-T.  Loops kept rolled: this runs once per
-// call and must not add registers to the kernel's Gauss-Newton loop.
+// L^-1 by forward substitution (lane c, in registers), D^-1, then L^-T; the
+// L entries are uniform LDS reads that do not wait on the chain (a rolled
+// loop through X in LDS paid a store-to-load round trip per FMA).
 __device__ __forceinline__ void ldlt15_inverse(const double* A, double* X, int lane) {
   if (lane < 15) {
     const int c = lane;
-#pragma unroll 1
+    double v[15];
+#pragma unroll
     for (int i = 0; i < 15; ++i) {
-      double v = i == c ? 1.0 : 0.0;
-#pragma unroll 1
-      for (int k = 0; k < i; ++k) v -= A[i * kLd + k] * X[k * 16 + c];
-      X[i * 16 + c] = v;
+      double s = i == c ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; ++k) s -= A[i * kLd + k] * v[k];
+      v[i] = s;
     }
-#pragma unroll 1
+#pragma unroll
     for (int i = 14; i >= 0; --i) {
-      double v = X[i * 16 + c] / A[i * kLd + i];
-#pragma unroll 1
-      for (int k = i + 1; k < 15; ++k) v -= A[k * kLd + i] * X[k * 16 + c];
-      X[i * 16 + c] = v;
+      double s = v[i] / A[i * kLd + i];
+#pragma unroll
+      for (int k = i + 1; k < 15; ++k) s -= A[k * kLd + i] * v[k];
+      v[i] = s;
     }
+#pragma unroll
+    for (int i = 0; i < 15; ++i) X[i * 16 + c] = v[i];
   }
   wave_sync();
 }
@@ -998,9 +1001,21 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
     // rounding) none is dropped and pinv = H_pp^-1, taken from the LDL^T of
     // H_pp (fast path, a few thousand cycles).  Otherwise the parallel cyclic
     // Jacobi below (wave 0, on a 16 x 16 padding) with the cut.
+    // The shifted test (wave 0, rows 0..14 of sh.H) and the factorisation of
+    // H_pp itself with its inverse (wave 1, rows 15..29) run side by side; a
+    // failed test discards wave 1's pinv for the Jacobi path's.
+    if (wave == 1) {
+      double* A1 = sh.H + 15 * kLd;
+      for (int k = lane; k < 225; k += 64) {
+        const int i = k / 15, j = k - 15 * (k / 15);
+        A1[i * kLd + j] = sh.HM[i * kLd + j];
+      }
+      wave_sync();
+      (void)ldlt15(A1, lane);
+      ldlt15_inverse(A1, sh.pinv, lane);
+    }
     if (wave == 0) {
       double* A = sh.H;   // 16 x 16 working copy (stride kLd)
-      double* V = sh.V;   // 16 x 16 eigenvectors (stride 16)
       double dmax = 0;
       for (int i = 0; i < 15; ++i) dmax = fmax(dmax, fabs(sh.HM[i * kLd + i]));
       const double tau = fmax(2e-6, 1e-12 * dmax);
@@ -1009,17 +1024,14 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
         A[i * kLd + j] = sh.HM[i * kLd + j] - (i == j ? tau : 0.0);
       }
       wave_sync();
-      const bool fast = ldlt15(A, lane);
-      if (fast) {
-        for (int k = lane; k < 225; k += 64) {
-          const int i = k / 15, j = k - 15 * (k / 15);
-          A[i * kLd + j] = sh.HM[i * kLd + j];
-        }
-        wave_sync();
-        (void)ldlt15(A, lane);
-        ldlt15_inverse(A, sh.pinv, lane);
-      }
-      if (!fast) {
+      const bool pd = ldlt15(A, lane);  // the whole wave; pd is uniform
+      if (lane == 0) sh.ok = pd;
+    }
+    __syncthreads();
+    if (wave == 0 && !sh.ok) {
+      double* A = sh.H;   // 16 x 16 working copy (stride kLd)
+      double* V = sh.V;   // 16 x 16 eigenvectors (stride 16)
+      {
       for (int k = lane; k < 256; k += 64) {
         const int i = k >> 4, j = k & 15;
         A[i * kLd + j] = (i < 15 && j < 15) ? sh.HM[i * kLd + j] : 0.0;
@@ -1114,7 +1126,7 @@ __global__ __launch_bounds__(kInThreads) void k_pose_inertial(
         }
         sh.pinv[i * 16 + j] = s;
       }
-      }  // !fast
+      }  // Jacobi
     }
     __syncthreads();
     // T = Hcb pinv (into sh.H rows), then H15 = Hcc - T Hbc
