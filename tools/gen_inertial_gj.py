@@ -90,20 +90,19 @@ def gen(n):
     out = [f"// ---- n = {n} ----------------------------------------------------------\n",
            f"template <>\n__device__ __forceinline__ int gj_pivots<{n}>(double (&rA)[{n + 1}], "
            f"double (&rB)[{n + 1}], int li, double& dA, double& dB, double tiny) {{\n",
-           "  int flags = 0;  // bit 0: a negative pivot, bit 1: a (near-)zero pivot\n"]
+           ]
     total = 0
     for k in range(n):
         src = "rB" if k >= 16 else "rA"
         out.append(f"  {{  // pivot {k}\n")
         out.append(f"    double d;\n    asm volatile(\"s_nop 1\\n\\tv_mov_b64_dpp %0, %1 row_newbcast:{k % 16} "
                    f"row_mask:0xf bank_mask:0xf\" : \"=v\"(d) : \"v\"({src}[{k}]));\n")
-        out.append("    flags |= (d < 0.0 ? 1 : 0) | (fabs(d) <= tiny ? 2 : 0);\n")
-        # the select and the flags at the pivot itself (an empty asm pins
-        # them): sunk to the solve's end they kept every pivot's d live
+        # the select at the pivot itself (an empty asm pins it): sunk to the
+        # solve's end it kept every pivot's d live
         if k < 16:
-            out.append(f"    dA = li == {k} ? d : dA;\n    asm volatile(\"\" : \"+v\"(dA), \"+v\"(flags));\n")
+            out.append(f"    dA = li == {k} ? d : dA;\n    asm volatile(\"\" : \"+v\"(dA));\n")
         else:
-            out.append(f"    dB = li == {k - 16} ? d : dB;\n    asm volatile(\"\" : \"+v\"(dB), \"+v\"(flags));\n")
+            out.append(f"    dB = li == {k - 16} ? d : dB;\n    asm volatile(\"\" : \"+v\"(dB));\n")
         rows_k = [i for i in range(n) if i != k and (i, k) in nz]
         cols_k = [j for j in range(k + 1, n) if (k, j) in nz] + [n]
         for i in rows_k:
@@ -121,7 +120,14 @@ def gen(n):
                 out.append(block(n, k, cols_k[s:s + per], halves))
             total += len(cols_k) * len(halves)
         out.append("  }\n")
-    out.append(f"  return flags;  // {total} FMAs (dense: {sum(n - k for k in range(n)) * (2 if two else 1)})\n}}\n\n")
+    # the flags from the pivots each lane kept (lane li: pivots li, li + 16),
+    # one ballot instead of compares at every pivot
+    out.append(f"  // {total} FMAs (dense: {sum(n - k for k in range(n)) * (2 if two else 1)})\n"
+               f"  // bit 0: a negative pivot, bit 1: a (near-)zero pivot (wave-uniform)\n"
+               f"  const bool vA = li < {n}, vB = li + 16 < {n};\n"
+               f"  const bool neg = (vA && dA < 0.0) || (vB && dB < 0.0);\n"
+               f"  const bool small = (vA && fabs(dA) <= tiny) || (vB && fabs(dB) <= tiny);\n"
+               f"  return (__ballot(neg) != 0 ? 1 : 0) | (__ballot(small) != 0 ? 2 : 0);\n}}\n\n")
     return "".join(out)
 
 
